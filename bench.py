@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X checksum path (BASELINE.json metric:
+"GiB/s device-resident batched record checksum; % of HBM3E read BW").
+
+One step = one pass of the hot path (lsmck_crc32_batch*) over one batch of
+synthetic records already resident in HBM.  Default workload (N = 1) is
+BASELINE config 2: 2^24 fixed 4 KiB SSTable blocks = 64 GiB per GPU.  With
+--gpus N (one process per GPU, launched by torch.distributed.run) every rank
+checksums its own 2^24-block shard of the global block stream (weak scaling,
+record-sharded, no data-path collective); the control plane (barrier, max of
+per-rank times) goes over torch.distributed.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|1]
+                  [--blocks-per-gpu B] [--no-cpu-baseline]
+
+Prints ONE JSON line on rank 0 (see DESIGN.md section 5 for every field).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch  # first: liblsmck must bind to the HIP runtime torch loaded (lsm_storage_engine_amd/_lib.py)
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from lsm_storage_engine_amd import _lib  # noqa: E402
+from lsm_storage_engine_amd.device import Context, gen_zipf_lengths  # noqa: E402
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, GB/s (MI355X_MICROARCH.md chip table)
+METRIC = "GiB/s device-resident batched record checksum; % of HBM3E read BW"
+SEED = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3])
+    ap.add_argument("--blocks-per-gpu", type=int, default=0, help="override the per-GPU record count")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-records", type=int, default=0)
+    return ap.parse_args()
+
+
+def traffic_from_profiles(workload_key):
+    """HBM bytes per launch from the committed PMC summary (profiles/pmc_traffic.json),
+    collected with rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes and
+    corrected as MI355X_MICROARCH.md prescribes (FETCH_SIZE x 2 on gfx950)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get(workload_key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    torch.cuda.set_device(local)
+    stream = torch.cuda.current_stream(local)
+    sptr = stream.cuda_stream
+    ctx = Context(local)
+
+    cfg = a.config
+    seed = SEED[cfg]
+    if cfg == 2:
+        nrec = a.blocks_per_gpu or (1 << 24)
+        rec_len = 4096
+        nbytes = nrec * rec_len
+        byte_off = rank * nbytes  # this rank's shard of the global block stream
+        workload = f"config2: {nrec} fixed 4 KiB SSTable blocks per GPU ({nbytes / GIB:.0f} GiB), device-resident"
+    elif cfg == 1:
+        nrec = a.blocks_per_gpu or (1 << 20)
+        rec_len = 256
+        nbytes = nrec * rec_len
+        byte_off = rank * nbytes
+        workload = f"config1: {nrec} x 256 B WAL payloads per GPU, device-resident"
+    else:
+        nrec = a.blocks_per_gpu or (1 << 26)
+        lens = gen_zipf_lengths(seed + rank, nrec)
+        offs = np.zeros(nrec, dtype=np.uint64)
+        np.cumsum(lens[:-1], out=offs[1:])
+        nbytes = int(offs[-1]) + int(lens[-1])
+        byte_off = 0
+        workload = (f"config3: {nrec} mixed-length records per GPU (64 B-64 KiB, Zipf s=1.5, packed, unaligned; "
+                    f"{nbytes / GIB:.1f} GiB), device-resident")
+
+    data = ctx.alloc(nbytes + 64)
+    ctx.gen_stream(data.ptr, seed, byte_off, nbytes, sptr)
+    out = ctx.alloc(4 * nrec)
+    if cfg == 3:
+        d_off, d_len = ctx.alloc(8 * nrec), ctx.alloc(4 * nrec)
+        d_off.upload(offs)
+        d_len.upload(lens)
+        payload = int(lens.astype(np.uint64).sum())
+
+        def step():
+            ctx.crc32_device(data.ptr, d_off.ptr, d_len.ptr, nrec, out.ptr, sptr)
+        algo_bytes = payload + 12 * nrec + 4 * nrec
+    else:
+        payload = nbytes
+
+        def step():
+            ctx.crc32_fixed_device(data.ptr, rec_len, rec_len, nrec, out.ptr, sptr)
+        algo_bytes = payload + 4 * nrec
+    torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        step()
+    ctx.sync(sptr)
+    torch.cuda.synchronize()
+
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(a.steps):
+        step()
+    ev1.record(stream)
+    ctx.sync(sptr)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    wall = t1 - t0
+    ev_ms = ev0.elapsed_time(ev1) / a.steps
+    t = torch.tensor([wall], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t[0])
+
+    ms_per_step = wall_max * 1000.0 / a.steps
+    total_payload = payload * world
+    value = total_payload / GIB / (wall_max / a.steps)
+    achieved_gbs = algo_bytes / (ev_ms * 1e-3) / 1e9
+    wkey = f"config{cfg}"
+    traffic = traffic_from_profiles(wkey)
+
+    res = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: splitmix64 counter stream generated in HBM (same bytes as oracle_gen_stream)",
+        "config": {
+            "workload": workload,
+            "records_per_gpu": nrec,
+            "payload_bytes_per_gpu": payload,
+            "parallelism": f"record-sharded x{world}, no data-path collective",
+            "checksum": "CRC-32/ISO-HDLC (crc::crc32::checksum_ieee)",
+        },
+        "hbm_frac_of_peak": round(value * GIB / 1e9 / world / HBM_PEAK_GBS, 4),
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved_gbs, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": "crc32_fixed_kernel" if cfg != 3 else "crc32_desc_kernel",
+            "algorithmic_bytes_per_launch": algo_bytes,
+            "launch_ms_hip_events": round(ev_ms, 4),
+        },
+        "cpu_baseline": None,
+    }
+
+    # CPU baseline + parity of the same sample (rank 0, N = 1 only)
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import oracle as O  # the checker / baseline, never the measured path
+        if cfg == 3:
+            ns = a.cpu_sample_records or (1 << 21)
+            ns = min(ns, nrec)
+            send = int(offs[ns - 1]) + int(lens[ns - 1])
+            host = O.gen_stream(seed, 0, send)
+            tc0 = time.perf_counter()
+            want = O.crc32_batch(host, offs[:ns], lens[:ns], threads=1)
+            tc = time.perf_counter() - tc0
+            sbytes = int(lens[:ns].astype(np.uint64).sum())
+            sample = f"first {ns} records of the same Zipf stream ({sbytes / GIB:.2f} GiB)"
+        else:
+            ns = a.cpu_sample_records or ((1 << 20) if cfg == 2 else (1 << 22))
+            ns = min(ns, nrec)
+            host = O.gen_stream(seed, byte_off, ns * rec_len)
+            tc0 = time.perf_counter()
+            want = O.crc32_fixed(host, rec_len, rec_len, ns, threads=1)
+            tc = time.perf_counter() - tc0
+            sbytes = ns * rec_len
+            sample = f"first {ns} records of the same stream ({sbytes / GIB:.2f} GiB)"
+        got = out.download(np.uint32, count=ns)
+        res["cpu_baseline"] = {
+            "value": round(sbytes / GIB / tc, 3),
+            "unit": "GiB/s",
+            "cores": 1,
+            "kind": "port",
+            "sample": sample + "; oracle Sarwate byte-at-a-time CRC-32 (= crc 1.x checksum_ieee), 1 thread",
+            "seconds": round(tc, 2),
+            "gpu_matches_on_sample": bool(np.array_equal(got, want)),
+        }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    ctx.sync(sptr)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

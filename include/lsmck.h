@@ -1,0 +1,215 @@
+/*
+ * lsmck.h -- C ABI of liblsmck.so, the MI355X-native checksum path of the
+ * lsm_storage_engine reference (myroslavlisniak/lsm_storage_engine).
+ *
+ * The reference has no plugin/FFI API; its checksum path sits behind two Rust
+ * seams:
+ *   (i)  crc::crc32::checksum_ieee(&[u8]) -> u32, crate `crc` ^1.7
+ *        (Cargo.toml:14), called at src/wal.rs:135,153 (replay verify) and
+ *        src/wal.rs:177,187 (append);
+ *   (ii) the crate-private Checksums API of src/checksums.rs:
+ *        calculate_checksum (:20-38), verify (:40-62), write_checksums (:64-80),
+ *        called from src/sync/sstable.rs:119,139,210 and
+ *        src/tokio/sstable.rs:34,88,189.
+ * Every entry point below names the reference item it replaces.  The Rust
+ * bindings a maintainer would add are in INTEGRATION.md.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  The caller owns every buffer; the library
+ *     never retains a caller pointer after the call returns (synchronous calls)
+ *     or after the work on `stream` completes (LSMCK_DEVICE calls).
+ *   - Return values: 0 = ok; < 0 = error (-EINVAL, -ENOMEM, -EIO, or
+ *     LSMCK_EHIP - hipError_t); > 0 = an integrity verdict documented at the
+ *     function.  lsmck_last_error() holds a thread-local message.
+ *   - Scalar entry points (section 1) run on the calling CPU thread.  They are
+ *     the per-record latency path (one WAL append = one call; a kernel launch
+ *     costs microseconds), are reentrant and keep no mutable global state.
+ *   - Batch entry points (section 3) run on the GPU and FAIL (return
+ *     LSMCK_ENODEV) when no GPU / HIP runtime is usable: there is no CPU
+ *     fallback for a batch.
+ */
+#ifndef LSMCK_H
+#define LSMCK_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LSMCK_ABI_VERSION 1
+
+/* error codes (negative) */
+#define LSMCK_EINVAL (-22)
+#define LSMCK_ENOMEM (-12)
+#define LSMCK_EIO (-5)
+#define LSMCK_ENODEV (-19)
+#define LSMCK_EHIP (-1000) /* LSMCK_EHIP - hipError_t */
+
+/* flags for batch calls */
+#define LSMCK_DEVICE 0x1u      /* base/off/len/out are device pointers; async on `stream` */
+#define LSMCK_HOST 0x0u        /* host (pageable) pointers; staged through pinned memory; synchronous */
+#define LSMCK_HOST_PINNED 0x2u /* host pointers already pinned (hipHostMalloc); DMA without a copy */
+
+/* ======================================================================== */
+/* 1. Scalar CPU entry points                                                */
+/* ======================================================================== */
+
+/* Replaces crc::crc32::checksum_ieee (crc ^1.7) at src/wal.rs:135,153,177,187.
+ * CRC-32/ISO-HDLC: reflected 0xEDB88320, init/xorout 0xFFFFFFFF.
+ * n == 0 accepts any p (an empty Rust slice passes a dangling non-null pointer)
+ * and returns 0. */
+uint32_t lsmck_crc32_ieee(const uint8_t* p, size_t n);
+
+/* crc of (A || B) from crc(A) and the bytes of B (zlib crc32() convention);
+ * lsmck_crc32_update(0, p, n) == lsmck_crc32_ieee(p, n). */
+uint32_t lsmck_crc32_update(uint32_t crc_a, const uint8_t* p, size_t n);
+
+/* crc of (A || B) from crc(A), crc(B) and |B|. */
+uint32_t lsmck_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+
+/* SHA-256 (sha2 ^0.10.1 Sha256, src/checksums.rs:21,34,36). */
+typedef struct {
+  uint32_t h[8];
+  uint64_t nbytes;
+  uint8_t buf[64];
+  uint32_t nbuf;
+} lsmck_sha256_ctx;
+void lsmck_sha256_init(lsmck_sha256_ctx* c);
+void lsmck_sha256_update(lsmck_sha256_ctx* c, const uint8_t* p, size_t n);
+void lsmck_sha256_final(lsmck_sha256_ctx* c, uint8_t out[32]);
+void lsmck_sha256(const uint8_t* p, size_t n, uint8_t out[32]);
+
+/* base64 ^0.13 `encode` (STANDARD alphabet, '=' padded), src/checksums.rs:37.
+ * Writes 4*ceil(n/3) chars plus a NUL; returns the char count. */
+size_t lsmck_base64_encode(const uint8_t* p, size_t n, char* out);
+
+/* Replaces Checksums::calculate_checksum(path) (src/checksums.rs:20-38):
+ * SHA-256 of the whole file, base64 -> out (44 chars + NUL).
+ * The reference panics when the file cannot be opened (:25); this returns
+ * -errno and the Rust shim re-raises the panic. */
+int lsmck_checksum_file(const char* path, char out[45]);
+
+/* Replaces Checksums::write_checksums(&SsTableMetadata) (src/checksums.rs:64-80):
+ * hashes the data and index files and writes
+ * {"index_checksum":"<b64>","data_checksum":"<b64>"} to checksum_path, opened
+ * write+create WITHOUT truncate exactly as the reference opens it (:75-78). */
+int lsmck_checksums_write(const char* data_path, const char* index_path, const char* checksum_path);
+
+/* Replaces Checksums::verify(&SsTableMetadata) (src/checksums.rs:40-62).
+ * Returns 0 when both digests match, LSMCK_DATA_MISMATCH / LSMCK_INDEX_MISMATCH
+ * where the reference panics (:49-60; data is checked first), -errno when a
+ * file cannot be read, LSMCK_EJSON when the checksum file is not valid JSON of
+ * the Checksums shape (the reference's serde_json error, :48). */
+#define LSMCK_DATA_MISMATCH 1
+#define LSMCK_INDEX_MISMATCH 2
+#define LSMCK_EJSON (-74)
+int lsmck_checksums_verify(const char* data_path, const char* index_path, const char* checksum_path);
+
+/* WAL record framing, CommandLog::log (src/wal.rs:165-196).
+ * Insert: [u8 1][u32 crc LE][u32 klen][u32 vlen][key][val], crc over key||val.
+ * Remove: [u8 2][u32 crc LE][u32 klen][key], crc over key.
+ * Return the record size (13+klen+vlen / 9+klen); out must hold that much. */
+size_t lsmck_wal_encode_insert(const uint8_t* key, uint32_t klen, const uint8_t* val, uint32_t vlen,
+                               uint8_t* out);
+size_t lsmck_wal_encode_remove(const uint8_t* key, uint32_t klen, uint8_t* out);
+
+/* ======================================================================== */
+/* 2. Device context                                                          */
+/* ======================================================================== */
+typedef struct lsmck_ctx lsmck_ctx;
+
+/* Binds a context to HIP device `device` (one context per GPU; thread-safe:
+ * concurrent calls on one context are serialised on its scratch). NULL on
+ * failure (see lsmck_last_error). */
+lsmck_ctx* lsmck_ctx_create(int device);
+void lsmck_ctx_destroy(lsmck_ctx* ctx);
+const char* lsmck_last_error(void);
+int lsmck_device_count(void);
+
+/* ======================================================================== */
+/* 3. Batch GPU entry points                                                  */
+/* ======================================================================== */
+
+/* CRC-32 of n records: record i = base[off[i] .. off[i]+len[i]).  The batch
+ * form of checksum_ieee for WAL replay / bulk append (src/wal.rs:135,153,177).
+ * stream: hipStream_t (NULL = the context's default stream). */
+int lsmck_crc32_batch(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len, size_t n,
+                      uint32_t* out, unsigned flags, void* stream);
+
+/* Fixed-size records: record i = base[i*stride .. i*stride+len). */
+int lsmck_crc32_batch_fixed(lsmck_ctx* ctx, const uint8_t* base, size_t stride, uint32_t len, size_t n,
+                            uint32_t* out, unsigned flags, void* stream);
+
+/* Verify: compares against expected[i].  Host-visible results: *n_bad and
+ * *first_bad (index of the first mismatching record in batch order, or n).
+ * Synchronous.  Returns 0 when every record matches, 1 otherwise. */
+int lsmck_crc32_verify_batch(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len,
+                             const uint32_t* expected, size_t n, unsigned flags, void* stream, uint64_t* n_bad,
+                             uint64_t* first_bad);
+
+/* SHA-256 of n messages -> out32[32*i .. 32*i+32).  The batch form of
+ * calculate_checksum's digest (src/checksums.rs:20-38). */
+int lsmck_sha256_batch(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len, size_t n,
+                       uint8_t* out32, unsigned flags, void* stream);
+int lsmck_sha256_batch_fixed(lsmck_ctx* ctx, const uint8_t* base, size_t stride, uint32_t len, size_t n,
+                             uint8_t* out32, unsigned flags, void* stream);
+
+/* WAL replay verify: the batch form of the CommandLog iterator + MemTable::from_log
+ * (src/wal.rs:68-84,122-163; src/memtable.rs:28-47) over an in-memory WAL image.
+ * Headers are walked on the host (each record's length lives in the previous
+ * header), every payload CRC is checked on the GPU in one batch.
+ * recs (optional, cap entries) receives the parsed records in log order.
+ * Returns
+ *   0                      clean end of log (header EOF ends iteration, wal.rs:76-77)
+ *   LSMCK_WAL_CORRUPTED    first bad record is an Insert: WalError::CorruptedData
+ *                          {checksum=*bad_crc, expected=*bad_expected} (wal.rs:136-141)
+ *   LSMCK_WAL_REMOVE_PANIC first bad record is a Remove: the reference panics (wal.rs:154-159)
+ *   LSMCK_WAL_BAD_TYPE     InvalidCommandType(*bad_crc) at record *bad_index (wal.rs:36)
+ * *nrec = records accepted before the stop.  flags: LSMCK_HOST or LSMCK_DEVICE
+ * for `wal` (the header walk always needs a host copy: with LSMCK_DEVICE the
+ * image is read back once). */
+#define LSMCK_WAL_CORRUPTED 1
+#define LSMCK_WAL_REMOVE_PANIC 2
+#define LSMCK_WAL_BAD_TYPE 3
+typedef struct {
+  uint64_t rec_off;     /* header offset */
+  uint64_t payload_off; /* key offset */
+  uint32_t klen, vlen;  /* vlen = 0 for Remove */
+  uint32_t crc;         /* stored checksum */
+  uint32_t type;        /* 1 Insert, 2 Remove */
+} lsmck_wal_rec;
+int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsigned flags, lsmck_wal_rec* recs,
+                            size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc,
+                            uint32_t* bad_expected);
+
+/* Whole-tree SSTable verify: the batch form of Checksums::verify over many
+ * tables (Db::load, src/tokio/db.rs:37-59 -> src/tokio/sstable.rs:34).
+ * Reads every data/index file, hashes all of them in one GPU batch, compares
+ * with each checksum file.  status[i] gets 0 / LSMCK_DATA_MISMATCH /
+ * LSMCK_INDEX_MISMATCH / -errno / LSMCK_EJSON for table i.  Returns the number
+ * of tables whose status is not 0. */
+int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, const char* const* index_paths,
+                                const char* const* checksum_paths, size_t n, int* status);
+
+/* ======================================================================== */
+/* 4. Plumbing for hosts without their own HIP bindings (tests, bench)        */
+/* ======================================================================== */
+void* lsmck_dev_alloc(lsmck_ctx* ctx, size_t bytes);       /* hipMalloc */
+void lsmck_dev_free(lsmck_ctx* ctx, void* p);
+void* lsmck_host_alloc_pinned(lsmck_ctx* ctx, size_t bytes); /* hipHostMalloc */
+void lsmck_host_free_pinned(lsmck_ctx* ctx, void* p);
+int lsmck_memcpy_h2d(lsmck_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream);
+int lsmck_memcpy_d2h(lsmck_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream);
+int lsmck_memset_dev(lsmck_ctx* ctx, void* dst, int value, size_t bytes, void* stream);
+int lsmck_stream_sync(lsmck_ctx* ctx, void* stream);
+/* Synthetic records: device byte stream, byte b = byte (b%8) of
+ * splitmix64(seed ^ (b/8)) for b in [byte_off, byte_off+n). */
+int lsmck_gen_stream(lsmck_ctx* ctx, uint8_t* dst_dev, uint64_t seed, uint64_t byte_off, size_t n, void* stream);
+/* Zipf(s) lengths on k=1..kmax, L = max(lmin, 64k - j), j ~ U{0..63} (host). */
+void lsmck_gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, size_t n, uint32_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LSMCK_H */

@@ -1,0 +1,857 @@
+// lsmck_api.cpp -- device context and batch dispatch of liblsmck.so
+// (include/lsmck.h sections 2-4).
+//
+// A context owns, per GPU: the CRC combination tables (x^(8*128*k) mod P,
+// init terms, slicing tables; ~0.5 MiB, resident in HBM and L2), the scratch
+// of the descriptor path (segment prefix sums, tile -> first record), and two
+// pinned staging slots for host-resident batches (H2D / kernel / D2H of chunk
+// c overlap the host-side packing of chunk c+1).
+#include <errno.h>
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "lsmck.h"
+#include "lsmck_device.h"
+#include "lsmck_internal.h"
+
+using lsmck::CrcParams;
+using lsmck::ShaParams;
+
+namespace {
+
+constexpr uint64_t kMaxSegsPerLaunch = (1ull << 32) - 64;  // 32-bit segment indices in the kernels
+constexpr size_t kChunkBytes = 64ull << 20;                // host staging chunk (payload)
+constexpr size_t kChunkRecs = 1u << 20;                    // host staging chunk (records)
+
+struct HipFail {
+  hipError_t e;
+};
+
+int hip_error(hipError_t e, const char* what) {
+  std::string m = std::string(what) + ": " + hipGetErrorString(e);
+  return lsmck_host::set_error(LSMCK_EHIP - (int)e, m.c_str());
+}
+
+#define HIPCHK(expr)                                  \
+  do {                                                \
+    hipError_t _e = (expr);                           \
+    if (_e != hipSuccess) return hip_error(_e, #expr); \
+  } while (0)
+
+int launch_rc(int rc, const char* what) {
+  if (rc == 0) return 0;
+  return hip_error((hipError_t)(-rc), what);
+}
+
+template <typename T>
+int ensure_dev(T** p, size_t* cap, size_t need) {
+  if (*cap >= need && *p) return 0;
+  size_t want = std::max(need, *cap * 3 / 2);
+  if (want == 0) want = 1;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  HIPCHK(hipMalloc((void**)p, want * sizeof(T)));
+  *cap = want;
+  return 0;
+}
+
+template <typename T>
+int ensure_pinned(T** p, size_t* cap, size_t need) {
+  if (*cap >= need && *p) return 0;
+  size_t want = std::max(need, *cap * 3 / 2);
+  if (want == 0) want = 1;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  HIPCHK(hipHostMalloc((void**)p, want * sizeof(T), hipHostMallocDefault));
+  *cap = want;
+  return 0;
+}
+
+// Scratch of the descriptor CRC path (one per in-flight launch).
+struct DescScratch {
+  uint32_t* seg_start = nullptr;
+  size_t cap_seg = 0;
+  uint32_t* block_sum = nullptr;
+  size_t cap_bs = 0;
+  uint32_t* tile_first = nullptr;
+  size_t cap_tf = 0;
+  uint32_t* total = nullptr;  // device, 1 u32
+  void release() {
+    if (seg_start) (void)hipFree(seg_start);
+    if (block_sum) (void)hipFree(block_sum);
+    if (tile_first) (void)hipFree(tile_first);
+    if (total) (void)hipFree(total);
+    *this = DescScratch();
+  }
+};
+
+// One pinned staging slot of the host-resident pipeline.
+struct Stage {
+  hipStream_t s = nullptr;
+  hipEvent_t done = nullptr;
+  bool busy = false;
+  // host (pinned)
+  uint8_t* h_pay = nullptr;
+  size_t cap_h_pay = 0;
+  uint64_t* h_off = nullptr;
+  size_t cap_h_off = 0;
+  uint32_t* h_len = nullptr;
+  size_t cap_h_len = 0;
+  uint8_t* h_out = nullptr;
+  size_t cap_h_out = 0;
+  // device
+  uint8_t* d_pay = nullptr;
+  size_t cap_d_pay = 0;
+  uint64_t* d_off = nullptr;
+  size_t cap_d_off = 0;
+  uint32_t* d_len = nullptr;
+  size_t cap_d_len = 0;
+  uint8_t* d_out = nullptr;
+  size_t cap_d_out = 0;
+  DescScratch scratch;
+  // bookkeeping of the chunk in flight
+  size_t rec0 = 0, nrec = 0;
+  void release() {
+    if (h_pay) (void)hipHostFree(h_pay);
+    if (h_off) (void)hipHostFree(h_off);
+    if (h_len) (void)hipHostFree(h_len);
+    if (h_out) (void)hipHostFree(h_out);
+    if (d_pay) (void)hipFree(d_pay);
+    if (d_off) (void)hipFree(d_off);
+    if (d_len) (void)hipFree(d_len);
+    if (d_out) (void)hipFree(d_out);
+    scratch.release();
+    if (done) (void)hipEventDestroy(done);
+    if (s) (void)hipStreamDestroy(s);
+    *this = Stage();
+  }
+};
+
+}  // namespace
+
+struct lsmck_ctx {
+  int dev = 0;
+  int ncu = 0;
+  hipStream_t stream0 = nullptr;
+  uint32_t* d_master = nullptr;  // 4 x 256 slicing tables
+  uint32_t* d_kseg = nullptr;    // 65536
+  uint32_t* d_khi = nullptr;     // 65536
+  uint32_t* d_tinit = nullptr;   // 129
+  std::mutex mu;
+  DescScratch scratch;           // device-mode descriptor scratch
+  hipEvent_t scratch_ev = nullptr;
+  uint32_t* h_total = nullptr;   // pinned
+  unsigned long long* d_verify = nullptr;  // [n_bad, first_bad]
+  unsigned long long* h_verify = nullptr;  // pinned
+  Stage stage[2];
+};
+
+namespace {
+
+struct DevGuard {
+  int prev = -1;
+  explicit DevGuard(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != d) (void)hipSetDevice(d);
+  }
+  ~DevGuard() {
+    int cur;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+hipStream_t pick_stream(lsmck_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream0; }
+
+int ensure_scratch(DescScratch& sc, size_t nrec, size_t nblocks) {
+  int rc;
+  if ((rc = ensure_dev(&sc.seg_start, &sc.cap_seg, nrec))) return rc;
+  if ((rc = ensure_dev(&sc.block_sum, &sc.cap_bs, nblocks))) return rc;
+  if (!sc.total) HIPCHK(hipMalloc((void**)&sc.total, 16));
+  return 0;
+}
+
+void fill_tables(lsmck_ctx* ctx, CrcParams* P) {
+  P->kseg = ctx->d_kseg;
+  P->khi = ctx->d_khi;
+  P->tinit = ctx->d_tinit;
+  P->master = ctx->d_master;
+}
+
+// Fixed-size CRC on device pointers, split so each launch has < 2^32 segments.
+int crc_fixed_device(lsmck_ctx* ctx, const uint8_t* base, size_t stride, uint32_t len, size_t n, uint32_t* out,
+                     hipStream_t st) {
+  if (n == 0) return 0;
+  if (len == 0) {
+    HIPCHK(hipMemsetAsync(out, 0, n * 4, st));
+    return 0;
+  }
+  uint64_t nsegr = (len + 127u) / 128u;
+  uint64_t per = kMaxSegsPerLaunch / nsegr;
+  // every record is stored whole by one lane when no record straddles a
+  // 64-segment tile; otherwise partial results are XOR-accumulated into zeros
+  bool straddle = (64 % nsegr) != 0;
+  if (straddle) HIPCHK(hipMemsetAsync(out, 0, n * 4, st));
+  for (size_t r0 = 0; r0 < n; r0 += per) {
+    size_t cnt = std::min<uint64_t>(per, n - r0);
+    CrcParams P{};
+    P.base = base + r0 * stride;
+    P.stride = stride;
+    P.flen = len;
+    P.nrec = cnt;
+    P.out = out + r0;
+    fill_tables(ctx, &P);
+    int rc = lsmk_launch_crc32_fixed(&P, ctx->ncu, st);
+    if (rc) return launch_rc(rc, "crc32_fixed kernel");
+  }
+  return 0;
+}
+
+// Descriptor CRC on device pointers with known (host) total segment count
+// (host staging path) or unknown (device path: read back after the scan).
+int crc_desc_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const uint64_t* off, const uint32_t* len,
+                    size_t n, uint32_t* out, hipStream_t st, int64_t known_total, uint32_t* h_total) {
+  if (n == 0) return 0;
+  if (n >= (1ull << 32)) return lsmck_host::set_error(LSMCK_EINVAL, "more than 2^32-1 records in one batch");
+  size_t nb = (size_t)lsmk_scan_block_count(n);
+  int rc = ensure_scratch(sc, n, nb);
+  if (rc) return rc;
+  HIPCHK(hipMemsetAsync(out, 0, n * 4, st));
+  CrcParams P{};
+  P.base = base;
+  P.off = off;
+  P.len = len;
+  P.nrec = n;
+  P.seg_start = sc.seg_start;
+  P.total_segs = sc.total;
+  P.out = out;
+  fill_tables(ctx, &P);
+  rc = lsmk_launch_crc32_scan(&P, sc.block_sum, st);
+  if (rc) return launch_rc(rc, "crc32 scan");
+  uint64_t total;
+  if (known_total >= 0) {
+    total = (uint64_t)known_total;
+  } else {
+    HIPCHK(hipMemcpyAsync(h_total, sc.total, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    total = *h_total;
+  }
+  if (total >= kMaxSegsPerLaunch)
+    return lsmck_host::set_error(LSMCK_EINVAL, "batch exceeds 2^32 128-byte segments; split it");
+  if (total == 0) return 0;
+  size_t ntiles = (size_t)((total + 63) / 64);
+  if ((rc = ensure_dev(&sc.tile_first, &sc.cap_tf, ntiles))) return rc;
+  P.tile_first = sc.tile_first;
+  rc = lsmk_launch_crc32_desc(&P, sc.block_sum, ctx->ncu, st);
+  if (rc) return launch_rc(rc, "crc32_desc kernel");
+  return 0;
+}
+
+int sha_device(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len, size_t stride,
+               uint32_t flen, size_t n, const uint32_t* order, uint8_t* out32, hipStream_t st) {
+  (void)ctx;
+  ShaParams P{};
+  P.base = base;
+  P.off = off;
+  P.len = len;
+  P.stride = stride;
+  P.flen = flen;
+  P.nmsg = n;
+  P.order = order;
+  P.out = out32;
+  int rc = lsmk_launch_sha256(&P, st);
+  return rc ? launch_rc(rc, "sha256 kernel") : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Host-resident batches: chunked, double-buffered pipeline through pinned slots.
+enum Kind { CRC = 0, SHA = 1 };
+
+struct HostJob {
+  Kind kind;
+  const uint8_t* base;
+  const uint64_t* off;  // null -> fixed
+  const uint32_t* len;
+  size_t stride;
+  uint32_t flen;
+  size_t n;
+  uint8_t* out;  // 4 or 32 bytes per record
+  bool pinned;   // base is pinned: DMA straight from it (contiguous spans only)
+};
+
+int stage_init(Stage& S) {
+  if (!S.s) HIPCHK(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
+  if (!S.done) HIPCHK(hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
+  return 0;
+}
+
+// Wait for a slot's previous chunk and hand its results to the caller.
+int stage_retire(Stage& S, const HostJob& J) {
+  if (!S.busy) return 0;
+  HIPCHK(hipEventSynchronize(S.done));
+  size_t esz = J.kind == CRC ? 4 : 32;
+  memcpy(J.out + S.rec0 * esz, S.h_out, S.nrec * esz);
+  S.busy = false;
+  return 0;
+}
+
+int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
+  size_t esz = J.kind == CRC ? 4 : 32;
+  int rc;
+  for (auto& S : ctx->stage)
+    if ((rc = stage_init(S))) return rc;
+  size_t r = 0;
+  int slot = 0;
+  while (r < J.n) {
+    // choose the chunk [r, r1)
+    size_t r1 = r;
+    uint64_t bytes = 0;
+    uint64_t span_lo = UINT64_MAX, span_hi = 0;
+    bool mono = true;
+    uint64_t prev_end = 0;
+    while (r1 < J.n && (r1 - r) < kChunkRecs) {
+      uint64_t o = J.off ? J.off[r1] : (uint64_t)r1 * J.stride;
+      uint64_t l = J.off ? J.len[r1] : J.flen;
+      if (r1 > r && bytes + l > kChunkBytes) break;
+      if (r1 > r && o < prev_end) mono = false;
+      prev_end = o + l;
+      span_lo = std::min(span_lo, o);
+      span_hi = std::max(span_hi, o + l);
+      bytes += l;
+      ++r1;
+    }
+    size_t cnt = r1 - r;
+    if (span_lo == UINT64_MAX) span_lo = span_hi = 0;
+    // fixed-stride records always ship as their span (the kernel indexes by stride)
+    bool use_span = !J.off || (mono && (span_hi - span_lo) <= bytes + bytes / 4 + 4096);
+    Stage& S = ctx->stage[slot];
+    if ((rc = stage_retire(S, J))) return rc;
+    // descriptors (rebased) and payload
+    size_t pay_bytes = use_span ? (size_t)(span_hi - span_lo) : (size_t)bytes;
+    if ((rc = ensure_pinned(&S.h_out, &S.cap_h_out, cnt * esz))) return rc;
+    if ((rc = ensure_dev(&S.d_out, &S.cap_d_out, cnt * esz))) return rc;
+    if ((rc = ensure_dev(&S.d_pay, &S.cap_d_pay, pay_bytes + 16))) return rc;
+    const uint8_t* h_src = nullptr;
+    if (J.off) {
+      if ((rc = ensure_pinned(&S.h_off, &S.cap_h_off, cnt))) return rc;
+      if ((rc = ensure_pinned(&S.h_len, &S.cap_h_len, cnt))) return rc;
+      if ((rc = ensure_dev(&S.d_off, &S.cap_d_off, cnt))) return rc;
+      if ((rc = ensure_dev(&S.d_len, &S.cap_d_len, cnt))) return rc;
+      uint64_t pos = 0;
+      for (size_t i = 0; i < cnt; ++i) {
+        uint64_t o = J.off[r + i];
+        S.h_len[i] = J.len[r + i];
+        S.h_off[i] = use_span ? o - span_lo : pos;
+        pos += J.len[r + i];
+      }
+    }
+    if (use_span && J.pinned) {
+      h_src = J.base + span_lo;
+    } else {
+      if ((rc = ensure_pinned(&S.h_pay, &S.cap_h_pay, pay_bytes + 16))) return rc;
+      if (use_span) {
+        memcpy(S.h_pay, J.base + span_lo, pay_bytes);
+      } else {
+        uint64_t pos = 0;
+        for (size_t i = 0; i < cnt; ++i) {
+          memcpy(S.h_pay + pos, J.base + J.off[r + i], J.len[r + i]);
+          pos += J.len[r + i];
+        }
+      }
+      h_src = S.h_pay;
+    }
+    HIPCHK(hipMemcpyAsync(S.d_pay, h_src, pay_bytes, hipMemcpyHostToDevice, S.s));
+    if (J.off) {
+      HIPCHK(hipMemcpyAsync(S.d_off, S.h_off, cnt * 8, hipMemcpyHostToDevice, S.s));
+      HIPCHK(hipMemcpyAsync(S.d_len, S.h_len, cnt * 4, hipMemcpyHostToDevice, S.s));
+    }
+    if (J.kind == CRC) {
+      if (J.off) {
+        int64_t total = 0;
+        for (size_t i = 0; i < cnt; ++i) total += (S.h_len[i] + 127u) / 128u;
+        rc = crc_desc_device(ctx, S.scratch, S.d_pay, S.d_off, S.d_len, cnt, (uint32_t*)S.d_out, S.s, total, nullptr);
+      } else {
+        // fixed records: the span starts at record r
+        rc = crc_fixed_device(ctx, S.d_pay, J.stride, J.flen, cnt, (uint32_t*)S.d_out, S.s);
+      }
+    } else {
+      if (J.off)
+        rc = sha_device(ctx, S.d_pay, S.d_off, S.d_len, 0, 0, cnt, nullptr, S.d_out, S.s);
+      else
+        rc = sha_device(ctx, S.d_pay, nullptr, nullptr, J.stride, J.flen, cnt, nullptr, S.d_out, S.s);
+    }
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(S.h_out, S.d_out, cnt * esz, hipMemcpyDeviceToHost, S.s));
+    HIPCHK(hipEventRecord(S.done, S.s));
+    S.busy = true;
+    S.rec0 = r;
+    S.nrec = cnt;
+    r = r1;
+    slot ^= 1;
+  }
+  for (auto& S : ctx->stage)
+    if ((rc = stage_retire(S, J))) return rc;
+  return 0;
+}
+
+int check_ctx(lsmck_ctx* ctx) {
+  if (!ctx) return lsmck_host::set_error(LSMCK_EINVAL, "null context");
+  return 0;
+}
+
+}  // namespace
+
+// ===========================================================================
+extern "C" {
+
+int lsmck_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+lsmck_ctx* lsmck_ctx_create(int device) {
+  int n = lsmck_device_count();
+  if (n <= 0) {
+    lsmck_host::set_error(LSMCK_ENODEV, "no HIP device available");
+    return nullptr;
+  }
+  if (device < 0 || device >= n) {
+    lsmck_host::set_error(LSMCK_EINVAL, "device index out of range");
+    return nullptr;
+  }
+  DevGuard g(device);
+  hipDeviceProp_t pr;
+  if (hipGetDeviceProperties(&pr, device) != hipSuccess) {
+    lsmck_host::set_error(LSMCK_ENODEV, "hipGetDeviceProperties failed");
+    return nullptr;
+  }
+  if (strncmp(pr.gcnArchName, "gfx950", 6) != 0) {
+    std::string m = std::string("liblsmck is built for gfx950 (MI355X); device is ") + pr.gcnArchName;
+    lsmck_host::set_error(LSMCK_ENODEV, m.c_str());
+    return nullptr;
+  }
+  lsmck_ctx* ctx = new lsmck_ctx();
+  ctx->dev = device;
+  ctx->ncu = pr.multiProcessorCount;
+  // combination tables
+  std::vector<uint32_t> master(1024), kseg(65536), khi(65536), tinit(129);
+  const uint32_t* T = lsmck_host::crc_tables();
+  for (int t = 0; t < 4; ++t)
+    for (int e = 0; e < 256; ++e) master[t * 256 + e] = T[t * 256 + e];
+  uint32_t X = lsmck_host::x_pow_8n(128);  // one segment
+  kseg[0] = 1u << 31;
+  for (int k = 1; k < 65536; ++k) kseg[k] = lsmck_host::gf2_mulmod(kseg[k - 1], X);
+  uint32_t Y = lsmck_host::gf2_mulmod(kseg[65535], X);  // 65536 segments
+  khi[0] = 1u << 31;
+  for (int k = 1; k < 65536; ++k) khi[k] = lsmck_host::gf2_mulmod(khi[k - 1], Y);
+  for (int m = 0; m <= 128; ++m) tinit[m] = lsmck_host::gf2_mulmod(lsmck_host::x_pow_8n(m), 0xFFFFFFFFu);
+  bool ok = hipStreamCreateWithFlags(&ctx->stream0, hipStreamNonBlocking) == hipSuccess &&
+            hipMalloc((void**)&ctx->d_master, 4096) == hipSuccess &&
+            hipMalloc((void**)&ctx->d_kseg, 65536 * 4) == hipSuccess &&
+            hipMalloc((void**)&ctx->d_khi, 65536 * 4) == hipSuccess &&
+            hipMalloc((void**)&ctx->d_tinit, 129 * 4) == hipSuccess &&
+            hipMemcpy(ctx->d_master, master.data(), 4096, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(ctx->d_kseg, kseg.data(), 65536 * 4, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(ctx->d_khi, khi.data(), 65536 * 4, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(ctx->d_tinit, tinit.data(), 129 * 4, hipMemcpyHostToDevice) == hipSuccess &&
+            hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming) == hipSuccess &&
+            hipHostMalloc((void**)&ctx->h_total, 64, hipHostMallocDefault) == hipSuccess &&
+            hipHostMalloc((void**)&ctx->h_verify, 64, hipHostMallocDefault) == hipSuccess &&
+            hipMalloc((void**)&ctx->d_verify, 64) == hipSuccess;
+  if (!ok) {
+    lsmck_host::set_error(LSMCK_ENOMEM, "context allocation failed");
+    lsmck_ctx_destroy(ctx);
+    return nullptr;
+  }
+  return ctx;
+}
+
+void lsmck_ctx_destroy(lsmck_ctx* ctx) {
+  if (!ctx) return;
+  DevGuard g(ctx->dev);
+  (void)hipDeviceSynchronize();
+  for (auto& S : ctx->stage) S.release();
+  ctx->scratch.release();
+  if (ctx->d_master) (void)hipFree(ctx->d_master);
+  if (ctx->d_kseg) (void)hipFree(ctx->d_kseg);
+  if (ctx->d_khi) (void)hipFree(ctx->d_khi);
+  if (ctx->d_tinit) (void)hipFree(ctx->d_tinit);
+  if (ctx->d_verify) (void)hipFree(ctx->d_verify);
+  if (ctx->h_total) (void)hipHostFree(ctx->h_total);
+  if (ctx->h_verify) (void)hipHostFree(ctx->h_verify);
+  if (ctx->scratch_ev) (void)hipEventDestroy(ctx->scratch_ev);
+  if (ctx->stream0) (void)hipStreamDestroy(ctx->stream0);
+  delete ctx;
+}
+
+int lsmck_crc32_batch(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len, size_t n,
+                      uint32_t* out, unsigned flags, void* stream) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (n && (!off || !len || !out)) return lsmck_host::set_error(LSMCK_EINVAL, "null descriptor or output");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DevGuard g(ctx->dev);
+  if (flags & LSMCK_DEVICE) {
+    hipStream_t st = pick_stream(ctx, stream);
+    HIPCHK(hipStreamWaitEvent(st, ctx->scratch_ev, 0));
+    rc = crc_desc_device(ctx, ctx->scratch, base, off, len, n, out, st, -1, ctx->h_total);
+    HIPCHK(hipEventRecord(ctx->scratch_ev, st));
+    return rc;
+  }
+  HostJob J{CRC, base, off, len, 0, 0, n, (uint8_t*)out, (flags & LSMCK_HOST_PINNED) != 0};
+  return run_host_job(ctx, J);
+}
+
+int lsmck_crc32_batch_fixed(lsmck_ctx* ctx, const uint8_t* base, size_t stride, uint32_t len, size_t n,
+                            uint32_t* out, unsigned flags, void* stream) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (n && !out) return lsmck_host::set_error(LSMCK_EINVAL, "null output");
+  if (n > 1 && stride < len) return lsmck_host::set_error(LSMCK_EINVAL, "stride < len");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DevGuard g(ctx->dev);
+  if (flags & LSMCK_DEVICE) return crc_fixed_device(ctx, base, stride, len, n, out, pick_stream(ctx, stream));
+  HostJob J{CRC, base, nullptr, nullptr, stride, len, n, (uint8_t*)out, (flags & LSMCK_HOST_PINNED) != 0};
+  return run_host_job(ctx, J);
+}
+
+int lsmck_crc32_verify_batch(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len,
+                             const uint32_t* expected, size_t n, unsigned flags, void* stream, uint64_t* n_bad,
+                             uint64_t* first_bad) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (flags & LSMCK_DEVICE) {
+    uint32_t* d_crc = nullptr;
+    {
+      DevGuard g(ctx->dev);
+      HIPCHK(hipMalloc((void**)&d_crc, std::max<size_t>(n, 1) * 4));
+    }
+    rc = lsmck_crc32_batch(ctx, base, off, len, n, d_crc, flags, stream);
+    if (!rc) {
+      std::lock_guard<std::mutex> lk(ctx->mu);
+      DevGuard g(ctx->dev);
+      hipStream_t st = pick_stream(ctx, stream);
+      unsigned long long init[2] = {0ull, ~0ull};
+      hipError_t e = hipMemcpyAsync(ctx->d_verify, init, 16, hipMemcpyHostToDevice, st);
+      if (e == hipSuccess) rc = lsmk_launch_crc32_compare(d_crc, expected, n, ctx->d_verify, ctx->d_verify + 1, st);
+      if (e == hipSuccess && !rc) e = hipMemcpyAsync(ctx->h_verify, ctx->d_verify, 16, hipMemcpyDeviceToHost, st);
+      if (e == hipSuccess && !rc) e = hipStreamSynchronize(st);
+      if (e != hipSuccess) rc = hip_error(e, "verify");
+      else if (rc) rc = launch_rc(rc, "compare kernel");
+      if (!rc) {
+        if (n_bad) *n_bad = ctx->h_verify[0];
+        if (first_bad) *first_bad = ctx->h_verify[0] ? ctx->h_verify[1] : n;
+        rc = ctx->h_verify[0] ? 1 : 0;
+      }
+    }
+    DevGuard g(ctx->dev);
+    (void)hipFree(d_crc);
+    return rc;
+  }
+  std::vector<uint32_t> crc(n);
+  rc = lsmck_crc32_batch(ctx, base, off, len, n, crc.data(), flags, stream);
+  if (rc) return rc;
+  uint64_t bad = 0, first = n;
+  for (size_t i = 0; i < n; ++i)
+    if (crc[i] != expected[i]) {
+      if (!bad) first = i;
+      ++bad;
+    }
+  if (n_bad) *n_bad = bad;
+  if (first_bad) *first_bad = first;
+  return bad ? 1 : 0;
+}
+
+int lsmck_sha256_batch(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len, size_t n,
+                       uint8_t* out32, unsigned flags, void* stream) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (n && (!off || !len || !out32)) return lsmck_host::set_error(LSMCK_EINVAL, "null descriptor or output");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DevGuard g(ctx->dev);
+  if (flags & LSMCK_DEVICE)
+    return sha_device(ctx, base, off, len, 0, 0, n, nullptr, out32, pick_stream(ctx, stream));
+  HostJob J{SHA, base, off, len, 0, 0, n, out32, (flags & LSMCK_HOST_PINNED) != 0};
+  return run_host_job(ctx, J);
+}
+
+int lsmck_sha256_batch_fixed(lsmck_ctx* ctx, const uint8_t* base, size_t stride, uint32_t len, size_t n,
+                             uint8_t* out32, unsigned flags, void* stream) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (n && !out32) return lsmck_host::set_error(LSMCK_EINVAL, "null output");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DevGuard g(ctx->dev);
+  if (flags & LSMCK_DEVICE)
+    return sha_device(ctx, base, nullptr, nullptr, stride, len, n, nullptr, out32, pick_stream(ctx, stream));
+  HostJob J{SHA, base, nullptr, nullptr, stride, len, n, out32, (flags & LSMCK_HOST_PINNED) != 0};
+  return run_host_job(ctx, J);
+}
+
+// ---------------------------------------------------------------------------
+// WAL replay verify (src/wal.rs:68-84, 122-163; src/memtable.rs:28-47)
+static uint32_t rd_u32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsigned flags, lsmck_wal_rec* recs,
+                            size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  std::vector<uint8_t> host_copy;
+  const uint8_t* h = wal;
+  if (flags & LSMCK_DEVICE) {
+    host_copy.resize(n);
+    DevGuard g(ctx->dev);
+    HIPCHK(hipMemcpy(host_copy.data(), wal, n, hipMemcpyDeviceToHost));
+    h = host_copy.data();
+  }
+  // 1. header walk (serial: each record's length is in its own header)
+  std::vector<uint64_t> poff;
+  std::vector<uint32_t> plen, pcrc;
+  std::vector<uint8_t> ptype;
+  std::vector<uint64_t> roff;
+  std::vector<uint32_t> rk, rv;
+  size_t pos = 0;
+  int stop = 0;  // 0 clean, 3 bad type
+  uint64_t stop_index = 0;
+  uint32_t stop_type = 0;
+  for (;;) {
+    if (pos + 1 > n) break;
+    uint8_t t = h[pos];
+    if (t != 1 && t != 2) {
+      stop = LSMCK_WAL_BAD_TYPE;
+      stop_index = poff.size();
+      stop_type = t;
+      break;
+    }
+    size_t hdr = t == 1 ? 13 : 9;
+    if (pos + hdr > n) break;  // UnexpectedEof inside a header: end of log
+    uint32_t saved = rd_u32(h + pos + 1);
+    uint32_t klen = rd_u32(h + pos + 5);
+    uint32_t vlen = t == 1 ? rd_u32(h + pos + 9) : 0;
+    uint32_t dlen = klen + vlen;  // u32 as wal.rs:129
+    size_t avail = n - (pos + hdr);
+    size_t got = dlen <= avail ? dlen : avail;  // read_to_end on take(): short read at EOF
+    roff.push_back(pos);
+    poff.push_back(pos + hdr);
+    plen.push_back((uint32_t)got);
+    pcrc.push_back(saved);
+    ptype.push_back(t);
+    rk.push_back(klen);
+    rv.push_back(vlen);
+    pos += hdr + got;
+  }
+  size_t m = poff.size();
+  // 2. every payload CRC in one GPU batch
+  uint64_t nb = 0, first = m;
+  if (m) {
+    if (flags & LSMCK_DEVICE) {
+      std::lock_guard<std::mutex> lk(ctx->mu);
+      DevGuard g(ctx->dev);
+      uint64_t* d_off = nullptr;
+      uint32_t *d_len = nullptr, *d_exp = nullptr, *d_crc = nullptr;
+      hipError_t e = hipMalloc((void**)&d_off, m * 8);
+      if (e == hipSuccess) e = hipMalloc((void**)&d_len, m * 4);
+      if (e == hipSuccess) e = hipMalloc((void**)&d_crc, m * 4);
+      if (e == hipSuccess) e = hipMemcpy(d_off, poff.data(), m * 8, hipMemcpyHostToDevice);
+      if (e == hipSuccess) e = hipMemcpy(d_len, plen.data(), m * 4, hipMemcpyHostToDevice);
+      std::vector<uint32_t> crc(m);
+      if (e == hipSuccess) {
+        rc = crc_desc_device(ctx, ctx->scratch, wal, d_off, d_len, m, d_crc, ctx->stream0, -1, ctx->h_total);
+        if (!rc) e = hipMemcpyAsync(crc.data(), d_crc, m * 4, hipMemcpyDeviceToHost, ctx->stream0);
+        if (!rc && e == hipSuccess) e = hipStreamSynchronize(ctx->stream0);
+      }
+      (void)d_exp;
+      if (d_off) (void)hipFree(d_off);
+      if (d_len) (void)hipFree(d_len);
+      if (d_crc) (void)hipFree(d_crc);
+      if (e != hipSuccess) return hip_error(e, "wal replay verify");
+      if (rc) return rc;
+      for (size_t i = 0; i < m; ++i)
+        if (crc[i] != pcrc[i]) {
+          if (!nb) first = i;
+          ++nb;
+        }
+    } else {
+      rc = lsmck_crc32_verify_batch(ctx, h, poff.data(), plen.data(), pcrc.data(), m, flags, nullptr, &nb, &first);
+      if (rc < 0) return rc;
+    }
+  }
+  // 3. the reference stops at the first failing record in log order
+  size_t accepted = m;
+  int result = 0;
+  if (nb) {
+    accepted = (size_t)first;
+    result = ptype[first] == 1 ? LSMCK_WAL_CORRUPTED : LSMCK_WAL_REMOVE_PANIC;
+    if (bad_index) *bad_index = first;
+    if (bad_expected) *bad_expected = pcrc[first];
+    if (bad_crc) *bad_crc = lsmck_crc32_ieee(h + poff[first], plen[first]);
+  } else if (stop == LSMCK_WAL_BAD_TYPE) {
+    result = LSMCK_WAL_BAD_TYPE;
+    if (bad_index) *bad_index = stop_index;
+    if (bad_crc) *bad_crc = stop_type;
+  }
+  if (recs)
+    for (size_t i = 0; i < accepted && i < cap; ++i) {
+      recs[i].rec_off = roff[i];
+      recs[i].payload_off = poff[i];
+      recs[i].klen = rk[i];
+      recs[i].vlen = rv[i];
+      recs[i].crc = pcrc[i];
+      recs[i].type = ptype[i];
+    }
+  if (nrec) *nrec = accepted;
+  return result;
+}
+
+// ---------------------------------------------------------------------------
+// Whole-tree SSTable verify: all data + index files hashed in one GPU batch.
+static int read_file(const char* path, std::vector<uint8_t>* buf) {
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -errno;
+  struct stat stt;
+  if (fstat(fd, &stt) == 0 && stt.st_size > 0) buf->reserve(buf->size() + (size_t)stt.st_size);
+  uint8_t tmp[1 << 16];
+  for (;;) {
+    ssize_t k = read(fd, tmp, sizeof tmp);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      int e = errno;
+      close(fd);
+      return -e;
+    }
+    if (k == 0) break;
+    buf->insert(buf->end(), tmp, tmp + k);
+  }
+  close(fd);
+  return 0;
+}
+
+int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, const char* const* index_paths,
+                                const char* const* checksum_paths, size_t n, int* status) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  std::vector<uint8_t> blob;
+  std::vector<uint64_t> off(2 * n, 0);
+  std::vector<uint32_t> len(2 * n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    status[i] = 0;
+    for (int w = 0; w < 2; ++w) {
+      const char* p = w == 0 ? data_paths[i] : index_paths[i];
+      size_t before = blob.size();
+      int e = read_file(p, &blob);
+      if (e) {
+        if (!status[i]) status[i] = e;
+        blob.resize(before);
+      }
+      if (blob.size() - before > 0xFFFFFFFFull) {
+        status[i] = LSMCK_EINVAL;
+        blob.resize(before);
+      }
+      off[2 * i + w] = before;
+      len[2 * i + w] = (uint32_t)(blob.size() - before);
+    }
+  }
+  std::vector<uint8_t> dig(64 * n);
+  if (n) {
+    rc = lsmck_sha256_batch(ctx, blob.data(), off.data(), len.data(), 2 * n, dig.data(), LSMCK_HOST, nullptr);
+    if (rc) return rc;
+  }
+  int bad = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (status[i] == 0) {
+      char db[45], ib[45];
+      lsmck_base64_encode(&dig[64 * i], 32, db);
+      lsmck_base64_encode(&dig[64 * i + 32], 32, ib);
+      std::string wi, wd;
+      int e = lsmck_host::read_checksum_json(checksum_paths[i], &wi, &wd);
+      if (e) status[i] = e;
+      else if (wd != db) status[i] = LSMCK_DATA_MISMATCH;
+      else if (wi != ib) status[i] = LSMCK_INDEX_MISMATCH;
+    }
+    if (status[i]) ++bad;
+  }
+  return bad;
+}
+
+// ---------------------------------------------------------------------------
+void* lsmck_dev_alloc(lsmck_ctx* ctx, size_t bytes) {
+  if (!ctx) return nullptr;
+  DevGuard g(ctx->dev);
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
+  if (e != hipSuccess) {
+    hip_error(e, "hipMalloc");
+    return nullptr;
+  }
+  return p;
+}
+void lsmck_dev_free(lsmck_ctx* ctx, void* p) {
+  if (!ctx || !p) return;
+  DevGuard g(ctx->dev);
+  (void)hipFree(p);
+}
+void* lsmck_host_alloc_pinned(lsmck_ctx* ctx, size_t bytes) {
+  if (!ctx) return nullptr;
+  DevGuard g(ctx->dev);
+  void* p = nullptr;
+  hipError_t e = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    hip_error(e, "hipHostMalloc");
+    return nullptr;
+  }
+  return p;
+}
+void lsmck_host_free_pinned(lsmck_ctx* ctx, void* p) {
+  if (!ctx || !p) return;
+  DevGuard g(ctx->dev);
+  (void)hipHostFree(p);
+}
+int lsmck_memcpy_h2d(lsmck_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream) {
+  if (!ctx) return LSMCK_EINVAL;
+  DevGuard g(ctx->dev);
+  hipStream_t st = pick_stream(ctx, stream);
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return 0;
+}
+int lsmck_memcpy_d2h(lsmck_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream) {
+  if (!ctx) return LSMCK_EINVAL;
+  DevGuard g(ctx->dev);
+  hipStream_t st = pick_stream(ctx, stream);
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return 0;
+}
+int lsmck_memset_dev(lsmck_ctx* ctx, void* dst, int value, size_t bytes, void* stream) {
+  if (!ctx) return LSMCK_EINVAL;
+  DevGuard g(ctx->dev);
+  HIPCHK(hipMemsetAsync(dst, value, bytes, pick_stream(ctx, stream)));
+  return 0;
+}
+int lsmck_stream_sync(lsmck_ctx* ctx, void* stream) {
+  if (!ctx) return LSMCK_EINVAL;
+  DevGuard g(ctx->dev);
+  HIPCHK(hipStreamSynchronize(pick_stream(ctx, stream)));
+  return 0;
+}
+int lsmck_gen_stream(lsmck_ctx* ctx, uint8_t* dst_dev, uint64_t seed, uint64_t byte_off, size_t n, void* stream) {
+  if (!ctx) return LSMCK_EINVAL;
+  DevGuard g(ctx->dev);
+  int rc = lsmk_launch_gen_stream(dst_dev, seed, byte_off, n, pick_stream(ctx, stream));
+  return rc ? launch_rc(rc, "gen_stream kernel") : 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,53 @@
+// lsmck_device.h -- parameter blocks shared by the HIP kernels and the host
+// dispatcher (lsmck_api.cpp).  Internal to liblsmck.so; not part of the C ABI.
+#ifndef LSMCK_DEVICE_H
+#define LSMCK_DEVICE_H
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lsmck {
+
+// CRC-32 batch job.  Records are either fixed ([r*stride, r*stride+flen)) or
+// described by (off[r], len[r]) relative to `base`.
+struct CrcParams {
+  const unsigned char* base;
+  const uint64_t* off;        // descriptor mode
+  const uint32_t* len;        // descriptor mode
+  uint64_t stride;            // fixed mode
+  uint32_t flen;              // fixed mode
+  uint64_t nrec;
+  uint32_t* seg_start;        // descriptor mode scratch: exclusive prefix of ceil(len/128)
+  uint32_t* tile_first;       // descriptor mode scratch: record of segment 64*t
+  uint32_t* total_segs;       // descriptor mode scratch: total segments (device)
+  uint32_t* out;              // nrec CRCs (zeroed before the launch)
+  const uint32_t* kseg;       // x^(8*128*k) mod P, k < 2^16
+  const uint32_t* khi;        // x^(8*128*65536*k) mod P, k < 2^16
+  const uint32_t* tinit;      // 0xFFFFFFFF (x) x^(8*m) mod P, m = 0..128
+  const uint32_t* master;     // slicing-by-4 tables T0..T3 (4 x 256)
+};
+
+// SHA-256 batch job (lane per message).
+struct ShaParams {
+  const unsigned char* base;
+  const uint64_t* off;        // null -> fixed mode
+  const uint32_t* len;
+  uint64_t stride;
+  uint32_t flen;
+  uint64_t nmsg;
+  const uint32_t* order;      // optional permutation (longest first), may be null
+  unsigned char* out;         // 32 bytes per message
+};
+
+}  // namespace lsmck
+
+extern "C" {
+int lsmk_launch_crc32_fixed(const lsmck::CrcParams* P, int ncu, hipStream_t st);
+uint64_t lsmk_scan_block_count(uint64_t n);
+int lsmk_launch_crc32_scan(const lsmck::CrcParams* P, uint32_t* block_sum, hipStream_t st);
+int lsmk_launch_crc32_desc(const lsmck::CrcParams* P, const uint32_t* block_sum, int ncu, hipStream_t st);
+int lsmk_launch_sha256(const lsmck::ShaParams* P, hipStream_t st);
+int lsmk_launch_crc32_compare(const uint32_t* crc, const uint32_t* expected, uint64_t n,
+                               unsigned long long* n_bad, unsigned long long* first_bad, hipStream_t st);
+int lsmk_launch_gen_stream(unsigned char* dst, uint64_t seed, uint64_t byte_off, uint64_t n, hipStream_t st);
+}
+#endif

@@ -1,0 +1,200 @@
+// lsmck_sha256.hip -- batched SHA-256 (FIPS 180-4) over independent messages,
+// gfx950.  This is the digest src/checksums.rs:20-38 computes over a whole
+// SSTable data / index file (sha2 ^0.10.1, Cargo.toml:11); the host side
+// (lsmck_api.cpp) adds base64 (checksums.rs:37) and the JSON record.
+//
+// Merkle-Damgard is sequential inside one message, so parallelism is across
+// messages: one lane owns one message and runs all of its compression blocks.
+// The kernel is int32-VALU bound (~1.4k VALU ops per 64-B block, rotates are
+// v_alignbit, Ch/Maj are v_bitop3), not HBM bound; DESIGN.md prices it
+// against the VALU roof.  Loads are dword-aligned with a v_alignbyte funnel
+// and never touch a dword outside the message.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lsmck_device.h"
+
+namespace lsmck {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__constant__ uint32_t kSha256K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+
+__device__ __forceinline__ void sha256_compress(uint32_t (&h)[8], uint32_t (&w)[16]) {
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    uint32_t wt;
+    if (t < 16) {
+      wt = w[t];
+    } else {
+      uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+      uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
+      uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+      wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+      w[t & 15] = wt;
+    }
+    uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+    uint32_t ch = (e & f) ^ (~e & g);
+    uint32_t t1 = hh + S1 + ch + kSha256K[t] + wt;
+    uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    hh = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + S0 + mj;
+  }
+  h[0] += a;
+  h[1] += b;
+  h[2] += c;
+  h[3] += d;
+  h[4] += e;
+  h[5] += f;
+  h[6] += g;
+  h[7] += hh;
+}
+
+__device__ __forceinline__ uint32_t ld32(const unsigned char* p) { return *(const uint32_t*)p; }
+__device__ __forceinline__ u32x4 ld128(const unsigned char* p) { return *(const u32x4*)p; }
+
+// Loads the 64 message bytes [p0, p0+64) of a message starting at absolute
+// address A with length len, as 16 little-endian words; only dwords that
+// intersect [A, A+len) are read (others are 0; the caller masks and pads).
+__device__ __forceinline__ void load_block(uintptr_t A, uint64_t len, uint64_t p0, uint32_t (&wle)[16]) {
+  const uintptr_t s = A + p0;
+  const uintptr_t a4 = s & ~(uintptr_t)3;
+  const uint32_t sh = (uint32_t)(s & 3);
+  // one past the last dword touching the message (an empty message touches none)
+  const uintptr_t end4 = len ? ((A + len + 3) & ~(uintptr_t)3) : (A & ~(uintptr_t)3);
+  const unsigned char* p = (const unsigned char*)a4;
+  uint32_t d[17];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    u32x4 v;
+    uintptr_t ga = a4 + 16 * g;
+    if (ga + 16 <= end4) {
+      v = ld128(p + 16 * g);
+    } else {
+      v.x = (ga + 0 < end4) ? ld32(p + 16 * g + 0) : 0u;
+      v.y = (ga + 4 < end4) ? ld32(p + 16 * g + 4) : 0u;
+      v.z = (ga + 8 < end4) ? ld32(p + 16 * g + 8) : 0u;
+      v.w = (ga + 12 < end4) ? ld32(p + 16 * g + 12) : 0u;
+    }
+    d[4 * g + 0] = v.x;
+    d[4 * g + 1] = v.y;
+    d[4 * g + 2] = v.z;
+    d[4 * g + 3] = v.w;
+  }
+  d[16] = (sh && a4 + 64 < end4) ? ld32(p + 64) : 0u;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) wle[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+}
+
+__global__ __launch_bounds__(256) void sha256_kernel(ShaParams P) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.nmsg) return;
+  uint64_t m = P.order ? P.order[i] : i;
+  uint64_t off = P.off ? P.off[m] : m * P.stride;
+  uint64_t len = P.len ? P.len[m] : P.flen;
+  const uintptr_t A = (uintptr_t)(P.base + off);
+  uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                   0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  const uint64_t nb = (len + 9 + 63) >> 6;
+  const uint64_t bits = len << 3;
+  for (uint64_t b = 0; b < nb; ++b) {
+    const uint64_t p0 = b << 6;
+    uint32_t w[16];
+    load_block(A, len, p0, w);
+    if (p0 + 64 > len) {
+      // tail: mask bytes past the end, append 0x80, and the bit length in the final block
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        int64_t c = (int64_t)len - (int64_t)(p0 + 4 * t);  // data bytes in this word
+        uint32_t mask = c >= 4 ? 0xFFFFFFFFu : (c <= 0 ? 0u : ((1u << (8 * c)) - 1u));
+        uint32_t pad = (c >= 0 && c < 4) ? (0x80u << (8 * c)) : 0u;
+        w[t] = (w[t] & mask) | pad;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t) w[t] = __builtin_bswap32(w[t]);
+    if (b == nb - 1) {
+      w[14] = (uint32_t)(bits >> 32);
+      w[15] = (uint32_t)bits;
+    }
+    sha256_compress(h, w);
+  }
+  u32x4* o = (u32x4*)(P.out + 32 * m);
+  u32x4 o0 = {__builtin_bswap32(h[0]), __builtin_bswap32(h[1]), __builtin_bswap32(h[2]), __builtin_bswap32(h[3])};
+  u32x4 o1 = {__builtin_bswap32(h[4]), __builtin_bswap32(h[5]), __builtin_bswap32(h[6]), __builtin_bswap32(h[7])};
+  o[0] = o0;
+  o[1] = o1;
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic input generator (bench / tests): byte b of the stream is byte
+// (b % 8) of splitmix64(seed ^ (b / 8)); same definition as the oracle's
+// oracle_gen_stream, so host and device see identical records without a copy.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void gen_stream_kernel(unsigned char* dst, uint64_t seed, uint64_t byte_off,
+                                                         uint64_t n) {
+  uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  if ((byte_off & 7) == 0 && ((uintptr_t)dst & 15) == 0) {
+    uint64_t n16 = n >> 4;
+    uint64_t w0 = byte_off >> 3;
+    for (uint64_t i = tid; i < n16; i += stride) {
+      uint64_t a = splitmix64(seed ^ (w0 + 2 * i)), b = splitmix64(seed ^ (w0 + 2 * i + 1));
+      u32x4 v = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+      *(u32x4*)(dst + 16 * i) = v;
+    }
+    for (uint64_t i = (n16 << 4) + tid; i < n; i += stride) {
+      uint64_t bb = byte_off + i;
+      dst[i] = (unsigned char)(splitmix64(seed ^ (bb >> 3)) >> (8 * (bb & 7)));
+    }
+  } else {
+    for (uint64_t i = tid; i < n; i += stride) {
+      uint64_t bb = byte_off + i;
+      dst[i] = (unsigned char)(splitmix64(seed ^ (bb >> 3)) >> (8 * (bb & 7)));
+    }
+  }
+}
+
+}  // namespace lsmck
+
+using namespace lsmck;
+
+extern "C" int lsmk_launch_sha256(const ShaParams* P, hipStream_t st) {
+  if (P->nmsg == 0) return 0;
+  uint64_t blocks = (P->nmsg + 255) / 256;
+  hipLaunchKernelGGL(sha256_kernel, dim3((unsigned)blocks), dim3(256), 0, st, *P);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -(int)e;
+}
+
+extern "C" int lsmk_launch_gen_stream(unsigned char* dst, uint64_t seed, uint64_t byte_off, uint64_t n,
+                                       hipStream_t st) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(gen_stream_kernel, dim3(8192), dim3(256), 0, st, dst, seed, byte_off, n);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -(int)e;
+}

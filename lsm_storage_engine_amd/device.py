@@ -1,0 +1,201 @@
+"""GPU context and batch entry points (include/lsmck.h sections 2-4).
+
+``Context`` owns one liblsmck context (one MI355X).  Host-array methods take
+numpy arrays and return numpy arrays (the library stages them through pinned
+memory); ``*_device`` methods take raw device pointers (ints) and run
+asynchronously on ``stream`` (a hipStream_t as int, or None for the context's
+stream) -- that is the device-resident hot path the bench times.
+
+There is no CPU fallback: constructing a Context without a usable gfx950 GPU
+raises.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+class DeviceBuffer:
+    def __init__(self, ctx, nbytes):
+        self.ctx = ctx
+        self.nbytes = nbytes
+        self.ptr = _lib.load().lsmck_dev_alloc(ctx.handle, nbytes)
+        if not self.ptr:
+            raise MemoryError(f"hipMalloc({nbytes}): {_lib.last_error()}")
+
+    def free(self):
+        if self.ptr:
+            _lib.load().lsmck_dev_free(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+    def upload(self, arr, offset=0):
+        a = np.ascontiguousarray(arr)
+        assert offset + a.nbytes <= self.nbytes
+        _lib.check(_lib.load().lsmck_memcpy_h2d(self.ctx.handle, self.ptr + offset, a.ctypes.data, a.nbytes, None),
+                   "h2d")
+
+    def download(self, dtype=np.uint8, count=None, offset=0):
+        dt = np.dtype(dtype)
+        count = (self.nbytes - offset) // dt.itemsize if count is None else count
+        out = np.empty(count, dtype=dt)
+        _lib.check(_lib.load().lsmck_memcpy_d2h(self.ctx.handle, out.ctypes.data, self.ptr + offset, out.nbytes, None),
+                   "d2h")
+        return out
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Context:
+    def __init__(self, device=0):
+        lib = _lib.load()
+        self.lib = lib
+        self.handle = lib.lsmck_ctx_create(device)
+        if not self.handle:
+            raise RuntimeError(f"lsmck_ctx_create({device}) failed: {_lib.last_error()}")
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            self.lib.lsmck_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- memory -------------------------------------------------------------
+    def alloc(self, nbytes):
+        return DeviceBuffer(self, nbytes)
+
+    def sync(self, stream=None):
+        _lib.check(self.lib.lsmck_stream_sync(self.handle, stream), "sync")
+
+    def memset(self, ptr, value, nbytes, stream=None):
+        _lib.check(self.lib.lsmck_memset_dev(self.handle, ptr, value, nbytes, stream), "memset")
+
+    def gen_stream(self, dst_ptr, seed, byte_off, nbytes, stream=None):
+        _lib.check(self.lib.lsmck_gen_stream(self.handle, dst_ptr, seed, byte_off, nbytes, stream), "gen_stream")
+
+    # --- CRC-32, host arrays ------------------------------------------------
+    def crc32(self, data, off, length, pinned=False):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        n = len(off)
+        out = np.empty(n, dtype=np.uint32)
+        flags = _lib.HOST_PINNED if pinned else _lib.HOST
+        _lib.check(self.lib.lsmck_crc32_batch(self.handle, data.ctypes.data, off.ctypes.data, length.ctypes.data, n,
+                                              out.ctypes.data, flags, None), "crc32_batch")
+        return out
+
+    def crc32_fixed(self, data, stride, length, n):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        out = np.empty(n, dtype=np.uint32)
+        _lib.check(self.lib.lsmck_crc32_batch_fixed(self.handle, data.ctypes.data, stride, length, n, out.ctypes.data,
+                                                    _lib.HOST, None), "crc32_batch_fixed")
+        return out
+
+    def crc32_verify(self, data, off, length, expected):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        expected = np.ascontiguousarray(expected, dtype=np.uint32)
+        nb, fb = C.c_uint64(), C.c_uint64()
+        rc = _lib.check(self.lib.lsmck_crc32_verify_batch(self.handle, data.ctypes.data, off.ctypes.data,
+                                                          length.ctypes.data, expected.ctypes.data, len(off),
+                                                          _lib.HOST, None, C.byref(nb), C.byref(fb)), "verify")
+        return rc, nb.value, fb.value
+
+    # --- CRC-32, device pointers (async on stream) ----------------------------
+    def crc32_device(self, base, off, length, n, out, stream=None):
+        _lib.check(self.lib.lsmck_crc32_batch(self.handle, base, off, length, n, out, _lib.DEVICE, stream),
+                   "crc32_batch(device)")
+
+    def crc32_fixed_device(self, base, stride, length, n, out, stream=None):
+        _lib.check(self.lib.lsmck_crc32_batch_fixed(self.handle, base, stride, length, n, out, _lib.DEVICE, stream),
+                   "crc32_batch_fixed(device)")
+
+    def crc32_verify_device(self, base, off, length, expected, n, stream=None):
+        nb, fb = C.c_uint64(), C.c_uint64()
+        rc = _lib.check(self.lib.lsmck_crc32_verify_batch(self.handle, base, off, length, expected, n, _lib.DEVICE,
+                                                          stream, C.byref(nb), C.byref(fb)), "verify(device)")
+        return rc, nb.value, fb.value
+
+    # --- SHA-256 --------------------------------------------------------------
+    def sha256(self, data, off, length):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        n = len(off)
+        out = np.empty((n, 32), dtype=np.uint8)
+        _lib.check(self.lib.lsmck_sha256_batch(self.handle, data.ctypes.data, off.ctypes.data, length.ctypes.data, n,
+                                               out.ctypes.data, _lib.HOST, None), "sha256_batch")
+        return out
+
+    def sha256_fixed(self, data, stride, length, n):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        out = np.empty((n, 32), dtype=np.uint8)
+        _lib.check(self.lib.lsmck_sha256_batch_fixed(self.handle, data.ctypes.data, stride, length, n,
+                                                     out.ctypes.data, _lib.HOST, None), "sha256_batch_fixed")
+        return out
+
+    def sha256_device(self, base, off, length, n, out, stream=None):
+        _lib.check(self.lib.lsmck_sha256_batch(self.handle, base, off, length, n, out, _lib.DEVICE, stream),
+                   "sha256_batch(device)")
+
+    def sha256_fixed_device(self, base, stride, length, n, out, stream=None):
+        _lib.check(self.lib.lsmck_sha256_batch_fixed(self.handle, base, stride, length, n, out, _lib.DEVICE, stream),
+                   "sha256_batch_fixed(device)")
+
+    # --- WAL / SSTable batch verify ---------------------------------------------
+    def wal_replay_verify(self, image, device_ptr=None):
+        """Returns (records, status, (bad_index, bad_crc, bad_expected))."""
+        if device_ptr is None:
+            img = np.frombuffer(bytes(image), dtype=np.uint8)
+            ptr, n, flags = img.ctypes.data, len(img), _lib.HOST
+        else:
+            ptr, n, flags = device_ptr, image, _lib.DEVICE
+        cap = n // 9 + 1
+        recs = (_lib.WalRec * cap)()
+        nrec = C.c_size_t()
+        bi, bc, be = C.c_uint64(), C.c_uint32(), C.c_uint32()
+        rc = _lib.check(self.lib.lsmck_wal_replay_verify(self.handle, ptr, n, flags, recs, cap, C.byref(nrec),
+                                                         C.byref(bi), C.byref(bc), C.byref(be)), "wal_replay_verify")
+        return list(recs[:nrec.value]), rc, (bi.value, bc.value, be.value)
+
+    def checksums_verify_many(self, triples):
+        n = len(triples)
+        arr = C.c_char_p * max(n, 1)
+        d = arr(*[str(t[0]).encode() for t in triples])
+        i = arr(*[str(t[1]).encode() for t in triples])
+        c = arr(*[str(t[2]).encode() for t in triples])
+        status = (C.c_int * max(n, 1))()
+        _lib.check(self.lib.lsmck_checksums_verify_many(self.handle, d, i, c, n, status), "checksums_verify_many")
+        return list(status[:n])
+
+
+def device_count():
+    return _lib.load().lsmck_device_count()
+
+
+def gen_zipf_lengths(seed, n, s=1.5, kmax=1024, lmin=64):
+    out = np.empty(n, dtype=np.uint32)
+    _lib.load().lsmck_gen_zipf_lengths(seed, s, kmax, lmin, n, out.ctypes.data)
+    return out

@@ -1,0 +1,249 @@
+"""liblsmck.so on the CPU: the C ABI loads and exports every symbol of
+include/lsmck.h, the scalar entry points agree with the oracle and the golden
+vectors, and the host-side mirrors of wal.rs / checksums.rs behave like the
+reference's own tests.  No GPU compute call is made here."""
+import ctypes as C
+import os
+import re
+import shutil
+
+import numpy as np
+import pytest
+
+from lsm_storage_engine_amd import _lib, crc32, wal
+from lsm_storage_engine_amd.checksums import Checksums, ChecksumPanic
+from lsm_storage_engine_amd.sstable_metadata import SsTableMetadata
+from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "lsmck.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(lsmck_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_every_declared_symbol_is_exported():
+    lib = _lib.load()
+    names = header_functions()
+    assert len(names) >= 30
+    for n in names:
+        assert hasattr(lib, n), n
+    # and the binding table covers the header exactly
+    assert sorted(s[0] for s in _lib.SIGNATURES) == names
+
+
+def test_only_c_abi_exported():
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    syms = [l.split()[-1] for l in out.splitlines() if " T " in l]
+    assert syms and all(s.startswith("lsmck_") for s in syms), [s for s in syms if not s.startswith("lsmck_")]
+    assert set(syms) == set(header_functions())
+
+
+def test_crc32_scalar_golden(golden, blob):
+    for e in golden["crc32_text"]:
+        assert crc32.checksum_ieee(e["text"].encode()) == e["crc"]
+    for e in golden["crc32_slices"]:
+        assert crc32.checksum_ieee(blob[e["off"]:e["off"] + e["len"]]) == e["crc"], e
+    # n == 0 with a null pointer (an empty Rust slice may be dangling)
+    assert _lib.load().lsmck_crc32_ieee(None, 0) == 0
+
+
+def test_crc32_update_combine(blob):
+    rng = np.random.default_rng(1)
+    for _ in range(200):
+        a = int(rng.integers(0, 3000))
+        b = int(rng.integers(0, 3000))
+        A, B = blob[:a], blob[a:a + b]
+        ca, cb = crc32.checksum_ieee(A), crc32.checksum_ieee(B)
+        assert crc32.update(ca, B) == O.crc32(A + B)
+        assert crc32.combine(ca, cb, len(B)) == O.crc32(A + B)
+
+
+def test_sha256_scalar_streaming(golden, blob):
+    lib = _lib.load()
+    for e in golden["sha256_slices"][::7]:
+        data = blob[e["off"]:e["off"] + e["len"]]
+        out = (C.c_uint8 * 32)()
+        lib.lsmck_sha256(data, len(data), out)
+        assert bytes(out).hex() == e["sha256"]
+        # odd-sized updates, as checksums.rs streams 1 KiB reads
+        c = _lib.Sha256Ctx()
+        lib.lsmck_sha256_init(C.byref(c))
+        i = 0
+        step = 1
+        while i < len(data):
+            chunk = data[i:i + step]
+            lib.lsmck_sha256_update(C.byref(c), chunk, len(chunk))
+            i += step
+            step = step * 3 % 1031 + 1
+        lib.lsmck_sha256_final(C.byref(c), out)
+        assert bytes(out).hex() == e["sha256"]
+
+
+def test_base64(golden):
+    lib = _lib.load()
+    for e in golden["base64"]:
+        raw = bytes.fromhex(e["hex"])
+        out = C.create_string_buffer(16)
+        n = lib.lsmck_base64_encode(raw, len(raw), out)
+        assert out.value.decode() == e["b64"] and n == len(e["b64"])
+
+
+def test_wal_encode_matches_oracle(blob):
+    lib = _lib.load()
+    rng = np.random.default_rng(2)
+    for _ in range(100):
+        kl, vl = int(rng.integers(0, 50)), int(rng.integers(0, 900))
+        k, v = blob[:kl], blob[100:100 + vl]
+        out = (C.c_uint8 * (13 + kl + vl))()
+        n = lib.lsmck_wal_encode_insert(k, kl, v, vl, out)
+        assert bytes(out)[:n] == O.wal_insert(k, v)
+        n = lib.lsmck_wal_encode_remove(k, kl, out)
+        assert bytes(out)[:n] == O.wal_remove(k)
+
+
+# --- wal.rs / memtable.rs tests, restated ------------------------------------------
+def test_write_insert_log_record():  # wal.rs:219-232
+    log = wal.CommandLog.new_in_memory()
+    log.insert(b"key", b"value")
+    read = wal.CommandLog.new_in_memory(log.inner())
+    assert read.next_record() == wal.LogRecord.Insert(b"key", b"value")
+
+
+def test_write_remove_log_record():  # wal.rs:234-242
+    log = wal.CommandLog.new_in_memory()
+    log.remove(b"key")
+    read = wal.CommandLog.new_in_memory(log.inner())
+    assert read.next_record() == wal.LogRecord.Remove(b"key")
+
+
+def test_restore_from_log(golden):  # memtable.rs:113-134
+    log = wal.CommandLog.new_in_memory()
+    for r in [wal.Insert(b"key", b"value"), wal.Insert(b"key1", b"value1"), wal.Insert(b"key2", b"value2"),
+              wal.Remove(b"key2")]:
+        log.log(r)
+    assert log.inner().hex() == golden["wal"]["restore_from_log"]
+    table = wal.MemTable.from_log(wal.CommandLog.new_in_memory(log.inner()))
+    assert table.get(b"key1") == b"value1" and table.get(b"key2") is None
+
+
+def test_size_after_insert():  # memtable.rs:136-147
+    t = wal.MemTable()
+    t.insert(b"key", b"value")
+    assert t.size_in_bytes() == 8
+    t.remove(b"key1")
+    assert t.size_in_bytes() == 8
+    t.insert(b"key", b"v")
+    assert t.size_in_bytes() == 4
+    t.remove(b"key")
+    assert t.size_in_bytes() == 0
+
+
+def test_wal_iterator_errors(golden):
+    img = open(os.path.join(GOLDEN, "wal_2000.bin"), "rb").read()
+    recs = golden["wal_2000"]["records"]
+    got = list(wal.CommandLog.new_in_memory(img))
+    assert len(got) == 2000
+    i = next(i for i, r in enumerate(recs) if r["type"] == 1 and r["klen"] + r["vlen"] > 0 and i > 3)
+    b = bytearray(img)
+    b[recs[i]["off"] + 13] ^= 1
+    with pytest.raises(wal.CorruptedData) as ei:
+        list(wal.CommandLog.new_in_memory(bytes(b)))
+    assert ei.value.expected == recs[i]["crc"]
+    j = next(j for j, r in enumerate(recs) if r["type"] == 2 and r["klen"] > 0)
+    b = bytearray(img)
+    b[recs[j]["off"] + 9] ^= 1
+    with pytest.raises(wal.WalPanic):
+        list(wal.CommandLog.new_in_memory(bytes(b)))
+    b = bytearray(img)
+    b[recs[3]["off"]] = 9
+    with pytest.raises(wal.InvalidCommandType):
+        list(wal.CommandLog.new_in_memory(bytes(b)))
+    assert len(list(wal.CommandLog.new_in_memory(img[:recs[50]["off"] + 3]))) == 50
+
+
+def test_command_log_file_roundtrip(tmp_path):
+    p = tmp_path / "wal" / "wal.log"
+    log = wal.CommandLog.new(str(p))
+    log.insert(b"a", b"1")
+    log.remove(b"a")
+    log.file.seek(0)
+    assert list(log) == [wal.Insert(b"a", b"1"), wal.Remove(b"a")]
+    log.close()
+    assert not p.exists()
+
+
+# --- checksums.rs ---------------------------------------------------------------------
+def make_table(tmp_path, golden):
+    g = golden["sstable_test"]
+    m = SsTableMetadata.new(str(tmp_path), 0, timestamp_ms=1700000000000)
+    os.makedirs(os.path.dirname(m.data_path()), exist_ok=True)
+    shutil.copy(os.path.join(GOLDEN, g["data"]), m.data_path())
+    shutil.copy(os.path.join(GOLDEN, g["index"]), m.index_path())
+    return m
+
+
+def test_checksums_write_and_verify(tmp_path, golden):
+    m = make_table(tmp_path, golden)
+    assert m.checksum_path().endswith("level-0/checksum_1700000000000.db")
+    Checksums.write_checksums(m)
+    assert open(m.checksum_path()).read() == golden["sstable_test"]["json"]
+    Checksums.verify(m)
+    assert Checksums.calculate_checksum(m.data_path()) == O.file_checksum(m.data_path())
+
+
+def test_checksums_verify_failures(tmp_path, golden):
+    m = make_table(tmp_path, golden)
+    Checksums.write_checksums(m)
+    with open(m.data_path(), "r+b") as f:  # data first (checksums.rs:49)
+        f.seek(100)
+        f.write(b"X")
+    with open(m.index_path(), "r+b") as f:
+        f.seek(10)
+        f.write(b"Y")
+    with pytest.raises(ChecksumPanic, match=m.data_filename):
+        Checksums.verify(m)
+    shutil.copy(os.path.join(GOLDEN, golden["sstable_test"]["data"]), m.data_path())
+    with pytest.raises(ChecksumPanic, match=m.index_filename):
+        Checksums.verify(m)
+    shutil.copy(os.path.join(GOLDEN, golden["sstable_test"]["index"]), m.index_path())
+    Checksums.verify(m)
+    with open(m.checksum_path(), "w") as f:
+        f.write('{"index_checksum":"x"}')
+    with pytest.raises(ValueError, match="missing field"):
+        Checksums.verify(m)
+    os.remove(m.checksum_path())
+    with pytest.raises(OSError):
+        Checksums.verify(m)
+
+
+def test_checksum_json_reader_accepts_serde_variants(tmp_path, golden):
+    m = make_table(tmp_path, golden)
+    d = O.file_checksum(m.data_path())
+    i = O.file_checksum(m.index_path())
+    with open(m.checksum_path(), "w") as f:  # reordered, whitespace, unknown field
+        f.write(' {\n "data_checksum" : "%s", "extra": [1, {"a": "b"}],\n "index_checksum":"%s" } \n' % (d, i))
+    Checksums.verify(m)
+
+
+def test_metadata_json_roundtrip(tmp_path):
+    m = SsTableMetadata.new(str(tmp_path), 2, timestamp_ms=123)
+    os.makedirs(os.path.dirname(m.metadata_path()))
+    m.write_to_file()
+    m2 = SsTableMetadata.load(m.metadata_path())
+    assert m2.data_path() == m.data_path() and m2.level == 2 and m2.id == 123
+
+
+def test_batch_entry_points_fail_loudly_without_gpu():
+    lib = _lib.load()
+    if lib.lsmck_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    assert not lib.lsmck_ctx_create(0)
+    assert "device" in _lib.last_error().lower()
+    from lsm_storage_engine_amd.device import Context
+    with pytest.raises(RuntimeError):
+        Context(0)

@@ -1,0 +1,88 @@
+"""GPU parity for the batched SHA-256 (lsmck_sha256_batch / _fixed) and the
+whole-tree SSTable verify (lsmck_checksums_verify_many), against FIPS vectors,
+the golden slices, the oracle, and the reference's checksum-file semantics."""
+import os
+import shutil
+
+import numpy as np
+import pytest
+
+from lsm_storage_engine_amd import _lib
+from lsm_storage_engine_amd.checksums import Checksums
+from lsm_storage_engine_amd.sstable_metadata import SsTableMetadata
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_fips_and_golden_slices(ctx, golden, blob):
+    texts = [e["text"].encode() for e in golden["sha256_text"]]
+    data = np.frombuffer(b"".join(texts), dtype=np.uint8)
+    ln = np.array([len(t) for t in texts], dtype=np.uint32)
+    off = np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.uint64)
+    got = ctx.sha256(data, off, ln)
+    for i, e in enumerate(golden["sha256_text"]):
+        assert got[i].tobytes().hex() == e["sha256"]
+    B = np.frombuffer(blob, dtype=np.uint8)
+    sl = golden["sha256_slices"]
+    got = ctx.sha256(B, np.array([e["off"] for e in sl], np.uint64), np.array([e["len"] for e in sl], np.uint32))
+    for i, e in enumerate(sl):
+        assert got[i].tobytes().hex() == e["sha256"], e
+
+
+@pytest.mark.parametrize("length,stride,shift", [(4096, 4096, 0), (64, 64, 0), (55, 57, 1), (56, 59, 2),
+                                                 (1000, 1003, 3), (0, 8, 0), (100000, 100000, 0)])
+def test_fixed_vs_oracle(ctx, length, stride, shift):
+    n = max(1, min(20000, (32 << 20) // max(stride, 1)))
+    data = O.gen_stream(21, 0, n * stride + shift + 8)
+    base = data[shift:]
+    got = ctx.sha256_fixed(base, stride, length, n)
+    off = np.arange(n, dtype=np.uint64) * stride
+    want = O.sha256_batch(base, off, np.full(n, length, np.uint32), threads=8)
+    assert np.array_equal(got, want)
+
+
+def test_random_lengths_vs_oracle(ctx):
+    rng = np.random.default_rng(4)
+    n = 20000
+    ln = rng.integers(0, 3000, n).astype(np.uint32)
+    off = np.concatenate([[3], 3 + np.cumsum(ln)[:-1]]).astype(np.uint64)
+    data = O.gen_stream(22, 0, int(off[-1]) + int(ln[-1]) + 8)
+    assert np.array_equal(ctx.sha256(data, off, ln), O.sha256_batch(data, off, ln, threads=8))
+
+
+def test_device_path_fixed_4k(ctx):
+    n = 1 << 14
+    d = ctx.alloc(n * 4096)
+    ctx.gen_stream(d.ptr, 0x5EED0002, 0, n * 4096)
+    out = ctx.alloc(32 * n)
+    ctx.sha256_fixed_device(d.ptr, 4096, 4096, n, out.ptr)
+    ctx.sync()
+    host = O.gen_stream(0x5EED0002, 0, n * 4096)
+    want = O.sha256_batch(host, np.arange(n, dtype=np.uint64) * 4096, np.full(n, 4096, np.uint32), threads=8)
+    assert np.array_equal(out.download(np.uint8).reshape(n, 32), want)
+
+
+def test_verify_many_tree(ctx, tmp_path, golden):
+    g = golden["sstable_test"]
+    metas = []
+    for t in range(40):
+        m = SsTableMetadata.new(str(tmp_path), t % 5, timestamp_ms=1000 + t)
+        os.makedirs(os.path.dirname(m.data_path()), exist_ok=True)
+        data = open(os.path.join(GOLDEN, g["data"]), "rb").read() * (1 + t % 7)
+        with open(m.data_path(), "wb") as f:
+            f.write(data)
+        shutil.copy(os.path.join(GOLDEN, g["index"]), m.index_path())
+        Checksums.write_checksums(m)
+        metas.append(m)
+    assert Checksums.verify_many(ctx, metas) == [0] * 40
+    with open(metas[3].data_path(), "r+b") as f:
+        f.write(b"Z")
+    with open(metas[7].index_path(), "r+b") as f:
+        f.seek(50)
+        f.write(b"Z")
+    os.remove(metas[9].checksum_path())
+    st = Checksums.verify_many(ctx, metas)
+    assert st[3] == _lib.DATA_MISMATCH and st[7] == _lib.INDEX_MISMATCH and st[9] < 0
+    assert sum(1 for s in st if s) == 3
