@@ -70,8 +70,8 @@ def main():
     if world > 1:
         dist.init_process_group("gloo", init_method="env://")
     torch.cuda.set_device(local)
-    stream = torch.cuda.current_stream(local)
-    sptr = stream.cuda_stream
+    stream = torch.cuda.Stream(device=local)  # a real stream: the null stream's handle (0) means
+    sptr = stream.cuda_stream                 # "the context's own stream" to liblsmck
     ctx = Context(local)
 
     cfg = a.config
@@ -185,6 +185,7 @@ def main():
             "launch_ms_hip_events": round(ev_ms, 4),
         },
         "cpu_baseline": None,
+        "hip_runtime": _lib._foreign_hip_runtime_loaded(),
     }
 
     # CPU baseline + parity of the same sample (rank 0, N = 1 only)

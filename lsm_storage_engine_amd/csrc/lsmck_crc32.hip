@@ -107,26 +107,51 @@ __device__ __forceinline__ uint32_t crc_word(const unsigned char* smem, uint32_t
 __device__ __forceinline__ uint32_t ld32(const unsigned char* p) { return *(const uint32_t*)p; }
 __device__ __forceinline__ u32x4 ld128(const unsigned char* p) { return *(const u32x4*)p; }
 
-template <bool ALIGNED16>
-__device__ __forceinline__ void load_segment_fast(const unsigned char* s0, uint32_t (&w)[32]) {
-  // full segment, s0 = E-128 16-byte (ALIGNED16) or 4-byte aligned
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    u32x4 v = ld128(s0 + 16 * g);
-    w[4 * g + 0] = v.x;
-    w[4 * g + 1] = v.y;
-    w[4 * g + 2] = v.z;
-    w[4 * g + 3] = v.w;
-  }
-}
+struct SegInfo {
+  uint32_t rec;       // record index
+  uint32_t q;         // segment index from the record's front
+  uint32_t k;         // segments after this one
+  uint64_t rec_off;   // record offset from base
+  uint32_t rec_len;
+  bool valid;
+};
 
-__device__ __forceinline__ void load_segment_general(uintptr_t s0a, uint32_t lead, uint32_t (&w)[32]) {
-  const uintptr_t base4 = s0a & ~(uintptr_t)3;
-  const uint32_t sh = (uint32_t)(s0a & 3);
-  const uintptr_t ba = s0a + lead;  // first record byte of this segment
-  const uint32_t lo_i = (uint32_t)(((ba & ~(uintptr_t)3) - base4) >> 2);  // first dword to load
-  const unsigned char* p = (const unsigned char*)base4;
-  uint32_t d[33];
+// In-flight loads of one segment (issued one tile ahead of their use).
+struct SegLoad {
+  uint32_t d[33];  // dwords D_0..D_32 (D_32 only when the stream start is not dword aligned)
+  uint32_t K;      // x^(8*128*k) mod P for this segment (k < 2^16; larger k finish in seg_finish)
+  uint32_t TI;     // init term 0xFFFFFFFF (x) x^(8*len0) for a record's first segment, else 0
+  uint32_t sh;     // (E-128) & 3
+  uint32_t lead;   // stream bytes in front of the record (first segment only)
+};
+
+// Issue every global load of a segment; consumes nothing.  FAST: full
+// segment whose stream start is dword aligned (ALIGNED16: 16-byte aligned).
+template <bool FAST>
+__device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si, SegLoad& L) {
+  const uint64_t E = si.rec_off + si.rec_len - 128ull * si.k;  // segment end (offset from base)
+  const uint32_t seglen = (si.q == 0) ? si.rec_len - 128u * si.k : 128u;
+  L.lead = 128u - seglen;
+  L.K = P.kseg[si.k & 0xFFFFu];
+  L.TI = (si.q == 0) ? P.tinit[seglen] : 0u;
+  // pointer arithmetic on the kernel-argument pointer keeps these global_load (not flat_load)
+  const unsigned char* s0 = P.base + (E - 128);
+  if (FAST) {
+    L.sh = 0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      u32x4 v = ld128(s0 + 16 * g);
+      L.d[4 * g + 0] = v.x;
+      L.d[4 * g + 1] = v.y;
+      L.d[4 * g + 2] = v.z;
+      L.d[4 * g + 3] = v.w;
+    }
+    L.d[32] = 0;
+    return;
+  }
+  L.sh = (uint32_t)((uintptr_t)s0 & 3);
+  const unsigned char* p = s0 - L.sh;                                         // floor4(E-128)
+  const uint32_t lo_i = (L.sh + L.lead) >> 2;                                 // first dword to load
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
     u32x4 v;
@@ -138,24 +163,43 @@ __device__ __forceinline__ void load_segment_general(uintptr_t s0a, uint32_t lea
       v.z = (4u * g + 2 >= lo_i) ? ld32(p + 16 * g + 8) : 0u;
       v.w = (4u * g + 3 >= lo_i) ? ld32(p + 16 * g + 12) : 0u;
     }
-    d[4 * g + 0] = v.x;
-    d[4 * g + 1] = v.y;
-    d[4 * g + 2] = v.z;
-    d[4 * g + 3] = v.w;
+    L.d[4 * g + 0] = v.x;
+    L.d[4 * g + 1] = v.y;
+    L.d[4 * g + 2] = v.z;
+    L.d[4 * g + 3] = v.w;
   }
-  d[32] = sh ? ld32(p + 128) : 0u;
+  L.d[32] = L.sh ? ld32(p + 128) : 0u;
+}
+
+// Funnel, mask, raw slicing-by-4 CRC, init term, shift to the record's end.
+template <bool FAST>
+__device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const CrcParams& P, const SegInfo& si,
+                                               const SegLoad& L, uint32_t lo, uint32_t hi) {
+  uint32_t w[32];
+  if (FAST) {
 #pragma unroll
-  for (int j = 0; j < 32; ++j) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
-  // zero the stream bytes in front of the record (bytes of the same dword as B
-  // that belong to the previous record, and unloaded dwords' slots)
-  if (__any(lead != 0)) {
+    for (int j = 0; j < 32; ++j) w[j] = L.d[j];
+  } else {
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      int c = (int)lead - 4 * j;
-      uint32_t m = (c >= 4) ? 0u : ((c > 0) ? (0xFFFFFFFFu << (8 * c)) : 0xFFFFFFFFu);
-      w[j] &= m;
+    for (int j = 0; j < 32; ++j) w[j] = __builtin_amdgcn_alignbyte(L.d[j + 1], L.d[j], L.sh);
+    // zero the stream bytes in front of the record: bytes of B's dword that
+    // belong to the previous record, and the slots of dwords never loaded
+    if (__any(L.lead != 0)) {
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        int c = (int)L.lead - 4 * j;
+        uint32_t m = (c >= 4) ? 0u : ((c > 0) ? (0xFFFFFFFFu << (8 * c)) : 0xFFFFFFFFu);
+        w[j] &= m;
+      }
     }
   }
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) s = crc_word(smem, s, w[j], lo, hi);
+  s ^= L.TI;
+  uint32_t K = L.K;
+  if (si.k >> 16) K = gf2_mulmod(K, P.khi[si.k >> 16]);
+  return gf2_mulmod(s, K);
 }
 
 // ---------------------------------------------------------------------------
@@ -169,38 +213,6 @@ __device__ __forceinline__ uint32_t seg_suffix_xor(uint32_t v, uint32_t lane, ui
   return v;
 }
 
-struct SegInfo {
-  uint32_t rec;       // record index
-  uint32_t q;         // segment index from the record's front
-  uint32_t k;         // segments after this one
-  uint64_t rec_off;   // record offset from base
-  uint32_t rec_len;
-  bool valid;
-};
-
-// Per-lane CRC of one segment -> contribution to the record's register
-__device__ __forceinline__ uint32_t segment_contrib(const unsigned char* smem, const CrcParams& P, const SegInfo& si,
-                                                    uint32_t lo, uint32_t hi, bool fast, bool aligned16) {
-  const uint64_t E = si.rec_off + si.rec_len - 128ull * si.k;  // segment end (offset)
-  // the first segment holds len - 128*k bytes (1..128), every other one 128
-  uint32_t seglen = (si.q == 0) ? si.rec_len - 128u * si.k : 128u;
-  uint32_t lead = 128u - seglen;
-  uint32_t w[32];
-  const unsigned char* s0 = P.base + (E - 128);
-  if (fast) {
-    if (aligned16)
-      load_segment_fast<true>(s0, w);
-    else
-      load_segment_fast<false>(s0, w);
-  } else {
-    load_segment_general((uintptr_t)P.base + E - 128, lead, w);
-  }
-  uint32_t s = 0;
-#pragma unroll
-  for (int j = 0; j < 32; ++j) s = crc_word(smem, s, w[j], lo, hi);
-  if (si.q == 0) s ^= P.tinit[seglen];
-  return gf2_mulmod(s, seg_shift_factor(P.kseg, P.khi, si.k));
-}
 
 __device__ __forceinline__ void emit_record(const CrcParams& P, uint32_t v, const SegInfo& si, uint32_t lane,
                                             uint32_t run_end, bool head) {
@@ -213,9 +225,35 @@ __device__ __forceinline__ void emit_record(const CrcParams& P, uint32_t v, cons
   }
 }
 
+template <bool FAST>
+__device__ __forceinline__ void finish_tile(const unsigned char* smem, const CrcParams& P, const SegInfo& si,
+                                            const SegLoad& L, uint32_t lane, uint32_t lo, uint32_t hi) {
+  uint32_t v = seg_finish<FAST>(smem, P, si, L, lo, hi);
+  v = si.valid ? v : 0u;
+  uint32_t run_end = min(63u, lane + si.k);
+  v = seg_suffix_xor(v, lane, run_end);
+  emit_record(P, v, si, lane, run_end, lane == 0 || si.q == 0);
+}
+
 // ---------------------------------------------------------------------------
 // Fixed-size records: record r = [r*stride, r*stride + len).
-template <bool FAST, bool ALIGNED16>
+__device__ __forceinline__ SegInfo fixed_map(const CrcParams& P, uint32_t t, uint32_t lane, uint32_t nsegr,
+                                             uint32_t total) {
+  uint32_t g = t * 64u + lane;
+  SegInfo si;
+  si.valid = g < total;
+  uint32_t gg = si.valid ? g : total - 1u;
+  si.rec = gg / nsegr;
+  si.q = gg - si.rec * nsegr;
+  si.k = nsegr - 1u - si.q;
+  si.rec_off = (uint64_t)si.rec * P.stride;
+  si.rec_len = P.flen;
+  return si;
+}
+
+// Software pipelined: the loads of tile t+nwaves are in flight while tile t is
+// checksummed (sched_barrier keeps the compiler from sinking them to their use).
+template <bool FAST>
 __global__ __launch_bounds__(1024) void crc32_fixed_kernel(CrcParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   build_lds_tables(smem, P.master);
@@ -225,23 +263,30 @@ __global__ __launch_bounds__(1024) void crc32_fixed_kernel(CrcParams P) {
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   const uint32_t nsegr = (P.flen + 127u) >> 7;
-  const uint32_t total = nsegr * (uint32_t)P.nrec;  // host keeps this < 2^31
+  const uint32_t total = nsegr * (uint32_t)P.nrec;  // host keeps this < 2^32 - 64
   const uint32_t ntiles = (total + 63u) >> 6;
-  for (uint32_t t = wave; t < ntiles; t += nwaves) {
-    uint32_t g = t * 64u + lane;
-    SegInfo si;
-    si.valid = g < total;
-    uint32_t gg = si.valid ? g : total - 1u;
-    si.rec = gg / nsegr;
-    si.q = gg - si.rec * nsegr;
-    si.k = nsegr - 1u - si.q;
-    si.rec_off = (uint64_t)si.rec * P.stride;
-    si.rec_len = P.flen;
-    uint32_t v = segment_contrib(smem, P, si, lo, hi, FAST, ALIGNED16);
-    v = si.valid ? v : 0u;
-    uint32_t run_end = min(63u, lane + si.k);
-    v = seg_suffix_xor(v, lane, run_end);
-    emit_record(P, v, si, lane, run_end, lane == 0 || si.q == 0);
+  // ping-pong between two load slots A/B: a loaded register is never copied
+  // (a copy would force s_waitcnt vmcnt(0) on the prefetch)
+  uint32_t t = wave;
+  if (t >= ntiles) return;
+  SegInfo sa = fixed_map(P, t, lane, nsegr, total), sb;
+  SegLoad A, B;
+  seg_issue<FAST>(P, sa, A);
+  for (;;) {
+    uint32_t tb = (t + nwaves < ntiles) ? t + nwaves : t;  // always issue: exact vmcnt counting
+    sb = fixed_map(P, tb, lane, nsegr, total);
+    seg_issue<FAST>(P, sb, B);
+    __builtin_amdgcn_sched_barrier(0);
+    finish_tile<FAST>(smem, P, sa, A, lane, lo, hi);
+    t += nwaves;
+    if (t >= ntiles) break;
+    uint32_t ta = (t + nwaves < ntiles) ? t + nwaves : t;
+    sa = fixed_map(P, ta, lane, nsegr, total);
+    seg_issue<FAST>(P, sa, A);
+    __builtin_amdgcn_sched_barrier(0);
+    finish_tile<FAST>(smem, P, sb, B, lane, lo, hi);
+    t += nwaves;
+    if (t >= ntiles) break;
   }
 }
 
@@ -249,6 +294,47 @@ __global__ __launch_bounds__(1024) void crc32_fixed_kernel(CrcParams P) {
 // Descriptor records (offset u64, len u32), arbitrary alignment.
 // Prep: seg_start[r] = exclusive prefix of nseg(r) = ceil(len/128);
 //       tile_first[t] = record holding segment 64t.
+__device__ __forceinline__ SegInfo desc_map(const CrcParams& P, int* R, uint32_t t, uint32_t lane, uint32_t total) {
+  const uint32_t g = t * 64u + lane;
+  const uint32_t r0 = P.tile_first[t];
+  // lane -> record: the largest r with seg_start[r] <= g (empty records own nothing)
+  R[lane] = -1;
+  __builtin_amdgcn_wave_barrier();
+  uint64_t chunk = 0;
+  for (;;) {
+    uint64_t r = (uint64_t)r0 + chunk + lane;
+    uint32_t ss = r < P.nrec ? P.seg_start[r] : 0xFFFFFFFFu;
+    int64_t st = (int64_t)ss - (int64_t)t * 64;
+    if (ss != 0xFFFFFFFFu && st < 64) atomicMax(&R[st < 0 ? 0 : (int)st], (int)(chunk + lane));
+    // continue while the 64th record of this chunk still starts inside the tile
+    uint32_t last_ss = __shfl(ss, 63, 64);
+    chunk += 64;
+    if (last_ss == 0xFFFFFFFFu || (int64_t)last_ss - (int64_t)t * 64 >= 64) break;
+  }
+  __builtin_amdgcn_wave_barrier();
+  int mine = R[lane];
+  uint64_t starts = __ballot(mine >= 0);
+  uint64_t below = starts & ((lane == 63) ? ~0ull : ((2ull << lane) - 1ull));
+  uint32_t p = 63u - (uint32_t)__builtin_clzll(below | 1ull);
+  int jrec = __shfl(mine, (int)p, 64);
+  __builtin_amdgcn_wave_barrier();
+  SegInfo si;
+  si.valid = g < total;
+  si.rec = r0 + (uint32_t)(jrec < 0 ? 0 : jrec);
+  uint32_t rs = P.seg_start[si.rec];
+  si.rec_off = P.off[si.rec];
+  si.rec_len = P.len[si.rec];
+  uint32_t nseg = (si.rec_len + 127u) >> 7;
+  si.q = g - rs;
+  si.k = nseg - 1u - si.q;
+  if (!si.valid) {  // pad lanes: a harmless full segment of the last record (result discarded)
+    si.q = 1;
+    si.k = 0;
+    si.rec_len = si.rec_len < 128u ? 128u : si.rec_len;
+  }
+  return si;
+}
+
 __global__ __launch_bounds__(1024) void crc32_desc_kernel(CrcParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   build_lds_tables(smem, P.master);
@@ -260,49 +346,26 @@ __global__ __launch_bounds__(1024) void crc32_desc_kernel(CrcParams P) {
   int* R = (int*)(smem + LDS_TABLE_BYTES + (threadIdx.x >> 6) * WAVE_SCRATCH_BYTES);
   const uint32_t total = *P.total_segs;
   const uint32_t ntiles = (total + 63u) >> 6;
-  for (uint32_t t = wave; t < ntiles; t += nwaves) {
-    const uint32_t g = t * 64u + lane;
-    const uint32_t r0 = P.tile_first[t];
-    // lane -> record: the largest r with seg_start[r] <= g (empty records own nothing)
-    R[lane] = -1;
-    __builtin_amdgcn_wave_barrier();
-    uint64_t chunk = 0;
-    for (;;) {
-      uint64_t r = (uint64_t)r0 + chunk + lane;
-      uint32_t ss = r < P.nrec ? P.seg_start[r] : 0xFFFFFFFFu;
-      int64_t st = (int64_t)ss - (int64_t)t * 64;
-      if (ss != 0xFFFFFFFFu && st < 64) atomicMax(&R[st < 0 ? 0 : (int)st], (int)(chunk + lane));
-      // continue while the 64th record of this chunk still starts inside the tile
-      uint32_t last_ss = __shfl(ss, 63, 64);
-      chunk += 64;
-      if (last_ss == 0xFFFFFFFFu || (int64_t)last_ss - (int64_t)t * 64 >= 64) break;
-    }
-    __builtin_amdgcn_wave_barrier();
-    int mine = R[lane];
-    uint64_t starts = __ballot(mine >= 0);
-    uint64_t below = starts & ((lane == 63) ? ~0ull : ((2ull << lane) - 1ull));
-    uint32_t p = 63u - (uint32_t)__builtin_clzll(below | 1ull);
-    int jrec = __shfl(mine, (int)p, 64);
-    SegInfo si;
-    si.valid = g < total;
-    si.rec = r0 + (uint32_t)(jrec < 0 ? 0 : jrec);
-    uint32_t rs = P.seg_start[si.rec];
-    si.rec_off = P.off[si.rec];
-    si.rec_len = P.len[si.rec];
-    uint32_t nseg = (si.rec_len + 127u) >> 7;
-    si.q = g - rs;
-    si.k = nseg - 1u - si.q;
-    if (!si.valid) {
-      si.q = 1;
-      si.k = 0;
-      si.rec_len = 128;
-      si.rec_off = 0;
-    }
-    uint32_t v = si.valid ? segment_contrib(smem, P, si, lo, hi, false, false) : 0u;
-    uint32_t run_end = min(63u, lane + si.k);
-    v = seg_suffix_xor(v, lane, run_end);
-    emit_record(P, v, si, lane, run_end, lane == 0 || si.q == 0);
-    __builtin_amdgcn_wave_barrier();
+  uint32_t t = wave;
+  if (t >= ntiles) return;
+  SegInfo sa = desc_map(P, R, t, lane, total), sb;
+  SegLoad A, B;
+  seg_issue<false>(P, sa, A);
+  for (;;) {
+    uint32_t tb = (t + nwaves < ntiles) ? t + nwaves : t;
+    sb = desc_map(P, R, tb, lane, total);
+    seg_issue<false>(P, sb, B);
+    __builtin_amdgcn_sched_barrier(0);
+    finish_tile<false>(smem, P, sa, A, lane, lo, hi);
+    t += nwaves;
+    if (t >= ntiles) break;
+    uint32_t ta = (t + nwaves < ntiles) ? t + nwaves : t;
+    sa = desc_map(P, R, ta, lane, total);
+    seg_issue<false>(P, sa, A);
+    __builtin_amdgcn_sched_barrier(0);
+    finish_tile<false>(smem, P, sb, B, lane, lo, hi);
+    t += nwaves;
+    if (t >= ntiles) break;
   }
 }
 
@@ -414,18 +477,14 @@ using namespace lsmck;
 
 extern "C" int lsmk_launch_crc32_fixed(const CrcParams* P, int ncu, hipStream_t st) {
   size_t lds = LDS_TABLE_BYTES;
-  bool a16 = ((uintptr_t)P->base % 16 == 0) && (P->stride % 16 == 0) && (P->flen % 16 == 0);
   bool fast = ((uintptr_t)P->base % 4 == 0) && (P->stride % 4 == 0) && (P->flen % 128 == 0);
-  const void* fn = fast ? (a16 ? (const void*)crc32_fixed_kernel<true, true> : (const void*)crc32_fixed_kernel<true, false>)
-                        : (const void*)crc32_fixed_kernel<false, false>;
+  const void* fn = fast ? (const void*)crc32_fixed_kernel<true> : (const void*)crc32_fixed_kernel<false>;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return -(int)e;
-  if (fast && a16)
-    hipLaunchKernelGGL((crc32_fixed_kernel<true, true>), dim3(ncu), dim3(1024), lds, st, *P);
-  else if (fast)
-    hipLaunchKernelGGL((crc32_fixed_kernel<true, false>), dim3(ncu), dim3(1024), lds, st, *P);
+  if (fast)
+    hipLaunchKernelGGL((crc32_fixed_kernel<true>), dim3(ncu), dim3(1024), lds, st, *P);
   else
-    hipLaunchKernelGGL((crc32_fixed_kernel<false, false>), dim3(ncu), dim3(1024), lds, st, *P);
+    hipLaunchKernelGGL((crc32_fixed_kernel<false>), dim3(ncu), dim3(1024), lds, st, *P);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
 }
