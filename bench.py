@@ -17,6 +17,7 @@ Prints ONE JSON line on rank 0 (see DESIGN.md section 5 for every field).
 """
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -46,6 +47,8 @@ def parse():
     ap.add_argument("--blocks-per-gpu", type=int, default=0, help="override the per-GPU record count")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-records", type=int, default=0)
+    ap.add_argument("--variants", default="", help="comma list of crc_chains values to A/B in interleaved rounds")
+    ap.add_argument("--rounds", type=int, default=5)
     return ap.parse_args()
 
 
@@ -123,6 +126,39 @@ def main():
     ctx.sync(sptr)
     torch.cuda.synchronize()
 
+    ab = None
+    if a.variants:
+        # interleaved A/B rounds in ONE process (cdna_hip_programming.md 5.4 rule 24)
+        vs = a.variants.split(",")
+        ab = {v: [] for v in vs}
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(a.rounds):
+            for v in vs:
+                # "c<k>" = crc_chains k;  "g<k>" = crc_chains k with the generic multiply;
+                # "a<k>" = diagnostic ablation k (timing only); optional suffix
+                # "w<n>" = crc_wg_waves n (descriptor kernel)
+                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?", v)
+                if not m:
+                    raise SystemExit(f"bad variant {v!r}")
+                kind, num, waves = m.group(1), int(m.group(2)), int(m.group(3) or 0)
+                ctx.set_option("crc_chains", num if kind in "cg" else 0)
+                ctx.set_option("crc_generic_mul", 1 if kind == "g" else 0)
+                ctx.set_option("crc_ablate", num if kind == "a" else 0)
+                ctx.set_option("crc_wg_waves", waves)
+                step()
+                e0.record(stream)
+                for _ in range(a.steps):
+                    step()
+                e1.record(stream)
+                ctx.sync(sptr)
+                ab[v].append(e0.elapsed_time(e1) / a.steps)
+        ctx.set_option("crc_chains", 0)
+        ctx.set_option("crc_generic_mul", 0)
+        ctx.set_option("crc_ablate", 0)
+        ctx.set_option("crc_wg_waves", 0)
+        ab = {str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
+                       "GiBps_median": payload / GIB / (float(np.median(t)) * 1e-3)} for v, t in ab.items()}
+
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     if world > 1:
@@ -187,6 +223,8 @@ def main():
         "cpu_baseline": None,
         "hip_runtime": _lib._foreign_hip_runtime_loaded(),
     }
+    if ab is not None:
+        res["variants_ab"] = ab
 
     # CPU baseline + parity of the same sample (rank 0, N = 1 only)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -127,6 +127,21 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx);
 const char* lsmck_last_error(void);
 int lsmck_device_count(void);
 
+/* Tuning knobs of a context (no effect on results, only on speed):
+ *   "crc_chains"  independent CRC register chains per lane in the CRC kernels:
+ *                 1, 2 or 4 (0 = built-in default).  Used by bench.py --variants
+ *                 to A/B kernel variants in one process.
+ *   "crc_generic_mul"  1 = fixed records use the generic GF(2) multiply instead of
+ *                 per-lane precomputed columns (A/B switch); 0 = default.
+ *   "crc_ablate"  DIAGNOSTIC ONLY, results are invalid while set: 1 = the fixed
+ *                 kernel loads but does not checksum, 2 = checksums without
+ *                 loading; 0 = off.  Locates the kernel's ceiling.
+ *   "crc_wg_waves"  waves per workgroup of the descriptor CRC kernel: 12 or 16
+ *                 (0 = built-in default).  A/B switch: 12 waves leave 168 VGPRs
+ *                 per lane for the three-stage load pipeline, 16 leave 128.
+ * Returns 0, or LSMCK_EINVAL for an unknown key / value. */
+int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
+
 /* ======================================================================== */
 /* 3. Batch GPU entry points                                                  */
 /* ======================================================================== */

@@ -9,6 +9,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -84,13 +85,13 @@ struct DescScratch {
   size_t cap_seg = 0;
   uint32_t* block_sum = nullptr;
   size_t cap_bs = 0;
-  uint32_t* tile_first = nullptr;
+  uint32_t* tile_info = nullptr;  // 4 u32 per tile
   size_t cap_tf = 0;
   uint32_t* total = nullptr;  // device, 1 u32
   void release() {
     if (seg_start) (void)hipFree(seg_start);
     if (block_sum) (void)hipFree(block_sum);
-    if (tile_first) (void)hipFree(tile_first);
+    if (tile_info) (void)hipFree(tile_info);
     if (total) (void)hipFree(total);
     *this = DescScratch();
   }
@@ -148,6 +149,7 @@ struct lsmck_ctx {
   uint32_t* d_kseg = nullptr;    // 65536
   uint32_t* d_khi = nullptr;     // 65536
   uint32_t* d_tinit = nullptr;   // 129
+  uint32_t* d_zero = nullptr;    // 64 zero bytes
   std::mutex mu;
   DescScratch scratch;           // device-mode descriptor scratch
   hipEvent_t scratch_ev = nullptr;
@@ -155,6 +157,7 @@ struct lsmck_ctx {
   unsigned long long* d_verify = nullptr;  // [n_bad, first_bad]
   unsigned long long* h_verify = nullptr;  // pinned
   Stage stage[2];
+  int variant = 0;  // kernel variant for A/B timing (LSMCK_CRC_CHAINS=1|2|4); 0 = default
 };
 
 namespace {
@@ -186,6 +189,7 @@ void fill_tables(lsmck_ctx* ctx, CrcParams* P) {
   P->khi = ctx->d_khi;
   P->tinit = ctx->d_tinit;
   P->master = ctx->d_master;
+  P->zero = ctx->d_zero;
 }
 
 // Fixed-size CRC on device pointers, split so each launch has < 2^32 segments.
@@ -211,7 +215,7 @@ int crc_fixed_device(lsmck_ctx* ctx, const uint8_t* base, size_t stride, uint32_
     P.nrec = cnt;
     P.out = out + r0;
     fill_tables(ctx, &P);
-    int rc = lsmk_launch_crc32_fixed(&P, ctx->ncu, st);
+    int rc = lsmk_launch_crc32_fixed(&P, ctx->ncu, ctx->variant, st);
     if (rc) return launch_rc(rc, "crc32_fixed kernel");
   }
   return 0;
@@ -250,9 +254,10 @@ int crc_desc_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const 
     return lsmck_host::set_error(LSMCK_EINVAL, "batch exceeds 2^32 128-byte segments; split it");
   if (total == 0) return 0;
   size_t ntiles = (size_t)((total + 63) / 64);
-  if ((rc = ensure_dev(&sc.tile_first, &sc.cap_tf, ntiles))) return rc;
-  P.tile_first = sc.tile_first;
-  rc = lsmk_launch_crc32_desc(&P, sc.block_sum, ctx->ncu, st);
+  if ((rc = ensure_dev(&sc.tile_info, &sc.cap_tf, 4 * ntiles))) return rc;
+  HIPCHK(hipMemsetAsync(sc.tile_info, 0, 16 * ntiles, st));
+  P.tile_info = sc.tile_info;
+  rc = lsmk_launch_crc32_desc(&P, sc.block_sum, ctx->ncu, ctx->variant, st);
   if (rc) return launch_rc(rc, "crc32_desc kernel");
   return 0;
 }
@@ -378,7 +383,7 @@ int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
     if (J.kind == CRC) {
       if (J.off) {
         int64_t total = 0;
-        for (size_t i = 0; i < cnt; ++i) total += (S.h_len[i] + 127u) / 128u;
+        for (size_t i = 0; i < cnt; ++i) total += S.h_len[i] ? (S.h_len[i] + 127u) / 128u : 1u;
         rc = crc_desc_device(ctx, S.scratch, S.d_pay, S.d_off, S.d_len, cnt, (uint32_t*)S.d_out, S.s, total, nullptr);
       } else {
         // fixed records: the span starts at record r
@@ -443,12 +448,18 @@ lsmck_ctx* lsmck_ctx_create(int device) {
   }
   lsmck_ctx* ctx = new lsmck_ctx();
   ctx->dev = device;
+  if (const char* v = getenv("LSMCK_CRC_CHAINS")) ctx->variant = atoi(v);
   ctx->ncu = pr.multiProcessorCount;
   // combination tables
-  std::vector<uint32_t> master(1024), kseg(65536), khi(65536), tinit(129);
+  std::vector<uint32_t> master(4096), kseg(65536), khi(65536), tinit(130, 0u);
   const uint32_t* T = lsmck_host::crc_tables();
   for (int t = 0; t < 4; ++t)
     for (int e = 0; e < 256; ++e) master[t * 256 + e] = T[t * 256 + e];
+  for (int m = 1; m <= 3; ++m) {  // shift tables: register advanced over 32*m zero bytes
+    uint32_t X = lsmck_host::x_pow_8n(32 * m);
+    for (int j = 0; j < 4; ++j)
+      for (int b = 0; b < 256; ++b) master[1024 * m + 256 * j + b] = lsmck_host::gf2_mulmod(X, (uint32_t)b << (8 * j));
+  }
   uint32_t X = lsmck_host::x_pow_8n(128);  // one segment
   kseg[0] = 1u << 31;
   for (int k = 1; k < 65536; ++k) kseg[k] = lsmck_host::gf2_mulmod(kseg[k - 1], X);
@@ -457,14 +468,15 @@ lsmck_ctx* lsmck_ctx_create(int device) {
   for (int k = 1; k < 65536; ++k) khi[k] = lsmck_host::gf2_mulmod(khi[k - 1], Y);
   for (int m = 0; m <= 128; ++m) tinit[m] = lsmck_host::gf2_mulmod(lsmck_host::x_pow_8n(m), 0xFFFFFFFFu);
   bool ok = hipStreamCreateWithFlags(&ctx->stream0, hipStreamNonBlocking) == hipSuccess &&
-            hipMalloc((void**)&ctx->d_master, 4096) == hipSuccess &&
+            hipMalloc((void**)&ctx->d_master, 4096 * 4) == hipSuccess &&
             hipMalloc((void**)&ctx->d_kseg, 65536 * 4) == hipSuccess &&
             hipMalloc((void**)&ctx->d_khi, 65536 * 4) == hipSuccess &&
-            hipMalloc((void**)&ctx->d_tinit, 129 * 4) == hipSuccess &&
-            hipMemcpy(ctx->d_master, master.data(), 4096, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMalloc((void**)&ctx->d_tinit, 130 * 4) == hipSuccess &&
+            hipMalloc((void**)&ctx->d_zero, 64) == hipSuccess && hipMemset(ctx->d_zero, 0, 64) == hipSuccess &&
+            hipMemcpy(ctx->d_master, master.data(), 4096 * 4, hipMemcpyHostToDevice) == hipSuccess &&
             hipMemcpy(ctx->d_kseg, kseg.data(), 65536 * 4, hipMemcpyHostToDevice) == hipSuccess &&
             hipMemcpy(ctx->d_khi, khi.data(), 65536 * 4, hipMemcpyHostToDevice) == hipSuccess &&
-            hipMemcpy(ctx->d_tinit, tinit.data(), 129 * 4, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(ctx->d_tinit, tinit.data(), 130 * 4, hipMemcpyHostToDevice) == hipSuccess &&
             hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming) == hipSuccess &&
             hipHostMalloc((void**)&ctx->h_total, 64, hipHostMallocDefault) == hipSuccess &&
             hipHostMalloc((void**)&ctx->h_verify, 64, hipHostMallocDefault) == hipSuccess &&
@@ -477,6 +489,39 @@ lsmck_ctx* lsmck_ctx_create(int device) {
   return ctx;
 }
 
+int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!key) return lsmck_host::set_error(LSMCK_EINVAL, "null key");
+  if (!strcmp(key, "crc_chains")) {
+    if (value != 0 && value != 1 && value != 2 && value != 4)
+      return lsmck_host::set_error(LSMCK_EINVAL, "crc_chains must be 0, 1, 2 or 4");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (ctx->variant & ~0xF) | (int)value;
+    return 0;
+  }
+  if (!strcmp(key, "crc_generic_mul")) {  // A/B: 1 = per-lane LDS columns off for fixed records
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_generic_mul must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (ctx->variant & ~0x10) | (value ? 0x10 : 0);
+    return 0;
+  }
+  if (!strcmp(key, "crc_ablate")) {  // diagnostic only: timing ablations, results are garbage
+    if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0, 1 or 2");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (ctx->variant & 0xFF) | ((int)value << 8);
+    return 0;
+  }
+  if (!strcmp(key, "crc_wg_waves")) {  // A/B: waves per workgroup of the descriptor kernel
+    if (value != 0 && value != 12 && value != 16)
+      return lsmck_host::set_error(LSMCK_EINVAL, "crc_wg_waves must be 0, 12 or 16");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (ctx->variant & ~0x20) | (value == 12 ? 0x20 : 0);
+    return 0;
+  }
+  return lsmck_host::set_error(LSMCK_EINVAL, "unknown option");
+}
+
 void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   if (!ctx) return;
   DevGuard g(ctx->dev);
@@ -487,6 +532,7 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   if (ctx->d_kseg) (void)hipFree(ctx->d_kseg);
   if (ctx->d_khi) (void)hipFree(ctx->d_khi);
   if (ctx->d_tinit) (void)hipFree(ctx->d_tinit);
+  if (ctx->d_zero) (void)hipFree(ctx->d_zero);
   if (ctx->d_verify) (void)hipFree(ctx->d_verify);
   if (ctx->h_total) (void)hipHostFree(ctx->h_total);
   if (ctx->h_verify) (void)hipHostFree(ctx->h_verify);

@@ -41,8 +41,21 @@ namespace lsmck {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-#define LDS_TABLE_BYTES 131072u
+#define LDS_TABLE_BYTES 131072u  // slicing-by-4 tables, 32x bank-replicated
+#define LDS_SHIFT_OFF 131072u    // chain-combine tables: shift by 32, 64, 96 bytes (3 x 4 x 256 x 4 B)
+#define LDS_SHIFT_BYTES 12288u
+#define LDS_COLS_OFF (LDS_SHIFT_OFF + LDS_SHIFT_BYTES)  // fixed records: per-lane columns of x^(8*128*k)
+#define LDS_COLS_BYTES 8192u                               // [32/4][64 lanes][4] u32
+#define LDS_KHI_OFF (LDS_COLS_OFF + LDS_COLS_BYTES)  // khi[0..511]: x^(8*128*65536*j), j = k >> 16 (len < 2^32)
+#define LDS_KHI_BYTES 2048u
+#define LDS_SCRATCH_OFF (LDS_KHI_OFF + LDS_KHI_BYTES)
 #define WAVE_SCRATCH_BYTES 256u
+#ifndef LSMCK_DEFAULT_CHAINS
+#define LSMCK_DEFAULT_CHAINS 2       // fixed records (A/B: profiles/r01)
+#endif
+#ifndef LSMCK_DEFAULT_DESC_CHAINS
+#define LSMCK_DEFAULT_DESC_CHAINS 1  // descriptor records (A/B: profiles/r01)
+#endif
 
 // ---------------------------------------------------------------------------
 // GF(2) polynomial product modulo the reflected CRC-32 polynomial.
@@ -66,22 +79,45 @@ __device__ __forceinline__ uint32_t seg_shift_factor(const uint32_t* __restrict_
   return f;
 }
 
+// The kernels declare no static LDS, so the dynamic region starts at LDS
+// address 0: index an address_space(3) pointer directly (indexing smem + a
+// costs a v_add of the relocated base per lookup).
+typedef __attribute__((address_space(3))) const uint32_t lds_u32_t;
+typedef __attribute__((address_space(3))) const u32x4 lds_u32x4_t;
+__device__ __forceinline__ uint32_t lds_ld(const unsigned char* smem, uint32_t a) {
+  (void)smem;
+  return *(lds_u32_t*)(size_t)a;
+}
+__device__ __forceinline__ u32x4 lds_ld128(uint32_t a) { return *(lds_u32x4_t*)(size_t)a; }
+
 // ---------------------------------------------------------------------------
 // LDS tables.  Byte address of T_t[e], replica r:
 //   256*e + 4*r + 128*(t&1) + 65536*(t>>1)
 // T0 = Sarwate table, T_k[n] = (T_{k-1}[n] >> 8) ^ T0[T_{k-1}[n] & 0xFF].
-__device__ __forceinline__ void build_lds_tables(unsigned char* smem, const uint32_t* __restrict__ master) {
+__device__ __forceinline__ void build_lds_tables(unsigned char* smem, const uint32_t* __restrict__ master,
+                                                 const uint32_t* __restrict__ khi) {
   uint32_t* s32 = (uint32_t*)smem;
   for (uint32_t i = threadIdx.x; i < LDS_TABLE_BYTES / 4; i += blockDim.x) {
     uint32_t t = ((i >> 14) << 1) | ((i >> 5) & 1u);
     uint32_t e = (i >> 6) & 255u;
     s32[i] = master[t * 256u + e];
   }
+  // shift tables ST_m[j][b] = (b << 8j) (x) x^(8*32m) mod P, m = 1..3, plain layout
+  for (uint32_t i = threadIdx.x; i < LDS_SHIFT_BYTES / 4; i += blockDim.x) s32[LDS_SHIFT_OFF / 4 + i] = master[1024u + i];
+  // segment factors of records over 2^16 segments (8 MiB): from LDS, so the
+  // checksum loop issues no global load of its own (its waits would also
+  // wait for the next tile's prefetch)
+  for (uint32_t i = threadIdx.x; i < LDS_KHI_BYTES / 4; i += blockDim.x) s32[LDS_KHI_OFF / 4 + i] = khi[i];
 }
 
-__device__ __forceinline__ uint32_t lds_ld(const unsigned char* smem, uint32_t a) {
-  return *(const uint32_t*)(smem + a);
+// raw CRC register s advanced over 32*m zero bytes (m = 1..3): 4 plain-table lookups
+template <int M>
+__device__ __forceinline__ uint32_t shift_bytes32(const unsigned char* smem, uint32_t s) {
+  constexpr uint32_t base = LDS_SHIFT_OFF + (M - 1) * 4096u;
+  return lds_ld(smem, base + ((s & 0xFFu) << 2)) ^ lds_ld(smem, base + 1024u + (((s >> 8) & 0xFFu) << 2)) ^
+         lds_ld(smem, base + 2048u + (((s >> 16) & 0xFFu) << 2)) ^ lds_ld(smem, base + 3072u + ((s >> 24) << 2));
 }
+
 
 // One slicing-by-4 step of the raw CRC register: s' = F(s ^ w).
 // lo = lane4, hi = lane4 | 0x10000 (region of T2/T3).
@@ -121,23 +157,43 @@ struct SegLoad {
   uint32_t d[33];  // dwords D_0..D_32 (D_32 only when the stream start is not dword aligned)
   uint32_t K;      // x^(8*128*k) mod P for this segment (k < 2^16; larger k finish in seg_finish)
   uint32_t TI;     // init term 0xFFFFFFFF (x) x^(8*len0) for a record's first segment, else 0
-  uint32_t sh;     // (E-128) & 3
-  uint32_t lead;   // stream bytes in front of the record (first segment only)
+  // the segment's coordinates, copied at issue time (when they are resident):
+  // finish needs no SegInfo, so the map of a later tile may still be in flight
+  uint32_t rec, k;
+  uint32_t fl;     // packed SegLoad.fl fields below
 };
+// FL_SH: (E-128) & 3.  FL_BST: B - floor4(E-128).  FL_P16: floor4(E-128)/4 mod 4.
+// FL_RISKY: a page boundary lies inside B's group, in front of B's dword; the
+// group was loaded from floor16(B's dword) instead and seg_finish shifts it
+// into place.  FL_VALID: lane holds a real segment.  FL_FIRST: q == 0.
+#define FL_SH(f) ((f) & 3u)
+#define FL_BST(f) (((f) >> 2) & 0xFFu)
+#define FL_RISKY 0x400u
+#define FL_VALID 0x800u
+#define FL_FIRST 0x1000u
+#define FL_P16(f) (((f) >> 13) & 3u)
 
 // Issue every global load of a segment; consumes nothing.  FAST: full
 // segment whose stream start is dword aligned (ALIGNED16: 16-byte aligned).
-template <bool FAST>
+template <bool FAST, int ABLATE = 0>
 __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si, SegLoad& L) {
   const uint64_t E = si.rec_off + si.rec_len - 128ull * si.k;  // segment end (offset from base)
   const uint32_t seglen = (si.q == 0) ? si.rec_len - 128u * si.k : 128u;
-  L.lead = 128u - seglen;
+  const uint32_t lead = 128u - seglen;  // stream bytes in front of the record (first segment only)
+  L.rec = si.rec;
+  L.k = si.k;
+  const uint32_t flv = (si.valid ? FL_VALID : 0u) | (si.q == 0 ? FL_FIRST : 0u);
+  L.fl = flv;
   L.K = P.kseg[si.k & 0xFFFFu];
-  L.TI = (si.q == 0) ? P.tinit[seglen] : 0u;
+  L.TI = P.tinit[(si.q == 0) ? seglen : 129u];  // unconditional load (tinit[129] = 0): no branch in the issue block
   // pointer arithmetic on the kernel-argument pointer keeps these global_load (not flat_load)
   const unsigned char* s0 = P.base + (E - 128);
+  if (ABLATE == 2) {  // diagnostic: no payload loads (compute-only timing; results invalid)
+#pragma unroll
+    for (int j = 0; j < 33; ++j) L.d[j] = (uint32_t)E * 0x9E3779B1u + j;
+    return;
+  }
   if (FAST) {
-    L.sh = 0;
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       u32x4 v = ld128(s0 + 16 * g);
@@ -149,57 +205,146 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
     L.d[32] = 0;
     return;
   }
-  L.sh = (uint32_t)((uintptr_t)s0 & 3);
-  const unsigned char* p = s0 - L.sh;                                         // floor4(E-128)
-  const uint32_t lo_i = (L.sh + L.lead) >> 2;                                 // first dword to load
+  // General path, straight-line (no divergent branches: a branch merge here
+  // makes hipcc wait for the loads and the prefetch is lost).
+  //  - groups entirely in front of B's dword read a 64-byte zero buffer;
+  //  - the group holding B's dword is loaded whole: its bytes in front of B
+  //    (<= 12) are zeroed in seg_finish.  They are on B's page unless a page
+  //    boundary lies between the group start and B's dword ("risky", rare):
+  //    then the group is loaded from floor16(B's dword) -- that is the page
+  //    boundary itself, and a 16-byte aligned block never crosses a page --
+  //    and seg_finish shifts it up by 1..3 dwords into place;
+  //  - groups end at floor4(E-128)+128 <= E, D_32 at ceil4(E): no over-read.
+  const uint32_t sh = (uint32_t)((uintptr_t)s0 & 3);
+  const unsigned char* p = s0 - sh;     // floor4(E-128)
+  const uint32_t bstart = sh + lead;    // B - floor4(E-128)
+  const uint32_t lo_i = bstart >> 2;    // index of B's dword
+  const uint32_t gb = lo_i >> 2;        // group holding B's dword
+  const uintptr_t b4 = (uintptr_t)p + 4u * lo_i;
+  // bitwise &, not &&: a short-circuit branch here would merge wait states (see above)
+  const bool risky = ((lo_i & 3u) != 0u) & ((b4 & ~(uintptr_t)4095) > (uintptr_t)p + 16u * gb);
+  L.fl = flv | sh | (bstart << 2) | (risky ? FL_RISKY : 0u) | ((uint32_t)(((uintptr_t)p >> 2) & 3u) << 13);
+  const unsigned char* zero = (const unsigned char*)P.zero;
+  const unsigned char* pb16 = P.base + ((E - 128) - sh + 4u * lo_i) - (b4 & 15u);  // floor16(B's dword)
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
-    u32x4 v;
-    if (4u * g >= lo_i) {
-      v = ld128(p + 16 * g);
-    } else {
-      v.x = (4u * g + 0 >= lo_i) ? ld32(p + 16 * g + 0) : 0u;
-      v.y = (4u * g + 1 >= lo_i) ? ld32(p + 16 * g + 4) : 0u;
-      v.z = (4u * g + 2 >= lo_i) ? ld32(p + 16 * g + 8) : 0u;
-      v.w = (4u * g + 3 >= lo_i) ? ld32(p + 16 * g + 12) : 0u;
-    }
+    const bool skip = 4u * g + 3u < lo_i;
+    const bool rk = ((uint32_t)g == gb) & risky;
+    u32x4 v = ld128(rk ? pb16 : (skip ? zero : p + 16 * g));
     L.d[4 * g + 0] = v.x;
     L.d[4 * g + 1] = v.y;
     L.d[4 * g + 2] = v.z;
     L.d[4 * g + 3] = v.w;
   }
-  L.d[32] = L.sh ? ld32(p + 128) : 0u;
+  // D_32 only when the stream start is not dword aligned; an empty segment loads nothing
+  L.d[32] = ld32((sh && lead < 128u) ? p + 128 : zero);
 }
 
 // Funnel, mask, raw slicing-by-4 CRC, init term, shift to the record's end.
-template <bool FAST>
-__device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const CrcParams& P, const SegInfo& si,
-                                               const SegLoad& L, uint32_t lo, uint32_t hi) {
+// CHAINS independent register chains per lane (the segment's 128 bytes cut in
+// CHAINS pieces) hide the LDS lookup latency; they are recombined with the
+// shift-by-32m-bytes tables: raw(A||B) = shift_|B|(raw(A)) ^ raw(B).
+template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
+__device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const CrcParams& P, const SegLoad& L,
+                                               uint32_t lo, uint32_t hi) {
+  if (ABLATE == 1) {  // diagnostic: loads only (memory-path timing; results invalid)
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < 33; ++j) x ^= L.d[j];
+    return x ^ L.K ^ L.TI;
+  }
   uint32_t w[32];
   if (FAST) {
 #pragma unroll
     for (int j = 0; j < 32; ++j) w[j] = L.d[j];
   } else {
+    uint32_t d[33];
 #pragma unroll
-    for (int j = 0; j < 32; ++j) w[j] = __builtin_amdgcn_alignbyte(L.d[j + 1], L.d[j], L.sh);
-    // zero the stream bytes in front of the record: bytes of B's dword that
-    // belong to the previous record, and the slots of dwords never loaded
-    if (__any(L.lead != 0)) {
+    for (int j = 0; j < 33; ++j) d[j] = L.d[j];
+    const uint32_t sh = FL_SH(L.fl), bstart = FL_BST(L.fl), lo_i = bstart >> 2;
+    const uint32_t bm = 0xFFFFFFFFu << (8u * (bstart & 3u));  // keep-mask of B's dword
+    const bool risky = (L.fl & FL_RISKY) != 0u;
+    if (__any(risky)) {  // rare: B's group was loaded from floor16(B's dword), s dwords too low
+      const uint32_t r = lo_i & 3u, gb = lo_i >> 2;
+      const uint32_t s = r - ((FL_P16(L.fl) + r) & 3u);  // 1..3 for risky lanes
 #pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        int c = (int)L.lead - 4 * j;
-        uint32_t m = (c >= 4) ? 0u : ((c > 0) ? (0xFFFFFFFFu << (8 * c)) : 0xFFFFFFFFu);
-        w[j] &= m;
+      for (int g = 0; g < 8; ++g) {
+        const bool here = risky & ((uint32_t)g == gb);
+        const uint32_t x0 = d[4 * g], x1 = d[4 * g + 1], x2 = d[4 * g + 2];
+        // group[k] = x[k - s] for k >= r (>= s); dwords k < r are zeroed below
+        d[4 * g + 3] = here ? (s == 1u ? x2 : (s == 2u ? x1 : x0)) : d[4 * g + 3];
+        d[4 * g + 2] = here ? (s == 1u ? x1 : x0) : x2;
+        d[4 * g + 1] = here ? x0 : x1;
       }
     }
-  }
-  uint32_t s = 0;
+    if (__any(bstart != 0u)) {
+      // zero the loaded bytes in front of B inside B's group
+      const uint32_t r = lo_i & 3u, gb = lo_i >> 2;
+      uint32_t m[4];
 #pragma unroll
-  for (int j = 0; j < 32; ++j) s = crc_word(smem, s, w[j], lo, hi);
+      for (int k = 0; k < 4; ++k) m[k] = ((uint32_t)k < r) ? 0u : (((uint32_t)k == r) ? bm : 0xFFFFFFFFu);
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const bool here = (uint32_t)g == gb;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[4 * g + k] &= here ? m[k] : 0xFFFFFFFFu;
+      }
+      d[32] &= (lo_i == 32u) ? bm : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int j = 0; j < 32; ++j) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+  }
+  constexpr int WPC = 32 / CHAINS;  // words per chain
+  uint32_t c[CHAINS];
+#pragma unroll
+  for (int h = 0; h < CHAINS; ++h) c[h] = 0;
+#pragma unroll
+  for (int j = 0; j < WPC; ++j) {
+#pragma unroll
+    for (int h = 0; h < CHAINS; ++h) c[h] = crc_word(smem, c[h], w[h * WPC + j], lo, hi);
+  }
+  uint32_t s;
+  if constexpr (CHAINS == 1) {
+    s = c[0];
+  } else if constexpr (CHAINS == 2) {
+    s = shift_bytes32<2>(smem, c[0]) ^ c[1];
+  } else {
+    s = shift_bytes32<3>(smem, c[0]) ^ shift_bytes32<2>(smem, c[1]) ^ shift_bytes32<1>(smem, c[2]) ^ c[3];
+  }
   s ^= L.TI;
+  if constexpr (PERCOL) {
+    // s (x) K with the lane's 32 precomputed columns K*x^i: p ^= col_i if bit 31-i of s
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t p = 0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      u32x4 c = lds_ld128(LDS_COLS_OFF + g * 1024u + lane * 16u);
+      p ^= c.x & (uint32_t)((int32_t)(s << (4 * g + 0)) >> 31);
+      p ^= c.y & (uint32_t)((int32_t)(s << (4 * g + 1)) >> 31);
+      p ^= c.z & (uint32_t)((int32_t)(s << (4 * g + 2)) >> 31);
+      p ^= c.w & (uint32_t)((int32_t)(s << (4 * g + 3)) >> 31);
+    }
+    return p;
+  }
   uint32_t K = L.K;
-  if (si.k >> 16) K = gf2_mulmod(K, P.khi[si.k >> 16]);
+  if (L.k >> 16) K = gf2_mulmod(K, lds_ld(smem, LDS_KHI_OFF + ((L.k >> 16) << 2)));
   return gf2_mulmod(s, K);
+}
+
+// Per-lane columns K*x^i (i = 0..31) of the shift factor K = x^(8*128*k_lane)
+// for fixed records whose segment count divides 64: every tile starts on a
+// record boundary, so lane l always holds segment k = nsegr-1 - l%nsegr.
+__device__ __forceinline__ void build_lds_cols(const CrcParams& P, uint32_t nsegr) {
+  if (threadIdx.x >= 64) return;
+  const uint32_t lane = threadIdx.x;
+  uint32_t b = P.kseg[nsegr - 1u - lane % nsegr];
+  uint32_t* s32 = (uint32_t*)0;
+  (void)s32;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    *(__attribute__((address_space(3))) uint32_t*)(size_t)(LDS_COLS_OFF + (i >> 2) * 1024u + lane * 16u + (i & 3) * 4u) = b;
+    b = (b >> 1) ^ (0xEDB88320u & (0u - (b & 1u)));
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -213,26 +358,25 @@ __device__ __forceinline__ uint32_t seg_suffix_xor(uint32_t v, uint32_t lane, ui
   return v;
 }
 
-
-__device__ __forceinline__ void emit_record(const CrcParams& P, uint32_t v, const SegInfo& si, uint32_t lane,
-                                            uint32_t run_end, bool head) {
-  if (!si.valid || !head) return;
-  bool has_last = (lane + si.k) <= 63u;  // this tile holds the record's final segment
-  if (si.q == 0 && has_last) {
-    P.out[si.rec] = ~v;
+__device__ __forceinline__ void emit_record(const CrcParams& P, uint32_t v, const SegLoad& L, uint32_t lane,
+                                            bool head) {
+  if (!(L.fl & FL_VALID) || !head) return;
+  bool has_last = (lane + L.k) <= 63u;  // this tile holds the record's final segment
+  if ((L.fl & FL_FIRST) && has_last) {
+    P.out[L.rec] = ~v;
   } else {
-    atomicXor(&P.out[si.rec], has_last ? ~v : v);
+    atomicXor(&P.out[L.rec], has_last ? ~v : v);
   }
 }
 
-template <bool FAST>
-__device__ __forceinline__ void finish_tile(const unsigned char* smem, const CrcParams& P, const SegInfo& si,
-                                            const SegLoad& L, uint32_t lane, uint32_t lo, uint32_t hi) {
-  uint32_t v = seg_finish<FAST>(smem, P, si, L, lo, hi);
-  v = si.valid ? v : 0u;
-  uint32_t run_end = min(63u, lane + si.k);
+template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
+__device__ __forceinline__ void finish_tile(const unsigned char* smem, const CrcParams& P, const SegLoad& L,
+                                            uint32_t lane, uint32_t lo, uint32_t hi) {
+  uint32_t v = seg_finish<FAST, CHAINS, ABLATE, PERCOL>(smem, P, L, lo, hi);
+  v = (L.fl & FL_VALID) ? v : 0u;
+  uint32_t run_end = min(63u, lane + L.k);
   v = seg_suffix_xor(v, lane, run_end);
-  emit_record(P, v, si, lane, run_end, lane == 0 || si.q == 0);
+  emit_record(P, v, L, lane, lane == 0 || (L.fl & FL_FIRST));
 }
 
 // ---------------------------------------------------------------------------
@@ -253,120 +397,154 @@ __device__ __forceinline__ SegInfo fixed_map(const CrcParams& P, uint32_t t, uin
 
 // Software pipelined: the loads of tile t+nwaves are in flight while tile t is
 // checksummed (sched_barrier keeps the compiler from sinking them to their use).
-template <bool FAST>
+template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
 __global__ __launch_bounds__(1024) void crc32_fixed_kernel(CrcParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  build_lds_tables(smem, P.master);
+  build_lds_tables(smem, P.master, P.khi);
+  if (PERCOL) build_lds_cols(P, (P.flen + 127u) >> 7);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t lo = (lane & 31u) * 4u, hi = lo | 0x10000u;
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);  // uniform: scalar loop control
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   const uint32_t nsegr = (P.flen + 127u) >> 7;
   const uint32_t total = nsegr * (uint32_t)P.nrec;  // host keeps this < 2^32 - 64
   const uint32_t ntiles = (total + 63u) >> 6;
   // ping-pong between two load slots A/B: a loaded register is never copied
-  // (a copy would force s_waitcnt vmcnt(0) on the prefetch)
-  uint32_t t = wave;
-  if (t >= ntiles) return;
-  SegInfo sa = fixed_map(P, t, lane, nsegr, total), sb;
+  // (a copy would force s_waitcnt vmcnt(0) on the prefetch).  The loop has one
+  // exit, at the bottom, with a precomputed trip count: a break between the
+  // halves gives the CFG a second path into the header on which the other
+  // slot's loads are still outstanding, and the wait-count merge then waits
+  // for the prefetch at the top of every iteration.
+  const uint32_t t0 = wave;
+  if (t0 >= ntiles) return;
+  const uint32_t niter = (ntiles - t0 + nwaves - 1u) / nwaves;  // tiles of this wave, >= 1
+  uint32_t t = t0;
   SegLoad A, B;
-  seg_issue<FAST>(P, sa, A);
-  for (;;) {
-    uint32_t tb = (t + nwaves < ntiles) ? t + nwaves : t;  // always issue: exact vmcnt counting
-    sb = fixed_map(P, tb, lane, nsegr, total);
-    seg_issue<FAST>(P, sb, B);
+  seg_issue<FAST, ABLATE>(P, fixed_map(P, t, lane, nsegr, total), A);
+  for (uint32_t j = 2; j <= niter; j += 2) {
+    seg_issue<FAST, ABLATE>(P, fixed_map(P, t + nwaves, lane, nsegr, total), B);
     __builtin_amdgcn_sched_barrier(0);
-    finish_tile<FAST>(smem, P, sa, A, lane, lo, hi);
-    t += nwaves;
-    if (t >= ntiles) break;
-    uint32_t ta = (t + nwaves < ntiles) ? t + nwaves : t;
-    sa = fixed_map(P, ta, lane, nsegr, total);
-    seg_issue<FAST>(P, sa, A);
+    finish_tile<FAST, CHAINS, ABLATE, PERCOL>(smem, P, A, lane, lo, hi);
+    const uint32_t ta = (t + 2u * nwaves < ntiles) ? t + 2u * nwaves : t;  // past the end: reload, unused
+    seg_issue<FAST, ABLATE>(P, fixed_map(P, ta, lane, nsegr, total), A);
     __builtin_amdgcn_sched_barrier(0);
-    finish_tile<FAST>(smem, P, sb, B, lane, lo, hi);
-    t += nwaves;
-    if (t >= ntiles) break;
+    finish_tile<FAST, CHAINS, ABLATE, PERCOL>(smem, P, B, lane, lo, hi);
+    t += 2u * nwaves;
   }
+  if (niter & 1u) finish_tile<FAST, CHAINS, ABLATE, PERCOL>(smem, P, A, lane, lo, hi);
 }
 
 // ---------------------------------------------------------------------------
-// Descriptor records (offset u64, len u32), arbitrary alignment.
-// Prep: seg_start[r] = exclusive prefix of nseg(r) = ceil(len/128);
-//       tile_first[t] = record holding segment 64t.
-__device__ __forceinline__ SegInfo desc_map(const CrcParams& P, int* R, uint32_t t, uint32_t lane, uint32_t total) {
-  const uint32_t g = t * 64u + lane;
-  const uint32_t r0 = P.tile_first[t];
-  // lane -> record: the largest r with seg_start[r] <= g (empty records own nothing)
-  R[lane] = -1;
-  __builtin_amdgcn_wave_barrier();
-  uint64_t chunk = 0;
-  for (;;) {
-    uint64_t r = (uint64_t)r0 + chunk + lane;
-    uint32_t ss = r < P.nrec ? P.seg_start[r] : 0xFFFFFFFFu;
-    int64_t st = (int64_t)ss - (int64_t)t * 64;
-    if (ss != 0xFFFFFFFFu && st < 64) atomicMax(&R[st < 0 ? 0 : (int)st], (int)(chunk + lane));
-    // continue while the 64th record of this chunk still starts inside the tile
-    uint32_t last_ss = __shfl(ss, 63, 64);
-    chunk += 64;
-    if (last_ss == 0xFFFFFFFFu || (int64_t)last_ss - (int64_t)t * 64 >= 64) break;
-  }
-  __builtin_amdgcn_wave_barrier();
-  int mine = R[lane];
-  uint64_t starts = __ballot(mine >= 0);
-  uint64_t below = starts & ((lane == 63) ? ~0ull : ((2ull << lane) - 1ull));
-  uint32_t p = 63u - (uint32_t)__builtin_clzll(below | 1ull);
-  int jrec = __shfl(mine, (int)p, 64);
-  __builtin_amdgcn_wave_barrier();
+// Descriptor records (offset u64, len u32), arbitrary alignment and order.
+// Prep (scan kernels below): every record owns nseg = max(1, ceil(len/128))
+// consecutive segments (an empty record owns one empty segment, so every
+// record has a start lane); seg_start[r] = exclusive prefix of nseg; per
+// 64-segment tile, tile_info[t] = {r0 = record holding segment 64t,
+// q0 = its segment index there, 64-bit mask of record starts in the tile}.
+// A wave maps its lanes from that one 16-byte record (a scalar load):
+//   rec = r0 + (record starts at positions 1..lane)
+//   q   = lane - (last start <= lane), or q0 + lane if none.
+// stage 0 (three tiles ahead): the tile's 16-byte record.  A vector load
+// (lane l holds dword l&3), not a scalar one: it then retires in order with
+// the payload loads (vmcnt), while an s_load would share lgkmcnt with the LDS
+// lookups and force lgkmcnt(0) waits in the checksum loop.  Tiles outside
+// [0, ntiles) read a clamped entry (their lanes are all pad lanes).
+__device__ __forceinline__ uint32_t desc_tile(const CrcParams& P, int32_t x, int32_t nt, uint32_t lane) {
+  const int32_t c = x < 0 ? 0 : (x < nt ? x : nt - 1);
+  return P.tile_info[4ull * (uint32_t)c + (lane & 3u)];
+}
+
+// stage 1 (two tiles ahead): lane -> (rec, q); issues the off/len gathers
+__device__ __forceinline__ SegInfo desc_map_issue(const CrcParams& P, uint32_t tv, int32_t x, uint32_t lane,
+                                                  uint32_t total) {
+  // (readlane returns int: go through uint32_t, a direct widening would sign-extend)
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane(tv, 0), q0 = (uint32_t)__builtin_amdgcn_readlane(tv, 1);
+  const uint32_t mlo = (uint32_t)__builtin_amdgcn_readlane(tv, 2), mhi = (uint32_t)__builtin_amdgcn_readlane(tv, 3);
+  const uint64_t mask = (uint64_t)mlo | ((uint64_t)mhi << 32);
+  const uint64_t below = mask & ((lane == 63u) ? ~0ull : ((2ull << lane) - 1ull));
+  const uint32_t cnt = (uint32_t)__builtin_popcountll(below & ~1ull);
   SegInfo si;
-  si.valid = g < total;
-  si.rec = r0 + (uint32_t)(jrec < 0 ? 0 : jrec);
-  uint32_t rs = P.seg_start[si.rec];
-  si.rec_off = P.off[si.rec];
-  si.rec_len = P.len[si.rec];
-  uint32_t nseg = (si.rec_len + 127u) >> 7;
-  si.q = g - rs;
-  si.k = nseg - 1u - si.q;
-  if (!si.valid) {  // pad lanes: a harmless full segment of the last record (result discarded)
-    si.q = 1;
-    si.k = 0;
-    si.rec_len = si.rec_len < 128u ? 128u : si.rec_len;
-  }
+  si.valid = (x >= 0) & ((uint32_t)x * 64u + lane < total);
+  uint32_t rec = r0 + cnt;
+  rec = (si.valid && rec < P.nrec) ? rec : (uint32_t)P.nrec - 1u;
+  si.q = below ? lane - (63u - (uint32_t)__builtin_clzll(below)) : q0 + lane;
+  si.rec = rec;
+  si.rec_off = P.off[rec];
+  si.rec_len = P.len[rec];
+  si.k = 0;
   return si;
 }
 
-__global__ __launch_bounds__(1024) void crc32_desc_kernel(CrcParams P) {
+// stage 2 (one tile ahead, once the gathers have landed): segments after this one
+__device__ __forceinline__ void desc_map_complete(SegInfo& si) {
+  const uint32_t nseg = si.rec_len ? (si.rec_len + 127u) >> 7 : 1u;
+  si.k = nseg - 1u - si.q;
+  if (!si.valid) {  // pad lanes: an empty first segment (loads only the zero buffer; no store)
+    si.q = 0;
+    si.k = 0;
+    si.rec_len = 0;
+  }
+}
+
+// Three-stage software pipeline per wave (tile stride n = nwaves):
+//   tile_info(c+3n) | off/len gathers(c+2n) | payload loads(c+n) | checksum(c)
+// Each wait is for loads issued one half-iteration earlier, which are older
+// than the payload of tile c+n (vmcnt retires in order), so no dependent
+// gather round trip is exposed.  Unrolled 2x so that every stage alternates
+// between two register sets and no in-flight register is copied.  There is
+// no prologue and no skipped stage: the loop starts three tiles early on
+// virtual tiles (all pad lanes: zero-buffer loads, checksum computed and
+// dropped), so the loop header is only ever entered with the same loads in
+// flight in the same order -- a differently scheduled prologue, or a branch
+// around a stage, makes the wait-count merge at the header conservative.
+template <int CHAINS, int ABLATE = 0, int BLOCK = 1024>
+__global__ __launch_bounds__(BLOCK) void crc32_desc_kernel(CrcParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  build_lds_tables(smem, P.master);
+  build_lds_tables(smem, P.master, P.khi);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t lo = (lane & 31u) * 4u, hi = lo | 0x10000u;
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-  int* R = (int*)(smem + LDS_TABLE_BYTES + (threadIdx.x >> 6) * WAVE_SCRATCH_BYTES);
+  const int32_t wave = (int32_t)__builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int32_t n = (int32_t)((gridDim.x * blockDim.x) >> 6);
   const uint32_t total = *P.total_segs;
-  const uint32_t ntiles = (total + 63u) >> 6;
-  uint32_t t = wave;
-  if (t >= ntiles) return;
-  SegInfo sa = desc_map(P, R, t, lane, total), sb;
+  const int32_t nt = (int32_t)((total + 63u) >> 6);  // < 2^26
+  if (wave >= nt) return;
+  uint32_t T0 = 0, T1 = 0;  // virtual tiles: no loads needed, all lanes pad
+  SegInfo M0, M1;
+  M0.valid = M1.valid = false;
+  M0.q = M1.q = 0;
+  M0.rec = M1.rec = 0;
+  M0.rec_off = M1.rec_off = 0;
+  M0.rec_len = M1.rec_len = 0;
+  M0.k = M1.k = 0;
   SegLoad A, B;
-  seg_issue<false>(P, sa, A);
-  for (;;) {
-    uint32_t tb = (t + nwaves < ntiles) ? t + nwaves : t;
-    sb = desc_map(P, R, tb, lane, total);
-    seg_issue<false>(P, sb, B);
+  A.fl = 0;  // first virtual tile: no valid lane, nothing stored
+  A.k = 0;
+  A.rec = 0;
+  // half-steps: 3 virtual + the wave's real tiles; one bottom exit (see the
+  // fixed kernel), the odd last half-step after the loop only checksums
+  const int32_t H = 3 + (nt - wave + n - 1) / n;
+  int32_t c = wave - 3 * n;
+  for (int32_t j = 2; j <= H; j += 2) {
+    // in flight: A = payload(c), M1 = gathers(c+n), T0 = tile_info(c+2n)
+    M0 = desc_map_issue(P, T0, c + 2 * n, lane, total);
+    T1 = desc_tile(P, c + 3 * n, nt, lane);
+    desc_map_complete(M1);
+    seg_issue<false, ABLATE>(P, M1, B);
     __builtin_amdgcn_sched_barrier(0);
-    finish_tile<false>(smem, P, sa, A, lane, lo, hi);
-    t += nwaves;
-    if (t >= ntiles) break;
-    uint32_t ta = (t + nwaves < ntiles) ? t + nwaves : t;
-    sa = desc_map(P, R, ta, lane, total);
-    seg_issue<false>(P, sa, A);
+    finish_tile<false, CHAINS, ABLATE>(smem, P, A, lane, lo, hi);  // virtual tiles: pad lanes, no store
+    c += n;
+    // in flight: B = payload(c), M0 = gathers(c+n), T1 = tile_info(c+2n)
+    M1 = desc_map_issue(P, T1, c + 2 * n, lane, total);
+    T0 = desc_tile(P, c + 3 * n, nt, lane);
+    desc_map_complete(M0);
+    seg_issue<false, ABLATE>(P, M0, A);
     __builtin_amdgcn_sched_barrier(0);
-    finish_tile<false>(smem, P, sb, B, lane, lo, hi);
-    t += nwaves;
-    if (t >= ntiles) break;
+    finish_tile<false, CHAINS, ABLATE>(smem, P, B, lane, lo, hi);
+    c += n;
   }
+  if (H & 1) finish_tile<false, CHAINS, ABLATE>(smem, P, A, lane, lo, hi);
 }
 
 // ---------------------------------------------------------------------------
@@ -383,9 +561,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_phase1(const uint32_t* __rest
 #pragma unroll
   for (int i = 0; i < SCAN_ITEMS; ++i) {
     uint64_t r = base + i;
-    uint32_t l = r < n ? len[r] : 0u;
+    uint32_t ns = r < n ? (len[r] ? (len[r] + 127u) >> 7 : 1u) : 0u;
     v[i] = acc;
-    acc += (l + 127u) >> 7;
+    acc += ns;
   }
   // wave inclusive scan of acc
   uint32_t lane = threadIdx.x & 63u, x = acc;
@@ -457,15 +635,45 @@ __global__ __launch_bounds__(1024) void scan_phase2(uint32_t* __restrict__ block
 __global__ __launch_bounds__(1024) void scan_phase3(const uint32_t* __restrict__ len, uint64_t n,
                                                      uint32_t* __restrict__ seg_start,
                                                      const uint32_t* __restrict__ block_sum,
-                                                     uint32_t* __restrict__ tile_first) {
-  uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
+                                                     uint32_t* __restrict__ tile_info) {
+  const uint64_t r0w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63ull;
+  if (r0w >= n) return;  // whole wave past the end (wave-uniform)
+  const uint64_t r = min((uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n - 1);  // tail lanes repeat the last record
   uint32_t ss = seg_start[r] + block_sum[r / (SCAN_BLOCK * SCAN_ITEMS)];
-  seg_start[r] = ss;
-  uint32_t ns = (len[r] + 127u) >> 7;
-  if (ns == 0) return;
+  const bool own = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) < n;
+  if (own) seg_start[r] = ss;
+  uint32_t ns = len[r] ? (len[r] + 127u) >> 7 : 1u;
+  // record r starts at segment ss: OR its bit into the tile's start mask.
+  // Records are consecutive lanes and ss is non-decreasing, so records of one
+  // tile are a run of lanes: OR the run in registers, one store per run; only
+  // the runs touching the wave's first or last lane can share their tile with
+  // another wave and use atomicOr (tile_info is zeroed before this kernel).
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t T = ss >> 6;
+  unsigned long long bits = 1ull << (ss & 63u);
+  const uint32_t nvalid = (uint32_t)min((uint64_t)64, n - r0w);  // valid lanes in this wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    unsigned long long o = __shfl_down(bits, d, 64);
+    uint32_t oT = __shfl_down(T, d, 64);
+    if (lane + d < nvalid && oT == T) bits |= o;
+  }
+  const uint32_t prevT = __shfl_up(T, 1, 64);
+  const uint32_t firstT = __shfl(T, 0, 64), lastT = __shfl(T, (int)nvalid - 1, 64);
+  if (lane == 0 || prevT != T) {
+    unsigned long long* m = (unsigned long long*)(tile_info + 4ull * T + 2);
+    if (T == firstT || T == lastT)
+      atomicOr(m, bits);
+    else
+      *m = bits;
+  }
+  // tiles whose first segment lies in this record: r0 = r, q0 = 64t - ss
+  if (!own) return;
   uint32_t t0 = (ss + 63u) >> 6, t1 = (ss + ns - 1u) >> 6;
-  for (uint32_t t = t0; t <= t1; ++t) tile_first[t] = (uint32_t)r;
+  for (uint32_t t = t0; t <= t1; ++t) {
+    tile_info[4ull * t + 0] = (uint32_t)r;
+    tile_info[4ull * t + 1] = t * 64u - ss;
+  }
 }
 
 }  // namespace lsmck
@@ -475,18 +683,40 @@ __global__ __launch_bounds__(1024) void scan_phase3(const uint32_t* __restrict__
 using namespace lsmck;
 
 
-extern "C" int lsmk_launch_crc32_fixed(const CrcParams* P, int ncu, hipStream_t st) {
-  size_t lds = LDS_TABLE_BYTES;
-  bool fast = ((uintptr_t)P->base % 4 == 0) && (P->stride % 4 == 0) && (P->flen % 128 == 0);
-  const void* fn = fast ? (const void*)crc32_fixed_kernel<true> : (const void*)crc32_fixed_kernel<false>;
-  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
+static int launch_fixed(const CrcParams* P, int ncu, hipStream_t st) {
+  size_t lds = LDS_SCRATCH_OFF;
+  hipError_t e = hipFuncSetAttribute((const void*)crc32_fixed_kernel<FAST, CHAINS, ABLATE, PERCOL>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return -(int)e;
-  if (fast)
-    hipLaunchKernelGGL((crc32_fixed_kernel<true>), dim3(ncu), dim3(1024), lds, st, *P);
-  else
-    hipLaunchKernelGGL((crc32_fixed_kernel<false>), dim3(ncu), dim3(1024), lds, st, *P);
+  hipLaunchKernelGGL((crc32_fixed_kernel<FAST, CHAINS, ABLATE, PERCOL>), dim3(ncu), dim3(1024), lds, st, *P);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
+}
+
+// variant: number of independent CRC chains per lane (1, 2, 4); 0 = default
+extern "C" int lsmk_launch_crc32_fixed(const CrcParams* P, int ncu, int variant, hipStream_t st) {
+  bool fast = ((uintptr_t)P->base % 4 == 0) && (P->stride % 4 == 0) && (P->flen % 128 == 0);
+  int ch = (variant & 0xF) ? (variant & 0xF) : LSMCK_DEFAULT_CHAINS;
+  int ablate = variant >> 8;  // diagnostic ablations (results invalid): 1 loads only, 2 compute only
+  if (fast && ablate == 1) return launch_fixed<true, 2, 1>(P, ncu, st);
+  if (fast && ablate == 2) return launch_fixed<true, 2, 2>(P, ncu, st);
+  // per-lane shift columns when every tile starts on a record boundary (and k < 2^16)
+  const uint32_t nsegr = (P->flen + 127u) >> 7;
+  const bool percol = (64u % nsegr) == 0 && !(variant & 0x10);  // 0x10: force the generic multiply (A/B)
+  if (fast && percol) {
+    if (ch == 1) return launch_fixed<true, 1, 0, true>(P, ncu, st);
+    if (ch == 2) return launch_fixed<true, 2, 0, true>(P, ncu, st);
+    return launch_fixed<true, 4, 0, true>(P, ncu, st);
+  }
+  if (fast) {
+    if (ch == 1) return launch_fixed<true, 1>(P, ncu, st);
+    if (ch == 2) return launch_fixed<true, 2>(P, ncu, st);
+    return launch_fixed<true, 4>(P, ncu, st);
+  }
+  if (ch == 1) return launch_fixed<false, 1>(P, ncu, st);
+  if (ch == 2) return launch_fixed<false, 2>(P, ncu, st);
+  return launch_fixed<false, 4>(P, ncu, st);
 }
 
 extern "C" uint64_t lsmk_scan_block_count(uint64_t n) {
@@ -504,16 +734,32 @@ extern "C" int lsmk_launch_crc32_scan(const CrcParams* P, uint32_t* block_sum, h
   return e == hipSuccess ? 0 : -(int)e;
 }
 
-// phase 3 (+tile_first) and the checksum kernel; tile_first must hold
-// ceil(total/64) entries
-extern "C" int lsmk_launch_crc32_desc(const CrcParams* P, const uint32_t* block_sum, int ncu, hipStream_t st) {
+// phase 3 (+tile_info) and the checksum kernel; tile_info must hold
+// ceil(total/64) zeroed 16-byte entries
+extern "C" int lsmk_launch_crc32_desc(const CrcParams* P, const uint32_t* block_sum, int ncu, int variant,
+                                      hipStream_t st) {
   uint64_t n = P->nrec;
   hipLaunchKernelGGL(scan_phase3, dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0, st, P->len, n, P->seg_start,
-                     block_sum, P->tile_first);
-  size_t lds = LDS_TABLE_BYTES + 16 * WAVE_SCRATCH_BYTES;
-  hipError_t e = hipFuncSetAttribute((const void*)crc32_desc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                     block_sum, P->tile_info);
+  size_t lds = LDS_SCRATCH_OFF;
+  int ch = (variant & 0xF) ? (variant & 0xF) : LSMCK_DEFAULT_DESC_CHAINS;
+  int ablate = variant >> 8;
+  // 0x20: 12-wave workgroups (168 VGPRs per lane instead of 128)
+  const bool w12 = (variant & 0x20) != 0;
+  const int block = w12 ? 768 : 1024;
+  const void* fn = w12 ? (ablate == 1 ? (const void*)crc32_desc_kernel<1, 1, 768>
+                          : ablate == 2 ? (const void*)crc32_desc_kernel<1, 2, 768>
+                          : ch == 1 ? (const void*)crc32_desc_kernel<1, 0, 768>
+                          : ch == 2 ? (const void*)crc32_desc_kernel<2, 0, 768> : (const void*)crc32_desc_kernel<4, 0, 768>)
+                       : (ablate == 1 ? (const void*)crc32_desc_kernel<1, 1>
+                          : ablate == 2 ? (const void*)crc32_desc_kernel<1, 2>
+                          : ch == 1 ? (const void*)crc32_desc_kernel<1>
+                          : ch == 2 ? (const void*)crc32_desc_kernel<2> : (const void*)crc32_desc_kernel<4>);
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return -(int)e;
-  hipLaunchKernelGGL(crc32_desc_kernel, dim3(ncu), dim3(1024), lds, st, *P);
+  void* args[] = {(void*)P};
+  e = hipLaunchKernel(fn, dim3(ncu), dim3(block), args, lds, st);
+  if (e != hipSuccess) return -(int)e;
   e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
 }

@@ -80,6 +80,9 @@ class Context:
         except Exception:
             pass
 
+    def set_option(self, key, value):
+        _lib.check(self.lib.lsmck_ctx_set_option(self.handle, key.encode(), int(value)), f"set_option({key})")
+
     # --- memory -------------------------------------------------------------
     def alloc(self, nbytes):
         return DeviceBuffer(self, nbytes)

@@ -157,3 +157,68 @@ def test_config2_full_size_properties(ctx):
         assert a[i] == O.crc32(O.gen_stream(0x5EED0002, int(i) * 4096, 4096)), i
     for buf in (d, out_f, d_o, d_l, out_d):
         buf.free()
+
+
+@pytest.mark.parametrize("chains,generic", [(1, 0), (2, 0), (4, 0), (2, 1)])
+def test_kernel_variants_agree(ctx, chains, generic):
+    """Every CRC-chain variant (lsmck_ctx_set_option "crc_chains") is bit-exact."""
+    rng = np.random.default_rng(100 + chains)
+    n = 6000
+    ln = rng.integers(0, 9000, n).astype(np.uint32)
+    ln[:5] = [0, 1, 3, 128, 129]
+    off, total = _packed(ln, gap_rng=rng, align_shift=2)
+    data = O.gen_stream(40 + chains, 0, total + 8)
+    ctx.set_option("crc_chains", chains)
+    ctx.set_option("crc_generic_mul", generic)
+    try:
+        got = ctx.crc32(data, off, ln)
+        fixed = ctx.crc32_fixed(data, 4096, 4096, total // 4096)
+        small = ctx.crc32_fixed(data, 256, 256, total // 256)
+        odd = ctx.crc32_fixed(data[1:], 300, 297, (total - 8) // 300)
+    finally:
+        ctx.set_option("crc_chains", 0)
+        ctx.set_option("crc_generic_mul", 0)
+    assert np.array_equal(small, O.crc32_fixed(data, 256, 256, total // 256, threads=8))
+    assert np.array_equal(got, O.crc32_batch(data, off, ln, threads=8))
+    assert np.array_equal(fixed, O.crc32_fixed(data, 4096, 4096, total // 4096, threads=8))
+    assert np.array_equal(odd, O.crc32_fixed(data[1:], 300, 297, (total - 8) // 300, threads=8))
+
+
+def _device_crc(ctx, data, off, ln):
+    d_b, d_o, d_l, d_out = ctx.alloc(len(data)), ctx.alloc(off.nbytes), ctx.alloc(ln.nbytes), ctx.alloc(4 * len(off))
+    d_b.upload(data)
+    d_o.upload(off)
+    d_l.upload(ln)
+    ctx.crc32_device(d_b.ptr, d_o.ptr, d_l.ptr, len(off), d_out.ptr)
+    ctx.sync()
+    return d_out.download(np.uint32)
+
+
+def test_desc_records_just_after_page_boundary(ctx):
+    """Record starts 0..15 bytes after a 4 KiB boundary of a (page-aligned) device
+    buffer, every first-segment length: the group holding the record's first
+    dword straddles the boundary, so it is loaded from the 16-byte aligned block
+    at the boundary and shifted into place (seg_issue "risky" lanes)."""
+    data = O.gen_stream(0x5EED0010, 0, 1 << 20)
+    pages = np.arange(1, 200, dtype=np.uint64)
+    d = np.arange(0, 16, dtype=np.uint64)
+    lens = np.array([1, 2, 3, 4, 5, 7, 8, 12, 13, 16, 17, 100, 115, 116, 117, 127, 128, 129, 131, 140,
+                     244, 255, 256, 257, 1000], dtype=np.uint32)
+    P, D, L = np.meshgrid(pages, d, lens, indexing="ij")
+    off = (P * 4096 + D).ravel().astype(np.uint64)
+    ln = L.ravel().astype(np.uint32)
+    got = _device_crc(ctx, data, off, ln)
+    want = O.crc32_batch(data, off, ln, threads=8)
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, (bad[:10], off[bad[:10]], ln[bad[:10]])
+
+
+def test_desc_records_at_allocation_edges(ctx):
+    """Short records at offset 0 and flush with the end of the allocation
+    (pad lanes of the last tile read nothing beyond the last record)."""
+    n = 8192 + 37
+    data = O.gen_stream(0x5EED0011, 0, n)
+    for L in (1, 3, 5, 64, 127, 128, 129, 300):
+        off = np.array([0, n - L, 1, n - L - 1], dtype=np.uint64)
+        ln = np.full(4, L, dtype=np.uint32)
+        assert np.array_equal(_device_crc(ctx, data, off, ln), O.crc32_batch(data, off, ln)), L
