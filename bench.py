@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--cpu-sample-records", type=int, default=0)
     ap.add_argument("--variants", default="", help="comma list of crc_chains values to A/B in interleaved rounds")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--desc", action="store_true",
+                    help="diagnostic: config 2's fixed blocks through the descriptor entry point")
+    ap.add_argument("--pack-align", type=int, default=1,
+                    help="diagnostic: config 3 record offsets rounded up to this many bytes")
     return ap.parse_args()
 
 
@@ -95,16 +99,24 @@ def main():
         nrec = a.blocks_per_gpu or (1 << 26)
         lens = gen_zipf_lengths(seed + rank, nrec)
         offs = np.zeros(nrec, dtype=np.uint64)
-        np.cumsum(lens[:-1], out=offs[1:])
+        A = max(1, a.pack_align)
+        slot = ((lens.astype(np.uint64) + (A - 1)) // A) * A  # A = 1: packed back to back
+        np.cumsum(slot[:-1], out=offs[1:])
         nbytes = int(offs[-1]) + int(lens[-1])
         byte_off = 0
         workload = (f"config3: {nrec} mixed-length records per GPU (64 B-64 KiB, Zipf s=1.5, packed, unaligned; "
                     f"{nbytes / GIB:.1f} GiB), device-resident")
+        if A > 1:
+            workload += f" [diagnostic: offsets aligned to {A} B]"
 
     data = ctx.alloc(nbytes + 64)
     ctx.gen_stream(data.ptr, seed, byte_off, nbytes, sptr)
     out = ctx.alloc(4 * nrec)
-    if cfg == 3:
+    if cfg != 3 and a.desc:  # diagnostic: the same fixed blocks as descriptors
+        offs = np.arange(nrec, dtype=np.uint64) * np.uint64(rec_len)
+        lens = np.full(nrec, rec_len, dtype=np.uint32)
+        workload += " [diagnostic: descriptor entry point]"
+    if cfg == 3 or a.desc:
         d_off, d_len = ctx.alloc(8 * nrec), ctx.alloc(4 * nrec)
         d_off.upload(offs)
         d_len.upload(lens)
@@ -216,7 +228,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "crc32_fixed_kernel" if cfg != 3 else "crc32_desc_kernel",
+            "kernel": "crc32_desc_kernel" if (cfg == 3 or a.desc) else "crc32_fixed_kernel",
             "algorithmic_bytes_per_launch": algo_bytes,
             "launch_ms_hip_events": round(ev_ms, 4),
         },

@@ -135,7 +135,8 @@ int lsmck_device_count(void);
  *                 per-lane precomputed columns (A/B switch); 0 = default.
  *   "crc_ablate"  DIAGNOSTIC ONLY, results are invalid while set: 1 = the fixed
  *                 kernel loads but does not checksum, 2 = checksums without
- *                 loading; 0 = off.  Locates the kernel's ceiling.
+ *                 loading, 3 = payload loads only (no table gathers, no
+ *                 reduction or store); 0 = off.  Locates the kernel's ceiling.
  *   "crc_wg_waves"  waves per workgroup of the descriptor CRC kernel: 12 or 16
  *                 (0 = built-in default).  A/B switch: 12 waves leave 168 VGPRs
  *                 per lane for the three-stage load pipeline, 16 leave 128.

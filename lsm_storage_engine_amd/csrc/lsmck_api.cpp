@@ -81,15 +81,12 @@ int ensure_pinned(T** p, size_t* cap, size_t need) {
 
 // Scratch of the descriptor CRC path (one per in-flight launch).
 struct DescScratch {
-  uint32_t* seg_start = nullptr;
-  size_t cap_seg = 0;
-  uint32_t* block_sum = nullptr;
+  uint64_t* block_sum = nullptr;  // per 1024-record block
   size_t cap_bs = 0;
   uint32_t* tile_info = nullptr;  // 4 u32 per tile
   size_t cap_tf = 0;
-  uint32_t* total = nullptr;  // device, 1 u32
+  uint64_t* total = nullptr;  // device, 1 u64
   void release() {
-    if (seg_start) (void)hipFree(seg_start);
     if (block_sum) (void)hipFree(block_sum);
     if (tile_info) (void)hipFree(tile_info);
     if (total) (void)hipFree(total);
@@ -153,7 +150,7 @@ struct lsmck_ctx {
   std::mutex mu;
   DescScratch scratch;           // device-mode descriptor scratch
   hipEvent_t scratch_ev = nullptr;
-  uint32_t* h_total = nullptr;   // pinned
+  uint64_t* h_total = nullptr;   // pinned
   unsigned long long* d_verify = nullptr;  // [n_bad, first_bad]
   unsigned long long* h_verify = nullptr;  // pinned
   Stage stage[2];
@@ -176,9 +173,8 @@ struct DevGuard {
 
 hipStream_t pick_stream(lsmck_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream0; }
 
-int ensure_scratch(DescScratch& sc, size_t nrec, size_t nblocks) {
+int ensure_scratch(DescScratch& sc, size_t nblocks) {
   int rc;
-  if ((rc = ensure_dev(&sc.seg_start, &sc.cap_seg, nrec))) return rc;
   if ((rc = ensure_dev(&sc.block_sum, &sc.cap_bs, nblocks))) return rc;
   if (!sc.total) HIPCHK(hipMalloc((void**)&sc.total, 16));
   return 0;
@@ -224,11 +220,11 @@ int crc_fixed_device(lsmck_ctx* ctx, const uint8_t* base, size_t stride, uint32_
 // Descriptor CRC on device pointers with known (host) total segment count
 // (host staging path) or unknown (device path: read back after the scan).
 int crc_desc_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const uint64_t* off, const uint32_t* len,
-                    size_t n, uint32_t* out, hipStream_t st, int64_t known_total, uint32_t* h_total) {
+                    size_t n, uint32_t* out, hipStream_t st, int64_t known_total, uint64_t* h_total) {
   if (n == 0) return 0;
   if (n >= (1ull << 32)) return lsmck_host::set_error(LSMCK_EINVAL, "more than 2^32-1 records in one batch");
   size_t nb = (size_t)lsmk_scan_block_count(n);
-  int rc = ensure_scratch(sc, n, nb);
+  int rc = ensure_scratch(sc, nb);
   if (rc) return rc;
   HIPCHK(hipMemsetAsync(out, 0, n * 4, st));
   CrcParams P{};
@@ -236,7 +232,6 @@ int crc_desc_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const 
   P.off = off;
   P.len = len;
   P.nrec = n;
-  P.seg_start = sc.seg_start;
   P.total_segs = sc.total;
   P.out = out;
   fill_tables(ctx, &P);
@@ -246,7 +241,7 @@ int crc_desc_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const 
   if (known_total >= 0) {
     total = (uint64_t)known_total;
   } else {
-    HIPCHK(hipMemcpyAsync(h_total, sc.total, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h_total, sc.total, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     total = *h_total;
   }
@@ -507,7 +502,7 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     return 0;
   }
   if (!strcmp(key, "crc_ablate")) {  // diagnostic only: timing ablations, results are garbage
-    if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0, 1 or 2");
+    if (value < 0 || value > 3) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0..3");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->variant = (ctx->variant & 0xFF) | ((int)value << 8);
     return 0;

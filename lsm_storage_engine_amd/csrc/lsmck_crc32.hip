@@ -184,8 +184,13 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
   L.k = si.k;
   const uint32_t flv = (si.valid ? FL_VALID : 0u) | (si.q == 0 ? FL_FIRST : 0u);
   L.fl = flv;
-  L.K = P.kseg[si.k & 0xFFFFu];
-  L.TI = P.tinit[(si.q == 0) ? seglen : 129u];  // unconditional load (tinit[129] = 0): no branch in the issue block
+  if (ABLATE == 3) {  // diagnostic: payload loads only (no table gathers)
+    L.K = si.k;
+    L.TI = seglen;
+  } else {
+    L.K = P.kseg[si.k & 0xFFFFu];
+    L.TI = P.tinit[(si.q == 0) ? seglen : 129u];  // unconditional load (tinit[129] = 0): no branch in the issue block
+  }
   // pointer arithmetic on the kernel-argument pointer keeps these global_load (not flat_load)
   const unsigned char* s0 = P.base + (E - 128);
   if (ABLATE == 2) {  // diagnostic: no payload loads (compute-only timing; results invalid)
@@ -207,7 +212,12 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
   }
   // General path, straight-line (no divergent branches: a branch merge here
   // makes hipcc wait for the loads and the prefetch is lost).
-  //  - groups entirely in front of B's dword read a 64-byte zero buffer;
+  //  - groups entirely in front of B's dword are loaded from the 16-byte
+  //    aligned block holding the record's last byte (a safe address of this
+  //    lane's own lines) and zeroed in seg_finish.  A shared zero buffer would
+  //    be simpler, but lanes of one load instruction hitting one address cost
+  //    ~25% of the load path (tools/microbench_loads.hip); only empty
+  //    segments (empty records, pad lanes) still read it;
   //  - the group holding B's dword is loaded whole: its bytes in front of B
   //    (<= 12) are zeroed in seg_finish.  They are on B's page unless a page
   //    boundary lies between the group start and B's dword ("risky", rare):
@@ -224,20 +234,22 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
   // bitwise &, not &&: a short-circuit branch here would merge wait states (see above)
   const bool risky = ((lo_i & 3u) != 0u) & ((b4 & ~(uintptr_t)4095) > (uintptr_t)p + 16u * gb);
   L.fl = flv | sh | (bstart << 2) | (risky ? FL_RISKY : 0u) | ((uint32_t)(((uintptr_t)p >> 2) & 3u) << 13);
-  const unsigned char* zero = (const unsigned char*)P.zero;
   const unsigned char* pb16 = P.base + ((E - 128) - sh + 4u * lo_i) - (b4 & 15u);  // floor16(B's dword)
+  const unsigned char* last = P.base + (E - 1) - (((uintptr_t)P.base + (E - 1)) & 15u);  // floor16(E-1)
+  const unsigned char* filler = (lead < 128u) ? last : (const unsigned char*)P.zero;   // empty: zero buffer
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
     const bool skip = 4u * g + 3u < lo_i;
     const bool rk = ((uint32_t)g == gb) & risky;
-    u32x4 v = ld128(rk ? pb16 : (skip ? zero : p + 16 * g));
+    u32x4 v = ld128(rk ? pb16 : (skip ? filler : p + 16 * g));
     L.d[4 * g + 0] = v.x;
     L.d[4 * g + 1] = v.y;
     L.d[4 * g + 2] = v.z;
     L.d[4 * g + 3] = v.w;
   }
-  // D_32 only when the stream start is not dword aligned; an empty segment loads nothing
-  L.d[32] = ld32((sh && lead < 128u) ? p + 128 : zero);
+  // D_32 holds stream bytes only when the stream start is not dword aligned
+  // (otherwise the funnel ignores it: load any safe dword)
+  L.d[32] = ld32((sh && lead < 128u) ? p + 128 : filler);
 }
 
 // Funnel, mask, raw slicing-by-4 CRC, init term, shift to the record's end.
@@ -247,7 +259,7 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
 template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
 __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const CrcParams& P, const SegLoad& L,
                                                uint32_t lo, uint32_t hi) {
-  if (ABLATE == 1) {  // diagnostic: loads only (memory-path timing; results invalid)
+  if (ABLATE == 1 || ABLATE == 3) {  // diagnostic: loads only (memory-path timing; results invalid)
     uint32_t x = 0;
 #pragma unroll
     for (int j = 0; j < 33; ++j) x ^= L.d[j];
@@ -278,16 +290,18 @@ __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const 
       }
     }
     if (__any(bstart != 0u)) {
-      // zero the loaded bytes in front of B inside B's group
+      // zero everything in front of B: the filler groups before B's group and
+      // B's group's bytes in front of B (with lead = 0 this only clears bytes
+      // of D_0 in front of the stream start, which the funnel drops anyway)
       const uint32_t r = lo_i & 3u, gb = lo_i >> 2;
       uint32_t m[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) m[k] = ((uint32_t)k < r) ? 0u : (((uint32_t)k == r) ? bm : 0xFFFFFFFFu);
 #pragma unroll
       for (int g = 0; g < 8; ++g) {
-        const bool here = (uint32_t)g == gb;
+        const bool before = (uint32_t)g < gb, here = (uint32_t)g == gb;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) d[4 * g + k] &= here ? m[k] : 0xFFFFFFFFu;
+        for (int k = 0; k < 4; ++k) d[4 * g + k] &= before ? 0u : (here ? m[k] : 0xFFFFFFFFu);
       }
       d[32] &= (lo_i == 32u) ? bm : 0xFFFFFFFFu;
     }
@@ -348,14 +362,29 @@ __device__ __forceinline__ void build_lds_cols(const CrcParams& P, uint32_t nseg
 }
 
 // ---------------------------------------------------------------------------
-// Segmented XOR over a wave: each lane ends with the XOR of lanes [lane, run_end].
-__device__ __forceinline__ uint32_t seg_suffix_xor(uint32_t v, uint32_t lane, uint32_t run_end) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t o = __shfl_down(v, d, 64);
-    v ^= (lane + d <= run_end) ? o : 0u;
-  }
-  return v;
+// Segmented XOR over a wave, for record heads: XOR of lanes [lane, run_end]
+// = X[run_end] ^ X[lane-1] with X the inclusive prefix XOR of the wave.  The
+// prefix runs on the VALU through DPP (row_shr 1/2/4/8 inside each 16-lane
+// row, then row_bcast 15/31 across rows); only the gather of X[run_end] uses
+// the LDS crossbar (one ds_bpermute instead of six shuffles): the LDS pipe is
+// the checksum's bottleneck, the VALU has room.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {  // lanes without a source (or masked rows) read 0
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW_MASK, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_prefix_xor(uint32_t x) {
+  x ^= dpp0<0x111, 0xF>(x);  // row_shr:1
+  x ^= dpp0<0x112, 0xF>(x);  // row_shr:2
+  x ^= dpp0<0x114, 0xF>(x);  // row_shr:4
+  x ^= dpp0<0x118, 0xF>(x);  // row_shr:8
+  x ^= dpp0<0x142, 0xA>(x);  // row_bcast:15 -> rows 1, 3
+  x ^= dpp0<0x143, 0xC>(x);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+__device__ __forceinline__ uint32_t run_xor(uint32_t v, uint32_t run_end) {
+  const uint32_t X = wave_prefix_xor(v);
+  const uint32_t Xe = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(run_end << 2), (int)X);
+  return Xe ^ dpp0<0x138, 0xF>(X);  // wave_shr:1 -> X[lane-1], 0 for lane 0
 }
 
 __device__ __forceinline__ void emit_record(const CrcParams& P, uint32_t v, const SegLoad& L, uint32_t lane,
@@ -373,9 +402,12 @@ template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
 __device__ __forceinline__ void finish_tile(const unsigned char* smem, const CrcParams& P, const SegLoad& L,
                                             uint32_t lane, uint32_t lo, uint32_t hi) {
   uint32_t v = seg_finish<FAST, CHAINS, ABLATE, PERCOL>(smem, P, L, lo, hi);
+  if (ABLATE == 3) {  // no reduction, no store (unless a magic value: keeps the loads alive)
+    if (v == 0x9E3779B1u) P.out[0] = v;
+    return;
+  }
   v = (L.fl & FL_VALID) ? v : 0u;
-  uint32_t run_end = min(63u, lane + L.k);
-  v = seg_suffix_xor(v, lane, run_end);
+  v = run_xor(v, min(63u, lane + L.k));
   emit_record(P, v, L, lane, lane == 0 || (L.fl & FL_FIRST));
 }
 
@@ -507,7 +539,7 @@ __global__ __launch_bounds__(BLOCK) void crc32_desc_kernel(CrcParams P) {
   const uint32_t lo = (lane & 31u) * 4u, hi = lo | 0x10000u;
   const int32_t wave = (int32_t)__builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const int32_t n = (int32_t)((gridDim.x * blockDim.x) >> 6);
-  const uint32_t total = *P.total_segs;
+  const uint32_t total = (uint32_t)*P.total_segs;  // host checked < 2^32
   const int32_t nt = (int32_t)((total + 63u) >> 6);  // < 2^26
   if (wave >= nt) return;
   uint32_t T0 = 0, T1 = 0;  // virtual tiles: no loads needed, all lanes pad
@@ -548,131 +580,213 @@ __global__ __launch_bounds__(BLOCK) void crc32_desc_kernel(CrcParams P) {
 }
 
 // ---------------------------------------------------------------------------
-// Prep kernels for the descriptor path: three-phase exclusive scan of
-// nseg(r) = ceil(len/128), then tile_first.
-#define SCAN_ITEMS 4
+// Prep kernels for the descriptor path.  Every record owns
+// nseg = max(1, ceil(len/128)) consecutive segments; the checksum kernel only
+// needs tile_info (record starts per 64-segment tile), so no per-record
+// prefix array is materialised: phase 1 reduces nseg per 4096-record block,
+// phase 2 scans the block sums (u64: a batch may exceed 2^32 segments, which
+// the host rejects after reading the total), phase 3 re-reads len, rescans
+// inside its block and writes tile_info.  HBM traffic: len twice + tile_info.
+// Four records per thread (one 16-byte load): the kernels are bound by wave
+// launches and the cross-lane steps, not by bytes; scans run on DPP.
 #define SCAN_BLOCK 1024
-__global__ __launch_bounds__(SCAN_BLOCK) void scan_phase1(const uint32_t* __restrict__ len, uint64_t n,
-                                                           uint32_t* __restrict__ seg_start,
-                                                           uint32_t* __restrict__ block_sum) {
-  __shared__ uint32_t wsum[SCAN_BLOCK / 64];
-  uint64_t base = (uint64_t)blockIdx.x * SCAN_BLOCK * SCAN_ITEMS + (uint64_t)threadIdx.x * SCAN_ITEMS;
-  uint32_t v[SCAN_ITEMS], acc = 0;
+#define SCAN_ITEMS 4
+#define SCAN_RECS (SCAN_BLOCK * SCAN_ITEMS)
+__device__ __forceinline__ uint32_t rec_nseg(uint32_t len) { return len ? (len + 127u) >> 7 : 1u; }
+
+// the thread's four lengths (records >= n read as "absent": own = false)
+__device__ __forceinline__ void load_len4(const uint32_t* __restrict__ len, uint64_t n, uint64_t r0, uint32_t l[4]) {
+  if (r0 + 3 < n) {
+    u32x4 v = *(const u32x4*)(len + r0);  // dword-aligned 16-byte load
+    l[0] = v.x;
+    l[1] = v.y;
+    l[2] = v.z;
+    l[3] = v.w;
+  } else {
 #pragma unroll
-  for (int i = 0; i < SCAN_ITEMS; ++i) {
-    uint64_t r = base + i;
-    uint32_t ns = r < n ? (len[r] ? (len[r] + 127u) >> 7 : 1u) : 0u;
-    v[i] = acc;
-    acc += ns;
+    for (int j = 0; j < 4; ++j) l[j] = (r0 + j < n) ? len[r0 + j] : 0u;
   }
-  // wave inclusive scan of acc
-  uint32_t lane = threadIdx.x & 63u, x = acc;
+}
+
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ int dppv(int old, int x) {
+  return __builtin_amdgcn_update_dpp(old, x, CTRL, ROW_MASK, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_prefix_add(uint32_t x) {  // inclusive
+  x += (uint32_t)dppv<0x111, 0xF>(0, (int)x);
+  x += (uint32_t)dppv<0x112, 0xF>(0, (int)x);
+  x += (uint32_t)dppv<0x114, 0xF>(0, (int)x);
+  x += (uint32_t)dppv<0x118, 0xF>(0, (int)x);
+  x += (uint32_t)dppv<0x142, 0xA>(0, (int)x);
+  x += (uint32_t)dppv<0x143, 0xC>(0, (int)x);
+  return x;
+}
+__device__ __forceinline__ int wave_prefix_max(int x) {  // inclusive, identity -1
+  x = max(x, dppv<0x111, 0xF>(-1, x));
+  x = max(x, dppv<0x112, 0xF>(-1, x));
+  x = max(x, dppv<0x114, 0xF>(-1, x));
+  x = max(x, dppv<0x118, 0xF>(-1, x));
+  x = max(x, dppv<0x142, 0xA>(-1, x));
+  x = max(x, dppv<0x143, 0xC>(-1, x));
+  return x;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void scan_phase1(const uint32_t* __restrict__ len, uint64_t n,
+                                                           uint64_t* __restrict__ block_sum) {
+  __shared__ uint64_t wsum[SCAN_BLOCK / 64];
+  const uint64_t r0 = (uint64_t)blockIdx.x * SCAN_RECS + (uint64_t)threadIdx.x * SCAN_ITEMS;
+  uint32_t l[4];
+  load_len4(len, n, r0, l);
+  uint64_t x = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) x += (r0 + j < n) ? rec_nseg(l[j]) : 0u;
+  // a wave may hold 256 x 2^25 segments: reduce in u64
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  if ((threadIdx.x & 63u) == 0) wsum[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_BLOCK / 64; ++i) t += wsum[i];
+    block_sum[blockIdx.x] = t;
+  }
+}
+
+// single workgroup: exclusive scan of the block sums in place, total in *total.
+// Thread i owns the contiguous chunk [i*C, (i+1)*C).
+__global__ __launch_bounds__(1024) void scan_phase2(uint64_t* __restrict__ block_sum, uint32_t nblocks,
+                                                     uint64_t* __restrict__ total) {
+  __shared__ uint64_t wsum[16];
+  const uint32_t C = (nblocks + 1023u) / 1024u;
+  const uint32_t b0 = threadIdx.x * C, b1 = min(nblocks, b0 + C);
+  uint64_t mine = 0;
+  for (uint32_t b = b0; b < b1; ++b) mine += block_sum[b];
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t x = mine;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    uint32_t o = __shfl_up(x, d, 64);
+    uint64_t o = __shfl_up(x, d, 64);
     if (lane >= (uint32_t)d) x += o;
   }
-  if (lane == 63) wsum[threadIdx.x >> 6] = x;
+  if (lane == 63u) wsum[threadIdx.x >> 6] = x;
   __syncthreads();
-  if (threadIdx.x < 64) {
-    uint32_t y = threadIdx.x < SCAN_BLOCK / 64 ? wsum[threadIdx.x] : 0u;
-    uint32_t z = y;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      uint32_t o = __shfl_up(z, d, 64);
-      if (threadIdx.x >= (uint32_t)d) z += o;
+  if (threadIdx.x == 0) {
+    uint64_t acc = 0;
+    for (int i = 0; i < 16; ++i) {
+      uint64_t v = wsum[i];
+      wsum[i] = acc;
+      acc += v;
     }
-    if (threadIdx.x < SCAN_BLOCK / 64) wsum[threadIdx.x] = z - y;  // exclusive
-    if (threadIdx.x == SCAN_BLOCK / 64 - 1) block_sum[blockIdx.x] = z;
+    *total = acc;
   }
   __syncthreads();
-  uint32_t excl = x - acc + wsum[threadIdx.x >> 6];
-#pragma unroll
-  for (int i = 0; i < SCAN_ITEMS; ++i) {
-    uint64_t r = base + i;
-    if (r < n) seg_start[r] = excl + v[i];
+  uint64_t run = wsum[threadIdx.x >> 6] + x - mine;  // exclusive prefix of this chunk
+  for (uint32_t b = b0; b < b1; ++b) {
+    uint64_t v = block_sum[b];
+    block_sum[b] = run;
+    run += v;
   }
 }
 
-__global__ __launch_bounds__(1024) void scan_phase2(uint32_t* __restrict__ block_sum, uint32_t nblocks,
-                                                     uint32_t* __restrict__ total) {
-  // single workgroup: exclusive scan of block sums in place
-  __shared__ uint32_t wsum[16];
-  __shared__ uint32_t carry;
-  if (threadIdx.x == 0) carry = 0;
+// Start masks: records of one tile are a run of consecutive records (ss is
+// non-decreasing), so each run ORs its start bits into an LDS slot owned by
+// the run's first record (per wave: 256 records, 256 slots), and that record
+// stores the tile's mask: a plain store, or atomicOr for the wave's first and
+// last tile, which a neighbouring wave may share (tile_info is zeroed first).
+__global__ __launch_bounds__(SCAN_BLOCK) void scan_phase3(const uint32_t* __restrict__ len, uint64_t n,
+                                                           const uint64_t* __restrict__ block_sum,
+                                                           uint32_t* __restrict__ tile_info) {
+  __shared__ uint32_t wsum[SCAN_BLOCK / 64];
+  __shared__ unsigned long long slot[SCAN_BLOCK / 64][64 * SCAN_ITEMS];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint64_t r0 = (uint64_t)blockIdx.x * SCAN_RECS + (uint64_t)threadIdx.x * SCAN_ITEMS;
+  uint32_t l[4], ns[4], e[4];
+  load_len4(len, n, r0, l);
+  uint32_t tsum = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    ns[j] = (r0 + j < n) ? rec_nseg(l[j]) : 0u;
+    e[j] = tsum;
+    tsum += ns[j];
+  }
+  // block-exclusive prefix of the thread sums (u32: the host launches this
+  // only when the whole batch has < 2^32 segments)
+  const uint32_t x = wave_prefix_add(tsum);
+  if (lane == 63u) wsum[w] = x;
   __syncthreads();
-  for (uint32_t b0 = 0; b0 < nblocks; b0 += 1024) {
-    uint32_t i = b0 + threadIdx.x;
-    uint32_t y = i < nblocks ? block_sum[i] : 0u;
-    uint32_t lane = threadIdx.x & 63u, x = y;
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      uint32_t o = __shfl_up(x, d, 64);
-      if (lane >= (uint32_t)d) x += o;
+    for (int i = 0; i < SCAN_BLOCK / 64; ++i) {
+      uint32_t v = wsum[i];
+      wsum[i] = acc;
+      acc += v;
     }
-    if (lane == 63) wsum[threadIdx.x >> 6] = x;
-    __syncthreads();
-    if (threadIdx.x < 64) {
-      uint32_t a = threadIdx.x < 16 ? wsum[threadIdx.x] : 0u, z = a;
+  }
+  __syncthreads();
+  const uint64_t wr0 = (uint64_t)blockIdx.x * SCAN_RECS + (uint64_t)w * 64u * SCAN_ITEMS;  // wave's first record
+  if (wr0 >= n) return;  // whole wave past the end (wave-uniform, after the barriers)
+  const uint32_t base = (uint32_t)block_sum[blockIdx.x] + wsum[w] + (x - tsum);
+  uint32_t ss[4], T[4];
+  bool own[4];
 #pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        uint32_t o = __shfl_up(z, d, 64);
-        if (threadIdx.x >= (uint32_t)d) z += o;
-      }
-      if (threadIdx.x < 16) wsum[threadIdx.x] = z - a;
+  for (int j = 0; j < 4; ++j) {
+    ss[j] = base + e[j];
+    T[j] = ss[j] >> 6;
+    own[j] = r0 + j < n;
+  }
+  // run heads: a record whose tile differs from its predecessor's (record 0 of
+  // the wave always); h[j] = index in the wave of the head of j's run
+  const uint32_t prevT3 = (uint32_t)dppv<0x138, 0xF>(-1, (int)T[3]);  // wave_shr:1: lane-1's last tile
+  bool head[4];
+  head[0] = own[0] && (lane == 0 || prevT3 != T[0]);
+#pragma unroll
+  for (int j = 1; j < 4; ++j) head[j] = own[j] && T[j] != T[j - 1];
+  int lasth = -1;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) lasth = head[j] ? (int)(lane * 4u + j) : lasth;
+  const int before = dppv<0x138, 0xF>(-1, wave_prefix_max(lasth));  // last head in lanes < lane
+  int h[4];
+  int cur = before;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    cur = head[j] ? (int)(lane * 4u + j) : cur;
+    h[j] = cur;
+  }
+  unsigned long long* sl = slot[w];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (head[j]) sl[h[j]] = 0ull;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (own[j]) atomicOr(&sl[h[j]], 1ull << (ss[j] & 63u));
+  // the wave's first and last tiles (last own record: index min(255, n-1-wr0))
+  const uint32_t nown = (uint32_t)min((uint64_t)(64 * SCAN_ITEMS), n - wr0);
+  const uint32_t firstT = (uint32_t)__builtin_amdgcn_readfirstlane((int)T[0]);
+  const uint32_t ll = (nown - 1u) >> 2, lj = (nown - 1u) & 3u;
+  const uint32_t Tl = lj == 0 ? T[0] : (lj == 1 ? T[1] : (lj == 2 ? T[2] : T[3]));
+  const uint32_t lastT = (uint32_t)__builtin_amdgcn_readlane((int)Tl, (int)ll);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (head[j]) {
+      const unsigned long long m = sl[h[j]];
+      unsigned long long* gm = (unsigned long long*)(tile_info + 4ull * T[j] + 2);
+      if (T[j] == firstT || T[j] == lastT)
+        atomicOr(gm, m);
+      else
+        *gm = m;
     }
-    __syncthreads();
-    uint32_t c = carry;
-    uint32_t ex = c + wsum[threadIdx.x >> 6] + x - y;
-    if (i < nblocks) block_sum[i] = ex;
-    __syncthreads();
-    if (threadIdx.x == 1023) carry = ex + y;
-    __syncthreads();
   }
-  if (threadIdx.x == 0) *total = carry;
-}
-
-__global__ __launch_bounds__(1024) void scan_phase3(const uint32_t* __restrict__ len, uint64_t n,
-                                                     uint32_t* __restrict__ seg_start,
-                                                     const uint32_t* __restrict__ block_sum,
-                                                     uint32_t* __restrict__ tile_info) {
-  const uint64_t r0w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63ull;
-  if (r0w >= n) return;  // whole wave past the end (wave-uniform)
-  const uint64_t r = min((uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n - 1);  // tail lanes repeat the last record
-  uint32_t ss = seg_start[r] + block_sum[r / (SCAN_BLOCK * SCAN_ITEMS)];
-  const bool own = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) < n;
-  if (own) seg_start[r] = ss;
-  uint32_t ns = len[r] ? (len[r] + 127u) >> 7 : 1u;
-  // record r starts at segment ss: OR its bit into the tile's start mask.
-  // Records are consecutive lanes and ss is non-decreasing, so records of one
-  // tile are a run of lanes: OR the run in registers, one store per run; only
-  // the runs touching the wave's first or last lane can share their tile with
-  // another wave and use atomicOr (tile_info is zeroed before this kernel).
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t T = ss >> 6;
-  unsigned long long bits = 1ull << (ss & 63u);
-  const uint32_t nvalid = (uint32_t)min((uint64_t)64, n - r0w);  // valid lanes in this wave
+  // tiles whose first segment lies in record r: r0 = r, q0 = 64t - ss
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    unsigned long long o = __shfl_down(bits, d, 64);
-    uint32_t oT = __shfl_down(T, d, 64);
-    if (lane + d < nvalid && oT == T) bits |= o;
-  }
-  const uint32_t prevT = __shfl_up(T, 1, 64);
-  const uint32_t firstT = __shfl(T, 0, 64), lastT = __shfl(T, (int)nvalid - 1, 64);
-  if (lane == 0 || prevT != T) {
-    unsigned long long* m = (unsigned long long*)(tile_info + 4ull * T + 2);
-    if (T == firstT || T == lastT)
-      atomicOr(m, bits);
-    else
-      *m = bits;
-  }
-  // tiles whose first segment lies in this record: r0 = r, q0 = 64t - ss
-  if (!own) return;
-  uint32_t t0 = (ss + 63u) >> 6, t1 = (ss + ns - 1u) >> 6;
-  for (uint32_t t = t0; t <= t1; ++t) {
-    tile_info[4ull * t + 0] = (uint32_t)r;
-    tile_info[4ull * t + 1] = t * 64u - ss;
+  for (int j = 0; j < 4; ++j) {
+    if (!own[j]) continue;
+    const uint32_t t0 = (ss[j] + 63u) >> 6, t1 = (ss[j] + ns[j] - 1u) >> 6;
+    for (uint32_t t = t0; t <= t1; ++t) {
+      tile_info[4ull * t + 0] = (uint32_t)(r0 + j);
+      tile_info[4ull * t + 1] = t * 64u - ss[j];
+    }
   }
 }
 
@@ -701,6 +815,7 @@ extern "C" int lsmk_launch_crc32_fixed(const CrcParams* P, int ncu, int variant,
   int ablate = variant >> 8;  // diagnostic ablations (results invalid): 1 loads only, 2 compute only
   if (fast && ablate == 1) return launch_fixed<true, 2, 1>(P, ncu, st);
   if (fast && ablate == 2) return launch_fixed<true, 2, 2>(P, ncu, st);
+  if (fast && ablate == 3) return launch_fixed<true, 2, 3>(P, ncu, st);
   // per-lane shift columns when every tile starts on a record boundary (and k < 2^16)
   const uint32_t nsegr = (P->flen + 127u) >> 7;
   const bool percol = (64u % nsegr) == 0 && !(variant & 0x10);  // 0x10: force the generic multiply (A/B)
@@ -719,27 +834,24 @@ extern "C" int lsmk_launch_crc32_fixed(const CrcParams* P, int ncu, int variant,
   return launch_fixed<false, 4>(P, ncu, st);
 }
 
-extern "C" uint64_t lsmk_scan_block_count(uint64_t n) {
-  uint64_t per = (uint64_t)SCAN_BLOCK * SCAN_ITEMS;
-  return (n + per - 1) / per;
-}
+extern "C" uint64_t lsmk_scan_block_count(uint64_t n) { return (n + SCAN_RECS - 1) / SCAN_RECS; }
 
-// phase 1+2: seg_start (block-local) and the total segment count (device)
-extern "C" int lsmk_launch_crc32_scan(const CrcParams* P, uint32_t* block_sum, hipStream_t st) {
+// phase 1+2: block sums and the total segment count (device, u64)
+extern "C" int lsmk_launch_crc32_scan(const CrcParams* P, uint64_t* block_sum, hipStream_t st) {
   uint64_t n = P->nrec;
   uint32_t nb = (uint32_t)lsmk_scan_block_count(n);
-  hipLaunchKernelGGL(scan_phase1, dim3(nb), dim3(SCAN_BLOCK), 0, st, P->len, n, P->seg_start, block_sum);
+  hipLaunchKernelGGL(scan_phase1, dim3(nb), dim3(SCAN_BLOCK), 0, st, P->len, n, block_sum);
   hipLaunchKernelGGL(scan_phase2, dim3(1), dim3(1024), 0, st, block_sum, nb, P->total_segs);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
 }
 
-// phase 3 (+tile_info) and the checksum kernel; tile_info must hold
-// ceil(total/64) zeroed 16-byte entries
-extern "C" int lsmk_launch_crc32_desc(const CrcParams* P, const uint32_t* block_sum, int ncu, int variant,
+// phase 3 (tile_info) and the checksum kernel; tile_info must hold
+// ceil(total/64) zeroed 16-byte entries and total < 2^32
+extern "C" int lsmk_launch_crc32_desc(const CrcParams* P, const uint64_t* block_sum, int ncu, int variant,
                                       hipStream_t st) {
   uint64_t n = P->nrec;
-  hipLaunchKernelGGL(scan_phase3, dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0, st, P->len, n, P->seg_start,
+  hipLaunchKernelGGL(scan_phase3, dim3((unsigned)lsmk_scan_block_count(n)), dim3(SCAN_BLOCK), 0, st, P->len, n,
                      block_sum, P->tile_info);
   size_t lds = LDS_SCRATCH_OFF;
   int ch = (variant & 0xF) ? (variant & 0xF) : LSMCK_DEFAULT_DESC_CHAINS;
@@ -748,10 +860,12 @@ extern "C" int lsmk_launch_crc32_desc(const CrcParams* P, const uint32_t* block_
   const bool w12 = (variant & 0x20) != 0;
   const int block = w12 ? 768 : 1024;
   const void* fn = w12 ? (ablate == 1 ? (const void*)crc32_desc_kernel<1, 1, 768>
+                          : ablate == 3 ? (const void*)crc32_desc_kernel<1, 3, 768>
                           : ablate == 2 ? (const void*)crc32_desc_kernel<1, 2, 768>
                           : ch == 1 ? (const void*)crc32_desc_kernel<1, 0, 768>
                           : ch == 2 ? (const void*)crc32_desc_kernel<2, 0, 768> : (const void*)crc32_desc_kernel<4, 0, 768>)
                        : (ablate == 1 ? (const void*)crc32_desc_kernel<1, 1>
+                          : ablate == 3 ? (const void*)crc32_desc_kernel<1, 3>
                           : ablate == 2 ? (const void*)crc32_desc_kernel<1, 2>
                           : ch == 1 ? (const void*)crc32_desc_kernel<1>
                           : ch == 2 ? (const void*)crc32_desc_kernel<2> : (const void*)crc32_desc_kernel<4>);

@@ -16,9 +16,8 @@ struct CrcParams {
   uint64_t stride;            // fixed mode
   uint32_t flen;              // fixed mode
   uint64_t nrec;
-  uint32_t* seg_start;        // descriptor mode scratch: exclusive prefix of max(1, ceil(len/128))
   uint32_t* tile_info;        // descriptor mode scratch: per 64-segment tile {r0, q0, start mask lo, hi}
-  uint32_t* total_segs;       // descriptor mode scratch: total segments (device)
+  uint64_t* total_segs;       // descriptor mode scratch: total segments (device)
   uint32_t* out;              // nrec CRCs (zeroed before the launch)
   const uint32_t* kseg;       // x^(8*128*k) mod P, k < 2^16
   const uint32_t* khi;        // x^(8*128*65536*k) mod P, k < 2^16
@@ -44,8 +43,8 @@ struct ShaParams {
 extern "C" {
 int lsmk_launch_crc32_fixed(const lsmck::CrcParams* P, int ncu, int variant, hipStream_t st);
 uint64_t lsmk_scan_block_count(uint64_t n);
-int lsmk_launch_crc32_scan(const lsmck::CrcParams* P, uint32_t* block_sum, hipStream_t st);
-int lsmk_launch_crc32_desc(const lsmck::CrcParams* P, const uint32_t* block_sum, int ncu, int variant, hipStream_t st);
+int lsmk_launch_crc32_scan(const lsmck::CrcParams* P, uint64_t* block_sum, hipStream_t st);
+int lsmk_launch_crc32_desc(const lsmck::CrcParams* P, const uint64_t* block_sum, int ncu, int variant, hipStream_t st);
 int lsmk_launch_sha256(const lsmck::ShaParams* P, hipStream_t st);
 int lsmk_launch_crc32_compare(const uint32_t* crc, const uint32_t* expected, uint64_t n,
                                unsigned long long* n_bad, unsigned long long* first_bad, hipStream_t st);
