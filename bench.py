@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--cpu-sample-records", type=int, default=0)
     ap.add_argument("--variants", default="", help="comma list of crc_chains values to A/B in interleaved rounds")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--no-host-roundtrip", action="store_true",
+                    help="skip the host-resident (pinned H2D + kernel + D2H) sample")
     ap.add_argument("--desc", action="store_true",
                     help="diagnostic: config 2's fixed blocks through the descriptor entry point")
     ap.add_argument("--pack-align", type=int, default=1,
@@ -237,6 +239,43 @@ def main():
     }
     if ab is not None:
         res["variants_ab"] = ab
+
+    # Host round trip (north_star: the path starts and ends in host memory):
+    # a sample of the same records in pinned host memory, one synchronous
+    # lsmck_crc32_batch* per step = H2D DMA + kernel + D2H, chunked and
+    # double-buffered inside liblsmck.  Reported beside `value`, never as it.
+    if rank == 0 and world == 1 and not a.no_host_roundtrip:
+        if cfg == 3 or a.desc:
+            hn = min(nrec, 1 << 21)
+            hbytes = int(offs[hn - 1]) + int(lens[hn - 1])
+        else:
+            hn = min(nrec, (4 << 30) // rec_len)
+            hbytes = hn * rec_len
+        pb = ctx.alloc_pinned(hbytes)
+        ctx.memcpy_d2h(pb.ptr, data.ptr, hbytes)
+        if cfg == 3 or a.desc:
+            hoff, hlen = offs[:hn].copy(), lens[:hn].copy()
+
+            def hstep():
+                return ctx.crc32(pb.array, hoff, hlen, pinned=True)
+            hpay = int(hlen.astype(np.uint64).sum())
+        else:
+            def hstep():
+                return ctx.crc32_fixed(pb.array, rec_len, rec_len, hn, pinned=True)
+            hpay = hbytes
+        hres = hstep()
+        hsteps = 3
+        th0 = time.perf_counter()
+        for _ in range(hsteps):
+            hres = hstep()
+        th = (time.perf_counter() - th0) / hsteps
+        res["host_roundtrip"] = {
+            "value": round(hpay / GIB / th, 2), "unit": "GiB/s", "ms_per_step": round(th * 1e3, 2),
+            "sample": f"first {hn} records ({hpay / GIB:.2f} GiB) in pinned host memory; "
+                      "synchronous lsmck_crc32_batch* with LSMCK_HOST_PINNED (H2D DMA + kernel + D2H)",
+            "matches_device_result": bool(np.array_equal(hres, out.download(np.uint32, count=hn))),
+        }
+        pb.free()
 
     # CPU baseline + parity of the same sample (rank 0, N = 1 only)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

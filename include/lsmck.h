@@ -136,7 +136,10 @@ int lsmck_device_count(void);
  *   "crc_ablate"  DIAGNOSTIC ONLY, results are invalid while set: 1 = the fixed
  *                 kernel loads but does not checksum, 2 = checksums without
  *                 loading, 3 = payload loads only (no table gathers, no
- *                 reduction or store); 0 = off.  Locates the kernel's ceiling.
+ *                 reduction or store); 4..6 (descriptor kernel, valid only
+ *                 for 4 KiB records at 4 KiB stride): 3 with tile_info
+ *                 synthesized, + off/len synthesized, + aligned loads;
+ *                 0 = off.  Locates the kernels' ceilings.
  *   "crc_wg_waves"  waves per workgroup of the descriptor CRC kernel: 12 or 16
  *                 (0 = built-in default).  A/B switch: 12 waves leave 168 VGPRs
  *                 per lane for the three-stage load pipeline, 16 leave 128.

@@ -146,7 +146,7 @@ struct lsmck_ctx {
   uint32_t* d_kseg = nullptr;    // 65536
   uint32_t* d_khi = nullptr;     // 65536
   uint32_t* d_tinit = nullptr;   // 129
-  uint32_t* d_zero = nullptr;    // 64 zero bytes
+  uint32_t* d_zero = nullptr;    // 256 zero bytes
   std::mutex mu;
   DescScratch scratch;           // device-mode descriptor scratch
   hipEvent_t scratch_ev = nullptr;
@@ -467,7 +467,7 @@ lsmck_ctx* lsmck_ctx_create(int device) {
             hipMalloc((void**)&ctx->d_kseg, 65536 * 4) == hipSuccess &&
             hipMalloc((void**)&ctx->d_khi, 65536 * 4) == hipSuccess &&
             hipMalloc((void**)&ctx->d_tinit, 130 * 4) == hipSuccess &&
-            hipMalloc((void**)&ctx->d_zero, 64) == hipSuccess && hipMemset(ctx->d_zero, 0, 64) == hipSuccess &&
+            hipMalloc((void**)&ctx->d_zero, 256) == hipSuccess && hipMemset(ctx->d_zero, 0, 256) == hipSuccess &&
             hipMemcpy(ctx->d_master, master.data(), 4096 * 4, hipMemcpyHostToDevice) == hipSuccess &&
             hipMemcpy(ctx->d_kseg, kseg.data(), 65536 * 4, hipMemcpyHostToDevice) == hipSuccess &&
             hipMemcpy(ctx->d_khi, khi.data(), 65536 * 4, hipMemcpyHostToDevice) == hipSuccess &&
@@ -502,7 +502,7 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     return 0;
   }
   if (!strcmp(key, "crc_ablate")) {  // diagnostic only: timing ablations, results are garbage
-    if (value < 0 || value > 3) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0..3");
+    if (value < 0 || value > 7) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0..7");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->variant = (ctx->variant & 0xFF) | ((int)value << 8);
     return 0;

@@ -54,7 +54,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #define LSMCK_DEFAULT_CHAINS 2       // fixed records (A/B: profiles/r01)
 #endif
 #ifndef LSMCK_DEFAULT_DESC_CHAINS
-#define LSMCK_DEFAULT_DESC_CHAINS 1  // descriptor records (A/B: profiles/r01)
+#define LSMCK_DEFAULT_DESC_CHAINS 2  // descriptor records (A/B: profiles/r01)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -162,16 +162,15 @@ struct SegLoad {
   uint32_t rec, k;
   uint32_t fl;     // packed SegLoad.fl fields below
 };
-// FL_SH: (E-128) & 3.  FL_BST: B - floor4(E-128).  FL_P16: floor4(E-128)/4 mod 4.
-// FL_RISKY: a page boundary lies inside B's group, in front of B's dword; the
-// group was loaded from floor16(B's dword) instead and seg_finish shifts it
-// into place.  FL_VALID: lane holds a real segment.  FL_FIRST: q == 0.
+// FL_SH: (E-128) & 3.  FL_BST: B - floor4(E-128).  FL_VALID: lane holds a
+// real segment.  FL_FIRST: q == 0.  FL_M: the load window was moved up by
+// m dwords to the start of B's page (see seg_issue); seg_finish moves the
+// registers back.
 #define FL_SH(f) ((f) & 3u)
 #define FL_BST(f) (((f) >> 2) & 0xFFu)
-#define FL_RISKY 0x400u
-#define FL_VALID 0x800u
-#define FL_FIRST 0x1000u
-#define FL_P16(f) (((f) >> 13) & 3u)
+#define FL_VALID 0x400u
+#define FL_FIRST 0x800u
+#define FL_M(f) (((f) >> 12) & 0x3Fu)
 
 // Issue every global load of a segment; consumes nothing.  FAST: full
 // segment whose stream start is dword aligned (ALIGNED16: 16-byte aligned).
@@ -184,7 +183,7 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
   L.k = si.k;
   const uint32_t flv = (si.valid ? FL_VALID : 0u) | (si.q == 0 ? FL_FIRST : 0u);
   L.fl = flv;
-  if (ABLATE == 3) {  // diagnostic: payload loads only (no table gathers)
+  if (ABLATE >= 3) {  // diagnostic: payload loads only (no table gathers)
     L.K = si.k;
     L.TI = seglen;
   } else {
@@ -210,46 +209,45 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
     L.d[32] = 0;
     return;
   }
-  // General path, straight-line (no divergent branches: a branch merge here
-  // makes hipcc wait for the loads and the prefetch is lost).
-  //  - groups entirely in front of B's dword are loaded from the 16-byte
-  //    aligned block holding the record's last byte (a safe address of this
-  //    lane's own lines) and zeroed in seg_finish.  A shared zero buffer would
-  //    be simpler, but lanes of one load instruction hitting one address cost
-  //    ~25% of the load path (tools/microbench_loads.hip); only empty
-  //    segments (empty records, pad lanes) still read it;
-  //  - the group holding B's dword is loaded whole: its bytes in front of B
-  //    (<= 12) are zeroed in seg_finish.  They are on B's page unless a page
-  //    boundary lies between the group start and B's dword ("risky", rare):
-  //    then the group is loaded from floor16(B's dword) -- that is the page
-  //    boundary itself, and a 16-byte aligned block never crosses a page --
-  //    and seg_finish shifts it up by 1..3 dwords into place;
-  //  - groups end at floor4(E-128)+128 <= E, D_32 at ceil4(E): no over-read.
+  // General path: one base pointer per lane, eight 16-byte loads at
+  // immediate offsets (per-group addresses cost ~30% of the load path:
+  // crc_ablate 3 vs 6), straight-line (a divergent branch here makes hipcc
+  // wait for the loads and the prefetch is lost).
+  //  - window [p, p+128), p = floor4(E-128): it never passes E.  Bytes of it
+  //    in front of B (first segments) are zeroed in seg_finish;
+  //  - they are on B's page unless a page boundary lies in (p, B].  A page
+  //    boundary is dword aligned, so it can only fall in front of B's dword,
+  //    never inside the stream of a non-first segment.  Then the window starts
+  //    at the boundary instead (m = 1..32 dwords higher; it ends at most 131
+  //    bytes into B's page) and seg_finish shifts the registers back up;
+  //  - D_32 (stream bytes only when the stream start is not dword aligned)
+  //    is the dword at p+128, which holds E-1 when it is needed; otherwise a
+  //    dword inside the window is loaded and ignored;
+  //  - an empty segment (empty record, pad lane) reads a zero buffer.
   const uint32_t sh = (uint32_t)((uintptr_t)s0 & 3);
-  const unsigned char* p = s0 - sh;     // floor4(E-128)
-  const uint32_t bstart = sh + lead;    // B - floor4(E-128)
-  const uint32_t lo_i = bstart >> 2;    // index of B's dword
-  const uint32_t gb = lo_i >> 2;        // group holding B's dword
-  const uintptr_t b4 = (uintptr_t)p + 4u * lo_i;
-  // bitwise &, not &&: a short-circuit branch here would merge wait states (see above)
-  const bool risky = ((lo_i & 3u) != 0u) & ((b4 & ~(uintptr_t)4095) > (uintptr_t)p + 16u * gb);
-  L.fl = flv | sh | (bstart << 2) | (risky ? FL_RISKY : 0u) | ((uint32_t)(((uintptr_t)p >> 2) & 3u) << 13);
-  const unsigned char* pb16 = P.base + ((E - 128) - sh + 4u * lo_i) - (b4 & 15u);  // floor16(B's dword)
-  const unsigned char* last = P.base + (E - 1) - (((uintptr_t)P.base + (E - 1)) & 15u);  // floor16(E-1)
-  const unsigned char* filler = (lead < 128u) ? last : (const unsigned char*)P.zero;   // empty: zero buffer
+  const unsigned char* p = s0 - sh;  // floor4(E-128)
+  const uint32_t bstart = sh + lead; // B - p
+  const bool empty = lead >= 128u;
+  const uintptr_t pa = (uintptr_t)p;
+  const uintptr_t pg = (pa + bstart) & ~(uintptr_t)4095;  // B's page
+  const bool cross = !empty & (pg > pa);
+  const uint32_t m = cross ? (uint32_t)(pg - pa) >> 2 : 0u;  // 1..32
+  L.fl = flv | sh | (bstart << 2) | (m << 12);
+  // pointer arithmetic from the kernel-argument pointers keeps these global_load
+  const unsigned char* w = empty ? (const unsigned char*)P.zero : p + 4u * m;
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
-    const bool skip = 4u * g + 3u < lo_i;
-    const bool rk = ((uint32_t)g == gb) & risky;
-    u32x4 v = ld128(rk ? pb16 : (skip ? filler : p + 16 * g));
+    u32x4 v = ld128(w + 16 * g);
     L.d[4 * g + 0] = v.x;
     L.d[4 * g + 1] = v.y;
     L.d[4 * g + 2] = v.z;
     L.d[4 * g + 3] = v.w;
   }
-  // D_32 holds stream bytes only when the stream start is not dword aligned
-  // (otherwise the funnel ignores it: load any safe dword)
-  L.d[32] = ld32((sh && lead < 128u) ? p + 128 : filler);
+  if (ABLATE == 7) {  // diagnostic: no D_32 load
+    L.d[32] = sh;
+    return;
+  }
+  L.d[32] = ld32(w + ((sh != 0u && m == 0u) ? 128 : 124));
 }
 
 // Funnel, mask, raw slicing-by-4 CRC, init term, shift to the record's end.
@@ -259,7 +257,7 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
 template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
 __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const CrcParams& P, const SegLoad& L,
                                                uint32_t lo, uint32_t hi) {
-  if (ABLATE == 1 || ABLATE == 3) {  // diagnostic: loads only (memory-path timing; results invalid)
+  if (ABLATE == 1 || ABLATE >= 3) {  // diagnostic: loads only (memory-path timing; results invalid)
     uint32_t x = 0;
 #pragma unroll
     for (int j = 0; j < 33; ++j) x ^= L.d[j];
@@ -275,33 +273,29 @@ __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const 
     for (int j = 0; j < 33; ++j) d[j] = L.d[j];
     const uint32_t sh = FL_SH(L.fl), bstart = FL_BST(L.fl), lo_i = bstart >> 2;
     const uint32_t bm = 0xFFFFFFFFu << (8u * (bstart & 3u));  // keep-mask of B's dword
-    const bool risky = (L.fl & FL_RISKY) != 0u;
-    if (__any(risky)) {  // rare: B's group was loaded from floor16(B's dword), s dwords too low
-      const uint32_t r = lo_i & 3u, gb = lo_i >> 2;
-      const uint32_t s = r - ((FL_P16(L.fl) + r) & 3u);  // 1..3 for risky lanes
+    const uint32_t m = FL_M(L.fl);
+    if (__any(m != 0u)) {  // rare: the window started at B's page, m dwords up: shift back
 #pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        const bool here = risky & ((uint32_t)g == gb);
-        const uint32_t x0 = d[4 * g], x1 = d[4 * g + 1], x2 = d[4 * g + 2];
-        // group[k] = x[k - s] for k >= r (>= s); dwords k < r are zeroed below
-        d[4 * g + 3] = here ? (s == 1u ? x2 : (s == 2u ? x1 : x0)) : d[4 * g + 3];
-        d[4 * g + 2] = here ? (s == 1u ? x1 : x0) : x2;
-        d[4 * g + 1] = here ? x0 : x1;
+      for (int b = 0; b < 6; ++b) {
+        const int s = 1 << b;
+        const bool on = (m >> b) & 1u;
+#pragma unroll
+        for (int j = 32; j >= 0; --j) d[j] = on ? (j >= s ? d[j - s] : 0u) : d[j];
       }
     }
     if (__any(bstart != 0u)) {
-      // zero everything in front of B: the filler groups before B's group and
-      // B's group's bytes in front of B (with lead = 0 this only clears bytes
+      // zero the window in front of B: the groups before B's group and the
+      // bytes of B's group in front of B (with lead = 0 this only clears bytes
       // of D_0 in front of the stream start, which the funnel drops anyway)
       const uint32_t r = lo_i & 3u, gb = lo_i >> 2;
-      uint32_t m[4];
+      uint32_t mk[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) m[k] = ((uint32_t)k < r) ? 0u : (((uint32_t)k == r) ? bm : 0xFFFFFFFFu);
+      for (int k = 0; k < 4; ++k) mk[k] = ((uint32_t)k < r) ? 0u : (((uint32_t)k == r) ? bm : 0xFFFFFFFFu);
 #pragma unroll
       for (int g = 0; g < 8; ++g) {
         const bool before = (uint32_t)g < gb, here = (uint32_t)g == gb;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) d[4 * g + k] &= before ? 0u : (here ? m[k] : 0xFFFFFFFFu);
+        for (int k = 0; k < 4; ++k) d[4 * g + k] &= before ? 0u : (here ? mk[k] : 0xFFFFFFFFu);
       }
       d[32] &= (lo_i == 32u) ? bm : 0xFFFFFFFFu;
     }
@@ -402,7 +396,7 @@ template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
 __device__ __forceinline__ void finish_tile(const unsigned char* smem, const CrcParams& P, const SegLoad& L,
                                             uint32_t lane, uint32_t lo, uint32_t hi) {
   uint32_t v = seg_finish<FAST, CHAINS, ABLATE, PERCOL>(smem, P, L, lo, hi);
-  if (ABLATE == 3) {  // no reduction, no store (unless a magic value: keeps the loads alive)
+  if (ABLATE >= 3) {  // no reduction, no store (unless a magic value: keeps the loads alive)
     if (v == 0x9E3779B1u) P.out[0] = v;
     return;
   }
@@ -482,12 +476,18 @@ __global__ __launch_bounds__(1024) void crc32_fixed_kernel(CrcParams P) {
 // the payload loads (vmcnt), while an s_load would share lgkmcnt with the LDS
 // lookups and force lgkmcnt(0) waits in the checksum loop.  Tiles outside
 // [0, ntiles) read a clamped entry (their lanes are all pad lanes).
+template <int ABLATE = 0>
 __device__ __forceinline__ uint32_t desc_tile(const CrcParams& P, int32_t x, int32_t nt, uint32_t lane) {
   const int32_t c = x < 0 ? 0 : (x < nt ? x : nt - 1);
+  if (ABLATE >= 4 && ABLATE <= 6) {  // diagnostic, config-2 layout only (4 KiB records): synthesized, not loaded
+    const uint32_t q = lane & 3u;
+    return q == 0 ? 2u * (uint32_t)c : (q == 1 ? 0u : 1u);
+  }
   return P.tile_info[4ull * (uint32_t)c + (lane & 3u)];
 }
 
 // stage 1 (two tiles ahead): lane -> (rec, q); issues the off/len gathers
+template <int ABLATE = 0>
 __device__ __forceinline__ SegInfo desc_map_issue(const CrcParams& P, uint32_t tv, int32_t x, uint32_t lane,
                                                   uint32_t total) {
   // (readlane returns int: go through uint32_t, a direct widening would sign-extend)
@@ -502,8 +502,13 @@ __device__ __forceinline__ SegInfo desc_map_issue(const CrcParams& P, uint32_t t
   rec = (si.valid && rec < P.nrec) ? rec : (uint32_t)P.nrec - 1u;
   si.q = below ? lane - (63u - (uint32_t)__builtin_clzll(below)) : q0 + lane;
   si.rec = rec;
-  si.rec_off = P.off[rec];
-  si.rec_len = P.len[rec];
+  if (ABLATE == 5 || ABLATE == 6) {  // diagnostic, config-2 layout only: synthesized descriptors
+    si.rec_off = (uint64_t)rec * 4096u;
+    si.rec_len = 4096u;
+  } else {
+    si.rec_off = P.off[rec];
+    si.rec_len = P.len[rec];
+  }
   si.k = 0;
   return si;
 }
@@ -547,7 +552,9 @@ __global__ __launch_bounds__(BLOCK) void crc32_desc_kernel(CrcParams P) {
   M0.valid = M1.valid = false;
   M0.q = M1.q = 0;
   M0.rec = M1.rec = 0;
-  M0.rec_off = M1.rec_off = 0;
+  // (the general loads send an empty segment to the zero buffer; the aligned
+  // loads of diagnostic 6 read [E-128, E) and need E >= 128)
+  M0.rec_off = M1.rec_off = (ABLATE == 6) ? 128u : 0u;
   M0.rec_len = M1.rec_len = 0;
   M0.k = M1.k = 0;
   SegLoad A, B;
@@ -560,18 +567,18 @@ __global__ __launch_bounds__(BLOCK) void crc32_desc_kernel(CrcParams P) {
   int32_t c = wave - 3 * n;
   for (int32_t j = 2; j <= H; j += 2) {
     // in flight: A = payload(c), M1 = gathers(c+n), T0 = tile_info(c+2n)
-    M0 = desc_map_issue(P, T0, c + 2 * n, lane, total);
-    T1 = desc_tile(P, c + 3 * n, nt, lane);
+    M0 = desc_map_issue<ABLATE>(P, T0, c + 2 * n, lane, total);
+    T1 = desc_tile<ABLATE>(P, c + 3 * n, nt, lane);
     desc_map_complete(M1);
-    seg_issue<false, ABLATE>(P, M1, B);
+    seg_issue<(ABLATE == 6), ABLATE>(P, M1, B);
     __builtin_amdgcn_sched_barrier(0);
     finish_tile<false, CHAINS, ABLATE>(smem, P, A, lane, lo, hi);  // virtual tiles: pad lanes, no store
     c += n;
     // in flight: B = payload(c), M0 = gathers(c+n), T1 = tile_info(c+2n)
-    M1 = desc_map_issue(P, T1, c + 2 * n, lane, total);
-    T0 = desc_tile(P, c + 3 * n, nt, lane);
+    M1 = desc_map_issue<ABLATE>(P, T1, c + 2 * n, lane, total);
+    T0 = desc_tile<ABLATE>(P, c + 3 * n, nt, lane);
     desc_map_complete(M0);
-    seg_issue<false, ABLATE>(P, M0, A);
+    seg_issue<(ABLATE == 6), ABLATE>(P, M0, A);
     __builtin_amdgcn_sched_barrier(0);
     finish_tile<false, CHAINS, ABLATE>(smem, P, B, lane, lo, hi);
     c += n;
@@ -866,6 +873,10 @@ extern "C" int lsmk_launch_crc32_desc(const CrcParams* P, const uint64_t* block_
                           : ch == 2 ? (const void*)crc32_desc_kernel<2, 0, 768> : (const void*)crc32_desc_kernel<4, 0, 768>)
                        : (ablate == 1 ? (const void*)crc32_desc_kernel<1, 1>
                           : ablate == 3 ? (const void*)crc32_desc_kernel<1, 3>
+                          : ablate == 4 ? (const void*)crc32_desc_kernel<1, 4>
+                          : ablate == 5 ? (const void*)crc32_desc_kernel<1, 5>
+                          : ablate == 6 ? (const void*)crc32_desc_kernel<1, 6>
+                          : ablate == 7 ? (const void*)crc32_desc_kernel<1, 7>
                           : ablate == 2 ? (const void*)crc32_desc_kernel<1, 2>
                           : ch == 1 ? (const void*)crc32_desc_kernel<1>
                           : ch == 2 ? (const void*)crc32_desc_kernel<2> : (const void*)crc32_desc_kernel<4>);

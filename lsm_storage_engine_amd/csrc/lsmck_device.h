@@ -23,7 +23,7 @@ struct CrcParams {
   const uint32_t* khi;        // x^(8*128*65536*k) mod P, k < 2^16
   const uint32_t* tinit;      // 0xFFFFFFFF (x) x^(8*m) mod P, m = 0..128; [129] = 0
   const uint32_t* master;     // slicing-by-4 tables T0..T3 (4 x 256), then shift tables ST_1..ST_3 (3 x 4 x 256)
-  const uint32_t* zero;       // 64 zero bytes (16-aligned): target of the loads a segment must not make
+  const uint32_t* zero;       // 256 zero bytes (16-aligned): the load window of empty segments
 };
 
 // SHA-256 batch job (lane per message).

@@ -54,6 +54,32 @@ class DeviceBuffer:
             pass
 
 
+class PinnedBuffer:
+    """Page-locked host memory (hipHostMalloc through liblsmck); ``array`` is a
+    uint8 numpy view.  Batch calls given these arrays with pinned=True DMA
+    straight from / to them (LSMCK_HOST_PINNED)."""
+
+    def __init__(self, ctx, nbytes):
+        self.ctx = ctx
+        self.nbytes = nbytes
+        self.ptr = _lib.load().lsmck_host_alloc_pinned(ctx.handle, max(1, nbytes))
+        if not self.ptr:
+            raise MemoryError(f"hipHostMalloc({nbytes}): {_lib.last_error()}")
+        self.array = np.ctypeslib.as_array((C.c_uint8 * max(1, nbytes)).from_address(self.ptr))[:nbytes]
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            _lib.load().lsmck_host_free_pinned(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class Context:
     def __init__(self, device=0):
         lib = _lib.load()
@@ -87,6 +113,12 @@ class Context:
     def alloc(self, nbytes):
         return DeviceBuffer(self, nbytes)
 
+    def alloc_pinned(self, nbytes):
+        return PinnedBuffer(self, nbytes)
+
+    def memcpy_d2h(self, dst_ptr, src_ptr, nbytes, stream=None):
+        _lib.check(self.lib.lsmck_memcpy_d2h(self.handle, dst_ptr, src_ptr, nbytes, stream), "d2h")
+
     def sync(self, stream=None):
         _lib.check(self.lib.lsmck_stream_sync(self.handle, stream), "sync")
 
@@ -108,11 +140,12 @@ class Context:
                                               out.ctypes.data, flags, None), "crc32_batch")
         return out
 
-    def crc32_fixed(self, data, stride, length, n):
+    def crc32_fixed(self, data, stride, length, n, pinned=False):
         data = np.ascontiguousarray(data, dtype=np.uint8)
         out = np.empty(n, dtype=np.uint32)
+        flags = _lib.HOST_PINNED if pinned else _lib.HOST
         _lib.check(self.lib.lsmck_crc32_batch_fixed(self.handle, data.ctypes.data, stride, length, n, out.ctypes.data,
-                                                    _lib.HOST, None), "crc32_batch_fixed")
+                                                    flags, None), "crc32_batch_fixed")
         return out
 
     def crc32_verify(self, data, off, length, expected):
