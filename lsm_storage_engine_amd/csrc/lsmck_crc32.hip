@@ -48,7 +48,12 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #define LDS_COLS_BYTES 8192u                               // [32/4][64 lanes][4] u32
 #define LDS_KHI_OFF (LDS_COLS_OFF + LDS_COLS_BYTES)  // khi[0..511]: x^(8*128*65536*j), j = k >> 16 (len < 2^32)
 #define LDS_KHI_BYTES 2048u
-#define LDS_SCRATCH_OFF (LDS_KHI_OFF + LDS_KHI_BYTES)
+// per-segment factor K = x^(8*128*k) = klo[k & 511] (x) kmid[(k >> 9) & 127] (x) khi[k >> 16],
+// and the init terms tinit[len0]: all from LDS, so the issue path gathers no tables
+#define LDS_KLO_OFF (LDS_KHI_OFF + LDS_KHI_BYTES)
+#define LDS_KMID_OFF (LDS_KLO_OFF + 2048u)
+#define LDS_TINIT_OFF (LDS_KMID_OFF + 512u)
+#define LDS_SCRATCH_OFF (LDS_TINIT_OFF + 544u)
 #define WAVE_SCRATCH_BYTES 256u
 #ifndef LSMCK_DEFAULT_CHAINS
 #define LSMCK_DEFAULT_CHAINS 2       // fixed records (A/B: profiles/r01)
@@ -94,8 +99,8 @@ __device__ __forceinline__ u32x4 lds_ld128(uint32_t a) { return *(lds_u32x4_t*)(
 // LDS tables.  Byte address of T_t[e], replica r:
 //   256*e + 4*r + 128*(t&1) + 65536*(t>>1)
 // T0 = Sarwate table, T_k[n] = (T_{k-1}[n] >> 8) ^ T0[T_{k-1}[n] & 0xFF].
-__device__ __forceinline__ void build_lds_tables(unsigned char* smem, const uint32_t* __restrict__ master,
-                                                 const uint32_t* __restrict__ khi) {
+__device__ __forceinline__ void build_lds_tables(unsigned char* smem, const CrcParams& P) {
+  const uint32_t* __restrict__ master = P.master;
   uint32_t* s32 = (uint32_t*)smem;
   for (uint32_t i = threadIdx.x; i < LDS_TABLE_BYTES / 4; i += blockDim.x) {
     uint32_t t = ((i >> 14) << 1) | ((i >> 5) & 1u);
@@ -107,7 +112,10 @@ __device__ __forceinline__ void build_lds_tables(unsigned char* smem, const uint
   // segment factors of records over 2^16 segments (8 MiB): from LDS, so the
   // checksum loop issues no global load of its own (its waits would also
   // wait for the next tile's prefetch)
-  for (uint32_t i = threadIdx.x; i < LDS_KHI_BYTES / 4; i += blockDim.x) s32[LDS_KHI_OFF / 4 + i] = khi[i];
+  for (uint32_t i = threadIdx.x; i < LDS_KHI_BYTES / 4; i += blockDim.x) s32[LDS_KHI_OFF / 4 + i] = P.khi[i];
+  for (uint32_t i = threadIdx.x; i < 512u; i += blockDim.x) s32[LDS_KLO_OFF / 4 + i] = P.kseg[i];
+  for (uint32_t i = threadIdx.x; i < 128u; i += blockDim.x) s32[LDS_KMID_OFF / 4 + i] = P.kseg[512u * i];
+  for (uint32_t i = threadIdx.x; i < 130u; i += blockDim.x) s32[LDS_TINIT_OFF / 4 + i] = P.tinit[i];
 }
 
 // raw CRC register s advanced over 32*m zero bytes (m = 1..3): 4 plain-table lookups
@@ -155,8 +163,6 @@ struct SegInfo {
 // In-flight loads of one segment (issued one tile ahead of their use).
 struct SegLoad {
   uint32_t d[33];  // dwords D_0..D_32 (D_32 only when the stream start is not dword aligned)
-  uint32_t K;      // x^(8*128*k) mod P for this segment (k < 2^16; larger k finish in seg_finish)
-  uint32_t TI;     // init term 0xFFFFFFFF (x) x^(8*len0) for a record's first segment, else 0
   // the segment's coordinates, copied at issue time (when they are resident):
   // finish needs no SegInfo, so the map of a later tile may still be in flight
   uint32_t rec, k;
@@ -183,13 +189,6 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
   L.k = si.k;
   const uint32_t flv = (si.valid ? FL_VALID : 0u) | (si.q == 0 ? FL_FIRST : 0u);
   L.fl = flv;
-  if (ABLATE >= 3) {  // diagnostic: payload loads only (no table gathers)
-    L.K = si.k;
-    L.TI = seglen;
-  } else {
-    L.K = P.kseg[si.k & 0xFFFFu];
-    L.TI = P.tinit[(si.q == 0) ? seglen : 129u];  // unconditional load (tinit[129] = 0): no branch in the issue block
-  }
   // pointer arithmetic on the kernel-argument pointer keeps these global_load (not flat_load)
   const unsigned char* s0 = P.base + (E - 128);
   if (ABLATE == 2) {  // diagnostic: no payload loads (compute-only timing; results invalid)
@@ -261,7 +260,7 @@ __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const 
     uint32_t x = 0;
 #pragma unroll
     for (int j = 0; j < 33; ++j) x ^= L.d[j];
-    return x ^ L.K ^ L.TI;
+    return x ^ L.k ^ L.fl;
   }
   uint32_t w[32];
   if (FAST) {
@@ -319,7 +318,9 @@ __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const 
   } else {
     s = shift_bytes32<3>(smem, c[0]) ^ shift_bytes32<2>(smem, c[1]) ^ shift_bytes32<1>(smem, c[2]) ^ c[3];
   }
-  s ^= L.TI;
+  // init term of a record's first segment: 0xFFFFFFFF (x) x^(8*len0), len0 = 128 - lead
+  const uint32_t lead0 = FL_BST(L.fl) - FL_SH(L.fl);
+  s ^= (L.fl & FL_FIRST) ? lds_ld(smem, LDS_TINIT_OFF + ((128u - lead0) << 2)) : 0u;
   if constexpr (PERCOL) {
     // s (x) K with the lane's 32 precomputed columns K*x^i: p ^= col_i if bit 31-i of s
     const uint32_t lane = threadIdx.x & 63u;
@@ -334,8 +335,11 @@ __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const 
     }
     return p;
   }
-  uint32_t K = L.K;
-  if (L.k >> 16) K = gf2_mulmod(K, lds_ld(smem, LDS_KHI_OFF + ((L.k >> 16) << 2)));
+  uint32_t K = lds_ld(smem, LDS_KLO_OFF + ((L.k & 511u) << 2));
+  if (__any(L.k >= 512u)) {  // records over 64 KiB (identity factors for the other lanes)
+    K = gf2_mulmod(K, lds_ld(smem, LDS_KMID_OFF + (((L.k >> 9) & 127u) << 2)));
+    if (__any(L.k >= 65536u)) K = gf2_mulmod(K, lds_ld(smem, LDS_KHI_OFF + ((L.k >> 16) << 2)));
+  }
   return gf2_mulmod(s, K);
 }
 
@@ -426,7 +430,7 @@ __device__ __forceinline__ SegInfo fixed_map(const CrcParams& P, uint32_t t, uin
 template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
 __global__ __launch_bounds__(1024) void crc32_fixed_kernel(CrcParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  build_lds_tables(smem, P.master, P.khi);
+  build_lds_tables(smem, P);
   if (PERCOL) build_lds_cols(P, (P.flen + 127u) >> 7);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
@@ -538,7 +542,7 @@ __device__ __forceinline__ void desc_map_complete(SegInfo& si) {
 template <int CHAINS, int ABLATE = 0, int BLOCK = 1024>
 __global__ __launch_bounds__(BLOCK) void crc32_desc_kernel(CrcParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  build_lds_tables(smem, P.master, P.khi);
+  build_lds_tables(smem, P);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t lo = (lane & 31u) * 4u, hi = lo | 0x10000u;
