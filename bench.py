@@ -199,7 +199,7 @@ def main():
     total_payload = payload * world
     value = total_payload / GIB / (wall_max / a.steps)
     achieved_gbs = algo_bytes / (ev_ms * 1e-3) / 1e9
-    wkey = f"config{cfg}"
+    wkey = None if (a.desc or a.pack_align > 1) else f"config{cfg}"  # diagnostics have no committed traffic
     traffic = traffic_from_profiles(wkey)
 
     res = {
