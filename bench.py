@@ -150,8 +150,9 @@ def main():
             for v in vs:
                 # "c<k>" = crc_chains k;  "g<k>" = crc_chains k with the generic multiply;
                 # "a<k>" = diagnostic ablation k (timing only); optional suffix
-                # "w<n>" = crc_wg_waves n (descriptor kernel)
-                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?", v)
+                # "w<n>" = crc_wg_waves n (descriptor kernel); "l<n>" = crc_loads n
+                # (1 global, 2 raw buffer)
+                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?", v)
                 if not m:
                     raise SystemExit(f"bad variant {v!r}")
                 kind, num, waves = m.group(1), int(m.group(2)), int(m.group(3) or 0)
@@ -159,6 +160,7 @@ def main():
                 ctx.set_option("crc_generic_mul", 1 if kind == "g" else 0)
                 ctx.set_option("crc_ablate", num if kind == "a" else 0)
                 ctx.set_option("crc_wg_waves", waves)
+                ctx.set_option("crc_loads", int(m.group(4) or 0))
                 step()
                 e0.record(stream)
                 for _ in range(a.steps):
@@ -170,6 +172,7 @@ def main():
         ctx.set_option("crc_generic_mul", 0)
         ctx.set_option("crc_ablate", 0)
         ctx.set_option("crc_wg_waves", 0)
+        ctx.set_option("crc_loads", 0)
         ab = {str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                        "GiBps_median": payload / GIB / (float(np.median(t)) * 1e-3)} for v, t in ab.items()}
 

@@ -143,6 +143,9 @@ int lsmck_device_count(void);
  *   "crc_wg_waves"  waves per workgroup of the descriptor CRC kernel: 12 or 16
  *                 (0 = built-in default).  A/B switch: 12 waves leave 168 VGPRs
  *                 per lane for the three-stage load pipeline, 16 leave 128.
+ *   "crc_loads"   payload load instruction of the fixed-record CRC kernel:
+ *                 1 = global_load, 2 = raw buffer_load from a per-tile base
+ *                 (0 = built-in default).  A/B switch.
  * Returns 0, or LSMCK_EINVAL for an unknown key / value. */
 int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
 

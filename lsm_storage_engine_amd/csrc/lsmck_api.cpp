@@ -514,6 +514,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->variant = (ctx->variant & ~0x20) | (value == 12 ? 0x20 : 0);
     return 0;
   }
+  if (!strcmp(key, "crc_loads")) {  // A/B: payload load instruction, 0 default, 1 global, 2 raw buffer
+    if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_loads must be 0, 1 or 2");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (ctx->variant & ~0xC0) | (value == 1 ? 0x40 : 0) | (value == 2 ? 0x80 : 0);
+    return 0;
+  }
   return lsmck_host::set_error(LSMCK_EINVAL, "unknown option");
 }
 

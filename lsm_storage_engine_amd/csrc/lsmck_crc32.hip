@@ -58,6 +58,9 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef LSMCK_DEFAULT_CHAINS
 #define LSMCK_DEFAULT_CHAINS 2       // fixed records (A/B: profiles/r01)
 #endif
+#ifndef LSMCK_DEFAULT_BUFLOADS
+#define LSMCK_DEFAULT_BUFLOADS 1     // fixed records: raw buffer loads (A/B: profiles/r01)
+#endif
 #ifndef LSMCK_DEFAULT_DESC_CHAINS
 #define LSMCK_DEFAULT_DESC_CHAINS 2  // descriptor records (A/B: profiles/r01)
 #endif
@@ -180,8 +183,20 @@ struct SegLoad {
 
 // Issue every global load of a segment; consumes nothing.  FAST: full
 // segment whose stream start is dword aligned (ALIGNED16: 16-byte aligned).
-template <bool FAST, int ABLATE = 0>
-__device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si, SegLoad& L) {
+// Buffer resource over the 2 GiB window at `b` (wave-uniform): raw buffer
+// loads take a 32-bit lane offset from one SGPR base, and hipcc issues them in
+// program order (address-ascending per lane); see BUF below.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t window_rsrc(const unsigned char* b) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(b), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+
+// BUF (FAST only): the eight 16-byte loads are raw buffer loads from the
+// wave-uniform tile base `tbase` (offset from P.base; the host guarantees the
+// tile's segments lie within 2^31 bytes of it).  tools/microbench_policy.hip:
+// this load shape streams at 6.43 TB/s as buffer loads and 5.39 TB/s as
+// global loads, which hipcc issues out of address order (48,32,0,16,112,...).
+template <bool FAST, int ABLATE = 0, bool BUF = false>
+__device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si, SegLoad& L, uint64_t tbase = 0) {
   const uint64_t E = si.rec_off + si.rec_len - 128ull * si.k;  // segment end (offset from base)
   const uint32_t seglen = (si.q == 0) ? si.rec_len - 128u * si.k : 128u;
   const uint32_t lead = 128u - seglen;  // stream bytes in front of the record (first segment only)
@@ -194,6 +209,20 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
   if (ABLATE == 2) {  // diagnostic: no payload loads (compute-only timing; results invalid)
 #pragma unroll
     for (int j = 0; j < 33; ++j) L.d[j] = (uint32_t)E * 0x9E3779B1u + j;
+    return;
+  }
+  if (FAST && BUF) {
+    const __amdgpu_buffer_rsrc_t r = window_rsrc(P.base + tbase);
+    const uint32_t vo = (uint32_t)(E - 128 - tbase);
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      auto v = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 16u * g, 0, 0);
+      L.d[4 * g + 0] = v[0];
+      L.d[4 * g + 1] = v[1];
+      L.d[4 * g + 2] = v[2];
+      L.d[4 * g + 3] = v[3];
+    }
+    L.d[32] = 0;
     return;
   }
   if (FAST) {
@@ -427,7 +456,65 @@ __device__ __forceinline__ SegInfo fixed_map(const CrcParams& P, uint32_t t, uin
 
 // Software pipelined: the loads of tile t+nwaves are in flight while tile t is
 // checksummed (sched_barrier keeps the compiler from sinking them to their use).
-template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
+// Fixed records whose segment count divides 64 (PERCOL), buffer loads: every
+// tile starts on a record boundary, so a lane's byte offset from its tile's
+// first record, (lane/nsegr)*stride + 128*(lane%nsegr), is the same in every
+// tile.  The eight load offsets are computed once, before the loop, and kept
+// in eight VGPRs (hidden from the compiler, which would otherwise fold them
+// into one VGPR + immediate offsets): tools/microbench_policy.hip measured this
+// load shape at 6.39 TB/s, the same loads with offset:16..112 immediates at
+// 5.53 TB/s, and with the offsets recomputed per tile at 5.45 TB/s.
+// Pad lanes of the last tile fall past the batch's end: the descriptor's
+// range check returns zeros for them (their results are dropped).
+struct PercolMap {
+  uint32_t voff[8];  // lane offsets of the eight 16-byte loads
+  uint32_t lsh;      // log2(nsegr)
+  uint64_t tstride;  // bytes per tile (64/nsegr records)
+  uint64_t end;      // bytes from P.base to the last record's end
+};
+__device__ __forceinline__ PercolMap percol_map(const CrcParams& P, uint32_t lane, uint32_t nsegr) {
+  PercolMap M;
+  M.lsh = __builtin_ctz(nsegr);
+  const uint32_t lo = (uint32_t)((lane >> M.lsh) * P.stride) + 128u * (lane & (nsegr - 1u));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t o = lo + 16u * j;
+    asm volatile("" : "+v"(o));
+    M.voff[j] = o;
+  }
+  M.tstride = (uint64_t)(64u >> M.lsh) * P.stride;
+  M.end = (uint64_t)(P.nrec - 1) * P.stride + P.flen;
+  return M;
+}
+__device__ __forceinline__ void seg_issue_percol(const CrcParams& P, const PercolMap& M, uint32_t t, uint32_t lane,
+                                                 uint32_t nsegr, uint32_t total, SegLoad& L) {
+  const uint64_t tb = (uint64_t)t * M.tstride;
+  const uint64_t left = M.end - tb;  // t < ntiles: > 0
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char*>(P.base + tb), (short)0, (int)(left < 0x7FFFFFFFull ? left : 0x7FFFFFFFull), 0x00020000);
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b128(r, M.voff[g], 0, 0);
+    L.d[4 * g + 0] = v[0];
+    L.d[4 * g + 1] = v[1];
+    L.d[4 * g + 2] = v[2];
+    L.d[4 * g + 3] = v[3];
+  }
+  L.d[32] = 0;
+  const uint32_t gi = t * 64u + lane;
+  const uint32_t q = gi & (nsegr - 1u);
+  L.rec = gi >> M.lsh;
+  L.k = nsegr - 1u - q;
+  L.fl = (gi < total ? FL_VALID : 0u) | (q == 0u ? FL_FIRST : 0u);
+}
+
+// wave-uniform base of tile t for buffer loads: the start of the record
+// holding the tile's first segment
+__device__ __forceinline__ uint64_t fixed_tile_base(const CrcParams& P, uint32_t t, uint32_t nsegr) {
+  return (uint64_t)((t * 64u) / nsegr) * P.stride;
+}
+
+template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false, bool BUF = false>
 __global__ __launch_bounds__(1024) void crc32_fixed_kernel(CrcParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   build_lds_tables(smem, P);
@@ -451,13 +538,30 @@ __global__ __launch_bounds__(1024) void crc32_fixed_kernel(CrcParams P) {
   const uint32_t niter = (ntiles - t0 + nwaves - 1u) / nwaves;  // tiles of this wave, >= 1
   uint32_t t = t0;
   SegLoad A, B;
-  seg_issue<FAST, ABLATE>(P, fixed_map(P, t, lane, nsegr, total), A);
+  if constexpr (FAST && PERCOL && BUF) {
+    const PercolMap M = percol_map(P, lane, nsegr);
+    seg_issue_percol(P, M, t, lane, nsegr, total, A);
+    for (uint32_t j = 2; j <= niter; j += 2) {
+      seg_issue_percol(P, M, t + nwaves, lane, nsegr, total, B);
+      __builtin_amdgcn_sched_barrier(0);
+      finish_tile<FAST, CHAINS, ABLATE, PERCOL>(smem, P, A, lane, lo, hi);
+      const uint32_t ta = (t + 2u * nwaves < ntiles) ? t + 2u * nwaves : t;  // past the end: reload, unused
+      seg_issue_percol(P, M, ta, lane, nsegr, total, A);
+      __builtin_amdgcn_sched_barrier(0);
+      finish_tile<FAST, CHAINS, ABLATE, PERCOL>(smem, P, B, lane, lo, hi);
+      t += 2u * nwaves;
+    }
+    if (niter & 1u) finish_tile<FAST, CHAINS, ABLATE, PERCOL>(smem, P, A, lane, lo, hi);
+    return;
+  }
+  seg_issue<FAST, ABLATE, BUF>(P, fixed_map(P, t, lane, nsegr, total), A, fixed_tile_base(P, t, nsegr));
   for (uint32_t j = 2; j <= niter; j += 2) {
-    seg_issue<FAST, ABLATE>(P, fixed_map(P, t + nwaves, lane, nsegr, total), B);
+    const uint32_t tb = t + nwaves;
+    seg_issue<FAST, ABLATE, BUF>(P, fixed_map(P, tb, lane, nsegr, total), B, fixed_tile_base(P, tb, nsegr));
     __builtin_amdgcn_sched_barrier(0);
     finish_tile<FAST, CHAINS, ABLATE, PERCOL>(smem, P, A, lane, lo, hi);
     const uint32_t ta = (t + 2u * nwaves < ntiles) ? t + 2u * nwaves : t;  // past the end: reload, unused
-    seg_issue<FAST, ABLATE>(P, fixed_map(P, ta, lane, nsegr, total), A);
+    seg_issue<FAST, ABLATE, BUF>(P, fixed_map(P, ta, lane, nsegr, total), A, fixed_tile_base(P, ta, nsegr));
     __builtin_amdgcn_sched_barrier(0);
     finish_tile<FAST, CHAINS, ABLATE, PERCOL>(smem, P, B, lane, lo, hi);
     t += 2u * nwaves;
@@ -808,13 +912,13 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_phase3(const uint32_t* __rest
 using namespace lsmck;
 
 
-template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
+template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false, bool BUF = false>
 static int launch_fixed(const CrcParams* P, int ncu, hipStream_t st) {
   size_t lds = LDS_SCRATCH_OFF;
-  hipError_t e = hipFuncSetAttribute((const void*)crc32_fixed_kernel<FAST, CHAINS, ABLATE, PERCOL>,
+  hipError_t e = hipFuncSetAttribute((const void*)crc32_fixed_kernel<FAST, CHAINS, ABLATE, PERCOL, BUF>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return -(int)e;
-  hipLaunchKernelGGL((crc32_fixed_kernel<FAST, CHAINS, ABLATE, PERCOL>), dim3(ncu), dim3(1024), lds, st, *P);
+  hipLaunchKernelGGL((crc32_fixed_kernel<FAST, CHAINS, ABLATE, PERCOL, BUF>), dim3(ncu), dim3(1024), lds, st, *P);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
 }
@@ -826,14 +930,33 @@ extern "C" int lsmk_launch_crc32_fixed(const CrcParams* P, int ncu, int variant,
   int ablate = variant >> 8;  // diagnostic ablations (results invalid): 1 loads only, 2 compute only
   if (fast && ablate == 1) return launch_fixed<true, 2, 1>(P, ncu, st);
   if (fast && ablate == 2) return launch_fixed<true, 2, 2>(P, ncu, st);
-  if (fast && ablate == 3) return launch_fixed<true, 2, 3>(P, ncu, st);
   // per-lane shift columns when every tile starts on a record boundary (and k < 2^16)
   const uint32_t nsegr = (P->flen + 127u) >> 7;
   const bool percol = (64u % nsegr) == 0 && !(variant & 0x10);  // 0x10: force the generic multiply (A/B)
+  // buffer loads: every tile's segments within 2^31 bytes of its first record
+  // (64 records of the stride); 0x40 forces global loads, 0x80 buffer loads
+  const bool buf_ok = (uint64_t)P->stride * 65u + P->flen < (1ull << 31);
+  // default: buffer loads with loop-invariant offsets where every tile starts on
+  // a record boundary (percol); per-tile offsets measured no faster than global
+  // loads (profiles/r01/ablations.md), so the other layouts keep global loads
+  const bool buf = buf_ok && ((variant & 0x80) || (LSMCK_DEFAULT_BUFLOADS && percol && !(variant & 0x40)));
+  if (fast && ablate == 3 && buf && percol) return launch_fixed<true, 2, 3, true, true>(P, ncu, st);
+  if (fast && ablate == 3 && buf) return launch_fixed<true, 2, 3, false, true>(P, ncu, st);
+  if (fast && ablate == 3) return launch_fixed<true, 2, 3>(P, ncu, st);
+  if (fast && percol && buf) {
+    if (ch == 1) return launch_fixed<true, 1, 0, true, true>(P, ncu, st);
+    if (ch == 2) return launch_fixed<true, 2, 0, true, true>(P, ncu, st);
+    return launch_fixed<true, 4, 0, true, true>(P, ncu, st);
+  }
   if (fast && percol) {
     if (ch == 1) return launch_fixed<true, 1, 0, true>(P, ncu, st);
     if (ch == 2) return launch_fixed<true, 2, 0, true>(P, ncu, st);
     return launch_fixed<true, 4, 0, true>(P, ncu, st);
+  }
+  if (fast && buf) {
+    if (ch == 1) return launch_fixed<true, 1, 0, false, true>(P, ncu, st);
+    if (ch == 2) return launch_fixed<true, 2, 0, false, true>(P, ncu, st);
+    return launch_fixed<true, 4, 0, false, true>(P, ncu, st);
   }
   if (fast) {
     if (ch == 1) return launch_fixed<true, 1>(P, ncu, st);

@@ -159,9 +159,11 @@ def test_config2_full_size_properties(ctx):
         buf.free()
 
 
-@pytest.mark.parametrize("chains,generic", [(1, 0), (2, 0), (4, 0), (2, 1)])
-def test_kernel_variants_agree(ctx, chains, generic):
-    """Every CRC-chain variant (lsmck_ctx_set_option "crc_chains") is bit-exact."""
+@pytest.mark.parametrize("chains,generic,loads", [(1, 0, 0), (2, 0, 0), (4, 0, 0), (2, 1, 0),
+                                                  (2, 0, 1), (2, 0, 2), (1, 0, 2), (4, 1, 2)])
+def test_kernel_variants_agree(ctx, chains, generic, loads):
+    """Every kernel variant (lsmck_ctx_set_option "crc_chains", "crc_generic_mul",
+    "crc_loads") is bit-exact."""
     rng = np.random.default_rng(100 + chains)
     n = 6000
     ln = rng.integers(0, 9000, n).astype(np.uint32)
@@ -170,14 +172,19 @@ def test_kernel_variants_agree(ctx, chains, generic):
     data = O.gen_stream(40 + chains, 0, total + 8)
     ctx.set_option("crc_chains", chains)
     ctx.set_option("crc_generic_mul", generic)
+    ctx.set_option("crc_loads", loads)
     try:
         got = ctx.crc32(data, off, ln)
         fixed = ctx.crc32_fixed(data, 4096, 4096, total // 4096)
         small = ctx.crc32_fixed(data, 256, 256, total // 256)
         odd = ctx.crc32_fixed(data[1:], 300, 297, (total - 8) // 300)
+        # dword-aligned, whole segments, 3 per record: records straddle tiles
+        three = ctx.crc32_fixed(data[4:], 388, 384, (total - 8) // 388)
     finally:
         ctx.set_option("crc_chains", 0)
         ctx.set_option("crc_generic_mul", 0)
+        ctx.set_option("crc_loads", 0)
+    assert np.array_equal(three, O.crc32_fixed(data[4:], 388, 384, (total - 8) // 388, threads=8))
     assert np.array_equal(small, O.crc32_fixed(data, 256, 256, total // 256, threads=8))
     assert np.array_equal(got, O.crc32_batch(data, off, ln, threads=8))
     assert np.array_equal(fixed, O.crc32_fixed(data, 4096, 4096, total // 4096, threads=8))
