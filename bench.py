@@ -151,8 +151,8 @@ def main():
                 # "c<k>" = crc_chains k;  "g<k>" = crc_chains k with the generic multiply;
                 # "a<k>" = diagnostic ablation k (timing only); optional suffix
                 # "w<n>" = crc_wg_waves n (descriptor kernel); "l<n>" = crc_loads n
-                # (1 global, 2 raw buffer)
-                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?", v)
+                # (1 global, 2 raw buffer); "r<n>" = crc_ring n (1 = two-slot kernel)
+                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?(?:r(\d))?", v)
                 if not m:
                     raise SystemExit(f"bad variant {v!r}")
                 kind, num, waves = m.group(1), int(m.group(2)), int(m.group(3) or 0)
@@ -161,6 +161,7 @@ def main():
                 ctx.set_option("crc_ablate", num if kind == "a" else 0)
                 ctx.set_option("crc_wg_waves", waves)
                 ctx.set_option("crc_loads", int(m.group(4) or 0))
+                ctx.set_option("crc_ring", int(m.group(5) or 0))
                 step()
                 e0.record(stream)
                 for _ in range(a.steps):
@@ -173,6 +174,7 @@ def main():
         ctx.set_option("crc_ablate", 0)
         ctx.set_option("crc_wg_waves", 0)
         ctx.set_option("crc_loads", 0)
+        ctx.set_option("crc_ring", 0)
         ab = {str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                        "GiBps_median": payload / GIB / (float(np.median(t)) * 1e-3)} for v, t in ab.items()}
 
@@ -233,7 +235,9 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "crc32_desc_kernel" if (cfg == 3 or a.desc) else "crc32_fixed_kernel",
+            # fixed records whose segment count divides 64 (configs 1, 2) run the
+            # whole-tile ring kernel by default (lsmck_crc32.hip, LSMCK_DEFAULT_RING)
+            "kernel": "crc32_desc_kernel" if (cfg == 3 or a.desc) else "crc32_wring_kernel",
             "algorithmic_bytes_per_launch": algo_bytes,
             "launch_ms_hip_events": round(ev_ms, 4),
         },

@@ -146,6 +146,9 @@ int lsmck_device_count(void);
  *   "crc_loads"   payload load instruction of the fixed-record CRC kernel:
  *                 1 = global_load, 2 = raw buffer_load from a per-tile base
  *                 (0 = built-in default).  A/B switch.
+ *   "crc_ring"    fixed records whose segment count divides 64 (4 KiB, 256 B ...):
+ *                 1 = two-slot kernel, 2 or 3 = whole-tile ring kernel with that
+ *                 many load slots (0 = built-in default).  A/B switch.
  * Returns 0, or LSMCK_EINVAL for an unknown key / value. */
 int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
 

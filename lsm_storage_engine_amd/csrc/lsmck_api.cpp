@@ -504,7 +504,7 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
   if (!strcmp(key, "crc_ablate")) {  // diagnostic only: timing ablations, results are garbage
     if (value < 0 || value > 7) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0..7");
     std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & 0xFF) | ((int)value << 8);
+    ctx->variant = (ctx->variant & ~0xF00) | ((int)value << 8);
     return 0;
   }
   if (!strcmp(key, "crc_wg_waves")) {  // A/B: waves per workgroup of the descriptor kernel
@@ -512,6 +512,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
       return lsmck_host::set_error(LSMCK_EINVAL, "crc_wg_waves must be 0, 12 or 16");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->variant = (ctx->variant & ~0x20) | (value == 12 ? 0x20 : 0);
+    return 0;
+  }
+  if (!strcmp(key, "crc_ring")) {  // A/B: fixed-record ring kernel (0 default, 1 two-slot kernel, 2/3 ring slots)
+    if (value < 0 || value > 3) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ring must be 0..3");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (ctx->variant & ~0xF000) | ((int)value << 12);
     return 0;
   }
   if (!strcmp(key, "crc_loads")) {  // A/B: payload load instruction, 0 default, 1 global, 2 raw buffer

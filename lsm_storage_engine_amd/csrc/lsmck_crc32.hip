@@ -61,6 +61,9 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef LSMCK_DEFAULT_BUFLOADS
 #define LSMCK_DEFAULT_BUFLOADS 1     // fixed records: raw buffer loads (A/B: profiles/r01)
 #endif
+#ifndef LSMCK_DEFAULT_RING
+#define LSMCK_DEFAULT_RING 2         // fixed percol records: whole-tile ring slots (1 = two-slot kernel; A/B: profiles/r01)
+#endif
 #ifndef LSMCK_DEFAULT_DESC_CHAINS
 #define LSMCK_DEFAULT_DESC_CHAINS 2  // descriptor records (A/B: profiles/r01)
 #endif
@@ -154,6 +157,18 @@ __device__ __forceinline__ uint32_t crc_word(const unsigned char* smem, uint32_t
 __device__ __forceinline__ uint32_t ld32(const unsigned char* p) { return *(const uint32_t*)p; }
 __device__ __forceinline__ u32x4 ld128(const unsigned char* p) { return *(const u32x4*)p; }
 
+// Keep a load's address VGPRs live past the segment's loads.  Otherwise hipcc
+// lets the last load of a segment write its data over the address register
+// (e.g. `buffer_load_dwordx4 v[34:37], v34, ... offset:112`), and that form
+// streams 14-20% slower on gfx950: tools/microbench_policy.hip measured 12.4
+// vs 10.75 ms for 64 GB with the same addresses, and 13.0 vs 10.76 ms for
+// eight per-load offsets whose registers the next tile's loads overwrite
+// (profiles/r01/ablations.md, "Load instruction form").
+template <typename T>
+__device__ __forceinline__ void keep_live(const T& x) {
+  asm volatile("" ::"v"(x));
+}
+
 struct SegInfo {
   uint32_t rec;       // record index
   uint32_t q;         // segment index from the record's front
@@ -222,6 +237,7 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
       L.d[4 * g + 2] = v[2];
       L.d[4 * g + 3] = v[3];
     }
+    keep_live(vo);
     L.d[32] = 0;
     return;
   }
@@ -234,6 +250,7 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
       L.d[4 * g + 2] = v.z;
       L.d[4 * g + 3] = v.w;
     }
+    keep_live(s0);
     L.d[32] = 0;
     return;
   }
@@ -276,6 +293,7 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
     return;
   }
   L.d[32] = ld32(w + ((sh != 0u && m == 0u) ? 128 : 124));
+  keep_live(w);
 }
 
 // Funnel, mask, raw slicing-by-4 CRC, init term, shift to the record's end.
@@ -567,6 +585,78 @@ __global__ __launch_bounds__(1024) void crc32_fixed_kernel(CrcParams P) {
     t += 2u * nwaves;
   }
   if (niter & 1u) finish_tile<FAST, CHAINS, ABLATE, PERCOL>(smem, P, A, lane, lo, hi);
+}
+
+// ---------------------------------------------------------------------------
+// Whole-tile ring: R slots of a whole segment (SegLoad), R-1 tiles in flight
+// while one is checksummed (the two-slot kernel is R = 2 with eight offset
+// VGPRs).  One offset VGPR per lane (the eight loads use immediate offsets,
+// the register kept live past them: keep_live) so that three slots fit in the
+// 128 VGPRs of a 16-wave workgroup.  The checksum is the two-slot kernel's
+// finish_tile, unchanged.
+__device__ __forceinline__ void issue_whole(const CrcParams& P, const PercolMap& M, uint32_t vo, uint32_t t,
+                                            uint32_t lane, uint32_t nsegr, uint32_t total, SegLoad& L) {
+  const uint64_t tb = (uint64_t)t * M.tstride;
+  const uint64_t left = M.end - tb;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char*>(P.base + tb), (short)0, (int)(left < 0x7FFFFFFFull ? left : 0x7FFFFFFFull), 0x00020000);
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 16u * g, 0, 0);
+    L.d[4 * g + 0] = v[0];
+    L.d[4 * g + 1] = v[1];
+    L.d[4 * g + 2] = v[2];
+    L.d[4 * g + 3] = v[3];
+  }
+  keep_live(vo);
+  L.d[32] = 0;
+  const uint32_t gi = t * 64u + lane;
+  const uint32_t q = gi & (nsegr - 1u);
+  L.rec = gi >> M.lsh;
+  L.k = nsegr - 1u - q;
+  L.fl = (gi < total ? FL_VALID : 0u) | (q == 0u ? FL_FIRST : 0u);
+}
+template <int R, int ABLATE = 0>
+__global__ __launch_bounds__(1024) void crc32_wring_kernel(CrcParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t nsegr = P.flen >> 7;
+  build_lds_tables(smem, P);
+  build_lds_cols(P, nsegr);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lo = (lane & 31u) * 4u, hi = lo | 0x10000u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t total = nsegr * (uint32_t)P.nrec;
+  const uint32_t ntiles = (total + 63u) >> 6;
+  if (wave >= ntiles) return;
+  PercolMap M;
+  M.lsh = __builtin_ctz(nsegr);
+  M.tstride = (uint64_t)(64u >> M.lsh) * P.stride;
+  M.end = (uint64_t)(P.nrec - 1) * P.stride + P.flen;
+  const uint32_t vo = (uint32_t)((lane >> M.lsh) * P.stride) + 128u * (lane & (nsegr - 1u));
+  const uint32_t mine = (ntiles - wave + nwaves - 1u) / nwaves;
+  const uint32_t iters = (mine + R - 1u) / R;
+  // tiles past the wave's last one reload its first tile (in bounds) and are
+  // marked invalid (no store)
+  auto tile_of = [&](uint32_t i) -> uint32_t { return i < mine ? wave + i * nwaves : wave; };
+  SegLoad S[R];
+#pragma unroll
+  for (int k = 0; k < R - 1; ++k) {
+    issue_whole(P, M, vo, tile_of(k), lane, nsegr, (k < (int)mine) ? total : 0u, S[k]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  uint32_t n0 = 0;
+  for (uint32_t it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const uint32_t ni = n0 + k + R - 1;
+      issue_whole(P, M, vo, tile_of(ni), lane, nsegr, ni < mine ? total : 0u, S[(k + R - 1) % R]);
+      __builtin_amdgcn_sched_barrier(0);
+      finish_tile<true, 2, ABLATE, true>(smem, P, S[k % R], lane, lo, hi);
+    }
+    n0 += R;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -923,11 +1013,22 @@ static int launch_fixed(const CrcParams* P, int ncu, hipStream_t st) {
   return e == hipSuccess ? 0 : -(int)e;
 }
 
+template <int R, int ABLATE = 0>
+static int launch_wring(const CrcParams* P, int ncu, hipStream_t st) {
+  size_t lds = LDS_SCRATCH_OFF;
+  hipError_t e = hipFuncSetAttribute((const void*)crc32_wring_kernel<R, ABLATE>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return -(int)e;
+  hipLaunchKernelGGL((crc32_wring_kernel<R, ABLATE>), dim3(ncu), dim3(1024), lds, st, *P);
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : -(int)e;
+}
+
 // variant: number of independent CRC chains per lane (1, 2, 4); 0 = default
 extern "C" int lsmk_launch_crc32_fixed(const CrcParams* P, int ncu, int variant, hipStream_t st) {
   bool fast = ((uintptr_t)P->base % 4 == 0) && (P->stride % 4 == 0) && (P->flen % 128 == 0);
   int ch = (variant & 0xF) ? (variant & 0xF) : LSMCK_DEFAULT_CHAINS;
-  int ablate = variant >> 8;  // diagnostic ablations (results invalid): 1 loads only, 2 compute only
+  int ablate = (variant >> 8) & 0xF;  // diagnostic ablations (results invalid): 1 loads only, 2 compute only
   if (fast && ablate == 1) return launch_fixed<true, 2, 1>(P, ncu, st);
   if (fast && ablate == 2) return launch_fixed<true, 2, 2>(P, ncu, st);
   // per-lane shift columns when every tile starts on a record boundary (and k < 2^16)
@@ -940,6 +1041,13 @@ extern "C" int lsmk_launch_crc32_fixed(const CrcParams* P, int ncu, int variant,
   // a record boundary (percol); per-tile offsets measured no faster than global
   // loads (profiles/r01/ablations.md), so the other layouts keep global loads
   const bool buf = buf_ok && ((variant & 0x80) || (LSMCK_DEFAULT_BUFLOADS && percol && !(variant & 0x40)));
+  // ring kernel (variant bits 12-15: 1 = the two-slot kernel below, 2 or 3 =
+  // whole-tile ring of that many slots; 0 = LSMCK_DEFAULT_RING)
+  const int ring = ((variant >> 12) & 0xF) ? ((variant >> 12) & 0xF) : LSMCK_DEFAULT_RING;
+  if (fast && percol && buf && ring >= 2 && (ablate == 0 || ablate == 3)) {
+    if (ring == 2) return ablate ? launch_wring<2, 3>(P, ncu, st) : launch_wring<2, 0>(P, ncu, st);
+    return ablate ? launch_wring<3, 3>(P, ncu, st) : launch_wring<3, 0>(P, ncu, st);
+  }
   if (fast && ablate == 3 && buf && percol) return launch_fixed<true, 2, 3, true, true>(P, ncu, st);
   if (fast && ablate == 3 && buf) return launch_fixed<true, 2, 3, false, true>(P, ncu, st);
   if (fast && ablate == 3) return launch_fixed<true, 2, 3>(P, ncu, st);
@@ -989,7 +1097,7 @@ extern "C" int lsmk_launch_crc32_desc(const CrcParams* P, const uint64_t* block_
                      block_sum, P->tile_info);
   size_t lds = LDS_SCRATCH_OFF;
   int ch = (variant & 0xF) ? (variant & 0xF) : LSMCK_DEFAULT_DESC_CHAINS;
-  int ablate = variant >> 8;
+  int ablate = (variant >> 8) & 0xF;
   // 0x20: 12-wave workgroups (168 VGPRs per lane instead of 128)
   const bool w12 = (variant & 0x20) != 0;
   const int block = w12 ? 768 : 1024;

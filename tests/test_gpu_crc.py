@@ -131,6 +131,29 @@ def test_device_generated_fixed_4k(ctx):
     assert np.array_equal(out.download(np.uint32), O.crc32_fixed(host, 4096, 4096, n, threads=8))
 
 
+@pytest.mark.parametrize("ring", [0, 1, 2, 3])
+@pytest.mark.parametrize("length,n", [(4096, (1 << 15) + 37), (256, (1 << 18) + 5), (128, 5000), (8192, 3)])
+def test_fixed_ring_depths(ctx, ring, length, n):
+    """Fixed records whose segment count divides 64 run the whole-tile ring
+    kernel ("crc_ring" 2 or 3 slots; 1 = the two-slot kernel): several tiles per
+    wave with a remainder that is not a multiple of the ring's unroll, and
+    batches where most waves have no tile."""
+    nbytes = n * length
+    d = ctx.alloc(nbytes)
+    ctx.gen_stream(d.ptr, 0x5EED0020 + length, 0, nbytes)
+    out = ctx.alloc(4 * n)
+    ctx.set_option("crc_ring", ring)
+    try:
+        ctx.crc32_fixed_device(d.ptr, length, length, n, out.ptr)
+        ctx.sync()
+    finally:
+        ctx.set_option("crc_ring", 0)
+    host = O.gen_stream(0x5EED0020 + length, 0, nbytes)
+    assert np.array_equal(out.download(np.uint32), O.crc32_fixed(host, length, length, n, threads=8))
+    d.free()
+    out.free()
+
+
 def test_config2_full_size_properties(ctx):
     """BASELINE config 2 at full size (2^24 x 4 KiB = 64 GiB, device-resident):
     (1) the fixed-record kernel and the descriptor kernel (different code
@@ -159,11 +182,12 @@ def test_config2_full_size_properties(ctx):
         buf.free()
 
 
-@pytest.mark.parametrize("chains,generic,loads", [(1, 0, 0), (2, 0, 0), (4, 0, 0), (2, 1, 0),
-                                                  (2, 0, 1), (2, 0, 2), (1, 0, 2), (4, 1, 2)])
-def test_kernel_variants_agree(ctx, chains, generic, loads):
+@pytest.mark.parametrize("chains,generic,loads,ring", [(1, 0, 0, 1), (2, 0, 0, 1), (4, 0, 0, 1), (2, 1, 0, 1),
+                                                       (2, 0, 1, 1), (2, 0, 2, 1), (1, 0, 2, 1), (4, 1, 2, 1),
+                                                       (2, 0, 2, 2), (2, 0, 2, 3), (2, 0, 0, 0)])
+def test_kernel_variants_agree(ctx, chains, generic, loads, ring):
     """Every kernel variant (lsmck_ctx_set_option "crc_chains", "crc_generic_mul",
-    "crc_loads") is bit-exact."""
+    "crc_loads", "crc_ring") is bit-exact."""
     rng = np.random.default_rng(100 + chains)
     n = 6000
     ln = rng.integers(0, 9000, n).astype(np.uint32)
@@ -173,6 +197,7 @@ def test_kernel_variants_agree(ctx, chains, generic, loads):
     ctx.set_option("crc_chains", chains)
     ctx.set_option("crc_generic_mul", generic)
     ctx.set_option("crc_loads", loads)
+    ctx.set_option("crc_ring", ring)
     try:
         got = ctx.crc32(data, off, ln)
         fixed = ctx.crc32_fixed(data, 4096, 4096, total // 4096)
@@ -184,6 +209,7 @@ def test_kernel_variants_agree(ctx, chains, generic, loads):
         ctx.set_option("crc_chains", 0)
         ctx.set_option("crc_generic_mul", 0)
         ctx.set_option("crc_loads", 0)
+        ctx.set_option("crc_ring", 0)
     assert np.array_equal(three, O.crc32_fixed(data[4:], 388, 384, (total - 8) // 388, threads=8))
     assert np.array_equal(small, O.crc32_fixed(data, 256, 256, total // 256, threads=8))
     assert np.array_equal(got, O.crc32_batch(data, off, ln, threads=8))

@@ -154,6 +154,20 @@ __global__ __launch_bounds__(1024) void k_bisect(const unsigned char* __restrict
     }
     __amdgpu_buffer_rsrc_t r = make_rsrc(base + tb);
     if (FEAT & 16) asm volatile("" : "+v"(vo));  // hide the base: offsets fold to offset:16..112
+    if (FEAT & 64) {  // eight offsets computed first, then eight back-to-back loads, no immediates
+      uint32_t o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = vo + 16 * j;
+      asm volatile("" : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]), "+v"(o[4]), "+v"(o[5]), "+v"(o[6]), "+v"(o[7]));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        auto v = __builtin_amdgcn_raw_buffer_load_b128(r, o[j], 0, 0);
+        S.v[j] = *(u32x4*)&v;
+      }
+      if (FEAT & 128)  // keep the offset VGPRs live past the loads: no load overwrites an address register
+        asm volatile("" :: "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "v"(o[4]), "v"(o[5]), "v"(o[6]), "v"(o[7]));
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       uint32_t o = vo + 16 * j;
@@ -161,6 +175,7 @@ __global__ __launch_bounds__(1024) void k_bisect(const unsigned char* __restrict
       auto v = __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0);
       S.v[j] = *(u32x4*)&v;
     }
+    if (FEAT & 128) asm volatile("" :: "v"(vo));
   };
   uint32_t acc = 0;
   uint32_t t = first;
@@ -231,10 +246,10 @@ int main(int argc, char** argv) {
   // bisection of the kernel's loads-only ablation
   uint32_t* tab; CK(hipMalloc(&tab, 4096 * 4)); CK(hipMemset(tab, 0, 4096 * 4));
   MapP M{32u, 4096u, 4096ull, tab};
-  const void* bf[] = {(const void*)k_bisect<0>, (const void*)k_bisect<16>, (const void*)k_bisect<2>,
-                      (const void*)k_bisect<32>, (const void*)k_bisect<33>};
-  const char* bn[] = {"bisect: none", "bisect: none, imm offsets", "bisect: +address map",
-                      "bisect: xcd-contiguous", "bisect: xcd-contiguous + LDS build"};
+  const void* bf[] = {(const void*)k_bisect<0>, (const void*)k_bisect<16 | 128>, (const void*)k_bisect<2 | 128>,
+                      (const void*)k_bisect<66 | 128>, (const void*)k_bisect<80 | 128>};
+  const char* bn[] = {"bisect: none", "bisect: imm offsets, addr kept", "bisect: +address map, addr kept",
+                      "bisect: +map, 8 offsets, kept", "bisect: 8 offsets then 8 loads, kept"};
   size_t LB = 156704;
   float bb[5] = {1e30f, 1e30f, 1e30f, 1e30f, 1e30f};
   for (int r = 0; r < reps; ++r) {
