@@ -34,6 +34,8 @@ from lsm_storage_engine_amd.device import Context, gen_zipf_lengths  # noqa: E40
 
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, GB/s (MI355X_MICROARCH.md chip table)
+VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # int32 lane-ops/s: 256 CU x 128 lanes/clk x 2.4 GHz
+SHA_OPS_PER_BLOCK = 1534  # VALU instructions in sha256_kernel's compression block (gfx950 ISA count)
 METRIC = "GiB/s device-resident batched record checksum; % of HBM3E read BW"
 SEED = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003}
 
@@ -53,6 +55,9 @@ def parse():
                     help="skip the host-resident (pinned H2D + kernel + D2H) sample")
     ap.add_argument("--desc", action="store_true",
                     help="diagnostic: config 2's fixed blocks through the descriptor entry point")
+    ap.add_argument("--digest", default="crc32", choices=["crc32", "sha256"],
+                    help="crc32 = the WAL record checksum (headline); sha256 = the SSTable digest "
+                         "(checksums.rs) over the same records, reported against its int32 VALU roof")
     ap.add_argument("--pack-align", type=int, default=1,
                     help="diagnostic: config 3 record offsets rounded up to this many bytes")
     return ap.parse_args()
@@ -111,9 +116,10 @@ def main():
         if A > 1:
             workload += f" [diagnostic: offsets aligned to {A} B]"
 
+    sha = a.digest == "sha256"
     data = ctx.alloc(nbytes + 64)
     ctx.gen_stream(data.ptr, seed, byte_off, nbytes, sptr)
-    out = ctx.alloc(4 * nrec)
+    out = ctx.alloc((32 if sha else 4) * nrec)
     if cfg != 3 and a.desc:  # diagnostic: the same fixed blocks as descriptors
         offs = np.arange(nrec, dtype=np.uint64) * np.uint64(rec_len)
         lens = np.full(nrec, rec_len, dtype=np.uint32)
@@ -124,15 +130,24 @@ def main():
         d_len.upload(lens)
         payload = int(lens.astype(np.uint64).sum())
 
-        def step():
-            ctx.crc32_device(data.ptr, d_off.ptr, d_len.ptr, nrec, out.ptr, sptr)
-        algo_bytes = payload + 12 * nrec + 4 * nrec
+        if sha:
+            def step():
+                ctx.sha256_device(data.ptr, d_off.ptr, d_len.ptr, nrec, out.ptr, sptr)
+            sha_blocks = int(((lens.astype(np.uint64) + 9 + 63) // 64).sum())
+        else:
+            def step():
+                ctx.crc32_device(data.ptr, d_off.ptr, d_len.ptr, nrec, out.ptr, sptr)
+        algo_bytes = payload + 12 * nrec + (32 if sha else 4) * nrec
     else:
         payload = nbytes
-
-        def step():
-            ctx.crc32_fixed_device(data.ptr, rec_len, rec_len, nrec, out.ptr, sptr)
-        algo_bytes = payload + 4 * nrec
+        if sha:
+            def step():
+                ctx.sha256_fixed_device(data.ptr, rec_len, rec_len, nrec, out.ptr, sptr)
+            sha_blocks = nrec * ((rec_len + 9 + 63) // 64)
+        else:
+            def step():
+                ctx.crc32_fixed_device(data.ptr, rec_len, rec_len, nrec, out.ptr, sptr)
+        algo_bytes = payload + (32 if sha else 4) * nrec
     torch.cuda.synchronize()
 
     for _ in range(a.warmup):
@@ -246,12 +261,34 @@ def main():
     }
     if ab is not None:
         res["variants_ab"] = ab
+    if sha:
+        # SHA-256 is bound by int32 VALU issue, not HBM: one
+        # compression = SHA_OPS_PER_BLOCK VALU lane-ops (count of the compression
+        # loop's VALU instructions in the kernel ISA), chip peak 256 CU x 128
+        # lane-ops/clk x 2.4 GHz = 78.6 T lane-ops/s (MI355X_MICROARCH.md:
+        # 157.3 TFLOPS FP32 vector = 128 FMA lanes/clk/CU).
+        ops = sha_blocks * SHA_OPS_PER_BLOCK
+        res["config"]["checksum"] = "SHA-256 per record (sha2::Sha256, checksums.rs:20-38 applied per record)"
+        res["roofline"] = {
+            "bound": "valu",
+            "achieved": round(ops / (ev_ms * 1e-3) / 1e12, 2),
+            "peak": VALU_PEAK_TOPS,
+            "unit": "Tops (int32 lane-ops/s)",
+            "frac": round(ops / (ev_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
+            "traffic": None,
+            "kernel": "sha256_kernel",
+            "compression_blocks_per_launch": sha_blocks,
+            "ops_per_block": SHA_OPS_PER_BLOCK,
+            "hbm_GBps": round(algo_bytes / (ev_ms * 1e-3) / 1e9, 1),
+            "launch_ms_hip_events": round(ev_ms, 4),
+        }
+        res["hbm_frac_of_peak"] = round(algo_bytes / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
 
     # Host round trip (north_star: the path starts and ends in host memory):
     # a sample of the same records in pinned host memory, one synchronous
     # lsmck_crc32_batch* per step = H2D DMA + kernel + D2H, chunked and
     # double-buffered inside liblsmck.  Reported beside `value`, never as it.
-    if rank == 0 and world == 1 and not a.no_host_roundtrip:
+    if rank == 0 and world == 1 and not a.no_host_roundtrip and not sha:
         if cfg == 3 or a.desc:
             hn = min(nrec, 1 << 21)
             hbytes = int(offs[hn - 1]) + int(lens[hn - 1])
@@ -285,7 +322,30 @@ def main():
         pb.free()
 
     # CPU baseline + parity of the same sample (rank 0, N = 1 only)
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and sha:
+        from oracle import oracle as O  # the checker / baseline, never the measured path
+        ns = min(nrec, a.cpu_sample_records or (1 << 16))
+        if cfg == 3:
+            send = int(offs[ns - 1]) + int(lens[ns - 1])
+            host = O.gen_stream(seed, 0, send)
+            so, sl = offs[:ns], lens[:ns]
+        else:
+            host = O.gen_stream(seed, byte_off, ns * rec_len)
+            so = np.arange(ns, dtype=np.uint64) * np.uint64(rec_len)
+            sl = np.full(ns, rec_len, dtype=np.uint32)
+        tc0 = time.perf_counter()
+        want = O.sha256_batch(host, so, sl, threads=1)
+        tc = time.perf_counter() - tc0
+        sbytes = int(sl.astype(np.uint64).sum())
+        got = out.download(np.uint8, count=32 * ns).reshape(ns, 32)
+        res["cpu_baseline"] = {
+            "value": round(sbytes / GIB / tc, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"first {ns} records ({sbytes / GIB:.2f} GiB); oracle FIPS 180-4 SHA-256 (= sha2 0.10 "
+                      "Sha256, scalar, no SHA-NI), 1 thread",
+            "seconds": round(tc, 2),
+            "gpu_matches_on_sample": bool(np.array_equal(got, np.asarray(want).reshape(ns, 32))),
+        }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and not sha:
         from oracle import oracle as O  # the checker / baseline, never the measured path
         if cfg == 3:
             ns = a.cpu_sample_records or (1 << 21)

@@ -146,6 +146,9 @@ int lsmck_device_count(void);
  *   "crc_loads"   payload load instruction of the fixed-record CRC kernel:
  *                 1 = global_load, 2 = raw buffer_load from a per-tile base
  *                 (0 = built-in default).  A/B switch.
+ *   "sha_order"   variable-length SHA-256 batches of >= 2048 messages run in
+ *                 decreasing length order (1, default) or batch order (0).
+ *                 A/B switch; digests are identical either way.
  *   "crc_ring"    fixed records whose segment count divides 64 (4 KiB, 256 B ...):
  *                 1 = two-slot kernel, 2 or 3 = whole-tile ring kernel with that
  *                 many load slots (0 = built-in default).  A/B switch.

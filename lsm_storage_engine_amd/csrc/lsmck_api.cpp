@@ -86,10 +86,20 @@ struct DescScratch {
   uint32_t* tile_info = nullptr;  // 4 u32 per tile
   size_t cap_tf = 0;
   uint64_t* total = nullptr;  // device, 1 u64
+  // SHA-256 dispatch order (lsmck_order.hip)
+  uint16_t* sha_keys = nullptr;
+  size_t cap_keys = 0;
+  uint32_t* sha_order = nullptr;
+  size_t cap_order = 0;
+  unsigned char* sort_tmp = nullptr;
+  size_t cap_tmp = 0;
   void release() {
     if (block_sum) (void)hipFree(block_sum);
     if (tile_info) (void)hipFree(tile_info);
     if (total) (void)hipFree(total);
+    if (sha_keys) (void)hipFree(sha_keys);
+    if (sha_order) (void)hipFree(sha_order);
+    if (sort_tmp) (void)hipFree(sort_tmp);
     *this = DescScratch();
   }
 };
@@ -257,9 +267,27 @@ int crc_desc_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const 
   return 0;
 }
 
-int sha_device(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len, size_t stride,
-               uint32_t flen, size_t n, const uint32_t* order, uint8_t* out32, hipStream_t st) {
-  (void)ctx;
+// Variable-length batches of at least this many messages run in decreasing
+// length order (lsmck_order.hip); below it the sort costs more than the
+// divergence it removes.
+constexpr size_t kShaSortMin = 2048;
+
+int sha_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const uint64_t* off, const uint32_t* len,
+               size_t stride, uint32_t flen, size_t n, uint8_t* out32, hipStream_t st) {
+  const uint32_t* order = nullptr;
+  if (len && n >= kShaSortMin && !(ctx->variant & 0x10000)) {  // 0x10000: batch order (A/B)
+    if (n >= (1ull << 32)) return lsmck_host::set_error(LSMCK_EINVAL, "more than 2^32-1 messages in one batch");
+    int rc;
+    if ((rc = ensure_dev(&sc.sha_keys, &sc.cap_keys, n))) return rc;
+    if ((rc = ensure_dev(&sc.sha_order, &sc.cap_order, n))) return rc;
+    size_t tmp = 0;
+    rc = lsmk_sha_order(len, n, sc.sha_keys, sc.sha_order, nullptr, &tmp, st);
+    if (rc) return launch_rc(rc, "sha order (size query)");
+    if ((rc = ensure_dev(&sc.sort_tmp, &sc.cap_tmp, std::max<size_t>(tmp, 1)))) return rc;
+    rc = lsmk_sha_order(len, n, sc.sha_keys, sc.sha_order, sc.sort_tmp, &tmp, st);
+    if (rc) return launch_rc(rc, "sha order (radix sort)");
+    order = sc.sha_order;
+  }
   ShaParams P{};
   P.base = base;
   P.off = off;
@@ -386,9 +414,9 @@ int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
       }
     } else {
       if (J.off)
-        rc = sha_device(ctx, S.d_pay, S.d_off, S.d_len, 0, 0, cnt, nullptr, S.d_out, S.s);
+        rc = sha_device(ctx, S.scratch, S.d_pay, S.d_off, S.d_len, 0, 0, cnt, S.d_out, S.s);
       else
-        rc = sha_device(ctx, S.d_pay, nullptr, nullptr, J.stride, J.flen, cnt, nullptr, S.d_out, S.s);
+        rc = sha_device(ctx, S.scratch, S.d_pay, nullptr, nullptr, J.stride, J.flen, cnt, S.d_out, S.s);
     }
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(S.h_out, S.d_out, cnt * esz, hipMemcpyDeviceToHost, S.s));
@@ -520,6 +548,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->variant = (ctx->variant & ~0xF000) | ((int)value << 12);
     return 0;
   }
+  if (!strcmp(key, "sha_order")) {  // A/B: 1 = variable-length SHA batches in decreasing length order (default)
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "sha_order must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (ctx->variant & ~0x10000) | (value ? 0 : 0x10000);
+    return 0;
+  }
   if (!strcmp(key, "crc_loads")) {  // A/B: payload load instruction, 0 default, 1 global, 2 raw buffer
     if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_loads must be 0, 1 or 2");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -634,7 +668,7 @@ int lsmck_sha256_batch(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off,
   std::lock_guard<std::mutex> lk(ctx->mu);
   DevGuard g(ctx->dev);
   if (flags & LSMCK_DEVICE)
-    return sha_device(ctx, base, off, len, 0, 0, n, nullptr, out32, pick_stream(ctx, stream));
+    return sha_device(ctx, ctx->scratch, base, off, len, 0, 0, n, out32, pick_stream(ctx, stream));
   HostJob J{SHA, base, off, len, 0, 0, n, out32, (flags & LSMCK_HOST_PINNED) != 0};
   return run_host_job(ctx, J);
 }
@@ -647,7 +681,7 @@ int lsmck_sha256_batch_fixed(lsmck_ctx* ctx, const uint8_t* base, size_t stride,
   std::lock_guard<std::mutex> lk(ctx->mu);
   DevGuard g(ctx->dev);
   if (flags & LSMCK_DEVICE)
-    return sha_device(ctx, base, nullptr, nullptr, stride, len, n, nullptr, out32, pick_stream(ctx, stream));
+    return sha_device(ctx, ctx->scratch, base, nullptr, nullptr, stride, len, n, out32, pick_stream(ctx, stream));
   HostJob J{SHA, base, nullptr, nullptr, stride, len, n, out32, (flags & LSMCK_HOST_PINNED) != 0};
   return run_host_job(ctx, J);
 }

@@ -86,3 +86,28 @@ def test_verify_many_tree(ctx, tmp_path, golden):
     st = Checksums.verify_many(ctx, metas)
     assert st[3] == _lib.DATA_MISMATCH and st[7] == _lib.INDEX_MISMATCH and st[9] < 0
     assert sum(1 for s in st if s) == 3
+
+
+@pytest.mark.parametrize("order", [1, 0])
+def test_length_sorted_batch(ctx, order):
+    """Variable-length batches of >= 2048 messages run in decreasing length
+    order (lsmck_order.hip, "sha_order" 1) -- or batch order (0): the digests
+    land at each message's own index either way.  Zipf lengths (config 3's
+    shape) plus empty, 55/56/63/64-byte (padding edges) and > 64 KiB messages,
+    scattered and unsorted."""
+    rng = np.random.default_rng(77)
+    n = 6000
+    ln = O.gen_zipf_lengths(0x5EED0003, n).astype(np.uint32)
+    ln[:8] = [0, 1, 55, 56, 63, 64, 65, 119]
+    ln[8:12] = [70000, 131072, 200001, 65536]  # the log-spaced buckets
+    ln = ln[rng.permutation(n)]
+    off = np.zeros(n, dtype=np.uint64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.uint64) + rng.integers(0, 5, n - 1).astype(np.uint64))
+    total = int(off[-1]) + int(ln[-1])
+    data = O.gen_stream(0x5EED0031, 0, total + 8)
+    ctx.set_option("sha_order", order)
+    try:
+        got = ctx.sha256(data, off, ln)
+    finally:
+        ctx.set_option("sha_order", 1)
+    assert np.array_equal(got, O.sha256_batch(data, off, ln, threads=8))
