@@ -34,8 +34,12 @@ from lsm_storage_engine_amd.device import Context, gen_zipf_lengths  # noqa: E40
 
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, GB/s (MI355X_MICROARCH.md chip table)
-VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # int32 lane-ops/s: 256 CU x 128 lanes/clk x 2.4 GHz
-SHA_OPS_PER_BLOCK = 1534  # VALU instructions in sha256_kernel's compression block (gfx950 ISA count)
+VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # full-rate VALU issue slots/s: 256 CU x 128 lanes/clk x 2.4 GHz
+# VALU issue slots per SHA-256 compression in sha256_kernel's main loop (gfx950
+# ISA: 1,553 instructions = 576 v_alignbit_b32 + 241 v_add3_u32, which issue at
+# half rate (tools/microbench_valu.hip: 62 vs 103-110 lane-ops/clk/CU for
+# v_add_u32 / v_xor_b32 / v_bitop3_b32), + 736 full-rate; 576*2 + 241*2 + 736)
+SHA_OPS_PER_BLOCK = 2370
 METRIC = "GiB/s device-resident batched record checksum; % of HBM3E read BW"
 SEED = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003}
 
@@ -273,12 +277,12 @@ def main():
             "bound": "valu",
             "achieved": round(ops / (ev_ms * 1e-3) / 1e12, 2),
             "peak": VALU_PEAK_TOPS,
-            "unit": "Tops (int32 lane-ops/s)",
+            "unit": "T VALU issue slots/s (half-rate ops count 2)",
             "frac": round(ops / (ev_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
             "traffic": None,
             "kernel": "sha256_kernel",
             "compression_blocks_per_launch": sha_blocks,
-            "ops_per_block": SHA_OPS_PER_BLOCK,
+            "slots_per_block": SHA_OPS_PER_BLOCK,
             "hbm_GBps": round(algo_bytes / (ev_ms * 1e-3) / 1e9, 1),
             "launch_ms_hip_events": round(ev_ms, 4),
         }

@@ -109,6 +109,33 @@ __device__ __forceinline__ void load_block(uintptr_t A, uint64_t len, uint64_t p
   for (int j = 0; j < 16; ++j) wle[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
 }
 
+// One whole 64-byte block of message data whose 68-byte dword window
+// [a4, a4 + 68) lies inside the message's dwords: unconditional loads (the
+// software-pipelined main loop below issues them one block ahead).
+struct ShaWin {
+  uint32_t d[17];
+};
+__device__ __forceinline__ void issue_win(const unsigned char* base, uint64_t off, uint64_t p0, ShaWin& W) {
+  const unsigned char* s = base + off + p0;  // from the kernel-argument pointer: global_load
+  const unsigned char* p = s - ((uintptr_t)s & 3);
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    u32x4 v = ld128(p + 16 * g);
+    W.d[4 * g + 0] = v.x;
+    W.d[4 * g + 1] = v.y;
+    W.d[4 * g + 2] = v.z;
+    W.d[4 * g + 3] = v.w;
+  }
+  W.d[16] = ld32(p + 64);
+  asm volatile("" ::"v"(p));  // keep the address live: no load overwrites it (lsmck_crc32.hip keep_live)
+}
+__device__ __forceinline__ void compress_win(uint32_t (&h)[8], const ShaWin& W, uint32_t sh) {
+  uint32_t w[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) w[j] = __builtin_bswap32(__builtin_amdgcn_alignbyte(W.d[j + 1], W.d[j], sh));
+  sha256_compress(h, w);
+}
+
 __global__ __launch_bounds__(256) void sha256_kernel(ShaParams P) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P.nmsg) return;
@@ -120,7 +147,42 @@ __global__ __launch_bounds__(256) void sha256_kernel(ShaParams P) {
                    0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
   const uint64_t nb = (len + 9 + 63) >> 6;
   const uint64_t bits = len << 3;
-  for (uint64_t b = 0; b < nb; ++b) {
+  // Main loop: blocks entirely of message data whose dword window stays inside
+  // the message (no masking, no padding), software pipelined: the next block's
+  // loads are in flight while this one is compressed.  A lane-per-message
+  // kernel otherwise waits a full memory round trip per block (measured 49% of
+  // the VALU roof without).  Slots A/B alternate so that no
+  // loaded register is copied; the loads past the lane's last main block
+  // reload that block (in bounds, unused).
+  const uint32_t sh = (uint32_t)(A & 3);
+  const uintptr_t end4 = (A + len + 3) & ~(uintptr_t)3;
+  const uintptr_t a40 = A & ~(uintptr_t)3;
+  // blocks b with p0 + 64 <= len and a4(b) + 68 <= end4 (a4(b) = a40 + 64b)
+  uint64_t nmain = len >> 6;
+  if (len && end4 >= a40 + 68) {
+    const uint64_t nsafe = (end4 - a40 - 68) / 64 + 1;
+    nmain = nmain < nsafe ? nmain : nsafe;
+  } else {
+    nmain = 0;
+  }
+  uint64_t b = 0;
+  if (nmain) {
+    ShaWin WA, WB;
+    issue_win(P.base, off, 0, WA);
+    for (; b + 1 < nmain; b += 2) {
+      issue_win(P.base, off, (b + 1) << 6, WB);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the compression
+      compress_win(h, WA, sh);
+      issue_win(P.base, off, (b + 2 < nmain ? b + 2 : b + 1) << 6, WA);
+      __builtin_amdgcn_sched_barrier(0);
+      compress_win(h, WB, sh);
+    }
+    if (b < nmain) {  // odd count: the last main block is in WA
+      compress_win(h, WA, sh);
+      ++b;
+    }
+  }
+  for (; b < nb; ++b) {
     const uint64_t p0 = b << 6;
     uint32_t w[16];
     load_block(A, len, p0, w);

@@ -1,0 +1,75 @@
+// VALU issue-rate microbenchmark for the SHA-256 kernel's instruction mix on
+// gfx950: lane-ops per clock per CU of v_add_u32, v_xor_b32, v_alignbit_b32,
+// v_bitop3_b32, v_add3_u32, and the SHA round mix, with 8 independent chains
+// per lane and 8 waves per SIMD.  Calibrates the "peak" of the SHA roofline.
+// Build: hipcc -O3 --offload-arch=gfx950 tools/microbench_valu.hip -o tools/microbench_valu
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
+  fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); exit(1);} } while (0)
+
+constexpr int CH = 8;     // independent chains per lane
+constexpr int UNR = 32;   // unrolled steps per loop trip
+
+// inline asm: the compiler cannot fold the chains
+template <int OP>
+__device__ __forceinline__ uint32_t step(uint32_t x, uint32_t k, uint32_t m) {
+  uint32_t r;
+  if (OP == 0) asm("v_add_u32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(k));
+  if (OP == 1) asm("v_xor_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(k));
+  if (OP == 2) asm("v_alignbit_b32 %0, %1, %1, 7" : "=v"(r) : "v"(x));
+  if (OP == 3) asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(x), "v"(k), "v"(m));
+  if (OP == 4) asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(k), "v"(m));
+  return r;
+}
+
+template <int OP>
+__global__ __launch_bounds__(512) void k_valu(uint32_t* out, int iters, uint32_t k, uint32_t m) {
+  uint32_t c[CH];
+#pragma unroll
+  for (int i = 0; i < CH; ++i) c[i] = threadIdx.x * 0x9E3779B1u + i;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+#pragma unroll
+      for (int i = 0; i < CH; ++i) c[i] = step<OP>(c[i], k + i, m);
+    }
+  }
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < CH; ++i) r ^= c[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+
+int main(int argc, char** argv) {
+  int iters = argc > 1 ? atoi(argv[1]) : 2000;
+  hipDeviceProp_t pr; CK(hipGetDeviceProperties(&pr, 0));
+  int ncu = pr.multiProcessorCount;
+  int blocks = ncu * 4;  // 4 x 512 threads = 32 waves per CU = 8 per SIMD
+  uint32_t* out; CK(hipMalloc(&out, (size_t)blocks * 512 * 4));
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  const char* names[] = {"v_add_u32", "v_xor_b32", "v_alignbit_b32", "v_bitop3_b32", "v_add3_u32"};
+  const void* fns[] = {(const void*)k_valu<0>, (const void*)k_valu<1>, (const void*)k_valu<2>,
+                       (const void*)k_valu<3>, (const void*)k_valu<4>};
+  for (int i = 0; i < 5; ++i) {
+    uint32_t k = 12345, m = 777;
+    void* args[] = {&out, &iters, &k, &m};
+    CK(hipLaunchKernel(fns[i], dim3(blocks), dim3(512), args, 0, 0));
+    CK(hipDeviceSynchronize());
+    float best = 1e30f;
+    for (int r = 0; r < 3; ++r) {
+      CK(hipEventRecord(e0));
+      CK(hipLaunchKernel(fns[i], dim3(blocks), dim3(512), args, 0, 0));
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      if (ms < best) best = ms;
+    }
+    double lane_ops = (double)blocks * 512 * iters * UNR * CH;
+    printf("%-16s : %8.3f ms  %7.2f T lane-ops/s  %6.1f lane-ops/clk/CU @2.4GHz\n", names[i], best,
+           lane_ops / best / 1e9, lane_ops / (best * 1e-3) / ncu / 2.4e9);
+  }
+  return 0;
+}
