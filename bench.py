@@ -223,7 +223,8 @@ def main():
     total_payload = payload * world
     value = total_payload / GIB / (wall_max / a.steps)
     achieved_gbs = algo_bytes / (ev_ms * 1e-3) / 1e9
-    wkey = None if (a.desc or a.pack_align > 1) else f"config{cfg}"  # diagnostics have no committed traffic
+    # diagnostics have no committed traffic
+    wkey = None if (a.desc or a.pack_align > 1) else f"{'sha256_' if sha else ''}config{cfg}"
     traffic = traffic_from_profiles(wkey)
 
     res = {
@@ -279,7 +280,7 @@ def main():
             "peak": VALU_PEAK_TOPS,
             "unit": "T VALU issue slots/s (half-rate ops count 2)",
             "frac": round(ops / (ev_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
-            "traffic": None,
+            "traffic": traffic,
             "kernel": "sha256_kernel",
             "compression_blocks_per_launch": sha_blocks,
             "slots_per_block": SHA_OPS_PER_BLOCK,

@@ -23,6 +23,13 @@ __device__ __forceinline__ uint32_t step(uint32_t x, uint32_t k, uint32_t m) {
   if (OP == 2) asm("v_alignbit_b32 %0, %1, %1, 7" : "=v"(r) : "v"(x));
   if (OP == 3) asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(x), "v"(k), "v"(m));
   if (OP == 4) asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(k), "v"(m));
+  if (OP == 5) asm("v_perm_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(k), "v"(m));
+  if (OP == 6) asm("v_alignbyte_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(k), "v"(m));
+  if (OP == 7) asm("v_bfe_i32 %0, %1, 3, 1" : "=v"(r) : "v"(x));
+  if (OP == 8) asm("v_lshl_or_b32 %0, %1, 3, %2" : "=v"(r) : "v"(x), "v"(k));
+  if (OP == 9) asm("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(k), "v"(m));
+  if (OP == 10) asm("v_cndmask_b32 %0, %1, %2, vcc" : "=v"(r) : "v"(x), "v"(k));
+  if (OP == 11) asm("v_lshrrev_b32 %0, 3, %1" : "=v"(r) : "v"(x));
   return r;
 }
 
@@ -51,10 +58,14 @@ int main(int argc, char** argv) {
   int blocks = ncu * 4;  // 4 x 512 threads = 32 waves per CU = 8 per SIMD
   uint32_t* out; CK(hipMalloc(&out, (size_t)blocks * 512 * 4));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  const char* names[] = {"v_add_u32", "v_xor_b32", "v_alignbit_b32", "v_bitop3_b32", "v_add3_u32"};
+  const char* names[] = {"v_add_u32", "v_xor_b32", "v_alignbit_b32", "v_bitop3_b32", "v_add3_u32", "v_perm_b32",
+                         "v_alignbyte_b32", "v_bfe_i32", "v_lshl_or_b32", "v_xad_u32", "v_cndmask_b32",
+                         "v_lshrrev_b32"};
   const void* fns[] = {(const void*)k_valu<0>, (const void*)k_valu<1>, (const void*)k_valu<2>,
-                       (const void*)k_valu<3>, (const void*)k_valu<4>};
-  for (int i = 0; i < 5; ++i) {
+                       (const void*)k_valu<3>, (const void*)k_valu<4>, (const void*)k_valu<5>,
+                       (const void*)k_valu<6>, (const void*)k_valu<7>, (const void*)k_valu<8>,
+                       (const void*)k_valu<9>, (const void*)k_valu<10>, (const void*)k_valu<11>};
+  for (int i = 0; i < 12; ++i) {
     uint32_t k = 12345, m = 777;
     void* args[] = {&out, &iters, &k, &m};
     CK(hipLaunchKernel(fns[i], dim3(blocks), dim3(512), args, 0, 0));

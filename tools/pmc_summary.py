@@ -29,7 +29,7 @@ def main():
     write = per_kernel(wd, "WRITE_SIZE")
     res = {}
     for k in sorted(set(fetch) | set(write)):
-        if "crc32_fixed_kernel" not in k and "crc32_desc_kernel" not in k and "sha256_kernel" not in k:
+        if not any(n in k for n in ("crc32_fixed_kernel", "crc32_wring_kernel", "crc32_desc_kernel", "sha256_kernel")):
             continue
         f = fetch.get(k, [])
         w = write.get(k, [])
