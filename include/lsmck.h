@@ -149,6 +149,9 @@ int lsmck_device_count(void);
  *   "sha_order"   variable-length SHA-256 batches of >= 2048 messages run in
  *                 decreasing length order (1, default) or batch order (0).
  *                 A/B switch; digests are identical either way.
+ *   "tree_active_files" / "tree_slice_bytes"  lsmck_checksums_verify_many's
+ *                 files in flight (0 = 8192) and bytes of a file per round
+ *                 (0 = 64 KiB; a multiple of 64).  Tests use small values.
  *   "crc_ring"    fixed records whose segment count divides 64 (4 KiB, 256 B ...):
  *                 1 = two-slot kernel, 2 or 3 = whole-tile ring kernel with that
  *                 many load slots (0 = built-in default).  A/B switch.
@@ -213,10 +216,13 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
 
 /* Whole-tree SSTable verify: the batch form of Checksums::verify over many
  * tables (Db::load, src/tokio/db.rs:37-59 -> src/tokio/sstable.rs:34).
- * Reads every data/index file, hashes all of them in one GPU batch, compares
- * with each checksum file.  status[i] gets 0 / LSMCK_DATA_MISMATCH /
- * LSMCK_INDEX_MISMATCH / -errno / LSMCK_EJSON for table i.  Returns the number
- * of tables whose status is not 0. */
+ * Streams every data/index file in slices: 8192 files in flight, 64 KiB of
+ * each per round, 16 reader threads filling one pinned slot while the GPU
+ * hashes the previous round (per-file SHA-256 state carried on the device),
+ * then compares with each checksum file.  status[i] gets 0 /
+ * LSMCK_DATA_MISMATCH / LSMCK_INDEX_MISMATCH / -errno / LSMCK_EJSON for table
+ * i (-EAGAIN: a file shrank while it was read).  Returns the number of tables
+ * whose status is not 0. */
 int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, const char* const* index_paths,
                                 const char* const* checksum_paths, size_t n, int* status);
 

@@ -75,7 +75,7 @@ SIGNATURES = [
     ("lsmck_sha256_batch", C.c_int, [vp, vp, vp, vp, sz, vp, C.c_uint, vp]),
     ("lsmck_sha256_batch_fixed", C.c_int, [vp, vp, sz, C.c_uint32, sz, vp, C.c_uint, vp]),
     ("lsmck_wal_replay_verify", C.c_int,
-     [vp, vp, sz, C.c_uint, C.POINTER(WalRec), sz, C.POINTER(sz), u64p, u32p, u32p]),
+     [vp, vp, sz, C.c_uint, vp, sz, C.POINTER(sz), u64p, u32p, u32p]),  # recs: lsmck_wal_rec[cap]
     ("lsmck_checksums_verify_many", C.c_int,
      [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), sz, C.POINTER(C.c_int)]),
     ("lsmck_dev_alloc", vp, [vp, sz]),

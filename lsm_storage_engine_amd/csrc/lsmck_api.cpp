@@ -15,9 +15,11 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "lsmck.h"
@@ -128,6 +130,11 @@ struct Stage {
   uint8_t* d_out = nullptr;
   size_t cap_d_out = 0;
   DescScratch scratch;
+  // whole-tree verify: slice descriptors of the round in this slot
+  lsmck::ShaSlice* h_slices = nullptr;
+  size_t cap_h_slices = 0;
+  lsmck::ShaSlice* d_slices = nullptr;
+  size_t cap_d_slices = 0;
   // bookkeeping of the chunk in flight
   size_t rec0 = 0, nrec = 0;
   void release() {
@@ -139,6 +146,8 @@ struct Stage {
     if (d_off) (void)hipFree(d_off);
     if (d_len) (void)hipFree(d_len);
     if (d_out) (void)hipFree(d_out);
+    if (h_slices) (void)hipHostFree(h_slices);
+    if (d_slices) (void)hipFree(d_slices);
     scratch.release();
     if (done) (void)hipEventDestroy(done);
     if (s) (void)hipStreamDestroy(s);
@@ -165,6 +174,15 @@ struct lsmck_ctx {
   unsigned long long* h_verify = nullptr;  // pinned
   Stage stage[2];
   int variant = 0;  // kernel variant for A/B timing (LSMCK_CRC_CHAINS=1|2|4); 0 = default
+  uint32_t tree_active = 0;  // whole-tree verify: files in flight (0 = kTreeActive)
+  uint32_t tree_slice = 0;   // whole-tree verify: bytes of a file per round (0 = kTreeSlice)
+  struct {
+    uint32_t* state = nullptr;  // 8 u32 per active slot
+    size_t cap_state = 0;
+    unsigned char* digests = nullptr;  // 32 B per file of the call
+    size_t cap_digests = 0;
+    hipEvent_t kernel_done = nullptr;
+  } tree;
 };
 
 namespace {
@@ -548,6 +566,19 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->variant = (ctx->variant & ~0xF000) | ((int)value << 12);
     return 0;
   }
+  if (!strcmp(key, "tree_active_files")) {  // whole-tree verify: files in flight (0 = 8192); tests use few
+    if (value < 0 || value > (1l << 20)) return lsmck_host::set_error(LSMCK_EINVAL, "tree_active_files: 0..2^20");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->tree_active = (uint32_t)value;
+    return 0;
+  }
+  if (!strcmp(key, "tree_slice_bytes")) {  // whole-tree verify: bytes per file per round (0 = 64 KiB)
+    if (value < 0 || value % 64 || value > (1l << 30))
+      return lsmck_host::set_error(LSMCK_EINVAL, "tree_slice_bytes: a multiple of 64, <= 2^30");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->tree_slice = (uint32_t)value;
+    return 0;
+  }
   if (!strcmp(key, "sha_order")) {  // A/B: 1 = variable-length SHA batches in decreasing length order (default)
     if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "sha_order must be 0 or 1");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -569,6 +600,9 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   (void)hipDeviceSynchronize();
   for (auto& S : ctx->stage) S.release();
   ctx->scratch.release();
+  if (ctx->tree.state) (void)hipFree(ctx->tree.state);
+  if (ctx->tree.digests) (void)hipFree(ctx->tree.digests);
+  if (ctx->tree.kernel_done) (void)hipEventDestroy(ctx->tree.kernel_done);
   if (ctx->d_master) (void)hipFree(ctx->d_master);
   if (ctx->d_kseg) (void)hipFree(ctx->d_kseg);
   if (ctx->d_khi) (void)hipFree(ctx->d_khi);
@@ -804,60 +838,181 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
 }
 
 // ---------------------------------------------------------------------------
-// Whole-tree SSTable verify: all data + index files hashed in one GPU batch.
-static int read_file(const char* path, std::vector<uint8_t>* buf) {
+// Whole-tree SSTable verify (Db::load: src/tokio/db.rs:37-59 -> SsTable::load
+// -> Checksums::verify, checksums.rs:40-62, for every table of the tree).
+//
+// SHA-256 is sequential inside a file, so the GPU's parallelism is the number
+// of files hashed at once: one lane hashes ~16 MB/s, a whole tree needs
+// thousands of files in flight.  The files are therefore streamed in SLICES:
+// up to kTreeActive files are open at once, and each ROUND takes the next
+// kTreeSlice bytes of every active file (its remaining bytes on its last
+// round).  Reader threads pread a round's slices into one pinned slot while
+// the GPU runs the previous round from the other; sha256_slices_kernel carries
+// each file's SHA state between rounds in a device table (32 B per active
+// slot) and writes the digest when the file's last slice is hashed.  A file
+// that finishes frees its slot for the next file of the tree.  Host memory is
+// two slots of kTreeActive * kTreeSlice bytes whatever the tree's size; the
+// digests (32 B per file) come back in one copy at the end.
+namespace {
+
+constexpr uint32_t kTreeActive = 8192;        // files in flight
+constexpr uint32_t kTreeSlice = 64u << 10;    // bytes of a file per round (multiple of 64; A/B: DESIGN.md 8)
+constexpr unsigned kTreeReaders = 16;  // the GPU box gives a process 16 CPUs
+
+// pread exactly n bytes at offset off of path into dst
+int pread_range(const char* path, uint8_t* dst, uint64_t off, uint64_t n) {
   int fd = open(path, O_RDONLY | O_CLOEXEC);
   if (fd < 0) return -errno;
-  struct stat stt;
-  if (fstat(fd, &stt) == 0 && stt.st_size > 0) buf->reserve(buf->size() + (size_t)stt.st_size);
-  uint8_t tmp[1 << 16];
-  for (;;) {
-    ssize_t k = read(fd, tmp, sizeof tmp);
+  uint64_t got = 0;
+  int rc = 0;
+  while (got < n) {
+    ssize_t k = pread(fd, dst + got, (size_t)std::min<uint64_t>(n - got, 1ull << 30), (off_t)(off + got));
     if (k < 0) {
       if (errno == EINTR) continue;
-      int e = errno;
-      close(fd);
-      return -e;
+      rc = -errno;
+      break;
     }
     if (k == 0) break;
-    buf->insert(buf->end(), tmp, tmp + k);
+    got += (uint64_t)k;
   }
   close(fd);
-  return 0;
+  if (rc == 0 && got != n) rc = -EAGAIN;  // the file shrank while the tree was read
+  return rc;
 }
+
+}  // namespace
 
 int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, const char* const* index_paths,
                                 const char* const* checksum_paths, size_t n, int* status) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
-  std::vector<uint8_t> blob;
-  std::vector<uint64_t> off(2 * n, 0);
-  std::vector<uint32_t> len(2 * n, 0);
+  if (n && (!data_paths || !index_paths || !checksum_paths || !status))
+    return lsmck_host::set_error(LSMCK_EINVAL, "null path array or status");
+  if (2 * n >= (1ull << 32)) return lsmck_host::set_error(LSMCK_EINVAL, "too many tables");
+  // file 2i = table i's data file, 2i+1 its index file
+  const size_t nf = 2 * n;
+  std::vector<const char*> paths(nf);
+  std::vector<uint64_t> fsize(nf, 0);
+  std::vector<int> ferr(nf, 0);
   for (size_t i = 0; i < n; ++i) {
-    status[i] = 0;
-    for (int w = 0; w < 2; ++w) {
-      const char* p = w == 0 ? data_paths[i] : index_paths[i];
-      size_t before = blob.size();
-      int e = read_file(p, &blob);
-      if (e) {
-        if (!status[i]) status[i] = e;
-        blob.resize(before);
-      }
-      if (blob.size() - before > 0xFFFFFFFFull) {
-        status[i] = LSMCK_EINVAL;
-        blob.resize(before);
-      }
-      off[2 * i + w] = before;
-      len[2 * i + w] = (uint32_t)(blob.size() - before);
-    }
+    paths[2 * i] = data_paths[i];
+    paths[2 * i + 1] = index_paths[i];
   }
-  std::vector<uint8_t> dig(64 * n);
-  if (n) {
-    rc = lsmck_sha256_batch(ctx, blob.data(), off.data(), len.data(), 2 * n, dig.data(), LSMCK_HOST, nullptr);
-    if (rc) return rc;
+  for (size_t f = 0; f < nf; ++f) {
+    struct stat st;
+    if (stat(paths[f], &st) != 0) ferr[f] = -errno;
+    else fsize[f] = (uint64_t)st.st_size;
+  }
+  const uint32_t active_max = ctx->tree_active ? ctx->tree_active : kTreeActive;
+  const uint32_t slice = ctx->tree_slice ? ctx->tree_slice : kTreeSlice;
+  std::vector<uint8_t> dig(32 * std::max<size_t>(nf, 1), 0);
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard g(ctx->dev);
+    for (auto& S : ctx->stage)
+      if ((rc = stage_init(S))) return rc;
+    auto& T = ctx->tree;
+    if ((rc = ensure_dev(&T.state, &T.cap_state, 8ull * active_max))) return rc;
+    if ((rc = ensure_dev(&T.digests, &T.cap_digests, 32 * std::max<size_t>(nf, 1)))) return rc;
+    if (!T.kernel_done) HIPCHK(hipEventCreateWithFlags(&T.kernel_done, hipEventDisableTiming));
+    // active slots: file index and bytes already scheduled
+    std::vector<size_t> slot_file(active_max, SIZE_MAX);
+    std::vector<uint64_t> slot_done(active_max, 0);
+    std::vector<uint32_t> free_slots;
+    for (uint32_t k = active_max; k-- > 0;) free_slots.push_back(k);
+    size_t next_file = 0, active = 0;
+    bool busy[2] = {false, false}, any_kernel = false;
+    int sl = 0;
+    std::vector<uint64_t> rd_off;  // per slice: offset inside its file
+    for (;;) {
+      // admit files into free slots
+      while (!free_slots.empty() && next_file < nf) {
+        const size_t f = next_file++;
+        if (ferr[f]) continue;
+        const uint32_t k = free_slots.back();
+        free_slots.pop_back();
+        slot_file[k] = f;
+        slot_done[k] = 0;
+        ++active;
+      }
+      if (active == 0) break;
+      // the round's slices: the next `slice` bytes of every active file
+      Stage& S = ctx->stage[sl];
+      if (busy[sl]) {
+        HIPCHK(hipEventSynchronize(S.done));
+        busy[sl] = false;
+      }
+      std::vector<lsmck::ShaSlice> sv;
+      sv.reserve(active);
+      rd_off.clear();
+      uint64_t pay = 0;
+      for (uint32_t k = 0; k < active_max; ++k) {
+        if (slot_file[k] == SIZE_MAX) continue;
+        const size_t f = slot_file[k];
+        const uint64_t left = fsize[f] - slot_done[k];
+        const uint32_t len = (uint32_t)std::min<uint64_t>(left, slice);
+        lsmck::ShaSlice d{};
+        d.off = pay;
+        d.total = fsize[f];
+        d.len = len;
+        d.slot = k;
+        d.msg = (uint32_t)f;
+        d.flags = (slot_done[k] == 0 ? SHA_SLICE_FIRST : 0u) | (len == left ? SHA_SLICE_LAST : 0u);
+        sv.push_back(d);
+        rd_off.push_back(slot_done[k]);
+        pay += len;
+        slot_done[k] += len;
+        if (len == left) {  // last slice scheduled: the slot is free for the next round
+          slot_file[k] = SIZE_MAX;
+          free_slots.push_back(k);
+          --active;
+        }
+      }
+      const size_t cnt = sv.size();
+      if ((rc = ensure_pinned(&S.h_pay, &S.cap_h_pay, pay + 16))) return rc;
+      if ((rc = ensure_pinned(&S.h_slices, &S.cap_h_slices, cnt))) return rc;
+      if ((rc = ensure_dev(&S.d_pay, &S.cap_d_pay, pay + 16))) return rc;
+      if ((rc = ensure_dev(&S.d_slices, &S.cap_d_slices, cnt))) return rc;
+      memcpy(S.h_slices, sv.data(), cnt * sizeof(lsmck::ShaSlice));
+      // read the slices (overlaps the other slot's GPU work, already queued)
+      std::atomic<size_t> next{0};
+      auto work = [&]() {
+        for (size_t j; (j = next.fetch_add(1)) < cnt;) {
+          const lsmck::ShaSlice& d = sv[j];
+          int e = pread_range(paths[d.msg], S.h_pay + d.off, rd_off[j], d.len);
+          if (e) ferr[d.msg] = e;
+        }
+      };
+      const unsigned nt = (unsigned)std::min<size_t>(kTreeReaders, cnt);
+      std::vector<std::thread> th;
+      for (unsigned t = 1; t < nt; ++t) th.emplace_back(work);
+      work();
+      for (auto& t : th) t.join();
+      HIPCHK(hipMemcpyAsync(S.d_pay, S.h_pay, pay, hipMemcpyHostToDevice, S.s));
+      HIPCHK(hipMemcpyAsync(S.d_slices, S.h_slices, cnt * sizeof(lsmck::ShaSlice), hipMemcpyHostToDevice, S.s));
+      // the state carried between rounds orders the kernels across the two streams
+      if (any_kernel) HIPCHK(hipStreamWaitEvent(S.s, T.kernel_done, 0));
+      lsmck::ShaSliceParams P{};
+      P.base = S.d_pay;
+      P.slices = S.d_slices;
+      P.nslices = cnt;
+      P.state = T.state;
+      P.out = T.digests;
+      rc = lsmk_launch_sha256_slices(&P, S.s);
+      if (rc) return launch_rc(rc, "sha256 slices kernel");
+      HIPCHK(hipEventRecord(T.kernel_done, S.s));
+      HIPCHK(hipEventRecord(S.done, S.s));
+      busy[sl] = true;
+      any_kernel = true;
+      sl ^= 1;
+    }
+    for (int k = 0; k < 2; ++k)
+      if (busy[k]) HIPCHK(hipEventSynchronize(ctx->stage[k].done));
+    if (nf) HIPCHK(hipMemcpy(dig.data(), T.digests, 32 * nf, hipMemcpyDeviceToHost));
   }
   int bad = 0;
   for (size_t i = 0; i < n; ++i) {
+    status[i] = ferr[2 * i] ? ferr[2 * i] : ferr[2 * i + 1];
     if (status[i] == 0) {
       char db[45], ib[45];
       lsmck_base64_encode(&dig[64 * i], 32, db);
@@ -865,7 +1020,7 @@ int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, c
       std::string wi, wd;
       int e = lsmck_host::read_checksum_json(checksum_paths[i], &wi, &wd);
       if (e) status[i] = e;
-      else if (wd != db) status[i] = LSMCK_DATA_MISMATCH;
+      else if (wd != db) status[i] = LSMCK_DATA_MISMATCH;  // data first, as checksums.rs:49-60
       else if (wi != ib) status[i] = LSMCK_INDEX_MISMATCH;
     }
     if (status[i]) ++bad;

@@ -38,6 +38,25 @@ struct ShaParams {
   unsigned char* out;         // 32 bytes per message
 };
 
+// One slice of a message streamed through sha256_slices_kernel.
+#define SHA_SLICE_FIRST 1u
+#define SHA_SLICE_LAST 2u
+struct ShaSlice {
+  uint64_t off;    // slice bytes at base + off
+  uint64_t total;  // the message's length (used on its last slice)
+  uint32_t len;    // slice bytes: a multiple of 64 unless it is the message's last slice
+  uint32_t slot;   // state slot (8 u32) carrying the message between slices
+  uint32_t msg;    // message index: digest at out + 32 * msg
+  uint32_t flags;  // SHA_SLICE_FIRST | SHA_SLICE_LAST
+};
+struct ShaSliceParams {
+  const unsigned char* base;
+  const ShaSlice* slices;
+  uint64_t nslices;
+  uint32_t* state;
+  unsigned char* out;
+};
+
 }  // namespace lsmck
 
 extern "C" {
@@ -46,6 +65,7 @@ uint64_t lsmk_scan_block_count(uint64_t n);
 int lsmk_launch_crc32_scan(const lsmck::CrcParams* P, uint64_t* block_sum, hipStream_t st);
 int lsmk_launch_crc32_desc(const lsmck::CrcParams* P, const uint64_t* block_sum, int ncu, int variant, hipStream_t st);
 int lsmk_launch_sha256(const lsmck::ShaParams* P, hipStream_t st);
+int lsmk_launch_sha256_slices(const lsmck::ShaSliceParams* P, hipStream_t st);
 int lsmk_launch_crc32_compare(const uint32_t* crc, const uint32_t* expected, uint64_t n,
                                unsigned long long* n_bad, unsigned long long* first_bad, hipStream_t st);
 int lsmk_sha_order(const uint32_t* len, size_t n, uint16_t* keys_out, uint32_t* order, void* tmp, size_t* tmp_bytes,

@@ -136,17 +136,15 @@ __device__ __forceinline__ void compress_win(uint32_t (&h)[8], const ShaWin& W, 
   sha256_compress(h, w);
 }
 
-__global__ __launch_bounds__(256) void sha256_kernel(ShaParams P) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P.nmsg) return;
-  uint64_t m = P.order ? P.order[i] : i;
-  uint64_t off = P.off ? P.off[m] : m * P.stride;
-  uint64_t len = P.len ? P.len[m] : P.flen;
-  const uintptr_t A = (uintptr_t)(P.base + off);
-  uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
-                   0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-  const uint64_t nb = (len + 9 + 63) >> 6;
-  const uint64_t bits = len << 3;
+// Runs the compression over `len` bytes at base + off into h.  last: these are
+// the message's final bytes -- pad and append the bit length `bits` of the
+// whole message (the slice starts on a 64-byte boundary of the message).  Not
+// last: len is a multiple of 64 and no padding is added (a slice of a message
+// streamed through sha256_slices_kernel).
+__device__ __forceinline__ void sha256_run(uint32_t (&h)[8], const unsigned char* base, uint64_t off, uint64_t len,
+                                           bool last, uint64_t bits) {
+  const uintptr_t A = (uintptr_t)(base + off);
+  const uint64_t nb = last ? (len + 9 + 63) >> 6 : len >> 6;
   // Main loop: blocks entirely of message data whose dword window stays inside
   // the message (no masking, no padding), software pipelined: the next block's
   // loads are in flight while this one is compressed.  A lane-per-message
@@ -168,12 +166,12 @@ __global__ __launch_bounds__(256) void sha256_kernel(ShaParams P) {
   uint64_t b = 0;
   if (nmain) {
     ShaWin WA, WB;
-    issue_win(P.base, off, 0, WA);
+    issue_win(base, off, 0, WA);
     for (; b + 1 < nmain; b += 2) {
-      issue_win(P.base, off, (b + 1) << 6, WB);
+      issue_win(base, off, (b + 1) << 6, WB);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the compression
       compress_win(h, WA, sh);
-      issue_win(P.base, off, (b + 2 < nmain ? b + 2 : b + 1) << 6, WA);
+      issue_win(base, off, (b + 2 < nmain ? b + 2 : b + 1) << 6, WA);
       __builtin_amdgcn_sched_barrier(0);
       compress_win(h, WB, sh);
     }
@@ -198,17 +196,64 @@ __global__ __launch_bounds__(256) void sha256_kernel(ShaParams P) {
     }
 #pragma unroll
     for (int t = 0; t < 16; ++t) w[t] = __builtin_bswap32(w[t]);
-    if (b == nb - 1) {
+    if (last && b == nb - 1) {
       w[14] = (uint32_t)(bits >> 32);
       w[15] = (uint32_t)bits;
     }
     sha256_compress(h, w);
   }
-  u32x4* o = (u32x4*)(P.out + 32 * m);
+}
+
+__device__ __forceinline__ void sha256_iv(uint32_t (&h)[8]) {
+  h[0] = 0x6a09e667u; h[1] = 0xbb67ae85u; h[2] = 0x3c6ef372u; h[3] = 0xa54ff53au;
+  h[4] = 0x510e527fu; h[5] = 0x9b05688cu; h[6] = 0x1f83d9abu; h[7] = 0x5be0cd19u;
+}
+
+__device__ __forceinline__ void store_digest(unsigned char* out, const uint32_t (&h)[8]) {
+  u32x4* o = (u32x4*)out;
   u32x4 o0 = {__builtin_bswap32(h[0]), __builtin_bswap32(h[1]), __builtin_bswap32(h[2]), __builtin_bswap32(h[3])};
   u32x4 o1 = {__builtin_bswap32(h[4]), __builtin_bswap32(h[5]), __builtin_bswap32(h[6]), __builtin_bswap32(h[7])};
   o[0] = o0;
   o[1] = o1;
+}
+
+__global__ __launch_bounds__(256) void sha256_kernel(ShaParams P) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.nmsg) return;
+  uint64_t m = P.order ? P.order[i] : i;
+  uint64_t off = P.off ? P.off[m] : m * P.stride;
+  uint64_t len = P.len ? P.len[m] : P.flen;
+  uint32_t h[8];
+  sha256_iv(h);
+  sha256_run(h, P.base, off, len, true, len << 3);
+  store_digest(P.out + 32 * m, h);
+}
+
+// Many messages streamed in slices (whole-tree verify, lsmck_api.cpp): slice i
+// continues message D[i].msg from its state slot (or from the IV on the
+// message's first slice) over D[i].len bytes, then either stores the state
+// back or, on the message's last slice, finishes it and writes its digest.
+// One lane per slice, one 64-lane wave per workgroup: a round holds at most a
+// few thousand slices, spread over as many CUs as possible.
+__global__ __launch_bounds__(64) void sha256_slices_kernel(ShaSliceParams P) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.nslices) return;
+  const ShaSlice d = P.slices[i];
+  uint32_t h[8];
+  if (d.flags & SHA_SLICE_FIRST) {
+    sha256_iv(h);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = P.state[8u * d.slot + k];
+  }
+  const bool last = (d.flags & SHA_SLICE_LAST) != 0;
+  sha256_run(h, P.base, d.off, d.len, last, d.total << 3);
+  if (last) {
+    store_digest(P.out + 32ull * d.msg, h);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) P.state[8u * d.slot + k] = h[k];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -254,6 +299,14 @@ extern "C" int lsmk_launch_sha256(const ShaParams* P, hipStream_t st) {
   if (P->nmsg == 0) return 0;
   uint64_t blocks = (P->nmsg + 255) / 256;
   hipLaunchKernelGGL(sha256_kernel, dim3((unsigned)blocks), dim3(256), 0, st, *P);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -(int)e;
+}
+
+extern "C" int lsmk_launch_sha256_slices(const ShaSliceParams* P, hipStream_t st) {
+  if (P->nslices == 0) return 0;
+  uint64_t blocks = (P->nslices + 63) / 64;
+  hipLaunchKernelGGL(sha256_slices_kernel, dim3((unsigned)blocks), dim3(64), 0, st, *P);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
 }

@@ -208,13 +208,15 @@ class Context:
             ptr, n, flags = img.ctypes.data, len(img), _lib.HOST
         else:
             ptr, n, flags = device_ptr, image, _lib.DEVICE
-        cap = n // 9 + 1
-        recs = (_lib.WalRec * cap)()
+        cap = n // 9 + 1  # a record is at least 9 bytes (Remove of an empty key)
+        recs = np.empty(cap, dtype=WAL_REC_DTYPE)  # lsmck_wal_rec[cap], uninitialised: no 32-B-per-slot zeroing
         nrec = C.c_size_t()
         bi, bc, be = C.c_uint64(), C.c_uint32(), C.c_uint32()
-        rc = _lib.check(self.lib.lsmck_wal_replay_verify(self.handle, ptr, n, flags, recs, cap, C.byref(nrec),
-                                                         C.byref(bi), C.byref(bc), C.byref(be)), "wal_replay_verify")
-        return list(recs[:nrec.value]), rc, (bi.value, bc.value, be.value)
+        rc = _lib.check(self.lib.lsmck_wal_replay_verify(self.handle, ptr, n, flags, recs.ctypes.data, cap,
+                                                         C.byref(nrec), C.byref(bi), C.byref(bc), C.byref(be)),
+                        "wal_replay_verify")
+        # np.recarray: record fields read as attributes (r.payload_off), like the ctypes struct
+        return recs[:nrec.value].view(np.recarray), rc, (bi.value, bc.value, be.value)
 
     def checksums_verify_many(self, triples):
         n = len(triples)
@@ -225,6 +227,12 @@ class Context:
         status = (C.c_int * max(n, 1))()
         _lib.check(self.lib.lsmck_checksums_verify_many(self.handle, d, i, c, n, status), "checksums_verify_many")
         return list(status[:n])
+
+
+# include/lsmck.h lsmck_wal_rec (32 bytes, no padding)
+WAL_REC_DTYPE = np.dtype([("rec_off", "<u8"), ("payload_off", "<u8"), ("klen", "<u4"), ("vlen", "<u4"),
+                          ("crc", "<u4"), ("type", "<u4")])
+assert WAL_REC_DTYPE.itemsize == C.sizeof(_lib.WalRec)
 
 
 def device_count():

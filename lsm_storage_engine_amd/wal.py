@@ -173,14 +173,14 @@ class CommandLog:
         if status == _lib.WAL_BAD_TYPE:
             raise InvalidCommandType(bad[1])
         out = []
-        for r in records:
-            k0 = r.payload_off
-            key = img[k0:k0 + r.klen]
-            if r.type == INSERT:
-                out.append(Insert(key, img[k0 + r.klen:k0 + r.klen + r.vlen]))
+        for k0, kl, vl, t in zip(records.payload_off.tolist(), records.klen.tolist(), records.vlen.tolist(),
+                                 records.type.tolist()):
+            key = img[k0:k0 + kl]
+            if t == INSERT:
+                out.append(Insert(key, img[k0 + kl:k0 + kl + vl]))
             else:
                 out.append(Remove(key))
-        consumed = (records[-1].payload_off + records[-1].klen + records[-1].vlen) if records else 0
+        consumed = int(records[-1].payload_off + records[-1].klen + records[-1].vlen) if len(records) else 0
         self.file.seek(pos + consumed)
         return out
 

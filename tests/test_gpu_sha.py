@@ -88,6 +88,47 @@ def test_verify_many_tree(ctx, tmp_path, golden):
     assert sum(1 for s in st if s) == 3
 
 
+@pytest.mark.parametrize("active,slice_bytes", [(0, 0), (7, 4096), (64, 64), (1, 1 << 20)])
+def test_verify_many_streaming(ctx, tmp_path, active, slice_bytes):
+    """The slice-streamed whole-tree verify (defaults: 8192 files in flight,
+    64 KiB per round; then few files in flight and small slices, so files span
+    many rounds, slots are reused, and one slice per round): 300 tables of
+    0..300 KiB data files, empty files, a 3 MiB table, a missing data file, a
+    missing checksum file and single-byte corruptions.  Checksum files are
+    written by the oracle (FIPS SHA-256 + base64 + the checksums.rs JSON)."""
+    rng = np.random.default_rng(11)
+    metas = []
+    for t in range(300):
+        m = SsTableMetadata.new(str(tmp_path), t % 5, timestamp_ms=5000 + t)
+        os.makedirs(os.path.dirname(m.data_path()), exist_ok=True)
+        n = 0 if t % 37 == 0 else (3 << 20) + 7 if t == 150 else int(rng.integers(1, 300 << 10))
+        with open(m.data_path(), "wb") as f:
+            f.write(O.gen_stream(900 + t, 0, n).tobytes())
+        with open(m.index_path(), "wb") as f:
+            f.write(O.gen_stream(70000 + t, 0, int(rng.integers(0, 2000))).tobytes())
+        with open(m.checksum_path(), "w") as f:
+            f.write(O.checksums_json(O.file_checksum(m.index_path()), O.file_checksum(m.data_path())))
+        metas.append(m)
+    ctx.set_option("tree_active_files", active)
+    ctx.set_option("tree_slice_bytes", slice_bytes)
+    try:
+        assert Checksums.verify_many(ctx, metas) == [0] * 300
+        with open(metas[150].data_path(), "r+b") as f:  # the large table, last byte
+            f.seek((3 << 20) + 6)
+            f.write(b"\x00" if f.read(1) != b"\x00" else b"\x01")
+        with open(metas[201].index_path(), "ab") as f:
+            f.write(b"+")
+        os.remove(metas[77].data_path())
+        os.remove(metas[78].checksum_path())
+        st = Checksums.verify_many(ctx, metas)
+    finally:
+        ctx.set_option("tree_active_files", 0)
+        ctx.set_option("tree_slice_bytes", 0)
+    assert st[150] == _lib.DATA_MISMATCH and st[201] == _lib.INDEX_MISMATCH
+    assert st[77] < 0 and st[78] < 0
+    assert sum(1 for s in st if s) == 4
+
+
 @pytest.mark.parametrize("order", [1, 0])
 def test_length_sorted_batch(ctx, order):
     """Variable-length batches of >= 2048 messages run in decreasing length

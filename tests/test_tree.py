@@ -1,0 +1,106 @@
+"""Config 5 (end-to-end tree load verify): the synthetic tree is in the
+reference's on-disk layout (checked against the oracle on CPU), and
+load_verify() reproduces Db::load's checksum behaviour on the GPU (first bad
+table panics naming its data / index file, a corrupted WAL Insert is
+WalError::CorruptedData)."""
+import json
+import os
+import struct
+
+import pytest
+
+from lsm_storage_engine_amd import tree
+from lsm_storage_engine_amd.checksums import ChecksumPanic
+from lsm_storage_engine_amd.wal import CorruptedData
+from oracle import oracle as O
+
+
+@pytest.fixture(scope="module")
+def small_tree(tmp_path_factory):
+    base = str(tmp_path_factory.mktemp("tree"))
+    info = tree.synthesize_tree(base, 6 << 20, wal_records=3000, threads=4)
+    return base, info
+
+
+def test_tree_layout_matches_oracle(small_tree):
+    base, info = small_tree
+    metas = tree.list_tables(base)
+    assert len(metas) == info["tables"] and len(metas) >= tree.SSTABLE_MAX_LEVEL
+    assert [m.level for m in metas] == sorted(m.level for m in metas)
+    total = 0
+    for m in metas:
+        with open(m.checksum_path()) as f:
+            cj = f.read()
+        # checksums.rs:64-80 JSON, digests by the oracle (FIPS SHA-256 + base64 STANDARD)
+        assert cj == O.checksums_json(O.file_checksum(m.index_path()), O.file_checksum(m.data_path()))
+        data = open(m.data_path(), "rb").read()
+        pos, n, keys = 0, 0, []
+        while pos < len(data):  # datafile.rs:27-35 records fill the file exactly
+            kl, vl = struct.unpack_from("<II", data, pos)
+            keys.append((data[pos + 8:pos + 8 + kl], pos))
+            pos += 8 + kl + vl
+            n += 1
+        assert pos == len(data)
+        assert [k for k, _ in keys] == sorted(k for k, _ in keys)
+        idx = open(m.index_path(), "rb").read()  # bincode BTreeMap<Vec<u8>, u64>
+        cnt = struct.unpack_from("<Q", idx, 0)[0]
+        assert cnt == (n + tree.INDEX_STEP - 1) // tree.INDEX_STEP
+        p = 8
+        for i in range(cnt):
+            kl = struct.unpack_from("<Q", idx, p)[0]
+            key = idx[p + 8:p + 8 + kl]
+            off = struct.unpack_from("<Q", idx, p + 8 + kl)[0]
+            assert (key, off) == keys[i * tree.INDEX_STEP]
+            p += 16 + kl
+        assert p == len(idx)
+        meta = json.load(open(m.metadata_path()))
+        assert list(meta) == ["base_path", "id", "level", "metadata_filename", "checksum_filename",
+                              "data_filename", "index_filename", "bloom_filter_filename"]
+        total += len(data) + len(idx)
+    assert total == info["table_bytes"]
+    st, recs, _ = O.wal_replay(open(os.path.join(base, "wal", "wal.log"), "rb").read())
+    assert st == 0 and len(recs) == 3000
+
+
+@pytest.mark.gpu
+def test_load_verify_clean_and_corrupted(ctx, small_tree, tmp_path):
+    import shutil
+    base = str(tmp_path / "t")
+    shutil.copytree(small_tree[0], base)
+    metas = tree.list_tables(base)
+    for m in metas:  # metadata base_path points at the original tree: rewrite it
+        d = json.load(open(m.metadata_path()))
+        d["base_path"] = base
+        with open(m.metadata_path(), "w") as f:
+            f.write(json.dumps(d, separators=(",", ":")))
+    mem, rep = tree.load_verify(ctx, base)
+    assert rep["tables"] == len(metas) and rep["wal_records"] == 3000
+    _, recs, _ = O.wal_replay(open(os.path.join(base, "wal", "wal.log"), "rb").read())
+    assert mem.size() <= 3000 and mem.size() > 0
+    # the second table's index file corrupted: panic naming the index file
+    metas = tree.list_tables(base)
+    with open(metas[1].index_path(), "r+b") as f:
+        f.seek(9)
+        f.write(b"\xff")
+    with pytest.raises(ChecksumPanic, match=metas[1].index_filename):
+        tree.load_verify(ctx, base)
+    # ... and the first table's data file too: the first table in load order wins
+    with open(metas[0].data_path(), "r+b") as f:
+        f.seek(100)
+        f.write(b"\x00\x01\x02")
+    with pytest.raises(ChecksumPanic, match=metas[0].data_filename):
+        tree.load_verify(ctx, base)
+
+
+@pytest.mark.gpu
+def test_load_verify_corrupted_wal(ctx, tmp_path):
+    base = str(tmp_path / "w")
+    tree.synthesize_tree(base, 1 << 20, wal_records=500, threads=2)
+    wal = os.path.join(base, "wal", "wal.log")
+    img = bytearray(open(wal, "rb").read())
+    st, recs, _ = O.wal_replay(bytes(img))
+    ins = [r for r in recs if r.type == 1 and r.klen + r.vlen > 0]
+    img[ins[10].payload_off] ^= 0x40  # flip a payload bit of the 11th non-empty Insert
+    open(wal, "wb").write(bytes(img))
+    with pytest.raises(CorruptedData):
+        tree.load_verify(ctx, base)

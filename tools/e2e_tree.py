@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""BASELINE config 5, end to end: the checksum work of Db::load over an LSM tree
+on disk -- every SSTable's data + index file SHA-256-verified against its
+checksum file, and the WAL replayed with every record's CRC-32 checked
+(lsm_storage_engine_amd/tree.py; src/tokio/db.rs:37-73).
+
+  python3 tools/e2e_tree.py [--gib 16] [--dir /tmp/lsm_e2e] [--reps 3] [--keep]
+
+Writes a synthetic tree in the reference's on-disk layout (if --dir does not
+already hold one), then times load_verify() --reps times with the page cache
+warm (the tree was just written; dropping caches needs root, which the GPU box
+does not give).  Prints one JSON line.  The rate includes reading the files
+(16 reader threads, pread), the PCIe copies and the GPU batches; it is not a
+device-resident number.  A CPU baseline (the oracle's FIPS SHA-256, one
+thread, on the first tables) is timed beside it.
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import time
+
+import numpy as np
+import torch  # noqa: F401  (first: liblsmck binds to torch's HIP runtime)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from lsm_storage_engine_amd.device import Context  # noqa: E402
+from lsm_storage_engine_amd import tree  # noqa: E402
+
+GIB = float(1 << 30)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gib", type=float, default=16.0, help="SSTable data bytes of the tree (GiB)")
+    ap.add_argument("--dir", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "lsm_e2e"))
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--wal-records", type=int, default=500_000)
+    ap.add_argument("--keep", action="store_true")
+    ap.add_argument("--cpu-sample-gib", type=float, default=1.0)
+    ap.add_argument("--ab", default="", help="comma list of active:slice_bytes settings to A/B after the main reps")
+    a = ap.parse_args()
+
+    marker = os.path.join(a.dir, "e2e_tree.json")
+    if os.path.exists(marker):
+        with open(marker) as f:
+            synth = json.load(f)
+    else:
+        shutil.rmtree(a.dir, ignore_errors=True)
+        os.makedirs(a.dir)
+        synth = tree.synthesize_tree(a.dir, int(a.gib * GIB), wal_records=a.wal_records,
+                                     progress=lambda m: print(m, file=sys.stderr, flush=True))
+        with open(marker, "w") as f:
+            json.dump(synth, f)
+    print(f"tree: {synth}", file=sys.stderr, flush=True)
+
+    ctx = Context(0)
+    reports = []
+    for r in range(a.reps):
+        mem, rep = tree.load_verify(ctx, a.dir)
+        reports.append(rep)
+        print(f"rep {r}: {rep}", file=sys.stderr, flush=True)
+    best = min(reports, key=lambda x: x["total_s"])
+    ab = {}
+    for v in filter(None, a.ab.split(",")):
+        act, sl = (int(x) for x in v.split(":"))
+        ctx.set_option("tree_active_files", act)
+        ctx.set_option("tree_slice_bytes", sl)
+        t = min(tree.load_verify(ctx, a.dir)[1]["tables_s"] for _ in range(2))
+        ab[v] = round(best["table_bytes"] / GIB / t, 2)
+        print(f"ab {v}: {ab[v]} GiB/s", file=sys.stderr, flush=True)
+    ctx.set_option("tree_active_files", 0)
+    ctx.set_option("tree_slice_bytes", 0)
+    verified = best["table_bytes"] + best["wal_bytes"]
+
+    # CPU baseline: the oracle's SHA-256 (= sha2 0.10's algorithm; scalar, no
+    # SHA-NI), one thread, over the first tables' data + index files
+    from oracle import oracle as O
+    metas = tree.list_tables(a.dir)
+    done, t0 = 0, time.perf_counter()
+    for m in metas:
+        for p in (m.data_path(), m.index_path()):
+            O.file_checksum(p)
+            done += os.path.getsize(p)
+        if done >= a.cpu_sample_gib * GIB:
+            break
+    tc = time.perf_counter() - t0
+
+    res = {
+        "metric": "GiB/s end-to-end tree load verify (files on disk, page cache warm)",
+        "value": round(verified / GIB / best["total_s"], 2),
+        "unit": "GiB/s",
+        "config": {"workload": "config5: Db::load checksum work over a synthetic LSM tree in the reference layout",
+                   "tree_tables": best["tables"], "table_bytes": best["table_bytes"], "wal_bytes": best["wal_bytes"],
+                   "wal_records": best["wal_records"], "scaled_from": "100 GiB (BASELINE config 5)"},
+        "seconds": {k: round(best[k], 3) for k in ("list_s", "tables_s", "wal_s", "memtable_build_s", "total_s")},
+        "tables_GiBps": round(best["table_bytes"] / GIB / best["tables_s"], 2),
+        "wal_GiBps": round(best["wal_bytes"] / GIB / best["wal_s"], 2),
+        "reps": [round(x["total_s"], 3) for x in reports],
+        "cpu_baseline": {"value": round(done / GIB / tc, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+                         "sample": f"first {done / GIB:.2f} GiB of data+index files, oracle FIPS SHA-256 "
+                                   "(Checksums::calculate_checksum's digest), 1 thread"},
+        "synthesis_s": synth["seconds"],
+    }
+    if ab:
+        res["tables_GiBps_by_active_slice"] = ab
+    print(json.dumps(res), flush=True)
+    ctx.close()
+    if not a.keep:
+        shutil.rmtree(a.dir, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
