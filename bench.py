@@ -99,7 +99,8 @@ def main():
         rec_len = 4096
         nbytes = nrec * rec_len
         byte_off = rank * nbytes  # this rank's shard of the global block stream
-        workload = f"config2: {nrec} fixed 4 KiB SSTable blocks per GPU ({nbytes / GIB:.0f} GiB), device-resident"
+        cname = "config4 per-GPU shard" if nrec == (1 << 26) else "config2"
+        workload = f"{cname}: {nrec} fixed 4 KiB SSTable blocks per GPU ({nbytes / GIB:.0f} GiB), device-resident"
     elif cfg == 1:
         nrec = a.blocks_per_gpu or (1 << 20)
         rec_len = 256
@@ -224,7 +225,8 @@ def main():
     value = total_payload / GIB / (wall_max / a.steps)
     achieved_gbs = algo_bytes / (ev_ms * 1e-3) / 1e9
     # diagnostics have no committed traffic
-    wkey = None if (a.desc or a.pack_align > 1) else f"{'sha256_' if sha else ''}config{cfg}"
+    # (the committed traffic is per launch of the default record count only)
+    wkey = None if (a.desc or a.pack_align > 1 or a.blocks_per_gpu) else f"{'sha256_' if sha else ''}config{cfg}"
     traffic = traffic_from_profiles(wkey)
 
     res = {
