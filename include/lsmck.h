@@ -139,6 +139,10 @@ int lsmck_device_count(void);
  *                 reduction or store); 4..6 (descriptor kernel, valid only
  *                 for 4 KiB records at 4 KiB stride): 3 with tile_info
  *                 synthesized, + off/len synthesized, + aligned loads;
+ *                 7 = 3 without the D_32 load; descriptor kernel, no payload
+ *                 loads and 2 chains: 11 = all compute, 8 = without the
+ *                 segment-factor multiply, 9 = without the first-segment
+ *                 masks, 10 = without the alignbyte funnel;
  *                 0 = off.  Locates the kernels' ceilings.
  *   "crc_wg_waves"  waves per workgroup of the descriptor CRC kernel: 12 or 16
  *                 (0 = built-in default).  A/B switch: 12 waves leave 168 VGPRs

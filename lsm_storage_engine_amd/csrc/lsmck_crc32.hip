@@ -221,7 +221,7 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
   L.fl = flv;
   // pointer arithmetic on the kernel-argument pointer keeps these global_load (not flat_load)
   const unsigned char* s0 = P.base + (E - 128);
-  if (ABLATE == 2) {  // diagnostic: no payload loads (compute-only timing; results invalid)
+  if (ABLATE == 2 || ABLATE >= 8) {  // diagnostic: no payload loads (compute-only timing; results invalid)
 #pragma unroll
     for (int j = 0; j < 33; ++j) L.d[j] = (uint32_t)E * 0x9E3779B1u + j;
     return;
@@ -303,7 +303,7 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
 template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
 __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const CrcParams& P, const SegLoad& L,
                                                uint32_t lo, uint32_t hi) {
-  if (ABLATE == 1 || ABLATE >= 3) {  // diagnostic: loads only (memory-path timing; results invalid)
+  if (ABLATE == 1 || (ABLATE >= 3 && ABLATE <= 7)) {  // diagnostic: loads only (memory-path timing; results invalid)
     uint32_t x = 0;
 #pragma unroll
     for (int j = 0; j < 33; ++j) x ^= L.d[j];
@@ -329,7 +329,7 @@ __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const 
         for (int j = 32; j >= 0; --j) d[j] = on ? (j >= s ? d[j - s] : 0u) : d[j];
       }
     }
-    if (__any(bstart != 0u)) {
+    if (ABLATE != 9 && __any(bstart != 0u)) {  // (9: diagnostic, compute without the masks)
       // zero the window in front of B: the groups before B's group and the
       // bytes of B's group in front of B (with lead = 0 this only clears bytes
       // of D_0 in front of the stream start, which the funnel drops anyway)
@@ -346,7 +346,7 @@ __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const 
       d[32] &= (lo_i == 32u) ? bm : 0xFFFFFFFFu;
     }
 #pragma unroll
-    for (int j = 0; j < 32; ++j) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+    for (int j = 0; j < 32; ++j) w[j] = ABLATE == 10 ? d[j] : __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
   }
   constexpr int WPC = 32 / CHAINS;  // words per chain
   uint32_t c[CHAINS];
@@ -382,6 +382,7 @@ __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const 
     }
     return p;
   }
+  if (ABLATE == 8) return s;  // diagnostic: compute without the segment-factor multiply
   uint32_t K = lds_ld(smem, LDS_KLO_OFF + ((L.k & 511u) << 2));
   if (__any(L.k >= 512u)) {  // records over 64 KiB (identity factors for the other lanes)
     K = gf2_mulmod(K, lds_ld(smem, LDS_KMID_OFF + (((L.k >> 9) & 127u) << 2)));
@@ -447,7 +448,7 @@ template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
 __device__ __forceinline__ void finish_tile(const unsigned char* smem, const CrcParams& P, const SegLoad& L,
                                             uint32_t lane, uint32_t lo, uint32_t hi) {
   uint32_t v = seg_finish<FAST, CHAINS, ABLATE, PERCOL>(smem, P, L, lo, hi);
-  if (ABLATE >= 3) {  // no reduction, no store (unless a magic value: keeps the loads alive)
+  if (ABLATE >= 3 && ABLATE <= 7) {  // no reduction, no store (unless a magic value: keeps the loads alive)
     if (v == 0x9E3779B1u) P.out[0] = v;
     return;
   }
@@ -1113,6 +1114,10 @@ extern "C" int lsmk_launch_crc32_desc(const CrcParams* P, const uint64_t* block_
                           : ablate == 6 ? (const void*)crc32_desc_kernel<1, 6>
                           : ablate == 7 ? (const void*)crc32_desc_kernel<1, 7>
                           : ablate == 2 ? (const void*)crc32_desc_kernel<1, 2>
+                          : ablate == 8 ? (const void*)crc32_desc_kernel<2, 8>
+                          : ablate == 9 ? (const void*)crc32_desc_kernel<2, 9>
+                          : ablate == 10 ? (const void*)crc32_desc_kernel<2, 10>
+                          : ablate == 11 ? (const void*)crc32_desc_kernel<2, 2>
                           : ch == 1 ? (const void*)crc32_desc_kernel<1>
                           : ch == 2 ? (const void*)crc32_desc_kernel<2> : (const void*)crc32_desc_kernel<4>);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -126,6 +126,7 @@ __global__ __launch_bounds__(1024) void k_desc_like(const unsigned char* __restr
       x.v[j] = *(const u32x4*)q;
     }
     if (FEAT & 4) x.d32 = *(const uint32_t*)(p + 128 - mis + (mis ? 0 : 0));
+    if (FEAT & 16) asm volatile("" ::"v"(p));  // keep the address live (no load overwrites it)
     if (FEAT & 2) {
       uint32_t r = (t * 64 + lane) >> 3;
       x.o = off[r];
@@ -219,6 +220,12 @@ int main(int argc, char** argv) {
     }
     printf("%-44s : %8.3f ms  %7.1f GB/s\n", name, best, (double)nt1 * 8192 / best / 1e6);
   };
+  rund("desc-like: keep-live baseline (16-B aligned)", (const void*)k_desc_like<16>);
+  rund("desc-like: keep-live dword aligned", (const void*)k_desc_like<17>);
+  rund("desc-like: keep-live + gathers", (const void*)k_desc_like<18>);
+  rund("desc-like: keep-live dword aligned + D32", (const void*)k_desc_like<21>);
+  rund("desc-like: keep-live zero-buffer groups", (const void*)k_desc_like<24>);
+  rund("desc-like: keep-live all", (const void*)k_desc_like<31>);
   rund("desc-like: baseline (16-B aligned)", (const void*)k_desc_like<0>);
   rund("desc-like: dword aligned", (const void*)k_desc_like<1>);
   rund("desc-like: + gathers", (const void*)k_desc_like<2>);
