@@ -142,7 +142,9 @@ int lsmck_device_count(void);
  *                 7 = 3 without the D_32 load; descriptor kernel, no payload
  *                 loads and 2 chains: 11 = all compute, 8 = without the
  *                 segment-factor multiply, 9 = without the first-segment
- *                 masks, 10 = without the alignbyte funnel;
+ *                 masks, 10 = without the alignbyte funnel; 12 = loads only
+ *                 with the real descriptor map but the aligned (FAST) payload
+ *                 loads (4 KiB records at 4 KiB stride only);
  *                 0 = off.  Locates the kernels' ceilings.
  *   "crc_wg_waves"  waves per workgroup of the descriptor CRC kernel: 12 or 16
  *                 (0 = built-in default).  A/B switch: 12 waves leave 168 VGPRs
