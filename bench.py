@@ -85,6 +85,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("LSMCK_BENCH_SHARE_GPU"):  # rehearsal of the N-rank path on a 1-GPU box
+        local %= torch.cuda.device_count()
     if world > 1:
         dist.init_process_group("gloo", init_method="env://")
     torch.cuda.set_device(local)
