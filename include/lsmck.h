@@ -146,9 +146,10 @@ int lsmck_device_count(void);
  *                 with the real descriptor map but the aligned (FAST) payload
  *                 loads (4 KiB records at 4 KiB stride only);
  *                 0 = off.  Locates the kernels' ceilings.
- *   "crc_wg_waves"  waves per workgroup of the descriptor CRC kernel: 12 or 16
- *                 (0 = built-in default).  A/B switch: 12 waves leave 168 VGPRs
- *                 per lane for the three-stage load pipeline, 16 leave 128.
+ *   "crc_wg_waves"  waves per workgroup of the descriptor CRC kernel and of
+ *                 the whole-tile ring kernel: 12 or 16 (0 = built-in default).
+ *                 A/B switch: 12 waves leave 168 VGPRs per lane for the load
+ *                 pipeline, 16 leave 128.
  *   "crc_loads"   payload load instruction of the fixed-record CRC kernel:
  *                 1 = global_load, 2 = raw buffer_load from a per-tile base
  *                 (0 = built-in default).  A/B switch.

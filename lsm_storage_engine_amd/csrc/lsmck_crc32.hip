@@ -617,8 +617,8 @@ __device__ __forceinline__ void issue_whole(const CrcParams& P, const PercolMap&
   L.k = nsegr - 1u - q;
   L.fl = (gi < total ? FL_VALID : 0u) | (q == 0u ? FL_FIRST : 0u);
 }
-template <int R, int ABLATE = 0>
-__global__ __launch_bounds__(1024) void crc32_wring_kernel(CrcParams P) {
+template <int R, int ABLATE = 0, int BLOCK = 1024>
+__global__ __launch_bounds__(BLOCK) void crc32_wring_kernel(CrcParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t nsegr = P.flen >> 7;
   build_lds_tables(smem, P);
@@ -1014,13 +1014,13 @@ static int launch_fixed(const CrcParams* P, int ncu, hipStream_t st) {
   return e == hipSuccess ? 0 : -(int)e;
 }
 
-template <int R, int ABLATE = 0>
+template <int R, int ABLATE = 0, int BLOCK = 1024>
 static int launch_wring(const CrcParams* P, int ncu, hipStream_t st) {
   size_t lds = LDS_SCRATCH_OFF;
-  hipError_t e = hipFuncSetAttribute((const void*)crc32_wring_kernel<R, ABLATE>,
+  hipError_t e = hipFuncSetAttribute((const void*)crc32_wring_kernel<R, ABLATE, BLOCK>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return -(int)e;
-  hipLaunchKernelGGL((crc32_wring_kernel<R, ABLATE>), dim3(ncu), dim3(1024), lds, st, *P);
+  hipLaunchKernelGGL((crc32_wring_kernel<R, ABLATE, BLOCK>), dim3(ncu), dim3(BLOCK), lds, st, *P);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
 }
@@ -1046,6 +1046,10 @@ extern "C" int lsmk_launch_crc32_fixed(const CrcParams* P, int ncu, int variant,
   // whole-tile ring of that many slots; 0 = LSMCK_DEFAULT_RING)
   const int ring = ((variant >> 12) & 0xF) ? ((variant >> 12) & 0xF) : LSMCK_DEFAULT_RING;
   if (fast && percol && buf && ring >= 2 && (ablate == 0 || ablate == 3)) {
+    if (variant & 0x20) {  // 12-wave workgroups (168 VGPRs per lane): A/B of the 3-slot ring
+      if (ring == 2) return launch_wring<2, 0, 768>(P, ncu, st);
+      return ablate ? launch_wring<3, 3, 768>(P, ncu, st) : launch_wring<3, 0, 768>(P, ncu, st);
+    }
     if (ring == 2) return ablate ? launch_wring<2, 3>(P, ncu, st) : launch_wring<2, 0>(P, ncu, st);
     return ablate ? launch_wring<3, 3>(P, ncu, st) : launch_wring<3, 0>(P, ncu, st);
   }

@@ -131,9 +131,9 @@ def test_device_generated_fixed_4k(ctx):
     assert np.array_equal(out.download(np.uint32), O.crc32_fixed(host, 4096, 4096, n, threads=8))
 
 
-@pytest.mark.parametrize("ring", [0, 1, 2, 3])
+@pytest.mark.parametrize("ring,waves", [(0, 0), (1, 0), (2, 0), (3, 0), (2, 12), (3, 12)])
 @pytest.mark.parametrize("length,n", [(4096, (1 << 15) + 37), (256, (1 << 18) + 5), (128, 5000), (8192, 3)])
-def test_fixed_ring_depths(ctx, ring, length, n):
+def test_fixed_ring_depths(ctx, ring, waves, length, n):
     """Fixed records whose segment count divides 64 run the whole-tile ring
     kernel ("crc_ring" 2 or 3 slots; 1 = the two-slot kernel): several tiles per
     wave with a remainder that is not a multiple of the ring's unroll, and
@@ -143,11 +143,13 @@ def test_fixed_ring_depths(ctx, ring, length, n):
     ctx.gen_stream(d.ptr, 0x5EED0020 + length, 0, nbytes)
     out = ctx.alloc(4 * n)
     ctx.set_option("crc_ring", ring)
+    ctx.set_option("crc_wg_waves", waves)
     try:
         ctx.crc32_fixed_device(d.ptr, length, length, n, out.ptr)
         ctx.sync()
     finally:
         ctx.set_option("crc_ring", 0)
+        ctx.set_option("crc_wg_waves", 0)
     host = O.gen_stream(0x5EED0020 + length, 0, nbytes)
     assert np.array_equal(out.download(np.uint32), O.crc32_fixed(host, length, length, n, threads=8))
     d.free()
