@@ -158,7 +158,10 @@ int lsmck_device_count(void);
  *                 A/B switch; digests are identical either way.
  *   "tree_active_files" / "tree_slice_bytes"  lsmck_checksums_verify_many's
  *                 files in flight (0 = 8192) and bytes of a file per round
- *                 (0 = 64 KiB; a multiple of 64).  Tests use small values.
+ *                 (0 = 128 KiB; a multiple of 64).  Tests use small values.
+ *   "tree_open_files"  files kept open from their first slice to their last
+ *                 (-1 = default: as many as RLIMIT_NOFILE leaves after a
+ *                 1024-descriptor reserve; the rest reopen per slice).
  *   "crc_ring"    fixed records whose segment count divides 64 (4 KiB, 256 B ...):
  *                 1 = two-slot kernel, 2 or 3 = whole-tile ring kernel with that
  *                 many load slots (0 = built-in default).  A/B switch.
@@ -223,7 +226,7 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
 
 /* Whole-tree SSTable verify: the batch form of Checksums::verify over many
  * tables (Db::load, src/tokio/db.rs:37-59 -> src/tokio/sstable.rs:34).
- * Streams every data/index file in slices: 8192 files in flight, 64 KiB of
+ * Streams every data/index file in slices: 8192 files in flight, 128 KiB of
  * each per round, 16 reader threads filling one pinned slot while the GPU
  * hashes the previous round (per-file SHA-256 state carried on the device),
  * then compares with each checksum file.  status[i] gets 0 /
@@ -232,6 +235,41 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
  * whose status is not 0. */
 int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, const char* const* index_paths,
                                 const char* const* checksum_paths, size_t n, int* status);
+
+/* Db::load's whole checksum scan of a tree (src/tokio/db.rs:37-59): for
+ * level-0 .. level-4 under `base` (created if missing, fs::create_dir_all),
+ * every directory entry whose UTF-8 name contains "metadata" is parsed as
+ * SsTableMetadata JSON (sstable_metadata.rs:76-83) and the table it names --
+ * base_path/level-<level>/{data,index,checksum}_filename -- is verified as by
+ * lsmck_checksums_verify_many.  Directory listing and metadata parsing run on
+ * 16 host threads.  Returns 0 when every table verifies, 1 when some table
+ * does not (rep->first_* names the first one in load order: level, then
+ * read_dir order -- the table where the reference's loop panics or errors),
+ * or a negative error (creating or listing a level directory failed).
+ * first_status is a lsmck_checksums_verify_many status or LSMCK_META_PANIC:
+ * the metadata file is unreadable or not valid SsTableMetadata JSON, where
+ * the reference panics with "Can't open metadata file" / "Can't read metadata
+ * file, file with unknown format" (sstable_metadata.rs:77-83). */
+#define LSMCK_SSTABLE_MAX_LEVEL 5 /* src/tokio/db.rs:17 */
+#define LSMCK_META_PANIC 3
+typedef struct {
+  uint64_t tables;      /* metadata entries found */
+  uint64_t table_bytes; /* data + index bytes hashed */
+  uint64_t bad_tables;  /* tables with a non-zero status */
+  uint64_t first_index; /* load-order index of the first bad table (UINT64_MAX: none) */
+  int first_status;
+  int reserved;
+  double list_seconds;   /* listing + metadata parsing */
+  double verify_seconds; /* the lsmck_checksums_verify_many part, split as: */
+  double stat_seconds;   /*   sizing the files */
+  double read_seconds;   /*   reader threads filling the pinned slots */
+  double gpu_wait_seconds; /* waiting for a slot's copy + kernels, final digest copy */
+  double compare_seconds;  /*  reading the checksum files, comparing */
+  uint64_t rounds;         /*  slice rounds */
+  uint64_t fds_cached;     /*  files kept open between slices (RLIMIT_NOFILE bound) */
+  char first_metadata_path[4096];
+} lsmck_tree_report;
+int lsmck_tree_verify(lsmck_ctx* ctx, const char* base, lsmck_tree_report* rep);
 
 /* ======================================================================== */
 /* 4. Plumbing for hosts without their own HIP bindings (tests, bench)        */

@@ -28,6 +28,8 @@ INDEX_MISMATCH = 2
 WAL_CORRUPTED = 1
 WAL_REMOVE_PANIC = 2
 WAL_BAD_TYPE = 3
+META_PANIC = 3  # lsmck_tree_verify status: metadata file unreadable / not SsTableMetadata JSON
+SSTABLE_MAX_LEVEL = 5
 
 DEVICE = 0x1
 HOST = 0x0
@@ -47,6 +49,15 @@ class Sha256Ctx(C.Structure):
 class WalRec(C.Structure):
     _fields_ = [("rec_off", C.c_uint64), ("payload_off", C.c_uint64), ("klen", C.c_uint32),
                 ("vlen", C.c_uint32), ("crc", C.c_uint32), ("type", C.c_uint32)]
+
+
+class TreeReport(C.Structure):
+    _fields_ = [("tables", C.c_uint64), ("table_bytes", C.c_uint64), ("bad_tables", C.c_uint64),
+                ("first_index", C.c_uint64), ("first_status", C.c_int), ("reserved", C.c_int),
+                ("list_seconds", C.c_double), ("verify_seconds", C.c_double), ("stat_seconds", C.c_double),
+                ("read_seconds", C.c_double), ("gpu_wait_seconds", C.c_double), ("compare_seconds", C.c_double),
+                ("rounds", C.c_uint64), ("fds_cached", C.c_uint64),
+                ("first_metadata_path", C.c_char * 4096)]
 
 
 # (name, restype, argtypes) for every symbol of include/lsmck.h
@@ -78,6 +89,7 @@ SIGNATURES = [
      [vp, vp, sz, C.c_uint, vp, sz, C.POINTER(sz), u64p, u32p, u32p]),  # recs: lsmck_wal_rec[cap]
     ("lsmck_checksums_verify_many", C.c_int,
      [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), sz, C.POINTER(C.c_int)]),
+    ("lsmck_tree_verify", C.c_int, [vp, C.c_char_p, C.POINTER(TreeReport)]),
     ("lsmck_dev_alloc", vp, [vp, sz]),
     ("lsmck_dev_free", None, [vp, vp]),
     ("lsmck_host_alloc_pinned", vp, [vp, sz]),

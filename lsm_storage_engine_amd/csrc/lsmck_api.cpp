@@ -6,11 +6,15 @@
 // of the descriptor path (segment prefix sums, tile -> first record), and two
 // pinned staging slots for host-resident batches (H2D / kernel / D2H of chunk
 // c overlap the host-side packing of chunk c+1).
+#include <dirent.h>
 #include <errno.h>
 #include <fcntl.h>
+#include <stdio.h>
+#include <time.h>
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -176,6 +180,7 @@ struct lsmck_ctx {
   int variant = 0;  // kernel variant for A/B timing (LSMCK_CRC_CHAINS=1|2|4); 0 = default
   uint32_t tree_active = 0;  // whole-tree verify: files in flight (0 = kTreeActive)
   uint32_t tree_slice = 0;   // whole-tree verify: bytes of a file per round (0 = kTreeSlice)
+  long tree_open = -1;       // whole-tree verify: files kept open between slices (-1 = RLIMIT_NOFILE budget)
   struct {
     uint32_t* state = nullptr;  // 8 u32 per active slot
     size_t cap_state = 0;
@@ -572,11 +577,17 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->tree_active = (uint32_t)value;
     return 0;
   }
-  if (!strcmp(key, "tree_slice_bytes")) {  // whole-tree verify: bytes per file per round (0 = 64 KiB)
+  if (!strcmp(key, "tree_slice_bytes")) {  // whole-tree verify: bytes per file per round (0 = 128 KiB)
     if (value < 0 || value % 64 || value > (1l << 30))
       return lsmck_host::set_error(LSMCK_EINVAL, "tree_slice_bytes: a multiple of 64, <= 2^30");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->tree_slice = (uint32_t)value;
+    return 0;
+  }
+  if (!strcmp(key, "tree_open_files")) {  // whole-tree verify: cap on files kept open (-1 = rlimit budget)
+    if (value < -1) return lsmck_host::set_error(LSMCK_EINVAL, "tree_open_files: -1 or >= 0");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->tree_open = value;
     return 0;
   }
   if (!strcmp(key, "sha_order")) {  // A/B: 1 = variable-length SHA batches in decreasing length order (default)
@@ -856,35 +867,111 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
 namespace {
 
 constexpr uint32_t kTreeActive = 8192;        // files in flight
-constexpr uint32_t kTreeSlice = 64u << 10;    // bytes of a file per round (multiple of 64; A/B: DESIGN.md 8)
+constexpr uint32_t kTreeSlice = 128u << 10;   // bytes of a file per round (multiple of 64; A/B: DESIGN.md 7a)
 constexpr unsigned kTreeReaders = 16;  // the GPU box gives a process 16 CPUs
 
-// pread exactly n bytes at offset off of path into dst
-int pread_range(const char* path, uint8_t* dst, uint64_t off, uint64_t n) {
-  int fd = open(path, O_RDONLY | O_CLOEXEC);
-  if (fd < 0) return -errno;
+// pread exactly n bytes at offset off of fd into dst
+int pread_fd(int fd, uint8_t* dst, uint64_t off, uint64_t n) {
   uint64_t got = 0;
-  int rc = 0;
   while (got < n) {
     ssize_t k = pread(fd, dst + got, (size_t)std::min<uint64_t>(n - got, 1ull << 30), (off_t)(off + got));
     if (k < 0) {
       if (errno == EINTR) continue;
-      rc = -errno;
-      break;
+      return -errno;
     }
     if (k == 0) break;
     got += (uint64_t)k;
   }
-  close(fd);
-  if (rc == 0 && got != n) rc = -EAGAIN;  // the file shrank while the tree was read
-  return rc;
+  return got == n ? 0 : -EAGAIN;  // the file shrank while the tree was read
+}
+
+// A file stays open from its first slice to its last: open(2)/close(2) in a
+// multi-threaded process contend in the kernel (the fd table, the directory's
+// dentry) and cost ~9 us each at 16 threads -- reopening per 64 KiB slice was
+// most of the read phase.  Slots past the fd budget (RLIMIT_NOFILE minus a
+// reserve) reopen per slice instead.
+struct SlotFds {
+  std::vector<int> fd;
+  uint32_t cached = 0;  // slots [0, cached) keep their file open
+  explicit SlotFds(uint32_t slots) : fd(slots, -1) {
+    struct rlimit rl;
+    uint64_t budget = 0;
+    if (getrlimit(RLIMIT_NOFILE, &rl) == 0) {
+      const uint64_t cur = rl.rlim_cur == RLIM_INFINITY ? (1ull << 30) : (uint64_t)rl.rlim_cur;
+      budget = cur > 1024 ? cur - 1024 : 0;
+    }
+    cached = (uint32_t)std::min<uint64_t>(slots, budget);
+  }
+  ~SlotFds() {
+    for (int f : fd)
+      if (f >= 0) close(f);
+  }
+  void drop(uint32_t k) {
+    if (fd[k] >= 0) close(fd[k]);
+    fd[k] = -1;
+  }
+  // read one slice of `path` for slot k; `last` closes the file after it
+  int read(uint32_t k, const char* path, uint8_t* dst, uint64_t off, uint64_t n, bool last) {
+    int f = fd[k];
+    if (f < 0) {
+      f = open(path, O_RDONLY | O_CLOEXEC);
+      if (f < 0) return -errno;
+    }
+    int rc = pread_fd(f, dst, off, n);
+    if (last || rc || k >= cached) {
+      close(f);
+      f = -1;
+    }
+    fd[k] = f;
+    return rc;
+  }
+};
+
+double seconds_since(const struct timespec& t0) {
+  struct timespec t1;
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+struct Clock {
+  struct timespec t;
+  Clock() { clock_gettime(CLOCK_MONOTONIC, &t); }
+  double lap() {  // seconds since the last lap
+    double d = seconds_since(t);
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return d;
+  }
+};
+
+// where verify_tables' wall time goes (lsmck_tree_report)
+struct TreeTiming {
+  double stat = 0, read = 0, wait = 0, compare = 0;
+  uint64_t rounds = 0, bytes = 0;
+  uint32_t fds_cached = 0;
+};
+
+// fn(i) for i in [0, n) on up to kTreeReaders threads (file-system metadata
+// work: stat, small JSON reads -- latency bound, so run many at once)
+extern "C++" template <class F>
+void host_parallel(size_t n, F&& fn) {
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (size_t j; (j = next.fetch_add(1, std::memory_order_relaxed)) < n;) fn(j);
+  };
+  const unsigned nt = (unsigned)std::min<size_t>(kTreeReaders, n / 64 + 1);
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nt; ++t) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
 }
 
 }  // namespace
 
-int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, const char* const* index_paths,
-                                const char* const* checksum_paths, size_t n, int* status) {
+static int verify_tables(lsmck_ctx* ctx, const char* const* data_paths, const char* const* index_paths,
+                         const char* const* checksum_paths, size_t n, int* status, TreeTiming* tm) {
   int rc = check_ctx(ctx);
+  TreeTiming tdummy;
+  if (!tm) tm = &tdummy;
+  Clock clk;
   if (rc) return rc;
   if (n && (!data_paths || !index_paths || !checksum_paths || !status))
     return lsmck_host::set_error(LSMCK_EINVAL, "null path array or status");
@@ -898,11 +985,29 @@ int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, c
     paths[2 * i] = data_paths[i];
     paths[2 * i + 1] = index_paths[i];
   }
-  for (size_t f = 0; f < nf; ++f) {
+  host_parallel(nf, [&](size_t f) {
     struct stat st;
     if (stat(paths[f], &st) != 0) ferr[f] = -errno;
     else fsize[f] = (uint64_t)st.st_size;
-  }
+  });
+  tm->stat += clk.lap();
+  // the checksum files are read by two background threads while the table
+  // files stream (the readers leave the CPU idle while a slot's copy runs)
+  std::vector<std::string> want_i(n), want_d(n);
+  std::vector<int> want_rc(n, 0);
+  std::atomic<size_t> want_next{0};
+  struct Joiner {
+    std::vector<std::thread> t;
+    ~Joiner() {
+      for (auto& x : t)
+        if (x.joinable()) x.join();
+    }
+  } want_th;
+  for (int t = 0; t < (n >= 64 ? 2 : n ? 1 : 0); ++t)
+    want_th.t.emplace_back([&]() {
+      for (size_t i; (i = want_next.fetch_add(1, std::memory_order_relaxed)) < n;)
+        want_rc[i] = lsmck_host::read_checksum_json(checksum_paths[i], &want_i[i], &want_d[i]);
+    });
   const uint32_t active_max = ctx->tree_active ? ctx->tree_active : kTreeActive;
   const uint32_t slice = ctx->tree_slice ? ctx->tree_slice : kTreeSlice;
   std::vector<uint8_t> dig(32 * std::max<size_t>(nf, 1), 0);
@@ -924,6 +1029,9 @@ int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, c
     bool busy[2] = {false, false}, any_kernel = false;
     int sl = 0;
     std::vector<uint64_t> rd_off;  // per slice: offset inside its file
+    SlotFds fds(active_max);
+    if (ctx->tree_open >= 0) fds.cached = (uint32_t)std::min<long>(fds.cached, ctx->tree_open);
+    tm->fds_cached = fds.cached;
     for (;;) {
       // admit files into free slots
       while (!free_slots.empty() && next_file < nf) {
@@ -939,7 +1047,9 @@ int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, c
       // the round's slices: the next `slice` bytes of every active file
       Stage& S = ctx->stage[sl];
       if (busy[sl]) {
+        clk.lap();
         HIPCHK(hipEventSynchronize(S.done));
+        tm->wait += clk.lap();
         busy[sl] = false;
       }
       std::vector<lsmck::ShaSlice> sv;
@@ -975,11 +1085,16 @@ int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, c
       if ((rc = ensure_dev(&S.d_slices, &S.cap_d_slices, cnt))) return rc;
       memcpy(S.h_slices, sv.data(), cnt * sizeof(lsmck::ShaSlice));
       // read the slices (overlaps the other slot's GPU work, already queued)
+      clk.lap();
       std::atomic<size_t> next{0};
       auto work = [&]() {
         for (size_t j; (j = next.fetch_add(1)) < cnt;) {
           const lsmck::ShaSlice& d = sv[j];
-          int e = pread_range(paths[d.msg], S.h_pay + d.off, rd_off[j], d.len);
+          if (ferr[d.msg]) {  // an earlier slice of this file failed: skip the rest
+            if (d.flags & SHA_SLICE_LAST) fds.drop(d.slot);
+            continue;
+          }
+          int e = fds.read(d.slot, paths[d.msg], S.h_pay + d.off, rd_off[j], d.len, d.flags & SHA_SLICE_LAST);
           if (e) ferr[d.msg] = e;
         }
       };
@@ -988,6 +1103,8 @@ int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, c
       for (unsigned t = 1; t < nt; ++t) th.emplace_back(work);
       work();
       for (auto& t : th) t.join();
+      tm->read += clk.lap();
+      ++tm->rounds;
       HIPCHK(hipMemcpyAsync(S.d_pay, S.h_pay, pay, hipMemcpyHostToDevice, S.s));
       HIPCHK(hipMemcpyAsync(S.d_slices, S.h_slices, cnt * sizeof(lsmck::ShaSlice), hipMemcpyHostToDevice, S.s));
       // the state carried between rounds orders the kernels across the two streams
@@ -1006,26 +1123,159 @@ int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, c
       any_kernel = true;
       sl ^= 1;
     }
+    clk.lap();
     for (int k = 0; k < 2; ++k)
       if (busy[k]) HIPCHK(hipEventSynchronize(ctx->stage[k].done));
     if (nf) HIPCHK(hipMemcpy(dig.data(), T.digests, 32 * nf, hipMemcpyDeviceToHost));
+    tm->wait += clk.lap();
   }
-  int bad = 0;
-  for (size_t i = 0; i < n; ++i) {
+  for (auto& x : want_th.t) x.join();
+  want_th.t.clear();
+  host_parallel(n, [&](size_t i) {
     status[i] = ferr[2 * i] ? ferr[2 * i] : ferr[2 * i + 1];
     if (status[i] == 0) {
       char db[45], ib[45];
       lsmck_base64_encode(&dig[64 * i], 32, db);
       lsmck_base64_encode(&dig[64 * i + 32], 32, ib);
-      std::string wi, wd;
-      int e = lsmck_host::read_checksum_json(checksum_paths[i], &wi, &wd);
-      if (e) status[i] = e;
-      else if (wd != db) status[i] = LSMCK_DATA_MISMATCH;  // data first, as checksums.rs:49-60
-      else if (wi != ib) status[i] = LSMCK_INDEX_MISMATCH;
+      if (want_rc[i]) status[i] = want_rc[i];
+      else if (want_d[i] != db) status[i] = LSMCK_DATA_MISMATCH;  // data first, as checksums.rs:49-60
+      else if (want_i[i] != ib) status[i] = LSMCK_INDEX_MISMATCH;
     }
-    if (status[i]) ++bad;
-  }
+  });
+  int bad = 0;
+  for (size_t i = 0; i < n; ++i) bad += status[i] != 0;
+  tm->bytes = std::accumulate(fsize.begin(), fsize.end(), (uint64_t)0);
+  tm->compare += clk.lap();
   return bad;
+}
+
+int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, const char* const* index_paths,
+                                const char* const* checksum_paths, size_t n, int* status) {
+  return verify_tables(ctx, data_paths, index_paths, checksum_paths, n, status, nullptr);
+}
+
+// ---------------------------------------------------------------------------
+// Db::load's table scan (src/tokio/db.rs:37-59) in native code: per level
+// create_dir_all + read_dir, every entry whose (UTF-8) name contains
+// "metadata", SsTableMetadata::load (sstable_metadata.rs:76-83), then the
+// tables' checksum verify as one lsmck_checksums_verify_many batch.  The
+// reference verifies in read_dir order and stops at the first failure; the
+// batch verifies every table and reports the first failure in that order.
+namespace {
+
+bool valid_utf8(const char* s) {
+  const unsigned char* p = (const unsigned char*)s;
+  while (*p) {
+    unsigned c = *p, k;
+    uint32_t cp;
+    if (c < 0x80) {
+      ++p;
+      continue;
+    } else if ((c & 0xE0) == 0xC0) k = 1, cp = c & 0x1F;
+    else if ((c & 0xF0) == 0xE0) k = 2, cp = c & 0x0F;
+    else if ((c & 0xF8) == 0xF0) k = 3, cp = c & 0x07;
+    else return false;
+    for (unsigned j = 1; j <= k; ++j) {
+      if ((p[j] & 0xC0) != 0x80) return false;
+      cp = (cp << 6) | (p[j] & 0x3F);
+    }
+    if ((k == 1 && cp < 0x80) || (k == 2 && cp < 0x800) || (k == 3 && cp < 0x10000) || cp > 0x10FFFF ||
+        (cp >= 0xD800 && cp <= 0xDFFF))
+      return false;
+    p += k + 1;
+  }
+  return true;
+}
+
+int mkdir_p(const std::string& path) {  // fs::create_dir_all
+  struct stat st;
+  if (stat(path.c_str(), &st) == 0) return S_ISDIR(st.st_mode) ? 0 : -EEXIST;
+  size_t cut = path.find_last_of('/');
+  if (cut != std::string::npos && cut > 0) {
+    int rc = mkdir_p(path.substr(0, cut));
+    if (rc) return rc;
+  }
+  if (mkdir(path.c_str(), 0777) != 0 && errno != EEXIST) return -errno;
+  return 0;
+}
+
+}  // namespace
+
+int lsmck_tree_verify(lsmck_ctx* ctx, const char* base, lsmck_tree_report* rep) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!base || !rep) return lsmck_host::set_error(LSMCK_EINVAL, "null base path or report");
+  memset(rep, 0, sizeof *rep);
+  rep->first_index = UINT64_MAX;
+  struct timespec t0;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  std::vector<std::string> mpath;
+  for (int lv = 0; lv < LSMCK_SSTABLE_MAX_LEVEL; ++lv) {
+    const std::string dir = lsmck_host::path_push(base, "level-" + std::to_string(lv));
+    if ((rc = mkdir_p(dir))) return lsmck_host::set_errno_error(-rc, "create_dir_all", dir.c_str());
+    DIR* d = opendir(dir.c_str());
+    if (!d) return lsmck_host::set_errno_error(errno, "read_dir", dir.c_str());
+    for (;;) {
+      errno = 0;
+      struct dirent* e = readdir(d);
+      if (!e) {
+        if (errno) {
+          int er = errno;
+          closedir(d);
+          return lsmck_host::set_errno_error(er, "read_dir", dir.c_str());
+        }
+        break;
+      }
+      if (!strcmp(e->d_name, ".") || !strcmp(e->d_name, "..")) continue;
+      if (strstr(e->d_name, "metadata") && valid_utf8(e->d_name)) mpath.push_back(dir + "/" + e->d_name);
+    }
+    closedir(d);
+  }
+  const size_t n = mpath.size();
+  std::vector<lsmck_host::TableMeta> meta(n);
+  std::vector<int> st(n, 0);
+  host_parallel(n, [&](size_t i) {
+    if (lsmck_host::read_metadata_json(mpath[i].c_str(), &meta[i])) st[i] = LSMCK_META_PANIC;
+  });
+  // table paths: construct_path = base_path / level-<level> / file (sstable_metadata.rs:43-48)
+  std::vector<std::string> dp, ip, cp;
+  std::vector<size_t> which;
+  for (size_t i = 0; i < n; ++i) {
+    if (st[i]) continue;
+    const std::string lvdir =
+        lsmck_host::path_push(meta[i].base_path, "level-" + std::to_string(meta[i].level));
+    dp.push_back(lsmck_host::path_push(lvdir, meta[i].data_filename));
+    ip.push_back(lsmck_host::path_push(lvdir, meta[i].index_filename));
+    cp.push_back(lsmck_host::path_push(lvdir, meta[i].checksum_filename));
+    which.push_back(i);
+  }
+  rep->tables = n;
+  rep->list_seconds = seconds_since(t0);
+  const size_t m = which.size();
+  std::vector<const char*> dpp(m), ipp(m), cpp(m);
+  for (size_t j = 0; j < m; ++j) dpp[j] = dp[j].c_str(), ipp[j] = ip[j].c_str(), cpp[j] = cp[j].c_str();
+  std::vector<int> vst(std::max<size_t>(m, 1), 0);
+  TreeTiming tm;
+  rc = verify_tables(ctx, dpp.data(), ipp.data(), cpp.data(), m, vst.data(), &tm);
+  if (rc < 0) return rc;
+  rep->table_bytes = tm.bytes;
+  rep->rounds = tm.rounds;
+  rep->stat_seconds = tm.stat;
+  rep->read_seconds = tm.read;
+  rep->gpu_wait_seconds = tm.wait;
+  rep->compare_seconds = tm.compare;
+  rep->fds_cached = tm.fds_cached;
+  for (size_t j = 0; j < m; ++j) st[which[j]] = vst[j];
+  rep->verify_seconds = seconds_since(t0) - rep->list_seconds;
+  for (size_t i = 0; i < n; ++i) {
+    if (!st[i]) continue;
+    if (rep->bad_tables++ == 0) {
+      rep->first_index = i;
+      rep->first_status = st[i];
+      snprintf(rep->first_metadata_path, sizeof rep->first_metadata_path, "%s", mpath[i].c_str());
+    }
+  }
+  return rep->bad_tables ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------

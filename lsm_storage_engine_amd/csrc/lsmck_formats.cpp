@@ -4,6 +4,7 @@
 #include <fcntl.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
 
@@ -160,10 +161,10 @@ struct P {
 };
 }  // namespace
 
-int read_checksum_json(const char* path, std::string* index_b64, std::string* data_b64) {
+static int read_file(const char* path, std::string* buf) {
   int fd = open(path, O_RDONLY | O_CLOEXEC);
   if (fd < 0) return set_errno_error(errno, "open", path);
-  std::string buf;
+  buf->clear();
   char tmp[4096];
   for (;;) {
     ssize_t k = read(fd, tmp, sizeof tmp);
@@ -174,9 +175,15 @@ int read_checksum_json(const char* path, std::string* index_b64, std::string* da
       return set_errno_error(e, "read", path);
     }
     if (k == 0) break;
-    buf.append(tmp, (size_t)k);
+    buf->append(tmp, (size_t)k);
   }
   close(fd);
+  return 0;
+}
+
+int read_checksum_json(const char* path, std::string* index_b64, std::string* data_b64) {
+  std::string buf;
+  if (int rc = read_file(path, &buf)) return rc;
   P p{buf.data(), buf.size(), 0};
   bool have_i = false, have_d = false;
   if (!p.lit('{')) return set_error(LSMCK_EJSON, "checksum file: expected '{'");
@@ -237,6 +244,73 @@ void gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, size_t n
     int64_t L = 64 * (int64_t)(lo + 1) - (int64_t)(u2 & 63);
     out[r] = L < (int64_t)lmin ? lmin : (uint32_t)L;
   }
+}
+
+// serde_json::from_reader::<SsTableMetadata> (sstable_metadata.rs:7-17, 76-83):
+// all eight fields required, unknown fields ignored, duplicates rejected; `id`
+// must be a JSON integer that fits u128 and `level` one that fits u8 (serde's
+// invalid-type / out-of-range errors otherwise).
+static bool parse_uint(P& p, unsigned digits_max, const char* max_dec) {
+  p.ws();
+  size_t st = p.i;
+  while (p.i < p.n && p.s[p.i] >= '0' && p.s[p.i] <= '9') ++p.i;
+  size_t nd = p.i - st;
+  if (nd == 0 || (nd > 1 && p.s[st] == '0')) return false;
+  if (p.i < p.n && (p.s[p.i] == '.' || p.s[p.i] == 'e' || p.s[p.i] == 'E')) return false;
+  if (nd > digits_max) return false;
+  if (nd == digits_max && memcmp(p.s + st, max_dec, nd) > 0) return false;
+  return true;
+}
+
+int read_metadata_json(const char* path, TableMeta* m) {
+  std::string buf;
+  if (int rc = read_file(path, &buf)) return rc;
+  P p{buf.data(), buf.size(), 0};
+  static const char* const kNames[8] = {"base_path",     "id",             "level",          "metadata_filename",
+                                        "checksum_filename", "data_filename", "index_filename", "bloom_filter_filename"};
+  std::string* strs[8] = {&m->base_path, nullptr, nullptr, &m->metadata_filename, &m->checksum_filename,
+                          &m->data_filename, &m->index_filename, &m->bloom_filter_filename};
+  bool have[8] = {};
+  if (!p.lit('{')) return set_error(LSMCK_EJSON, "metadata file: expected '{'");
+  if (!p.lit('}')) {
+    for (;;) {
+      std::string key;
+      if (!p.str(&key) || !p.lit(':')) return set_error(LSMCK_EJSON, "metadata file: bad member");
+      int f = -1;
+      for (int k = 0; k < 8; ++k)
+        if (key == kNames[k]) f = k;
+      if (f >= 0 && have[f]) return set_error(LSMCK_EJSON, "metadata file: duplicate field");
+      if (f == 1) {
+        if (!parse_uint(p, 39, "340282366920938463463374607431768211455"))
+          return set_error(LSMCK_EJSON, "metadata file: id is not a u128");
+      } else if (f == 2) {
+        p.ws();
+        size_t st = p.i;
+        if (!parse_uint(p, 3, "255")) return set_error(LSMCK_EJSON, "metadata file: level is not a u8");
+        m->level = (unsigned)atoi(std::string(p.s + st, p.i - st).c_str());
+      } else if (f >= 0) {
+        if (!p.str(strs[f])) return set_error(LSMCK_EJSON, "metadata file: expected a string");
+      } else if (!p.skip_value()) {
+        return set_error(LSMCK_EJSON, "metadata file: bad value");
+      }
+      if (f >= 0) have[f] = true;
+      if (p.lit(',')) continue;
+      if (p.lit('}')) break;
+      return set_error(LSMCK_EJSON, "metadata file: expected ',' or '}'");
+    }
+  }
+  p.ws();
+  if (p.i != p.n) return set_error(LSMCK_EJSON, "metadata file: trailing characters");
+  for (int k = 0; k < 8; ++k)
+    if (!have[k]) return set_error(LSMCK_EJSON, (std::string("metadata file: missing field `") + kNames[k] + "`").c_str());
+  return 0;
+}
+
+// PathBuf::push: an absolute component replaces the path, otherwise joins with '/'
+std::string path_push(const std::string& a, const std::string& b) {
+  if (!b.empty() && b[0] == '/') return b;
+  if (a.empty() || a.back() == '/') return a + b;
+  return a + "/" + b;
 }
 
 }  // namespace lsmck_host

@@ -20,6 +20,14 @@ const uint32_t* crc_tables();  // [8][256] slicing tables, T0 first
 int write_checksum_json(const char* path, const char* index_b64, const char* data_b64);
 int read_checksum_json(const char* path, std::string* index_b64, std::string* data_b64);
 
+// metadata_<ts>.db JSON (src/sstable_metadata.rs:7-17, 76-83); id is validated, not kept
+struct TableMeta {
+  std::string base_path, metadata_filename, checksum_filename, data_filename, index_filename, bloom_filter_filename;
+  unsigned level = 0;
+};
+int read_metadata_json(const char* path, TableMeta* m);
+std::string path_push(const std::string& a, const std::string& b);
+
 void gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, size_t n, uint32_t* out);
 }  // namespace lsmck_host
 #endif

@@ -228,6 +228,21 @@ class Context:
         _lib.check(self.lib.lsmck_checksums_verify_many(self.handle, d, i, c, n, status), "checksums_verify_many")
         return list(status[:n])
 
+    def tree_verify(self, base):
+        """lsmck_tree_verify: Db::load's table scan + batch verify of the tree
+        under ``base``.  Returns a dict of the report (first_* describe the
+        first failing table in load order, or are None)."""
+        rep = _lib.TreeReport()
+        rc = _lib.check(self.lib.lsmck_tree_verify(self.handle, str(base).encode(), C.byref(rep)), "tree_verify")
+        bad = rc != 0
+        return {"tables": rep.tables, "table_bytes": rep.table_bytes, "bad_tables": rep.bad_tables,
+                "first_index": rep.first_index if bad else None, "first_status": rep.first_status if bad else None,
+                "first_metadata_path": rep.first_metadata_path.decode(errors="surrogateescape") if bad else None,
+                "list_seconds": rep.list_seconds, "verify_seconds": rep.verify_seconds,
+                "stat_seconds": rep.stat_seconds, "read_seconds": rep.read_seconds,
+                "gpu_wait_seconds": rep.gpu_wait_seconds, "compare_seconds": rep.compare_seconds,
+                "rounds": rep.rounds, "fds_cached": rep.fds_cached}
+
 
 # include/lsmck.h lsmck_wal_rec (32 bytes, no padding)
 WAL_REC_DTYPE = np.dtype([("rec_off", "<u8"), ("payload_off", "<u8"), ("klen", "<u4"), ("vlen", "<u4"),

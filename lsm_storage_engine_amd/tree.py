@@ -30,6 +30,7 @@ import zlib
 
 import numpy as np
 
+from . import _lib
 from .checksums import ChecksumPanic, Checksums, _raise_for
 from .sstable_metadata import SsTableMetadata
 from .wal import CommandLog, MemTable
@@ -155,19 +156,39 @@ def list_tables(base):
     return metas
 
 
+class MetadataPanic(RuntimeError):
+    """SsTableMetadata::load's panic (sstable_metadata.rs:76-83)."""
+
+
+def _raise_first(rep):
+    st, mpath = rep["first_status"], rep["first_metadata_path"]
+    if st == _lib.META_PANIC:
+        if not os.access(mpath, os.R_OK):
+            raise MetadataPanic("Can't open metadata file")
+        raise MetadataPanic("Can't read metadata file, file with unknown format")
+    _raise_for(st, SsTableMetadata.load(mpath))
+
+
+def scan_order(base):
+    """Metadata paths in Db::load's load order: level by level, read_dir order
+    within a level (db.rs:40-55) -- the order in which the reference verifies
+    tables and hence which failing table it panics on."""
+    out = []
+    for lv in range(SSTABLE_MAX_LEVEL):
+        d = os.path.join(base, f"level-{lv}")
+        out.extend(os.path.join(d, n) for n in os.listdir(d) if "metadata" in n)
+    return out
+
+
 def load_verify(ctx, base):
     """The checksum work of Db::load (db.rs:37-73) as two GPU batches.
-    Returns (memtable, report); raises ChecksumPanic / WalError where the
-    reference panics / errors."""
-    t0 = time.perf_counter()
-    metas = list_tables(base)
-    t1 = time.perf_counter()
-    status = Checksums.verify_many(ctx, metas)
-    t2 = time.perf_counter()
-    for m, st in zip(metas, status):
-        if st:
-            _raise_for(st, m)
-    nbytes = sum(os.path.getsize(m.data_path()) + os.path.getsize(m.index_path()) for m in metas)
+    Returns (memtable, report); raises ChecksumPanic / MetadataPanic /
+    WalError where the reference panics / errors.  The table scan (listing,
+    metadata parsing, verify) is native: lsmck_tree_verify."""
+    rep = ctx.tree_verify(base)
+    if rep["first_status"] is not None:
+        _raise_first(rep)
+    nbytes = rep["table_bytes"]
     # WAL: CommandLog::new + MemTable::from_log (db.rs:60-63); the checksum work
     # is one lsmck_wal_replay_verify batch (timed alone), the BTreeMap build after it
     wal_path = os.path.join(base, "wal", "wal.log")
@@ -182,9 +203,12 @@ def load_verify(ctx, base):
         t5 = time.perf_counter()
     finally:
         log.file.close()
-    return mem, {"tables": len(metas), "table_bytes": nbytes, "wal_bytes": len(img), "wal_records": len(records),
-                 "list_s": t1 - t0, "tables_s": t2 - t1, "wal_s": t4 - t3, "memtable_build_s": t5 - t4,
-                 "total_s": (t2 - t0) + (t4 - t3)}
+    list_s, tables_s = rep["list_seconds"], rep["verify_seconds"]
+    return mem, {"tables": rep["tables"], "table_bytes": nbytes, "wal_bytes": len(img), "wal_records": len(records),
+                 "list_s": list_s, "tables_s": tables_s, "wal_s": t4 - t3, "memtable_build_s": t5 - t4,
+                 "total_s": list_s + tables_s + (t4 - t3),
+                 "tables_split": {k: rep[k] for k in ("stat_seconds", "read_seconds", "gpu_wait_seconds",
+                                                      "compare_seconds", "rounds", "fds_cached")}}
 
 
-__all__ = ["synthesize_tree", "list_tables", "load_verify", "ChecksumPanic", "SSTABLE_MAX_LEVEL"]
+__all__ = ["synthesize_tree", "list_tables", "scan_order", "load_verify", "ChecksumPanic", "MetadataPanic", "SSTABLE_MAX_LEVEL"]

@@ -88,8 +88,9 @@ def test_verify_many_tree(ctx, tmp_path, golden):
     assert sum(1 for s in st if s) == 3
 
 
-@pytest.mark.parametrize("active,slice_bytes", [(0, 0), (7, 4096), (64, 64), (1, 1 << 20)])
-def test_verify_many_streaming(ctx, tmp_path, active, slice_bytes):
+@pytest.mark.parametrize("active,slice_bytes,open_files", [(0, 0, -1), (7, 4096, -1), (64, 64, -1), (1, 1 << 20, -1),
+                                                            (64, 4096, 10), (7, 4096, 0)])
+def test_verify_many_streaming(ctx, tmp_path, active, slice_bytes, open_files):
     """The slice-streamed whole-tree verify (defaults: 8192 files in flight,
     64 KiB per round; then few files in flight and small slices, so files span
     many rounds, slots are reused, and one slice per round): 300 tables of
@@ -111,6 +112,7 @@ def test_verify_many_streaming(ctx, tmp_path, active, slice_bytes):
         metas.append(m)
     ctx.set_option("tree_active_files", active)
     ctx.set_option("tree_slice_bytes", slice_bytes)
+    ctx.set_option("tree_open_files", open_files)  # files kept open between slices; the rest reopen
     try:
         assert Checksums.verify_many(ctx, metas) == [0] * 300
         with open(metas[150].data_path(), "r+b") as f:  # the large table, last byte
@@ -124,6 +126,7 @@ def test_verify_many_streaming(ctx, tmp_path, active, slice_bytes):
     finally:
         ctx.set_option("tree_active_files", 0)
         ctx.set_option("tree_slice_bytes", 0)
+        ctx.set_option("tree_open_files", -1)
     assert st[150] == _lib.DATA_MISMATCH and st[201] == _lib.INDEX_MISMATCH
     assert st[77] < 0 and st[78] < 0
     assert sum(1 for s in st if s) == 4

@@ -11,6 +11,7 @@ import pytest
 
 from lsm_storage_engine_amd import tree
 from lsm_storage_engine_amd.checksums import ChecksumPanic
+from lsm_storage_engine_amd.sstable_metadata import SsTableMetadata
 from lsm_storage_engine_amd.wal import CorruptedData
 from oracle import oracle as O
 
@@ -67,29 +68,37 @@ def test_load_verify_clean_and_corrupted(ctx, small_tree, tmp_path):
     import shutil
     base = str(tmp_path / "t")
     shutil.copytree(small_tree[0], base)
-    metas = tree.list_tables(base)
-    for m in metas:  # metadata base_path points at the original tree: rewrite it
-        d = json.load(open(m.metadata_path()))
+    for p in tree.scan_order(base):  # metadata base_path points at the original tree: rewrite it
+        d = json.load(open(p))
         d["base_path"] = base
-        with open(m.metadata_path(), "w") as f:
+        with open(p, "w") as f:
             f.write(json.dumps(d, separators=(",", ":")))
+    metas = tree.list_tables(base)
+    assert all(m.base_path == base for m in metas)
     mem, rep = tree.load_verify(ctx, base)
     assert rep["tables"] == len(metas) and rep["wal_records"] == 3000
     _, recs, _ = O.wal_replay(open(os.path.join(base, "wal", "wal.log"), "rb").read())
     assert mem.size() <= 3000 and mem.size() > 0
-    # the second table's index file corrupted: panic naming the index file
-    metas = tree.list_tables(base)
-    with open(metas[1].index_path(), "r+b") as f:
+    assert rep["table_bytes"] == small_tree[1]["table_bytes"]
+    # the second table (load order) has its index file corrupted: panic naming the index file
+    paths = tree.scan_order(base)
+    order = [SsTableMetadata.load(p) for p in paths]
+    with open(order[1].index_path(), "r+b") as f:
         f.seek(9)
         f.write(b"\xff")
-    with pytest.raises(ChecksumPanic, match=metas[1].index_filename):
+    with pytest.raises(ChecksumPanic, match=order[1].index_filename):
         tree.load_verify(ctx, base)
+    r = ctx.tree_verify(base)
+    assert (r["bad_tables"], r["first_index"], r["first_status"]) == (1, 1, 2)
     # ... and the first table's data file too: the first table in load order wins
-    with open(metas[0].data_path(), "r+b") as f:
+    with open(order[0].data_path(), "r+b") as f:
         f.seek(100)
         f.write(b"\x00\x01\x02")
-    with pytest.raises(ChecksumPanic, match=metas[0].data_filename):
+    with pytest.raises(ChecksumPanic, match=order[0].data_filename):
         tree.load_verify(ctx, base)
+    r = ctx.tree_verify(base)
+    assert (r["bad_tables"], r["first_index"], r["first_status"]) == (2, 0, 1)
+    assert r["first_metadata_path"] == paths[0] == order[0].metadata_path()
 
 
 @pytest.mark.gpu
@@ -104,3 +113,61 @@ def test_load_verify_corrupted_wal(ctx, tmp_path):
     open(wal, "wb").write(bytes(img))
     with pytest.raises(CorruptedData):
         tree.load_verify(ctx, base)
+
+
+# SsTableMetadata JSON as serde_json reads it (sstable_metadata.rs:7-17, 76-83):
+# (text with BASE / TS substituted, the reference's outcome)
+_F = ('"base_path":"BASE","id":TS,"level":0,"metadata_filename":"metadata_TS.db","checksum_filename":'
+      '"checksum_TS.db","data_filename":"data_TS.db","index_filename":"index_TS.db","bloom_filter_filename":"bloom_TS.db"')
+META_CASES = [
+    ("{" + _F + "}", "ok"),
+    (" {\n " + _F.replace(",", " ,\n\t") + " } \n", "ok"),                    # whitespace
+    ('{"extra":[1,{"a":"}"}],' + _F + ',"z":null}', "ok"),                     # unknown fields ignored
+    ("{" + _F.replace('"id":TS', '"id":340282366920938463463374607431768211455') + "}", "ok"),  # u128::MAX
+    ("{" + _F.replace('"id":TS', '"id":340282366920938463463374607431768211456') + "}", "panic"),  # 2^128
+    ("{" + _F.replace('"id":TS', '"id":1.5') + "}", "panic"),
+    ("{" + _F.replace('"id":TS', '"id":-1') + "}", "panic"),
+    ("{" + _F.replace('"id":TS', '"id":"TS"') + "}", "panic"),
+    ("{" + _F.replace('"level":0', '"level":256') + "}", "panic"),
+    ("{" + _F.replace('"level":0', '"level":00') + "}", "panic"),
+    ("{" + _F.replace(',"bloom_filter_filename":"bloom_TS.db"', "") + "}", "panic"),  # missing field
+    ("{" + _F + ',"level":0}', "panic"),                                       # duplicate field
+    ("{" + _F + "}x", "panic"),                                                # trailing characters
+    ("{" + _F.replace("data_TS.db", "da\\u0074a_TS.db") + "}", "ok"),        # escapes
+    ("", "panic"),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(len(META_CASES)))
+def test_tree_verify_metadata_json(ctx, tmp_path, case):
+    from lsm_storage_engine_amd import _lib, checksums
+    text, want = META_CASES[case]
+    base = str(tmp_path)
+    m = SsTableMetadata.new(base, 0, timestamp_ms=1_700_000_000_123)
+    os.makedirs(os.path.dirname(m.data_path()))
+    open(m.data_path(), "wb").write(b"records" * 100)
+    open(m.index_path(), "wb").write(b"index")
+    checksums.Checksums.write_checksums(m)
+    open(m.metadata_path(), "w").write(text.replace("BASE", base).replace("TS", str(m.id)))
+    open(os.path.join(base, "level-0", "not-a-table.db"), "w").write("{}")  # name lacks "metadata": skipped
+    r = ctx.tree_verify(base)
+    assert r["tables"] == 1
+    assert all(os.path.isdir(os.path.join(base, f"level-{lv}")) for lv in range(5))  # create_dir_all
+    if want == "ok":
+        assert r["bad_tables"] == 0 and r["table_bytes"] == 705
+    else:
+        assert r["first_status"] == _lib.META_PANIC
+        with pytest.raises(tree.MetadataPanic, match="unknown format"):
+            tree.load_verify(ctx, base)
+
+
+@pytest.mark.gpu
+def test_tree_verify_empty_and_missing_files(ctx, tmp_path):
+    base = str(tmp_path / "new")  # Db::load on a fresh path: creates the levels, no tables
+    r = ctx.tree_verify(base)
+    assert r["tables"] == 0 and r["bad_tables"] == 0
+    m = SsTableMetadata.new(base, 2, timestamp_ms=1_700_000_000_999)
+    m.write_to_file()  # a table whose data/index/checksum files are missing
+    r = ctx.tree_verify(base)
+    assert r["tables"] == 1 and r["first_status"] == -2  # ENOENT

@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--wal-records", type=int, default=500_000)
     ap.add_argument("--keep", action="store_true")
     ap.add_argument("--cpu-sample-gib", type=float, default=1.0)
-    ap.add_argument("--ab", default="", help="comma list of active:slice_bytes settings to A/B after the main reps")
+    ap.add_argument("--ab", default="", help="comma list of active:slice_bytes[:open_files] settings to A/B after the main reps")
     a = ap.parse_args()
 
     marker = os.path.join(a.dir, "e2e_tree.json")
@@ -66,14 +66,16 @@ def main():
     best = min(reports, key=lambda x: x["total_s"])
     ab = {}
     for v in filter(None, a.ab.split(",")):
-        act, sl = (int(x) for x in v.split(":"))
+        act, sl, op = ([int(x) for x in v.split(":")] + [-1])[:3]
         ctx.set_option("tree_active_files", act)
         ctx.set_option("tree_slice_bytes", sl)
+        ctx.set_option("tree_open_files", op)
         t = min(tree.load_verify(ctx, a.dir)[1]["tables_s"] for _ in range(2))
         ab[v] = round(best["table_bytes"] / GIB / t, 2)
         print(f"ab {v}: {ab[v]} GiB/s", file=sys.stderr, flush=True)
     ctx.set_option("tree_active_files", 0)
     ctx.set_option("tree_slice_bytes", 0)
+    ctx.set_option("tree_open_files", -1)
     verified = best["table_bytes"] + best["wal_bytes"]
 
     # CPU baseline: the oracle's SHA-256 (= sha2 0.10's algorithm; scalar, no
@@ -99,6 +101,7 @@ def main():
                    "baseline_config": "BASELINE config 5: a 100 GiB tree"},
         "seconds": {k: round(best[k], 3) for k in ("list_s", "tables_s", "wal_s", "memtable_build_s", "total_s")},
         "tables_GiBps": round(best["table_bytes"] / GIB / best["tables_s"], 2),
+        "tables_split_s": {k: round(v, 3) if isinstance(v, float) else v for k, v in best["tables_split"].items()},
         "wal_GiBps": round(best["wal_bytes"] / GIB / best["wal_s"], 2),
         "reps": [round(x["total_s"], 3) for x in reports],
         "cpu_baseline": {"value": round(done / GIB / tc, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
