@@ -159,6 +159,7 @@ int lsmck_device_count(void);
  *   "tree_active_files" / "tree_slice_bytes"  lsmck_checksums_verify_many's
  *                 files in flight (0 = 8192) and bytes of a file per round
  *                 (0 = 128 KiB; a multiple of 64).  Tests use small values.
+ *   "tree_list_threads"  lsmck_tree_verify's metadata parsing threads (0 = 8).
  *   "tree_open_files"  files kept open from their first slice to their last
  *                 (-1 = default: as many as RLIMIT_NOFILE leaves after a
  *                 1024-descriptor reserve; the rest reopen per slice).
@@ -241,8 +242,7 @@ int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, c
  * every directory entry whose UTF-8 name contains "metadata" is parsed as
  * SsTableMetadata JSON (sstable_metadata.rs:76-83) and the table it names --
  * base_path/level-<level>/{data,index,checksum}_filename -- is verified as by
- * lsmck_checksums_verify_many.  Directory listing and metadata parsing run on
- * 16 host threads.  Returns 0 when every table verifies, 1 when some table
+ * lsmck_checksums_verify_many.  Metadata parsing runs on 8 host threads.  Returns 0 when every table verifies, 1 when some table
  * does not (rep->first_* names the first one in load order: level, then
  * read_dir order -- the table where the reference's loop panics or errors),
  * or a negative error (creating or listing a level directory failed).

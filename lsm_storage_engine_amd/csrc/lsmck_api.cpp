@@ -181,6 +181,7 @@ struct lsmck_ctx {
   uint32_t tree_active = 0;  // whole-tree verify: files in flight (0 = kTreeActive)
   uint32_t tree_slice = 0;   // whole-tree verify: bytes of a file per round (0 = kTreeSlice)
   long tree_open = -1;       // whole-tree verify: files kept open between slices (-1 = RLIMIT_NOFILE budget)
+  unsigned tree_list_threads = 0;  // lsmck_tree_verify: metadata parsing threads (0 = kListThreads)
   struct {
     uint32_t* state = nullptr;  // 8 u32 per active slot
     size_t cap_state = 0;
@@ -590,6 +591,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->tree_open = value;
     return 0;
   }
+  if (!strcmp(key, "tree_list_threads")) {  // A/B: metadata parsing threads of lsmck_tree_verify (0 = 8)
+    if (value < 0 || value > 256) return lsmck_host::set_error(LSMCK_EINVAL, "tree_list_threads: 0..256");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->tree_list_threads = (unsigned)value;
+    return 0;
+  }
   if (!strcmp(key, "sha_order")) {  // A/B: 1 = variable-length SHA batches in decreasing length order (default)
     if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "sha_order must be 0 or 1");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -869,6 +876,7 @@ namespace {
 constexpr uint32_t kTreeActive = 8192;        // files in flight
 constexpr uint32_t kTreeSlice = 128u << 10;   // bytes of a file per round (multiple of 64; A/B: DESIGN.md 7a)
 constexpr unsigned kTreeReaders = 16;  // the GPU box gives a process 16 CPUs
+constexpr unsigned kListThreads = 8;   // lsmck_tree_verify's metadata parsing (A/B: DESIGN.md 7a)
 
 // pread exactly n bytes at offset off of fd into dst
 int pread_fd(int fd, uint8_t* dst, uint64_t off, uint64_t n) {
@@ -952,12 +960,12 @@ struct TreeTiming {
 // fn(i) for i in [0, n) on up to kTreeReaders threads (file-system metadata
 // work: stat, small JSON reads -- latency bound, so run many at once)
 extern "C++" template <class F>
-void host_parallel(size_t n, F&& fn) {
+void host_parallel(size_t n, F&& fn, unsigned max_threads = kTreeReaders) {
   std::atomic<size_t> next{0};
   auto work = [&]() {
     for (size_t j; (j = next.fetch_add(1, std::memory_order_relaxed)) < n;) fn(j);
   };
-  const unsigned nt = (unsigned)std::min<size_t>(kTreeReaders, n / 64 + 1);
+  const unsigned nt = (unsigned)std::min<size_t>(std::max(1u, max_threads), n / 64 + 1);
   std::vector<std::thread> th;
   for (unsigned t = 1; t < nt; ++t) th.emplace_back(work);
   work();
@@ -1234,9 +1242,11 @@ int lsmck_tree_verify(lsmck_ctx* ctx, const char* base, lsmck_tree_report* rep) 
   const size_t n = mpath.size();
   std::vector<lsmck_host::TableMeta> meta(n);
   std::vector<int> st(n, 0);
+  // 8 threads: small-file system calls contend in the kernel (229k metadata
+  // files: 1 thread 1.25 s, 4 1.01 s, 8 0.80 s, 16 0.89 s, 32 1.25 s)
   host_parallel(n, [&](size_t i) {
     if (lsmck_host::read_metadata_json(mpath[i].c_str(), &meta[i])) st[i] = LSMCK_META_PANIC;
-  });
+  }, ctx->tree_list_threads ? ctx->tree_list_threads : kListThreads);
   // table paths: construct_path = base_path / level-<level> / file (sstable_metadata.rs:43-48)
   std::vector<std::string> dp, ip, cp;
   std::vector<size_t> which;

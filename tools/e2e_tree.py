@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--wal-records", type=int, default=500_000)
     ap.add_argument("--keep", action="store_true")
     ap.add_argument("--cpu-sample-gib", type=float, default=1.0)
+    ap.add_argument("--list-threads", default="", help="comma list of tree_list_threads values to A/B (listing time)")
     ap.add_argument("--ab", default="", help="comma list of active:slice_bytes[:open_files] settings to A/B after the main reps")
     a = ap.parse_args()
 
@@ -76,6 +77,12 @@ def main():
     ctx.set_option("tree_active_files", 0)
     ctx.set_option("tree_slice_bytes", 0)
     ctx.set_option("tree_open_files", -1)
+    lt = {}
+    for v in filter(None, a.list_threads.split(",")):
+        ctx.set_option("tree_list_threads", int(v))
+        lt[v] = round(min(tree.load_verify(ctx, a.dir)[1]["list_s"] for _ in range(2)), 3)
+        print(f"list threads {v}: {lt[v]} s", file=sys.stderr, flush=True)
+    ctx.set_option("tree_list_threads", 0)
     verified = best["table_bytes"] + best["wal_bytes"]
 
     # CPU baseline: the oracle's SHA-256 (= sha2 0.10's algorithm; scalar, no
@@ -111,6 +118,8 @@ def main():
     }
     if ab:
         res["tables_GiBps_by_active_slice"] = ab
+    if lt:
+        res["list_s_by_threads"] = lt
     print(json.dumps(res), flush=True)
     ctx.close()
     if not a.keep:
