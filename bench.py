@@ -80,6 +80,10 @@ def traffic_from_profiles(workload_key):
         return None
 
 
+# host cores for the all-cores CPU row: the GPU box gives a process 16 CPUs
+CPU_ALL_CORES = int(os.environ.get("LSMCK_CPU_CORES", "16"))
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -354,6 +358,21 @@ def main():
             "seconds": round(tc, 2),
             "gpu_matches_on_sample": bool(np.array_equal(got, np.asarray(want).reshape(ns, 32))),
         }
+        # SURVEY 8d CPU rows (2) and (4): all host cores, and OpenSSL (hashlib; SHA-NI where the CPU has it)
+        tc0 = time.perf_counter()
+        O.sha256_batch(host, so, sl, threads=CPU_ALL_CORES)
+        tall = time.perf_counter() - tc0
+        import hashlib
+        mv = memoryview(host)
+        tc0 = time.perf_counter()
+        for o, l in zip(so.tolist(), sl.tolist()):
+            hashlib.sha256(mv[o:o + l]).digest()
+        tossl = time.perf_counter() - tc0
+        res["cpu_extra"] = {
+            "oracle_all_cores": {"value": round(sbytes / GIB / tall, 3), "unit": "GiB/s", "cores": CPU_ALL_CORES},
+            "openssl_hashlib_1_thread": {"value": round(sbytes / GIB / tossl, 3), "unit": "GiB/s", "cores": 1},
+            "sample": "the cpu_baseline sample",
+        }
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not sha:
         from oracle import oracle as O  # the checker / baseline, never the measured path
         if cfg == 3:
@@ -384,6 +403,27 @@ def main():
             "sample": sample + "; oracle Sarwate byte-at-a-time CRC-32 (= crc 1.x checksum_ieee), 1 thread",
             "seconds": round(tc, 2),
             "gpu_matches_on_sample": bool(np.array_equal(got, want)),
+        }
+        # SURVEY 8d CPU rows (2) and (3): all host cores (oracle), and zlib's crc32 (slicing / PCLMUL;
+        # faster than, and not, the reference's algorithm; informational)
+        so = offs[:ns] if cfg == 3 else np.arange(ns, dtype=np.uint64) * np.uint64(rec_len)
+        sl = lens[:ns] if cfg == 3 else np.full(ns, rec_len, dtype=np.uint32)
+        tc0 = time.perf_counter()
+        if cfg == 3:
+            O.crc32_batch(host, so, sl, threads=CPU_ALL_CORES)
+        else:
+            O.crc32_fixed(host, rec_len, rec_len, ns, threads=CPU_ALL_CORES)
+        tall = time.perf_counter() - tc0
+        import zlib
+        mv = memoryview(host)
+        tc0 = time.perf_counter()
+        zl = [zlib.crc32(mv[o:o + l]) for o, l in zip(so.tolist(), sl.tolist())]
+        tz = time.perf_counter() - tc0
+        res["cpu_extra"] = {
+            "oracle_all_cores": {"value": round(sbytes / GIB / tall, 3), "unit": "GiB/s", "cores": CPU_ALL_CORES},
+            "zlib_1_thread": {"value": round(sbytes / GIB / tz, 3), "unit": "GiB/s", "cores": 1,
+                              "matches": bool(np.array_equal(np.asarray(zl, dtype=np.uint32), want))},
+            "sample": "the cpu_baseline sample",
         }
     if rank == 0:
         print(json.dumps(res), flush=True)
