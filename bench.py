@@ -334,6 +334,19 @@ def main():
         }
         pb.free()
 
+    # summary digest: CRC-32 of the little-endian output array
+    # (CRCs, or the 32-B digests), for cross-run comparison
+    if rank == 0:
+        import zlib
+        res["summary_crc32"] = "%08x" % zlib.crc32(out.download(np.uint8, count=(32 if sha else 4) * nrec).tobytes())
+        # against the oracle's full-size value (tests/golden/make_summaries.py; default layouts only)
+        gpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "summaries.json")
+        if not a.blocks_per_gpu and a.pack_align <= 1 and os.path.exists(gpath):
+            with open(gpath) as f:
+                gold = json.load(f).get(f"config{cfg}", {}).get("summary_sha256" if sha else "summary_crc32")
+            if gold:
+                res["summary_matches_oracle"] = res["summary_crc32"] == gold
+
     # CPU baseline + parity of the same sample (rank 0, N = 1 only)
     if rank == 0 and world == 1 and not a.no_cpu_baseline and sha:
         from oracle import oracle as O  # the checker / baseline, never the measured path

@@ -1,0 +1,103 @@
+#!/usr/bin/env python3
+"""Summary digests of the BASELINE configs at full size ("Summary
+digest = CRC-32 of the output array, for cross-run comparison").
+
+For each config every record's digest is computed on the CPU by the oracle
+(oracle/: Sarwate CRC-32, FIPS 180-4 SHA-256; pinned against zlib and hashlib
+by tests/test_oracle.py) over the same splitmix64 byte stream the GPU generates
+(oracle_gen_stream == gen_stream_kernel), in 1 GiB chunks on a thread pool so
+host memory stays small.  The summary is zlib.crc32 of the output array: the
+little-endian u32 CRCs, or the 32-byte SHA-256 digests in record order.
+tests/test_gpu_crc.py / test_gpu_sha.py compare the GPU's full-size outputs
+with these values; bench.py prints the GPU's as "summary_crc32".
+
+  config 1: 2^20 x 256 B, seed 0x5EED0001
+  config 2: 2^24 x 4096 B, seed 0x5EED0002
+  config 3: 2^26 Zipf(1.5) records of 64 B - 64 KiB packed back to back,
+            lengths from the seed, bytes from the same seed
+
+Run:  python3 tests/golden/make_summaries.py [crc|sha|all]   (updates summaries.json here)
+"""
+import concurrent.futures as cf
+import json
+import os
+import sys
+import time
+import zlib
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+from oracle import oracle as O  # noqa: E402
+
+CHUNK = 1 << 30
+THREADS = int(os.environ.get("THREADS", "8"))
+OUT = os.path.join(HERE, "summaries.json")
+
+
+def _digest(data, off, ln, sha):
+    if sha:
+        return np.asarray(O.sha256_batch(data, off, ln, threads=1), dtype=np.uint8).tobytes()
+    return O.crc32_batch(data, off, ln, threads=1).astype("<u4").tobytes()
+
+
+def _chunks(offs, lens):
+    """record ranges [r0, r1) of about CHUNK payload bytes"""
+    ends = offs + lens.astype(np.uint64)
+    r0, n = 0, len(offs)
+    while r0 < n:
+        r1 = max(int(np.searchsorted(ends, offs[r0] + np.uint64(CHUNK), side="right")), r0 + 1)
+        yield r0, r1
+        r0 = r1
+
+
+def summary(seed, offs, lens, sha):
+    def job(rng):
+        r0, r1 = rng
+        base = int(offs[r0])
+        data = O.gen_stream(seed, base, int(offs[r1 - 1]) + int(lens[r1 - 1]) - base)
+        return _digest(data, offs[r0:r1] - np.uint64(base), lens[r0:r1], sha)
+    crc = 0
+    with cf.ThreadPoolExecutor(THREADS) as ex:  # ctypes calls release the GIL
+        for part in ex.map(job, list(_chunks(offs, lens))):
+            crc = zlib.crc32(part, crc)
+    return "%08x" % crc
+
+
+def layout(cfg):
+    if cfg == 1:
+        n, L = 1 << 20, 256
+    elif cfg == 2:
+        n, L = 1 << 24, 4096
+    else:
+        lens = O.gen_zipf_lengths(0x5EED0003, 1 << 26)
+        offs = np.zeros(len(lens), dtype=np.uint64)
+        np.cumsum(lens[:-1].astype(np.uint64), out=offs[1:])
+        return offs, lens
+    return np.arange(n, dtype=np.uint64) * np.uint64(L), np.full(n, L, dtype=np.uint32)
+
+
+def main():
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    res = json.load(open(OUT)) if os.path.exists(OUT) else {}
+    res["method"] = ("oracle digest per record (1 GiB chunks), zlib.crc32 of the output array "
+                     "(LE u32 CRCs / 32-B SHA-256 digests)")
+    t0 = time.time()
+    for cfg in (1, 2, 3):
+        seed = 0x5EED0000 + cfg
+        offs, lens = layout(cfg)
+        e = res.setdefault(f"config{cfg}", {})
+        e.update({"records": len(offs), "payload_bytes": int(offs[-1]) + int(lens[-1]), "seed": hex(seed)})
+        if what in ("crc", "all"):
+            e["summary_crc32"] = summary(seed, offs, lens, False)
+        if what in ("sha", "all") and cfg != 1:
+            e["summary_sha256"] = summary(seed, offs, lens, True)
+        print(f"config{cfg}", e, round(time.time() - t0, 1), flush=True)
+        with open(OUT, "w") as f:
+            json.dump(res, f, indent=1)
+            f.write("\n")
+
+
+if __name__ == "__main__":
+    main()

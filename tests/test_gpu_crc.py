@@ -156,6 +156,13 @@ def test_fixed_ring_depths(ctx, ring, waves, length, n):
     out.free()
 
 
+def _summaries():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "summaries.json")) as f:
+        return json.load(f)
+
+
 def test_config2_full_size_properties(ctx):
     """BASELINE config 2 at full size (2^24 x 4 KiB = 64 GiB, device-resident):
     (1) the fixed-record kernel and the descriptor kernel (different code
@@ -176,6 +183,9 @@ def test_config2_full_size_properties(ctx):
     ctx.sync()
     a, b = out_f.download(np.uint32), out_d.download(np.uint32)
     assert np.array_equal(a, b)
+    # (3) the summary digest of all 2^24 CRCs equals the oracle's (tests/golden/make_summaries.py)
+    import zlib
+    assert "%08x" % zlib.crc32(a.astype("<u4").tobytes()) == _summaries()["config2"]["summary_crc32"]
     rng = np.random.default_rng(5)
     idx = np.sort(rng.choice(n, 4096, replace=False))
     for i in idx[:4096]:
@@ -257,3 +267,50 @@ def test_desc_records_at_allocation_edges(ctx):
         off = np.array([0, n - L, 1, n - L - 1], dtype=np.uint64)
         ln = np.full(4, L, dtype=np.uint32)
         assert np.array_equal(_device_crc(ctx, data, off, ln), O.crc32_batch(data, off, ln)), L
+
+
+def test_config1_full_size(ctx):
+    """BASELINE config 1 at full size on the GPU (2^20 x 256 B, device
+    resident): every CRC equals the oracle's, and the summary digest (CRC-32 of
+    the output array) is the pinned value of tests/test_oracle.py."""
+    import zlib
+    CONFIG1_SUMMARY_CRC32 = 0x727D43C0  # tests/test_oracle.py (oracle == zlib at config 1)
+    assert "%08x" % CONFIG1_SUMMARY_CRC32 == _summaries()["config1"]["summary_crc32"]
+    n = 1 << 20
+    d = ctx.alloc(n * 256)
+    ctx.gen_stream(d.ptr, 0x5EED0001, 0, n * 256)
+    out = ctx.alloc(4 * n)
+    ctx.crc32_fixed_device(d.ptr, 256, 256, n, out.ptr)
+    ctx.sync()
+    got = out.download(np.uint32)
+    want = O.crc32_fixed(O.gen_stream(0x5EED0001, 0, n * 256), 256, 256, n, threads=8)
+    assert np.array_equal(got, want)
+    assert zlib.crc32(got.astype("<u4").tobytes()) == CONFIG1_SUMMARY_CRC32
+    d.free()
+    out.free()
+
+
+def test_config3_full_size_summary(ctx):
+    """BASELINE config 3 at full size (2^26 Zipf records, ~97 GiB packed,
+    device-resident): the CRC-32 of the whole output array equals the oracle's
+    (tests/golden/make_summaries.py), i.e. all 2^26 CRCs match."""
+    import zlib
+    from lsm_storage_engine_amd.device import gen_zipf_lengths
+    n = 1 << 26
+    ln = gen_zipf_lengths(0x5EED0003, n)
+    assert np.array_equal(ln[:4096], O.gen_zipf_lengths(0x5EED0003, 4096))
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum(ln[:-1].astype(np.uint64), out=off[1:])
+    total = int(off[-1]) + int(ln[-1])
+    assert total == _summaries()["config3"]["payload_bytes"]
+    d = ctx.alloc(total + 64)
+    ctx.gen_stream(d.ptr, 0x5EED0003, 0, total)
+    d_o, d_l, out = ctx.alloc(off.nbytes), ctx.alloc(ln.nbytes), ctx.alloc(4 * n)
+    d_o.upload(off)
+    d_l.upload(ln)
+    ctx.crc32_device(d.ptr, d_o.ptr, d_l.ptr, n, out.ptr)
+    ctx.sync()
+    got = out.download(np.uint32)
+    assert "%08x" % zlib.crc32(got.astype("<u4").tobytes()) == _summaries()["config3"]["summary_crc32"]
+    for buf in (d, d_o, d_l, out):
+        buf.free()

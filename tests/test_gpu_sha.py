@@ -155,3 +155,47 @@ def test_length_sorted_batch(ctx, order):
     finally:
         ctx.set_option("sha_order", 1)
     assert np.array_equal(got, O.sha256_batch(data, off, ln, threads=8))
+
+
+def _summaries():
+    import json
+    with open(os.path.join(os.path.dirname(__file__), "golden", "summaries.json")) as f:
+        return json.load(f)
+
+
+def test_config2_full_size_summary(ctx):
+    """SHA-256 of all 2^24 4 KiB blocks of BASELINE config 2 (64 GiB,
+    device-resident): CRC-32 of the 512 MiB digest array equals the oracle's
+    (tests/golden/make_summaries.py)."""
+    import zlib
+    n = 1 << 24
+    d = ctx.alloc(n * 4096)
+    ctx.gen_stream(d.ptr, 0x5EED0002, 0, n * 4096)
+    out = ctx.alloc(32 * n)
+    ctx.sha256_fixed_device(d.ptr, 4096, 4096, n, out.ptr)
+    ctx.sync()
+    assert "%08x" % zlib.crc32(out.download(np.uint8).tobytes()) == _summaries()["config2"]["summary_sha256"]
+    d.free()
+    out.free()
+
+
+def test_config3_full_size_summary(ctx):
+    """SHA-256 of all 2^26 Zipf records of BASELINE config 3 (~97 GiB packed,
+    device-resident, length-ordered dispatch): digest-array CRC equals the oracle's."""
+    import zlib
+    from lsm_storage_engine_amd.device import gen_zipf_lengths
+    n = 1 << 26
+    ln = gen_zipf_lengths(0x5EED0003, n)
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum(ln[:-1].astype(np.uint64), out=off[1:])
+    total = int(off[-1]) + int(ln[-1])
+    d = ctx.alloc(total + 64)
+    ctx.gen_stream(d.ptr, 0x5EED0003, 0, total)
+    d_o, d_l, out = ctx.alloc(off.nbytes), ctx.alloc(ln.nbytes), ctx.alloc(32 * n)
+    d_o.upload(off)
+    d_l.upload(ln)
+    ctx.sha256_device(d.ptr, d_o.ptr, d_l.ptr, n, out.ptr)
+    ctx.sync()
+    assert "%08x" % zlib.crc32(out.download(np.uint8).tobytes()) == _summaries()["config3"]["summary_sha256"]
+    for buf in (d, d_o, d_l, out):
+        buf.free()

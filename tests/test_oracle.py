@@ -121,3 +121,22 @@ def test_generators():
     assert L.min() >= 64 and L.max() <= 65536
     assert 1200 < L.mean() < 1900  # mean ~1538 B at s = 1.5
     assert abs((L == 64).mean() - 0.38) < 0.03
+
+
+# BASELINE config 1: 2^20 x 256 B records of the splitmix64 stream,
+# seed 0x5EED0001.  Summary digest = CRC-32 of the little-endian output array,
+# for cross-run comparison (bench.py reports the GPU's as "summary_crc32").
+CONFIG1_SUMMARY_CRC32 = 0x727D43C0
+
+
+def test_config1_full_size_oracle_vs_zlib():
+    """The oracle's Sarwate CRC at BASELINE config 1's full size against zlib's
+    crc32 (an independent implementation of CRC-32/ISO-HDLC), record by record."""
+    import zlib
+    n = 1 << 20
+    data = O.gen_stream(0x5EED0001, 0, n * 256)
+    out = O.crc32_fixed(data, 256, 256, n, threads=8)
+    mv = memoryview(data)
+    z = np.fromiter((zlib.crc32(mv[i * 256:(i + 1) * 256]) for i in range(n)), dtype=np.uint32, count=n)
+    assert np.array_equal(out, z)
+    assert zlib.crc32(out.astype("<u4").tobytes()) == CONFIG1_SUMMARY_CRC32
