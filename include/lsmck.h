@@ -144,7 +144,10 @@ int lsmck_device_count(void);
  *                 segment-factor multiply, 9 = without the first-segment
  *                 masks, 10 = without the alignbyte funnel; 12 = loads only
  *                 with the real descriptor map but the aligned (FAST) payload
- *                 loads (4 KiB records at 4 KiB stride only);
+ *                 loads (4 KiB records at 4 KiB stride only); packed
+ *                 batches only (record r+1 starts where r ends): 13 = loads
+ *                 only in a raw-buffer-load form of the general window,
+ *                 14 = the full kernel with that load form;
  *                 0 = off.  Locates the kernels' ceilings.
  *   "crc_wg_waves"  waves per workgroup of the descriptor CRC kernel and of
  *                 the whole-tile ring kernel: 12 or 16 (0 = built-in default).

@@ -554,7 +554,7 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     return 0;
   }
   if (!strcmp(key, "crc_ablate")) {  // diagnostic only: timing ablations, results are garbage
-    if (value < 0 || value > 12) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0..12");
+    if (value < 0 || value > 14) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0..14");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->variant = (ctx->variant & ~0xF00) | ((int)value << 8);
     return 0;

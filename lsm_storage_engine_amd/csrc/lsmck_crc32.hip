@@ -296,6 +296,49 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
   keep_live(w);
 }
 
+// Diagnostic load form (crc_ablate 13 / 14, packed batches only: record r+1
+// starts where r ends): the general form's window, zero-lane and page rules as
+// raw buffer loads, in program order, from a wave-uniform tile base (lane 0's
+// window start less 512 B; every later window of a packed tile starts at or
+// after it) instead of per-lane 64-bit global_load pointers.  Empty lanes load
+// from an out-of-range offset (zeros, no access).  The range ends 4 bytes past
+// the batch's last byte, inside the last dword.
+__device__ __forceinline__ void seg_issue_pk(const CrcParams& P, const SegInfo& si, SegLoad& L, uint64_t data_end) {
+  const uint64_t E = si.rec_off + si.rec_len - 128ull * si.k;
+  const uint32_t seglen = (si.q == 0) ? si.rec_len - 128u * si.k : 128u;
+  const uint32_t lead = 128u - seglen;
+  L.rec = si.rec;
+  L.k = si.k;
+  const uint32_t flv = (si.valid ? FL_VALID : 0u) | (si.q == 0 ? FL_FIRST : 0u);
+  const uint64_t w0 = E - 128;
+  const uint32_t sh = (uint32_t)(((uintptr_t)P.base + w0) & 3);
+  const uint64_t pw = w0 - sh;
+  const uint32_t bstart = sh + lead;
+  const bool empty = lead >= 128u;
+  const uintptr_t pa = (uintptr_t)P.base + pw;
+  const uintptr_t pg = (pa + bstart) & ~(uintptr_t)4095;
+  const bool cross = !empty & (pg > pa);
+  const uint32_t m = cross ? (uint32_t)(pg - pa) >> 2 : 0u;
+  L.fl = flv | sh | (bstart << 2) | (m << 12);
+  const uint32_t e_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pw);
+  const uint32_t e_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pw >> 32));
+  const uint64_t tb = (((uint64_t)e_hi << 32) | e_lo) - 512u;
+  const uint64_t span = data_end + 4u - tb;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char*>(P.base + tb), (short)0, (int)(span < 0x7FFFFFFFull ? span : 0x7FFFFFFFull), 0x00020000);
+  const uint32_t vo = empty ? 0x80000000u : (uint32_t)(pw + 4u * m - tb);
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 16u * g, 0, 0);
+    L.d[4 * g + 0] = v[0];
+    L.d[4 * g + 1] = v[1];
+    L.d[4 * g + 2] = v[2];
+    L.d[4 * g + 3] = v[3];
+  }
+  L.d[32] = __builtin_amdgcn_raw_buffer_load_b32(r, vo + ((sh != 0u && m == 0u) ? 128u : 124u), 0, 0);
+  keep_live(vo);
+}
+
 // Funnel, mask, raw slicing-by-4 CRC, init term, shift to the record's end.
 // CHAINS independent register chains per lane (the segment's 128 bytes cut in
 // CHAINS pieces) hide the LDS lookup latency; they are recombined with the
@@ -303,7 +346,7 @@ __device__ __forceinline__ void seg_issue(const CrcParams& P, const SegInfo& si,
 template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
 __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const CrcParams& P, const SegLoad& L,
                                                uint32_t lo, uint32_t hi) {
-  if (ABLATE == 1 || (ABLATE >= 3 && ABLATE <= 7) || ABLATE == 12) {  // diagnostic: loads only (results invalid)
+  if (ABLATE == 1 || (ABLATE >= 3 && ABLATE <= 7) || ABLATE == 12 || ABLATE == 13) {  // diagnostic: loads only (results invalid)
     uint32_t x = 0;
 #pragma unroll
     for (int j = 0; j < 33; ++j) x ^= L.d[j];
@@ -448,7 +491,7 @@ template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
 __device__ __forceinline__ void finish_tile(const unsigned char* smem, const CrcParams& P, const SegLoad& L,
                                             uint32_t lane, uint32_t lo, uint32_t hi) {
   uint32_t v = seg_finish<FAST, CHAINS, ABLATE, PERCOL>(smem, P, L, lo, hi);
-  if ((ABLATE >= 3 && ABLATE <= 7) || ABLATE == 12) {  // no reduction, no store (unless a magic value: keeps the loads alive)
+  if ((ABLATE >= 3 && ABLATE <= 7) || ABLATE == 12 || ABLATE == 13) {  // no reduction, no store (unless a magic value: keeps the loads alive)
     if (v == 0x9E3779B1u) P.out[0] = v;
     return;
   }
@@ -746,6 +789,7 @@ __global__ __launch_bounds__(BLOCK) void crc32_desc_kernel(CrcParams P) {
   const uint32_t total = (uint32_t)*P.total_segs;  // host checked < 2^32
   const int32_t nt = (int32_t)((total + 63u) >> 6);  // < 2^26
   if (wave >= nt) return;
+  const uint64_t data_end = (ABLATE == 13 || ABLATE == 14) ? P.off[P.nrec - 1] + P.len[P.nrec - 1] : 0;
   uint32_t T0 = 0, T1 = 0;  // virtual tiles: no loads needed, all lanes pad
   SegInfo M0, M1;
   M0.valid = M1.valid = false;
@@ -769,7 +813,10 @@ __global__ __launch_bounds__(BLOCK) void crc32_desc_kernel(CrcParams P) {
     M0 = desc_map_issue<ABLATE>(P, T0, c + 2 * n, lane, total);
     T1 = desc_tile<ABLATE>(P, c + 3 * n, nt, lane);
     desc_map_complete(M1);
-    seg_issue<(ABLATE == 6 || ABLATE == 12), ABLATE>(P, M1, B);
+    if constexpr (ABLATE == 13 || ABLATE == 14)
+      seg_issue_pk(P, M1, B, data_end);
+    else
+      seg_issue<(ABLATE == 6 || ABLATE == 12), ABLATE>(P, M1, B);
     __builtin_amdgcn_sched_barrier(0);
     finish_tile<false, CHAINS, ABLATE>(smem, P, A, lane, lo, hi);  // virtual tiles: pad lanes, no store
     c += n;
@@ -777,7 +824,10 @@ __global__ __launch_bounds__(BLOCK) void crc32_desc_kernel(CrcParams P) {
     M1 = desc_map_issue<ABLATE>(P, T1, c + 2 * n, lane, total);
     T0 = desc_tile<ABLATE>(P, c + 3 * n, nt, lane);
     desc_map_complete(M0);
-    seg_issue<(ABLATE == 6 || ABLATE == 12), ABLATE>(P, M0, A);
+    if constexpr (ABLATE == 13 || ABLATE == 14)
+      seg_issue_pk(P, M0, A, data_end);
+    else
+      seg_issue<(ABLATE == 6 || ABLATE == 12), ABLATE>(P, M0, A);
     __builtin_amdgcn_sched_barrier(0);
     finish_tile<false, CHAINS, ABLATE>(smem, P, B, lane, lo, hi);
     c += n;
@@ -1123,6 +1173,8 @@ extern "C" int lsmk_launch_crc32_desc(const CrcParams* P, const uint64_t* block_
                           : ablate == 10 ? (const void*)crc32_desc_kernel<2, 10>
                           : ablate == 11 ? (const void*)crc32_desc_kernel<2, 2>
                           : ablate == 12 ? (const void*)crc32_desc_kernel<1, 12>
+                          : ablate == 13 ? (const void*)crc32_desc_kernel<2, 13>
+                          : ablate == 14 ? (const void*)crc32_desc_kernel<2, 14>
                           : ch == 1 ? (const void*)crc32_desc_kernel<1>
                           : ch == 2 ? (const void*)crc32_desc_kernel<2> : (const void*)crc32_desc_kernel<4>);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
