@@ -14,6 +14,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
+from .shard import shard_by_bytes, shard_fixed
 
 
 def _p(a):
@@ -242,6 +243,65 @@ class Context:
                 "stat_seconds": rep.stat_seconds, "read_seconds": rep.read_seconds,
                 "gpu_wait_seconds": rep.gpu_wait_seconds, "compare_seconds": rep.compare_seconds,
                 "rounds": rep.rounds, "fds_cached": rep.fds_cached}
+
+
+class MultiContext:
+    """Host-resident batches split over several GPUs in one process (SURVEY
+    8e): one Context per device, one host thread each (the ctypes calls drop
+    the GIL), contiguous record ranges -- by bytes for variable-length records
+    (shard.shard_by_bytes), by count for fixed ones -- and no data exchange
+    between devices: each device's results land in its slice of the output.
+    Each device's host path streams its share through its own pinned slots,
+    so the PCIe links of the devices work in parallel."""
+
+    def __init__(self, devices=None, contexts=None):
+        if contexts is None:
+            devices = range(device_count()) if devices is None else devices
+            contexts = [Context(d) for d in devices]
+        if not contexts:
+            raise _lib.LsmckError(_lib.ENODEV, "MultiContext: no device")
+        self.ctxs = list(contexts)
+
+    def _parallel(self, bounds, fn):
+        import concurrent.futures as cf
+        with cf.ThreadPoolExecutor(len(self.ctxs)) as ex:
+            for f in [ex.submit(fn, k, int(bounds[k]), int(bounds[k + 1])) for k in range(len(self.ctxs))]:
+                f.result()
+
+    def _var(self, data, off, length, width, call):
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        out = np.empty((len(off), width) if width > 1 else len(off), dtype=np.uint8 if width > 1 else np.uint32)
+        b = shard_by_bytes(length, len(self.ctxs))
+
+        def part(k, r0, r1):
+            if r1 > r0:
+                out[r0:r1] = call(self.ctxs[k], data, off[r0:r1], length[r0:r1])
+        self._parallel(b, part)
+        return out
+
+    def _fixed(self, data, stride, length, n, width, call):
+        out = np.empty((n, width) if width > 1 else n, dtype=np.uint8 if width > 1 else np.uint32)
+        b = [shard_fixed(n, len(self.ctxs), k)[0] for k in range(len(self.ctxs))] + [n]
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+
+        def part(k, r0, r1):
+            if r1 > r0:
+                out[r0:r1] = call(self.ctxs[k], data[r0 * stride:], stride, length, r1 - r0)
+        self._parallel(b, part)
+        return out
+
+    def crc32(self, data, off, length):
+        return self._var(np.ascontiguousarray(data, dtype=np.uint8), off, length, 1, Context.crc32)
+
+    def crc32_fixed(self, data, stride, length, n):
+        return self._fixed(data, stride, length, n, 1, Context.crc32_fixed)
+
+    def sha256(self, data, off, length):
+        return self._var(np.ascontiguousarray(data, dtype=np.uint8), off, length, 32, Context.sha256)
+
+    def sha256_fixed(self, data, stride, length, n):
+        return self._fixed(data, stride, length, n, 32, Context.sha256_fixed)
 
 
 # include/lsmck.h lsmck_wal_rec (32 bytes, no padding)

@@ -314,3 +314,23 @@ def test_config3_full_size_summary(ctx):
     assert "%08x" % zlib.crc32(got.astype("<u4").tobytes()) == _summaries()["config3"]["summary_crc32"]
     for buf in (d, d_o, d_l, out):
         buf.free()
+
+
+def test_multicontext_host_batches():
+    """MultiContext: host batches split by bytes (variable) / count (fixed)
+    over several contexts, each on its own host thread (here 3 contexts on
+    device 0: the box has one GPU), identical to the oracle."""
+    from lsm_storage_engine_amd.device import Context, MultiContext
+    mc = MultiContext(contexts=[Context(0) for _ in range(3)])
+    ln = O.gen_zipf_lengths(0x5EED0040, 20000)
+    off, total = _packed(ln, align_shift=1)
+    data = O.gen_stream(0x5EED0041, 0, total + 8)
+    assert np.array_equal(mc.crc32(data, off, ln), O.crc32_batch(data, off, ln, threads=8))
+    assert np.array_equal(mc.sha256(data, off, ln), np.asarray(O.sha256_batch(data, off, ln, threads=8)).reshape(-1, 32))
+    n = 5001
+    blk = O.gen_stream(0x5EED0042, 0, n * 300)
+    assert np.array_equal(mc.crc32_fixed(blk, 300, 297, n), O.crc32_fixed(blk, 300, 297, n, threads=8))
+    want = np.asarray(O.sha256_batch(blk, np.arange(n, dtype=np.uint64) * 300, np.full(n, 297, np.uint32),
+                                     threads=8)).reshape(-1, 32)
+    assert np.array_equal(mc.sha256_fixed(blk, 300, 297, n), want)
+    assert len(mc.crc32(data, off[:2], ln[:2])) == 2  # fewer records than devices
