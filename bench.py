@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--cpu-sample-records", type=int, default=0)
     ap.add_argument("--variants", default="", help="comma list of crc_chains values to A/B in interleaved rounds")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--no-stream-ceiling", action="store_true",
+                    help="skip the loads-only ceiling run of the same kernel (roofline.loads_only_ceiling)")
     ap.add_argument("--no-host-roundtrip", action="store_true",
                     help="skip the host-resident (pinned H2D + kernel + D2H) sample")
     ap.add_argument("--desc", action="store_true",
@@ -438,6 +440,31 @@ def main():
                               "matches": bool(np.array_equal(np.asarray(zl, dtype=np.uint32), want))},
             "sample": "the cpu_baseline sample",
         }
+    # The kernel's own memory ceiling ("report against a measured
+    # streaming-read peak from the build's own read-only kernel"): the same
+    # kernel and launch with crc_ablate 3 -- payload loads only, no checksum,
+    # no store -- on the same buffer, timed like the bench line.  Last: it
+    # leaves `out` invalid, so every check of `out` above runs first.
+    if rank == 0 and world == 1 and not sha and not a.no_stream_ceiling and ab is None:
+        ctx.set_option("crc_ablate", 3)
+        try:
+            step()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(5):
+                step()
+            e1.record(stream)
+            ctx.sync(sptr)
+            lms = e0.elapsed_time(e1) / 5
+        finally:
+            ctx.set_option("crc_ablate", 0)
+        ceil_gbs = algo_bytes / (lms * 1e-3) / 1e9
+        res["roofline"]["loads_only_ceiling"] = {
+            "GBps": round(ceil_gbs, 1), "launch_ms": round(lms, 4),
+            "frac_of_ceiling": round(achieved_gbs / ceil_gbs, 4),
+            "how": "same kernel with crc_ablate 3: payload loads only (no checksum, no store), same buffer",
+        }
+
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.sync(sptr)
