@@ -161,11 +161,16 @@ struct P {
 };
 }  // namespace
 
+// Small JSON files (a few hundred bytes): one read(2) normally suffices.  A
+// read that returns less than asked is taken as end of file -- what a regular
+// file's read does -- which saves the extra read(2) that would return 0: a
+// whole-tree verify opens ~230k such files, and the system calls are its cost
+// (DESIGN.md 7a).
 static int read_file(const char* path, std::string* buf) {
   int fd = open(path, O_RDONLY | O_CLOEXEC);
   if (fd < 0) return set_errno_error(errno, "open", path);
   buf->clear();
-  char tmp[4096];
+  char tmp[16384];
   for (;;) {
     ssize_t k = read(fd, tmp, sizeof tmp);
     if (k < 0) {
@@ -174,8 +179,8 @@ static int read_file(const char* path, std::string* buf) {
       close(fd);
       return set_errno_error(e, "read", path);
     }
-    if (k == 0) break;
     buf->append(tmp, (size_t)k);
+    if ((size_t)k < sizeof tmp) break;
   }
   close(fd);
   return 0;
