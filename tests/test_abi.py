@@ -247,3 +247,49 @@ def test_batch_entry_points_fail_loudly_without_gpu():
     from lsm_storage_engine_amd.device import Context
     with pytest.raises(RuntimeError):
         Context(0)
+
+
+# Property tests: the scalar C ABI (the WAL append path and checksums.rs's
+# file digests) against independent implementations of the same algorithms,
+# on arbitrary inputs: zlib.crc32 (= crc 1.x checksum_ieee), hashlib.sha256
+# (= sha2 0.10) and base64.b64encode (= base64 0.13 STANDARD).
+from hypothesis import given, settings, strategies as st  # noqa: E402
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.binary(max_size=5000), st.binary(max_size=300))
+def test_property_crc32_scalar_vs_zlib(a, b):
+    import zlib
+    assert crc32.checksum_ieee(a) == zlib.crc32(a)
+    assert crc32.update(crc32.checksum_ieee(a), b) == zlib.crc32(a + b)
+    assert crc32.combine(zlib.crc32(a), zlib.crc32(b), len(b)) == zlib.crc32(a + b)
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.binary(max_size=3000), st.lists(st.integers(1, 200), max_size=20))
+def test_property_sha256_scalar_vs_hashlib(data, steps):
+    import hashlib
+    lib = _lib.load()
+    out = (C.c_uint8 * 32)()
+    lib.lsmck_sha256(data, len(data), out)
+    assert bytes(out) == hashlib.sha256(data).digest()
+    c = _lib.Sha256Ctx()
+    lib.lsmck_sha256_init(C.byref(c))
+    i, k = 0, 0
+    while i < len(data):  # arbitrary update boundaries
+        step = steps[k % len(steps)] if steps else 64
+        lib.lsmck_sha256_update(C.byref(c), data[i:i + step], len(data[i:i + step]))
+        i += step
+        k += 1
+    lib.lsmck_sha256_final(C.byref(c), out)
+    assert bytes(out) == hashlib.sha256(data).digest()
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.binary(max_size=200))
+def test_property_base64_vs_stdlib(raw):
+    import base64
+    out = C.create_string_buffer(4 * ((len(raw) + 2) // 3) + 1)
+    n = _lib.load().lsmck_base64_encode(raw, len(raw), out)
+    want = base64.b64encode(raw)
+    assert out.value == want and n == len(want)

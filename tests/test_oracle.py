@@ -140,3 +140,23 @@ def test_config1_full_size_oracle_vs_zlib():
     z = np.fromiter((zlib.crc32(mv[i * 256:(i + 1) * 256]) for i in range(n)), dtype=np.uint32, count=n)
     assert np.array_equal(out, z)
     assert zlib.crc32(out.astype("<u4").tobytes()) == CONFIG1_SUMMARY_CRC32
+
+
+# The oracle against independent implementations on arbitrary inputs
+# (hypothesis): zlib.crc32 and hashlib.sha256, one record and a batch.
+from hypothesis import given, settings, strategies as st  # noqa: E402
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.binary(max_size=700), min_size=1, max_size=40))
+def test_property_oracle_batches_vs_stdlib(recs):
+    import hashlib
+    import zlib
+    data = np.frombuffer(b"".join(recs) + b"\0" * 8, dtype=np.uint8)
+    ln = np.array([len(r) for r in recs], dtype=np.uint32)
+    off = np.zeros(len(recs), dtype=np.uint64)
+    np.cumsum(ln[:-1].astype(np.uint64), out=off[1:])
+    assert list(O.crc32_batch(data, off, ln)) == [zlib.crc32(r) for r in recs]
+    got = np.asarray(O.sha256_batch(data, off, ln)).reshape(-1, 32)
+    assert [bytes(g) for g in got] == [hashlib.sha256(r).digest() for r in recs]
+    assert O.crc32(recs[0]) == zlib.crc32(recs[0])
