@@ -334,3 +334,27 @@ def test_multicontext_host_batches():
                                      threads=8)).reshape(-1, 32)
     assert np.array_equal(mc.sha256_fixed(blk, 300, 297, n), want)
     assert len(mc.crc32(data, off[:2], ln[:2])) == 2  # fewer records than devices
+
+
+from hypothesis import given, settings, strategies as st  # noqa: E402
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.lists(st.binary(max_size=1500), min_size=1, max_size=300), st.integers(0, 7), st.booleans())
+def test_property_gpu_batches_vs_stdlib(ctx, recs, shift, packed):
+    """Arbitrary record sets (empty records, any lengths and alignments,
+    packed or with gaps) through the GPU batch paths against zlib.crc32 and
+    hashlib.sha256: independent implementations of crc 1.x and sha2 0.10."""
+    import hashlib
+    import zlib
+    gap = b"" if packed else b"\xa5" * 3
+    buf = bytearray(b"\x00" * shift)
+    off = []
+    for r in recs:
+        off.append(len(buf))
+        buf += r + gap
+    data = np.frombuffer(bytes(buf) + b"\0" * 8, dtype=np.uint8)
+    off = np.array(off, dtype=np.uint64)
+    ln = np.array([len(r) for r in recs], dtype=np.uint32)
+    assert list(ctx.crc32(data, off, ln)) == [zlib.crc32(r) for r in recs]
+    assert [bytes(d) for d in ctx.sha256(data, off, ln)] == [hashlib.sha256(r).digest() for r in recs]
