@@ -358,3 +358,23 @@ def test_property_gpu_batches_vs_stdlib(ctx, recs, shift, packed):
     ln = np.array([len(r) for r in recs], dtype=np.uint32)
     assert list(ctx.crc32(data, off, ln)) == [zlib.crc32(r) for r in recs]
     assert [bytes(d) for d in ctx.sha256(data, off, ln)] == [hashlib.sha256(r).digest() for r in recs]
+
+
+def test_empty_batches_every_entry_point(ctx):
+    """n = 0 everywhere: every batch entry point returns an empty result
+    without a launch (and without touching the null or dangling pointers an
+    empty Rust slice may carry)."""
+    data = np.zeros(16, dtype=np.uint8)
+    e64, e32 = np.zeros(0, dtype=np.uint64), np.zeros(0, dtype=np.uint32)
+    assert len(ctx.crc32(data, e64, e32)) == 0
+    assert len(ctx.crc32_fixed(data, 16, 16, 0)) == 0
+    assert len(ctx.sha256(data, e64, e32)) == 0
+    assert len(ctx.sha256_fixed(data, 16, 16, 0)) == 0
+    assert ctx.checksums_verify_many([]) == []
+    recs, rc, _ = ctx.wal_replay_verify(b"")
+    assert rc == 0 and len(recs) == 0
+    d = ctx.alloc(64)
+    out = ctx.alloc(64)
+    ctx.crc32_fixed_device(d.ptr, 16, 16, 0, out.ptr)
+    ctx.sha256_fixed_device(d.ptr, 16, 16, 0, out.ptr)
+    ctx.sync()
