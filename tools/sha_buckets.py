@@ -37,6 +37,9 @@ def timed(ctx, stream, fn, reps=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--records", type=int, default=1 << 24)
+    ap.add_argument("--presorted", action="store_true",
+                    help="pack each class's messages in decreasing block-count order, so a wave's lanes read "
+                         "neighbouring messages (locality / TLB-reach diagnostic)")
     a = ap.parse_args()
     ctx = Context(0)
     stream = torch.cuda.Stream()
@@ -47,6 +50,8 @@ def main():
     for lo, hi in CLASSES:
         sel = (nb_all >= lo) & (nb_all <= hi)
         ln = ln_all[sel].astype(np.uint32)
+        if a.presorted:
+            ln = ln[np.argsort(-((ln.astype(np.int64) + 72) >> 6), kind="stable")]
         n = len(ln)
         if n < 64:
             continue
