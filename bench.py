@@ -180,7 +180,9 @@ def main():
                 # "a<k>" = diagnostic ablation k (timing only); optional suffix
                 # "w<n>" = crc_wg_waves n (descriptor kernel); "l<n>" = crc_loads n
                 # (1 global, 2 raw buffer); "r<n>" = crc_ring n (1 = two-slot kernel)
-                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?(?:r(\d))?", v)
+                # "b<n>" = sha_bucket_shift n (SHA order: 2^n-block buckets for 128..1023 blocks)
+                # "f<n>" = sha_bucket_from n (first block count of the coarse buckets)
+                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?(?:r(\d))?(?:b(\d))?(?:f(\d+))?", v)
                 if not m:
                     raise SystemExit(f"bad variant {v!r}")
                 kind, num, waves = m.group(1), int(m.group(2)), int(m.group(3) or 0)
@@ -190,6 +192,8 @@ def main():
                 ctx.set_option("crc_wg_waves", waves)
                 ctx.set_option("crc_loads", int(m.group(4) or 0))
                 ctx.set_option("crc_ring", int(m.group(5) or 0))
+                ctx.set_option("sha_bucket_shift", int(m.group(6)) if m.group(6) is not None else 2)
+                ctx.set_option("sha_bucket_from", int(m.group(7) or 128))
                 step()
                 e0.record(stream)
                 for _ in range(a.steps):
@@ -203,6 +207,8 @@ def main():
         ctx.set_option("crc_wg_waves", 0)
         ctx.set_option("crc_loads", 0)
         ctx.set_option("crc_ring", 0)
+        ctx.set_option("sha_bucket_shift", 2)
+        ctx.set_option("sha_bucket_from", 128)
         ab = {str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                        "GiBps_median": payload / GIB / (float(np.median(t)) * 1e-3)} for v, t in ab.items()}
 

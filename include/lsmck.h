@@ -159,6 +159,10 @@ int lsmck_device_count(void);
  *   "sha_order"   variable-length SHA-256 batches of >= 2048 messages run in
  *                 decreasing length order (1, default) or batch order (0).
  *                 A/B switch; digests are identical either way.
+ *   "sha_bucket_shift" / "sha_bucket_from"  that order's length key: messages
+ *                 of from..1023 compression blocks share a bucket per
+ *                 2^shift blocks (defaults 2 and 128; shift 0 = exact block
+ *                 counts).  A/B switch; digests are identical either way.
  *   "tree_active_files" / "tree_slice_bytes"  lsmck_checksums_verify_many's
  *                 files in flight (0 = 8192) and bytes of a file per round
  *                 (0 = 128 KiB; a multiple of 64).  Tests use small values.

@@ -181,6 +181,8 @@ struct lsmck_ctx {
   uint32_t tree_active = 0;  // whole-tree verify: files in flight (0 = kTreeActive)
   uint32_t tree_slice = 0;   // whole-tree verify: bytes of a file per round (0 = kTreeSlice)
   long tree_open = -1;       // whole-tree verify: files kept open between slices (-1 = RLIMIT_NOFILE budget)
+  int sha_bucket_shift = 2;  // SHA order key: 2^shift-block buckets for from..1023 blocks (0 = exact; A/B: DESIGN.md 3.2)
+  int sha_bucket_from = 128;
   unsigned tree_list_threads = 0;  // lsmck_tree_verify: metadata parsing threads (0 = kListThreads)
   struct {
     uint32_t* state = nullptr;  // 8 u32 per active slot
@@ -305,10 +307,10 @@ int sha_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const uint6
     if ((rc = ensure_dev(&sc.sha_keys, &sc.cap_keys, n))) return rc;
     if ((rc = ensure_dev(&sc.sha_order, &sc.cap_order, n))) return rc;
     size_t tmp = 0;
-    rc = lsmk_sha_order(len, n, sc.sha_keys, sc.sha_order, nullptr, &tmp, st);
+    rc = lsmk_sha_order(len, n, sc.sha_keys, sc.sha_order, nullptr, &tmp, ctx->sha_bucket_shift, ctx->sha_bucket_from, st);
     if (rc) return launch_rc(rc, "sha order (size query)");
     if ((rc = ensure_dev(&sc.sort_tmp, &sc.cap_tmp, std::max<size_t>(tmp, 1)))) return rc;
-    rc = lsmk_sha_order(len, n, sc.sha_keys, sc.sha_order, sc.sort_tmp, &tmp, st);
+    rc = lsmk_sha_order(len, n, sc.sha_keys, sc.sha_order, sc.sort_tmp, &tmp, ctx->sha_bucket_shift, ctx->sha_bucket_from, st);
     if (rc) return launch_rc(rc, "sha order (radix sort)");
     order = sc.sha_order;
   }
@@ -595,6 +597,18 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     if (value < 0 || value > 256) return lsmck_host::set_error(LSMCK_EINVAL, "tree_list_threads: 0..256");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->tree_list_threads = (unsigned)value;
+    return 0;
+  }
+  if (!strcmp(key, "sha_bucket_from")) {  // A/B: first block count of the coarse SHA buckets
+    if (value < 2 || value > 1024) return lsmck_host::set_error(LSMCK_EINVAL, "sha_bucket_from: 2..1024");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->sha_bucket_from = (int)value;
+    return 0;
+  }
+  if (!strcmp(key, "sha_bucket_shift")) {  // A/B: coarser SHA length buckets (0 = exact block counts)
+    if (value < 0 || value > 6) return lsmck_host::set_error(LSMCK_EINVAL, "sha_bucket_shift: 0..6");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->sha_bucket_shift = (int)value;
     return 0;
   }
   if (!strcmp(key, "sha_order")) {  // A/B: 1 = variable-length SHA batches in decreasing length order (default)

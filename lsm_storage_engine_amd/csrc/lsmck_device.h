@@ -69,7 +69,7 @@ int lsmk_launch_sha256_slices(const lsmck::ShaSliceParams* P, hipStream_t st);
 int lsmk_launch_crc32_compare(const uint32_t* crc, const uint32_t* expected, uint64_t n,
                                unsigned long long* n_bad, unsigned long long* first_bad, hipStream_t st);
 int lsmk_sha_order(const uint32_t* len, size_t n, uint16_t* keys_out, uint32_t* order, void* tmp, size_t* tmp_bytes,
-                   hipStream_t st);
+                   int coarse, int from, hipStream_t st);
 int lsmk_launch_gen_stream(unsigned char* dst, uint64_t seed, uint64_t byte_off, uint64_t n, hipStream_t st);
 }
 #endif

@@ -132,8 +132,8 @@ def test_verify_many_streaming(ctx, tmp_path, active, slice_bytes, open_files):
     assert sum(1 for s in st if s) == 4
 
 
-@pytest.mark.parametrize("order", [1, 0])
-def test_length_sorted_batch(ctx, order):
+@pytest.mark.parametrize("order,shift,start", [(1, 2, 128), (1, 0, 128), (1, 3, 16), (0, 2, 128)])
+def test_length_sorted_batch(ctx, order, shift, start):
     """Variable-length batches of >= 2048 messages run in decreasing length
     order (lsmck_order.hip, "sha_order" 1) -- or batch order (0): the digests
     land at each message's own index either way.  Zipf lengths (config 3's
@@ -144,16 +144,21 @@ def test_length_sorted_batch(ctx, order):
     ln = O.gen_zipf_lengths(0x5EED0003, n).astype(np.uint32)
     ln[:8] = [0, 1, 55, 56, 63, 64, 65, 119]
     ln[8:12] = [70000, 131072, 200001, 65536]  # the log-spaced buckets
+    ln[12:16] = [127 * 64, 128 * 64 - 9, 1023 * 64 - 10, 1024 * 64 - 9]  # edges of the coarse buckets
     ln = ln[rng.permutation(n)]
     off = np.zeros(n, dtype=np.uint64)
     off[1:] = np.cumsum(ln[:-1].astype(np.uint64) + rng.integers(0, 5, n - 1).astype(np.uint64))
     total = int(off[-1]) + int(ln[-1])
     data = O.gen_stream(0x5EED0031, 0, total + 8)
     ctx.set_option("sha_order", order)
+    ctx.set_option("sha_bucket_shift", shift)
+    ctx.set_option("sha_bucket_from", start)
     try:
         got = ctx.sha256(data, off, ln)
     finally:
         ctx.set_option("sha_order", 1)
+        ctx.set_option("sha_bucket_shift", 2)
+        ctx.set_option("sha_bucket_from", 128)
     assert np.array_equal(got, O.sha256_batch(data, off, ln, threads=8))
 
 
