@@ -34,6 +34,15 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_a
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
+// Ch(e, f, g) = e ? f : g and Maj(a, b, c) in one v_bitop3_b32 each (truth
+// tables 0xCA, 0xE8; bit (x<<2 | y<<1 | z) of the table for inputs x, y, z).
+// hipcc builds Maj as v_xor + v_and + v_bitop3 otherwise: 128 VALU per block.
+__device__ __forceinline__ uint32_t ch3(uint32_t e, uint32_t f, uint32_t g) {
+  return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+}
+__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
 
 __device__ __forceinline__ void sha256_compress(uint32_t (&h)[8], uint32_t (&w)[16]) {
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
@@ -50,10 +59,10 @@ __device__ __forceinline__ void sha256_compress(uint32_t (&h)[8], uint32_t (&w)[
       w[t & 15] = wt;
     }
     uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
-    uint32_t ch = (e & f) ^ (~e & g);
+    uint32_t ch = ch3(e, f, g);
     uint32_t t1 = hh + S1 + ch + kSha256K[t] + wt;
     uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint32_t mj = maj3(a, b, c);
     hh = g;
     g = f;
     f = e;
