@@ -36,11 +36,13 @@ GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, GB/s (MI355X_MICROARCH.md chip table)
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # full-rate VALU issue slots/s: 256 CU x 128 lanes/clk x 2.4 GHz
 # VALU issue slots per SHA-256 compression in sha256_kernel's main loop (gfx950
-# ISA: 1,425 instructions = 576 v_alignbit_b32 + 241 v_add3_u32, which issue at
-# half rate (tools/microbench_valu.hip: 62 vs 103-110 lane-ops/clk/CU for
-# v_add_u32 / v_xor_b32 / v_bitop3_b32), + 608 full-rate; 576*2 + 241*2 + 608).
-# Ch and Maj are one v_bitop3_b32 each (r01 v6; was 1,553 instructions, 2,370).
-SHA_OPS_PER_BLOCK = 2242
+# ISA, per block: 576 v_alignbit_b32 + 241 v_add3_u32 + 16 v_perm_b32, which
+# issue at half rate (tools/microbench_valu.hip: 62 vs 103-110 lane-ops/clk/CU
+# for v_add_u32 / v_xor_b32 / v_bitop3_b32), + 572 full-rate (352 v_bitop3,
+# 118 v_add, 96 v_lshrrev, 6 other): 833*2 + 572 = 2,238.  r01 v6: Ch and Maj
+# are one v_bitop3 each, and the funnel + byte swap one v_perm (the earlier
+# kernel issued 1,553 instructions per block).
+SHA_OPS_PER_BLOCK = 2238
 METRIC = "GiB/s device-resident batched record checksum; % of HBM3E read BW"
 SEED = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003}
 

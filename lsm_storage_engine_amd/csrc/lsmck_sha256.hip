@@ -138,10 +138,14 @@ __device__ __forceinline__ void issue_win(const unsigned char* base, uint64_t of
   W.d[16] = ld32(p + 64);
   asm volatile("" ::"v"(p));  // keep the address live: no load overwrites it (lsmck_crc32.hip keep_live)
 }
+// Funnel shift by sh bytes and big-endian byte swap in one v_perm_b32 per
+// word: result byte k = byte (3 - k + sh) of {W.d[j+1]:W.d[j]} (selector
+// 0x00010203 + sh * 0x01010101) -- instead of v_alignbyte + v_perm.
 __device__ __forceinline__ void compress_win(uint32_t (&h)[8], const ShaWin& W, uint32_t sh) {
+  const uint32_t sel = 0x00010203u + sh * 0x01010101u;
   uint32_t w[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) w[j] = __builtin_bswap32(__builtin_amdgcn_alignbyte(W.d[j + 1], W.d[j], sh));
+  for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_perm(W.d[j + 1], W.d[j], sel);
   sha256_compress(h, w);
 }
 
