@@ -145,6 +145,20 @@ __device__ __forceinline__ uint32_t crc_word(const unsigned char* smem, uint32_t
   return lds_ld(smem, a0 + 128u) ^ lds_ld(smem, a1) ^ lds_ld(smem, a2 + 128u) ^ lds_ld(smem, a3);
 }
 
+// The same step on x = s ^ w already formed, folding in the NEXT word:
+// returns F(x) ^ w_next, the next step's x, as two v_bitop3_b32 (xor3) --
+// instead of three v_xor for F and one for the next s ^ w.
+__device__ __forceinline__ uint32_t crc_step_x(const unsigned char* smem, uint32_t x, uint32_t w_next, uint32_t lo,
+                                               uint32_t hi) {
+  uint32_t a0 = __builtin_amdgcn_perm(x, hi, 0x0c020400u);  // byte0 -> T3
+  uint32_t a1 = __builtin_amdgcn_perm(x, hi, 0x0c020500u);  // byte1 -> T2
+  uint32_t a2 = __builtin_amdgcn_perm(x, lo, 0x0c0c0600u);  // byte2 -> T1
+  uint32_t a3 = __builtin_amdgcn_perm(x, lo, 0x0c0c0700u);  // byte3 -> T0
+  const uint32_t l2 = lds_ld(smem, a2 + 128u), l3 = lds_ld(smem, a3);
+  const uint32_t t = __builtin_amdgcn_bitop3_b32(l2, l3, w_next, 0x96);
+  return __builtin_amdgcn_bitop3_b32(lds_ld(smem, a0 + 128u), lds_ld(smem, a1), t, 0x96);
+}
+
 // ---------------------------------------------------------------------------
 // Segment loading.
 //
@@ -392,13 +406,15 @@ __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const 
     for (int j = 0; j < 32; ++j) w[j] = ABLATE == 10 ? d[j] : __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
   }
   constexpr int WPC = 32 / CHAINS;  // words per chain
+  // each chain carries x = state ^ (its next word); the state starts at 0, so
+  // the first x is the first word, and the last step folds in 0
   uint32_t c[CHAINS];
 #pragma unroll
-  for (int h = 0; h < CHAINS; ++h) c[h] = 0;
+  for (int h = 0; h < CHAINS; ++h) c[h] = w[h * WPC];
 #pragma unroll
   for (int j = 0; j < WPC; ++j) {
 #pragma unroll
-    for (int h = 0; h < CHAINS; ++h) c[h] = crc_word(smem, c[h], w[h * WPC + j], lo, hi);
+    for (int h = 0; h < CHAINS; ++h) c[h] = crc_step_x(smem, c[h], j + 1 < WPC ? w[h * WPC + j + 1] : 0u, lo, hi);
   }
   uint32_t s;
   if constexpr (CHAINS == 1) {
@@ -418,10 +434,11 @@ __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const 
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       u32x4 c = lds_ld128(LDS_COLS_OFF + g * 1024u + lane * 16u);
-      p ^= c.x & (uint32_t)((int32_t)(s << (4 * g + 0)) >> 31);
-      p ^= c.y & (uint32_t)((int32_t)(s << (4 * g + 1)) >> 31);
-      p ^= c.z & (uint32_t)((int32_t)(s << (4 * g + 2)) >> 31);
-      p ^= c.w & (uint32_t)((int32_t)(s << (4 * g + 3)) >> 31);
+      // p ^= col & mask as one v_bitop3_b32 (truth table 0x78: a ^ (b & c))
+      p = __builtin_amdgcn_bitop3_b32(p, c.x, (uint32_t)((int32_t)(s << (4 * g + 0)) >> 31), 0x78);
+      p = __builtin_amdgcn_bitop3_b32(p, c.y, (uint32_t)((int32_t)(s << (4 * g + 1)) >> 31), 0x78);
+      p = __builtin_amdgcn_bitop3_b32(p, c.z, (uint32_t)((int32_t)(s << (4 * g + 2)) >> 31), 0x78);
+      p = __builtin_amdgcn_bitop3_b32(p, c.w, (uint32_t)((int32_t)(s << (4 * g + 3)) >> 31), 0x78);
     }
     return p;
   }
