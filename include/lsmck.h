@@ -167,6 +167,8 @@ int lsmck_device_count(void);
  *                 files in flight (0 = 8192) and bytes of a file per round
  *                 (0 = 128 KiB; a multiple of 64).  Tests use small values.
  *   "tree_list_threads"  lsmck_tree_verify's metadata parsing threads (0 = 8).
+ *   "wal_prefetch"  bytes lsmck_wal_replay_verify's header walk prefetches
+ *                 ahead of its position (default 4096; 0 = off).  A/B switch.
  *   "tree_open_files"  files kept open from their first slice to their last
  *                 (-1 = default: as many as RLIMIT_NOFILE leaves after a
  *                 1024-descriptor reserve; the rest reopen per slice).

@@ -184,6 +184,7 @@ struct lsmck_ctx {
   int sha_bucket_shift = 2;  // SHA order key: 2^shift-block buckets for from..1023 blocks (0 = exact; A/B: DESIGN.md 3.2)
   int sha_bucket_from = 128;
   unsigned tree_list_threads = 0;  // lsmck_tree_verify: metadata parsing threads (0 = kListThreads)
+  size_t wal_prefetch = 4096;  // lsmck_wal_replay_verify: host walk's prefetch distance in bytes (0 = off)
   struct {
     uint32_t* state = nullptr;  // 8 u32 per active slot
     size_t cap_state = 0;
@@ -599,6 +600,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->tree_list_threads = (unsigned)value;
     return 0;
   }
+  if (!strcmp(key, "wal_prefetch")) {  // A/B: bytes the WAL header walk prefetches ahead (0 = off)
+    if (value < 0 || value > (1l << 24)) return lsmck_host::set_error(LSMCK_EINVAL, "wal_prefetch: 0..16 MiB");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_prefetch = (size_t)value;
+    return 0;
+  }
   if (!strcmp(key, "sha_bucket_from")) {  // A/B: first block count of the coarse SHA buckets
     if (value < 2 || value > 1024) return lsmck_host::set_error(LSMCK_EINVAL, "sha_bucket_from: 2..1024");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -780,8 +787,18 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
   int stop = 0;  // 0 clean, 3 bad type
   uint64_t stop_index = 0;
   uint32_t stop_type = 0;
+  // The walk is a dependent chain -- each header's address comes from the
+  // previous header's lengths -- so without help every header is one DRAM
+  // round trip (~140 ns, 500k records in 72 ms, 1.7 GiB/s).  Every line up to
+  // `dist` bytes ahead is prefetched, turning the chain into a stream.
+  const size_t dist = ctx->wal_prefetch;
+  size_t pf = 0;
   for (;;) {
     if (pos + 1 > n) break;
+    if (dist) {
+      const size_t lim = std::min(n, pos + dist);
+      for (; pf < lim; pf += 64) __builtin_prefetch(h + pf, 0, 0);
+    }
     uint8_t t = h[pos];
     if (t != 1 && t != 2) {
       stop = LSMCK_WAL_BAD_TYPE;

@@ -205,7 +205,9 @@ class Context:
     def wal_replay_verify(self, image, device_ptr=None):
         """Returns (records, status, (bad_index, bad_crc, bad_expected))."""
         if device_ptr is None:
-            img = np.frombuffer(bytes(image), dtype=np.uint8)
+            # any buffer (bytes, bytearray, memoryview, a read-only mmap of the
+            # log file) is read in place: no copy of the image
+            img = np.frombuffer(image, dtype=np.uint8) if len(image) else np.zeros(1, dtype=np.uint8)[:0]
             ptr, n, flags = img.ctypes.data, len(img), _lib.HOST
         else:
             ptr, n, flags = device_ptr, image, _lib.DEVICE

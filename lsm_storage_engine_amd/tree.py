@@ -23,6 +23,7 @@ import base64
 import concurrent.futures as cf
 import hashlib
 import json
+import mmap
 import os
 import struct
 import time
@@ -195,16 +196,24 @@ def load_verify(ctx, base):
     log = CommandLog.new(wal_path)
     try:
         t3 = time.perf_counter()
-        img = log.file.read()
+        # the log is mapped, not read(): read() into a fresh bytes object costs
+        # page faults plus a copy (0.15 s for 0.24 GB, more than the verify);
+        # the host walk and the staged upload read the mapping in place
+        n = os.fstat(log.file.fileno()).st_size
+        mm = mmap.mmap(log.file.fileno(), n, access=mmap.ACCESS_READ) if n else None
+        img = mm if mm is not None else b""
         records, wst, bad = ctx.wal_replay_verify(img)
         t4 = time.perf_counter()
+        wal_bytes = len(img)
+        if mm is not None:
+            mm.close()
         log.file.seek(0)
         mem = MemTable.from_log(log, ctx)  # raises the reference's WalError / panic for a bad log
         t5 = time.perf_counter()
     finally:
         log.file.close()
     list_s, tables_s = rep["list_seconds"], rep["verify_seconds"]
-    return mem, {"tables": rep["tables"], "table_bytes": nbytes, "wal_bytes": len(img), "wal_records": len(records),
+    return mem, {"tables": rep["tables"], "table_bytes": nbytes, "wal_bytes": wal_bytes, "wal_records": len(records),
                  "list_s": list_s, "tables_s": tables_s, "wal_s": t4 - t3, "memtable_build_s": t5 - t4,
                  "total_s": list_s + tables_s + (t4 - t3),
                  "tables_split": {k: rep[k] for k in ("stat_seconds", "read_seconds", "gpu_wait_seconds",

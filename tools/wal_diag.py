@@ -1,0 +1,87 @@
+"""Where the WAL replay verify's time goes (config 5's WAL leg).
+
+Builds a WAL image like tree.synthesize_tree's (500k records, keys 1-39 B,
+values 0-999 B, 10% removes), then times, best of 5 each:
+  replay    lsmck_wal_replay_verify (header walk + CRC batch), and again
+            per wal_prefetch distance (A/B of the walk's prefetch)
+  verify    lsmck_crc32_verify_batch on the same descriptors, pageable host image
+  pinned    the same from a pinned copy of the image
+  device    the same on a device-resident copy
+Prints one JSON line.
+"""
+import json
+import os
+import struct
+import sys
+import time
+import zlib
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from lsm_storage_engine_amd.device import Context  # noqa: E402
+
+
+def best(fn, reps=5):
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t)
+    return min(ts)
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 500_000
+    rng = np.random.default_rng(5)
+    pool = rng.bytes(1 << 20)
+    kl = rng.integers(1, 40, size=n)
+    vl = rng.integers(0, 1000, size=n)
+    rm = rng.random(n) < 0.1
+    wal = bytearray()
+    off, ln, exp = [], [], []
+    for i in range(n):
+        o = (i * 7919) % ((1 << 20) - 1100)
+        key = pool[o:o + int(kl[i])]
+        d = key if rm[i] else key + pool[o + 40:o + 40 + int(vl[i])]
+        hdr = struct.pack("<BII", 2, zlib.crc32(d), len(key)) if rm[i] else \
+            struct.pack("<BIII", 1, zlib.crc32(d), len(key), int(vl[i]))
+        wal += hdr
+        off.append(len(wal))
+        ln.append(len(d))
+        exp.append(zlib.crc32(d))
+        wal += d
+    img = np.frombuffer(bytes(wal), dtype=np.uint8)
+    off = np.array(off, dtype=np.uint64)
+    ln = np.array(ln, dtype=np.uint32)
+    exp = np.array(exp, dtype=np.uint32)
+    ctx = Context(0)
+    res = {"wal_bytes": len(img), "records": n}
+    recs, st, _ = ctx.wal_replay_verify(img)
+    assert st == 0 and len(recs) == n
+    res["replay_total_s"] = best(lambda: ctx.wal_replay_verify(img))
+    for pf in (0, 1024, 4096, 16384, 65536):
+        ctx.set_option("wal_prefetch", pf)
+        res[f"replay_prefetch_{pf}_s"] = best(lambda: ctx.wal_replay_verify(img))
+    ctx.set_option("wal_prefetch", 4096)
+    res["verify_pageable_s"] = best(lambda: ctx.crc32_verify(img, off, ln, exp))
+    pin = ctx.alloc_pinned(len(img))
+    pin.array[:] = img
+    res["replay_pinned_image_s"] = best(lambda: ctx.wal_replay_verify(pin.array))
+    d = ctx.alloc(len(img))
+    d.upload(img)
+    ctx.sync()
+    res["replay_device_image_s"] = best(lambda: ctx.wal_replay_verify(len(img), device_ptr=d.ptr))
+    for k in list(res):
+        if k.endswith("_s"):
+            res[k.replace("_s", "_GiBps")] = round(len(img) / 2**30 / res[k], 2)
+            res[k] = round(res[k], 4)
+    print(json.dumps(res))
+    d.free()
+    pin.free()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
