@@ -169,6 +169,9 @@ int lsmck_device_count(void);
  *   "tree_list_threads"  lsmck_tree_verify's metadata parsing threads (0 = 8).
  *   "wal_prefetch"  bytes lsmck_wal_replay_verify's header walk prefetches
  *                 ahead of its position (default 4096; 0 = off).  A/B switch.
+ *   "wal_chunk_bytes"  lsmck_wal_replay_verify of a host image: CRC batches
+ *                 of this many payload bytes run on a helper thread while the
+ *                 walk goes on (default 32 MiB; 0 = one batch after the walk).
  *   "tree_open_files"  files kept open from their first slice to their last
  *                 (-1 = default: as many as RLIMIT_NOFILE leaves after a
  *                 1024-descriptor reserve; the rest reopen per slice).

@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <future>
 #include <mutex>
 #include <numeric>
 #include <string>
@@ -185,6 +186,7 @@ struct lsmck_ctx {
   int sha_bucket_from = 128;
   unsigned tree_list_threads = 0;  // lsmck_tree_verify: metadata parsing threads (0 = kListThreads)
   size_t wal_prefetch = 4096;  // lsmck_wal_replay_verify: host walk's prefetch distance in bytes (0 = off)
+  size_t wal_chunk = 32u << 20;  // lsmck_wal_replay_verify, host image: payload bytes per overlapped CRC batch (0 = one batch)
   struct {
     uint32_t* state = nullptr;  // 8 u32 per active slot
     size_t cap_state = 0;
@@ -600,6 +602,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->tree_list_threads = (unsigned)value;
     return 0;
   }
+  if (!strcmp(key, "wal_chunk_bytes")) {  // A/B: WAL replay CRC batches overlapped with the walk (0 = one batch after it)
+    if (value < 0) return lsmck_host::set_error(LSMCK_EINVAL, "wal_chunk_bytes: >= 0");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_chunk = (size_t)value;
+    return 0;
+  }
   if (!strcmp(key, "wal_prefetch")) {  // A/B: bytes the WAL header walk prefetches ahead (0 = off)
     if (value < 0 || value > (1l << 24)) return lsmck_host::set_error(LSMCK_EINVAL, "wal_prefetch: 0..16 MiB");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -793,6 +801,30 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
   // `dist` bytes ahead is prefetched, turning the chain into a stream.
   const size_t dist = ctx->wal_prefetch;
   size_t pf = 0;
+  // Host image: the CRCs of the records walked so far run as a batch on a
+  // helper thread while the walk goes on.  Each batch takes its own copy of
+  // its descriptors (the vectors move as they grow), batches serialise on the
+  // context's lock, and every helper is joined before the function returns
+  // (a std::async future's destructor waits).
+  const bool overlap = !(flags & LSMCK_DEVICE) && ctx->wal_chunk;
+  struct Part {
+    size_t r0, r1;
+    std::future<std::pair<int, std::vector<uint32_t>>> f;
+  };
+  std::vector<Part> parts;
+  size_t chunk_r0 = 0;
+  uint64_t chunk_bytes = 0;
+  auto launch = [&](size_t r1) {
+    std::vector<uint64_t> o(poff.begin() + chunk_r0, poff.begin() + r1);
+    std::vector<uint32_t> l(plen.begin() + chunk_r0, plen.begin() + r1);
+    parts.push_back({chunk_r0, r1, std::async(std::launch::async, [ctx, h, flags, o = std::move(o), l = std::move(l)]() {
+                       std::vector<uint32_t> c(o.size());
+                       int r = lsmck_crc32_batch(ctx, h, o.data(), l.data(), o.size(), c.data(), flags, nullptr);
+                       return std::make_pair(r, std::move(c));
+                     })});
+    chunk_r0 = r1;
+    chunk_bytes = 0;
+  };
   for (;;) {
     if (pos + 1 > n) break;
     if (dist) {
@@ -822,8 +854,10 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
     rk.push_back(klen);
     rv.push_back(vlen);
     pos += hdr + got;
+    if (overlap && (chunk_bytes += got) >= ctx->wal_chunk) launch(poff.size());
   }
   size_t m = poff.size();
+  if (overlap && chunk_r0 < m) launch(m);
   // 2. every payload CRC in one GPU batch
   uint64_t nb = 0, first = m;
   if (m) {
@@ -854,6 +888,19 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
           if (!nb) first = i;
           ++nb;
         }
+    } else if (overlap) {
+      int prc = 0;
+      for (auto& P : parts) {
+        auto res = P.f.get();
+        if (res.first && !prc) prc = res.first;
+        if (prc) continue;
+        for (size_t i = P.r0; i < P.r1; ++i)
+          if (res.second[i - P.r0] != pcrc[i]) {
+            if (!nb) first = i;
+            ++nb;
+          }
+      }
+      if (prc) return prc;
     } else {
       rc = lsmck_crc32_verify_batch(ctx, h, poff.data(), plen.data(), pcrc.data(), m, flags, nullptr, &nb, &first);
       if (rc < 0) return rc;

@@ -84,3 +84,28 @@ def test_big_generated_log(ctx):
             parts.append(O.wal_insert(k, blob[(7 * i) % 900000:(7 * i) % 900000 + vl].tobytes()))
     img = b"".join(parts)
     assert same(ctx, img) == 0
+
+
+@pytest.mark.parametrize("chunk", [1, 4096, 65536, 0])
+def test_overlapped_chunks(ctx, golden, chunk):
+    """The host-image replay runs its CRC batches while the walk goes on
+    (``wal_chunk_bytes``): any chunking reports the same records and the
+    same first bad record in log order, also when later chunks hold more bad
+    records and when a chunk ends at the bad record."""
+    img = load_img()
+    recs = golden["wal_2000"]["records"]
+    ctx.set_option("wal_chunk_bytes", chunk)
+    try:
+        assert same(ctx, img) == 0
+        for picks in ([1500, 20], [999, 1000, 1999], [0], [1999]):
+            b = bytearray(img)
+            for i in picks:
+                r = recs[i]
+                if r["klen"] + r["vlen"]:
+                    b[r["off"] + (13 if r["type"] == 1 else 9)] ^= 0x40
+            same(ctx, bytes(b))
+        b = bytearray(img)
+        b[recs[1200]["off"]] = 7  # bad type after some chunks were launched
+        assert same(ctx, bytes(b)) == 3
+    finally:
+        ctx.set_option("wal_chunk_bytes", 32 << 20)

@@ -3,7 +3,9 @@
 Builds a WAL image like tree.synthesize_tree's (500k records, keys 1-39 B,
 values 0-999 B, 10% removes), then times, best of 5 each:
   replay    lsmck_wal_replay_verify (header walk + CRC batch), and again
-            per wal_prefetch distance (A/B of the walk's prefetch)
+            per wal_prefetch distance (A/B of the walk's prefetch) and per
+            wal_chunk_bytes (CRC batches overlapped with the walk; 0 = one
+            batch after it)
   verify    lsmck_crc32_verify_batch on the same descriptors, pageable host image
   pinned    the same from a pinned copy of the image
   device    the same on a device-resident copy
@@ -65,6 +67,10 @@ def main():
         ctx.set_option("wal_prefetch", pf)
         res[f"replay_prefetch_{pf}_s"] = best(lambda: ctx.wal_replay_verify(img))
     ctx.set_option("wal_prefetch", 4096)
+    for ch in (0, 8 << 20, 32 << 20, 64 << 20):
+        ctx.set_option("wal_chunk_bytes", ch)
+        res[f"replay_chunk_{ch >> 20}MiB_s"] = best(lambda: ctx.wal_replay_verify(img))
+    ctx.set_option("wal_chunk_bytes", 32 << 20)
     res["verify_pageable_s"] = best(lambda: ctx.crc32_verify(img, off, ln, exp))
     pin = ctx.alloc_pinned(len(img))
     pin.array[:] = img
