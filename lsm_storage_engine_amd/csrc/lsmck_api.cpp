@@ -809,7 +809,12 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
   const bool overlap = !(flags & LSMCK_DEVICE) && ctx->wal_chunk;
   struct Part {
     size_t r0, r1;
-    std::future<std::pair<int, std::vector<uint32_t>>> f;
+    struct Out {
+      int rc;
+      std::vector<uint32_t> crc;
+      std::string err;  // lsmck_last_error() is thread-local: the helper's message travels back
+    };
+    std::future<Out> f;
   };
   std::vector<Part> parts;
   size_t chunk_r0 = 0;
@@ -818,9 +823,10 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
     std::vector<uint64_t> o(poff.begin() + chunk_r0, poff.begin() + r1);
     std::vector<uint32_t> l(plen.begin() + chunk_r0, plen.begin() + r1);
     parts.push_back({chunk_r0, r1, std::async(std::launch::async, [ctx, h, flags, o = std::move(o), l = std::move(l)]() {
-                       std::vector<uint32_t> c(o.size());
-                       int r = lsmck_crc32_batch(ctx, h, o.data(), l.data(), o.size(), c.data(), flags, nullptr);
-                       return std::make_pair(r, std::move(c));
+                       Part::Out out{0, std::vector<uint32_t>(o.size()), {}};
+                       out.rc = lsmck_crc32_batch(ctx, h, o.data(), l.data(), o.size(), out.crc.data(), flags, nullptr);
+                       if (out.rc) out.err = lsmck_last_error();
+                       return out;
                      })});
     chunk_r0 = r1;
     chunk_bytes = 0;
@@ -890,17 +896,21 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
         }
     } else if (overlap) {
       int prc = 0;
+      std::string perr;
       for (auto& P : parts) {
         auto res = P.f.get();
-        if (res.first && !prc) prc = res.first;
+        if (res.rc && !prc) {
+          prc = res.rc;
+          perr = res.err;
+        }
         if (prc) continue;
         for (size_t i = P.r0; i < P.r1; ++i)
-          if (res.second[i - P.r0] != pcrc[i]) {
+          if (res.crc[i - P.r0] != pcrc[i]) {
             if (!nb) first = i;
             ++nb;
           }
       }
-      if (prc) return prc;
+      if (prc) return lsmck_host::set_error(prc, perr.c_str());
     } else {
       rc = lsmck_crc32_verify_batch(ctx, h, poff.data(), plen.data(), pcrc.data(), m, flags, nullptr, &nb, &first);
       if (rc < 0) return rc;
