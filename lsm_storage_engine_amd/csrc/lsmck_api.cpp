@@ -186,6 +186,9 @@ struct lsmck_ctx {
   int sha_bucket_from = 128;
   unsigned tree_list_threads = 0;  // lsmck_tree_verify: metadata parsing threads (0 = kListThreads)
   size_t wal_prefetch = 4096;  // lsmck_wal_replay_verify: host walk's prefetch distance in bytes (0 = off)
+  uint8_t* wal_host = nullptr;  // lsmck_wal_replay_verify of a device image: pinned host copy (grow-only)
+  size_t wal_host_cap = 0;
+  std::mutex wal_mu;  // guards wal_host for the duration of one device-image replay
   size_t wal_chunk = 32u << 20;  // lsmck_wal_replay_verify, host image: payload bytes per overlapped CRC batch (0 = one batch)
   struct {
     uint32_t* state = nullptr;  // 8 u32 per active slot
@@ -658,6 +661,7 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   if (ctx->d_verify) (void)hipFree(ctx->d_verify);
   if (ctx->h_total) (void)hipHostFree(ctx->h_total);
   if (ctx->h_verify) (void)hipHostFree(ctx->h_verify);
+  if (ctx->wal_host) (void)hipHostFree(ctx->wal_host);
   if (ctx->scratch_ev) (void)hipEventDestroy(ctx->scratch_ev);
   if (ctx->stream0) (void)hipStreamDestroy(ctx->stream0);
   delete ctx;
@@ -777,13 +781,18 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
                             size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
-  std::vector<uint8_t> host_copy;
   const uint8_t* h = wal;
+  // Device image: the walk reads a host copy, made by DMA into a pinned
+  // buffer the context keeps (grow-only).  Copying into fresh pageable memory
+  // instead ran at 2.8 GiB/s for 0.24 GB: page faults plus HIP's bounce copy.
+  std::unique_lock<std::mutex> wal_lk(ctx->wal_mu, std::defer_lock);
   if (flags & LSMCK_DEVICE) {
-    host_copy.resize(n);
+    wal_lk.lock();
     DevGuard g(ctx->dev);
-    HIPCHK(hipMemcpy(host_copy.data(), wal, n, hipMemcpyDeviceToHost));
-    h = host_copy.data();
+    rc = ensure_pinned(&ctx->wal_host, &ctx->wal_host_cap, n);
+    if (rc) return rc;
+    if (n) HIPCHK(hipMemcpy(ctx->wal_host, wal, n, hipMemcpyDeviceToHost));
+    h = ctx->wal_host;
   }
   // 1. header walk (serial: each record's length is in its own header)
   std::vector<uint64_t> poff;
