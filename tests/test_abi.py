@@ -52,6 +52,18 @@ def test_crc32_scalar_golden(golden, blob):
     assert _lib.load().lsmck_crc32_ieee(None, 0) == 0
 
 
+def test_crc32_scalar_length_alignment_sweep(blob):
+    """Every length 0..700 at several misalignments, and the sizes around the
+    PCLMULQDQ folding's 64-byte minimum and 16-byte multiples, against the
+    oracle's Sarwate restatement (= crc 1.x)."""
+    lens = list(range(0, 701)) + [1023, 1024, 1025, 4095, 4096, 4097, 65535, 65536, 65537]
+    for n in lens:
+        for s in (0, 1, 5, 8, 15):
+            piece = blob[s:s + n]
+            assert len(piece) == n
+            assert crc32.checksum_ieee(piece) == O.crc32(piece), (n, s)
+
+
 def test_crc32_update_combine(blob):
     rng = np.random.default_rng(1)
     for _ in range(200):
