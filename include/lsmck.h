@@ -169,6 +169,8 @@ int lsmck_device_count(void);
  *   "tree_list_threads"  lsmck_tree_verify's metadata parsing threads (0 = 8).
  *   "wal_prefetch"  bytes lsmck_wal_replay_verify's header walk prefetches
  *                 ahead of its position (default 4096; 0 = off).  A/B switch.
+ *   "stage_threads"  host-memory batches: threads that copy a pageable chunk
+ *                 into its pinned staging slot (default 8; 1 = one memcpy).
  *   "wal_chunk_bytes"  lsmck_wal_replay_verify of a host image: CRC batches
  *                 of this many payload bytes run on a helper thread while the
  *                 walk goes on (default 32 MiB; 0 = one batch after the walk).

@@ -189,7 +189,8 @@ struct lsmck_ctx {
   uint8_t* wal_host = nullptr;  // lsmck_wal_replay_verify of a device image: pinned host copy (grow-only)
   size_t wal_host_cap = 0;
   std::mutex wal_mu;  // guards wal_host for the duration of one device-image replay
-  size_t wal_chunk = 32u << 20;  // lsmck_wal_replay_verify, host image: payload bytes per overlapped CRC batch (0 = one batch)
+  size_t wal_chunk = 32u << 20;
+  unsigned stage_threads = 8;  // host batches: threads copying a pageable chunk into its pinned slot (1 = memcpy)  // lsmck_wal_replay_verify, host image: payload bytes per overlapped CRC batch (0 = one batch)
   struct {
     uint32_t* state = nullptr;  // 8 u32 per active slot
     size_t cap_state = 0;
@@ -355,6 +356,24 @@ int stage_init(Stage& S) {
   return 0;
 }
 
+// Pageable payload into a pinned slot.  One thread copies at ~20 GiB/s, below
+// the PCIe link the slot then feeds; large chunks are split over `threads`
+// (contiguous byte ranges, 4 KiB-aligned cuts).
+void stage_copy(uint8_t* dst, const uint8_t* src, size_t n, unsigned threads) {
+  if (threads <= 1 || n < (8u << 20)) {
+    memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  const size_t part = ((n / threads) + 4095) & ~(size_t)4095;
+  for (unsigned t = 1; t < threads; ++t) {
+    const size_t a = std::min(n, t * part), b = std::min(n, (t + 1) * part);
+    if (a < b) pool.emplace_back([=] { memcpy(dst + a, src + a, b - a); });
+  }
+  memcpy(dst, src, std::min(n, part));
+  for (auto& th : pool) th.join();
+}
+
 // Wait for a slot's previous chunk and hand its results to the caller.
 int stage_retire(Stage& S, const HostJob& J) {
   if (!S.busy) return 0;
@@ -420,7 +439,7 @@ int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
     } else {
       if ((rc = ensure_pinned(&S.h_pay, &S.cap_h_pay, pay_bytes + 16))) return rc;
       if (use_span) {
-        memcpy(S.h_pay, J.base + span_lo, pay_bytes);
+        stage_copy(S.h_pay, J.base + span_lo, pay_bytes, ctx->stage_threads);
       } else {
         uint64_t pos = 0;
         for (size_t i = 0; i < cnt; ++i) {
@@ -603,6 +622,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     if (value < 0 || value > 256) return lsmck_host::set_error(LSMCK_EINVAL, "tree_list_threads: 0..256");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->tree_list_threads = (unsigned)value;
+    return 0;
+  }
+  if (!strcmp(key, "stage_threads")) {  // A/B: threads of the pageable -> pinned staging copy (1 = one memcpy)
+    if (value < 1 || value > 64) return lsmck_host::set_error(LSMCK_EINVAL, "stage_threads: 1..64");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->stage_threads = (unsigned)value;
     return 0;
   }
   if (!strcmp(key, "wal_chunk_bytes")) {  // A/B: WAL replay CRC batches overlapped with the walk (0 = one batch after it)

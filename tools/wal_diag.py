@@ -71,6 +71,11 @@ def main():
         ctx.set_option("wal_chunk_bytes", ch)
         res[f"replay_chunk_{ch >> 20}MiB_s"] = best(lambda: ctx.wal_replay_verify(img))
     ctx.set_option("wal_chunk_bytes", 32 << 20)
+    for th in (1, 4, 8, 16):
+        ctx.set_option("stage_threads", th)
+        res[f"verify_pageable_stage{th}_s"] = best(lambda: ctx.crc32_verify(img, off, ln, exp))
+        res[f"replay_stage{th}_s"] = best(lambda: ctx.wal_replay_verify(img))
+    ctx.set_option("stage_threads", 8)
     res["verify_pageable_s"] = best(lambda: ctx.crc32_verify(img, off, ln, exp))
     pin = ctx.alloc_pinned(len(img))
     pin.array[:] = img
@@ -81,7 +86,7 @@ def main():
     res["replay_device_image_s"] = best(lambda: ctx.wal_replay_verify(len(img), device_ptr=d.ptr))
     for k in list(res):
         if k.endswith("_s"):
-            res[k.replace("_s", "_GiBps")] = round(len(img) / 2**30 / res[k], 2)
+            res[k[:-2] + "_GiBps"] = round(len(img) / 2**30 / res[k], 2)
             res[k] = round(res[k], 4)
     print(json.dumps(res))
     d.free()
