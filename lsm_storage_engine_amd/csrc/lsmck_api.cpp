@@ -441,11 +441,16 @@ int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
       if (use_span) {
         stage_copy(S.h_pay, J.base + span_lo, pay_bytes, ctx->stage_threads);
       } else {
-        uint64_t pos = 0;
-        for (size_t i = 0; i < cnt; ++i) {
-          memcpy(S.h_pay + pos, J.base + J.off[r + i], J.len[r + i]);
-          pos += J.len[r + i];
-        }
+        // gather: record i lands at its packed position S.h_off[i]; large
+        // chunks split the records over stage_threads threads
+        const unsigned T = pay_bytes >= (8u << 20) ? std::max(1u, ctx->stage_threads) : 1u;
+        auto gather = [&](size_t i0, size_t i1) {
+          for (size_t i = i0; i < i1; ++i) memcpy(S.h_pay + S.h_off[i], J.base + J.off[r + i], J.len[r + i]);
+        };
+        std::vector<std::thread> pool;
+        for (unsigned t = 1; t < T; ++t) pool.emplace_back(gather, cnt * t / T, cnt * (t + 1) / T);
+        gather(0, cnt / T);
+        for (auto& th : pool) th.join();
       }
       h_src = S.h_pay;
     }
