@@ -5,10 +5,16 @@
 One step = one pass of the hot path (lsmck_crc32_batch*) over one batch of
 synthetic records already resident in HBM.  Default workload (N = 1) is
 BASELINE config 2: 2^24 fixed 4 KiB SSTable blocks = 64 GiB per GPU.  With
---gpus N (one process per GPU, launched by torch.distributed.run) every rank
-checksums its own 2^24-block shard of the global block stream (weak scaling,
-record-sharded, no data-path collective); the control plane (barrier, max of
-per-rank times) goes over torch.distributed.
+--gpus N > 1 the workload is BASELINE config 4: one process per GPU, and rank
+r checksums shard r = blocks [r*2^26, (r+1)*2^26) of the same global block
+stream, 2^26 x 4 KiB = 256 GiB per GPU (weak scaling, record-sharded, no
+data-path collective); the control plane (barrier, max of per-rank times, the
+per-rank summary digests) goes over torch.distributed (gloo).
+
+`python bench.py --gpus N` outside torch.distributed.run starts
+`torch.distributed.run --nproc-per-node N` on itself as a child process
+(before anything touches the GPU) and exits with its status; under a launcher
+WORLD_SIZE must equal --gpus.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|1]
                   [--blocks-per-gpu B] [--no-cpu-baseline]
@@ -23,14 +29,11 @@ import sys
 import time
 
 import numpy as np
-import torch  # first: liblsmck must bind to the HIP runtime torch loaded (lsm_storage_engine_amd/_lib.py)
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-from lsm_storage_engine_amd import _lib  # noqa: E402
-from lsm_storage_engine_amd.device import Context, gen_zipf_lengths  # noqa: E402
+# torch and liblsmck are imported in main(), after relaunch(): nothing may
+# touch the GPU in a process that then starts the N-rank launcher
 
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, GB/s (MI355X_MICROARCH.md chip table)
@@ -89,8 +92,47 @@ def traffic_from_profiles(workload_key):
 CPU_ALL_CORES = int(os.environ.get("LSMCK_CPU_CORES", "16"))
 
 
+def relaunch(a):
+    """--gpus N outside a launcher: run N ranks under torch.distributed.run as a
+    child process (one process per GPU) and return its exit status; under a
+    launcher, WORLD_SIZE must match --gpus.  Returns None to run in-process."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != a.gpus and not (a.gpus == 1 and int(ws) > 1 and "--gpus" not in sys.argv):
+            print(f"bench.py: WORLD_SIZE={ws} but --gpus {a.gpus}", file=sys.stderr)
+            return 2
+        return None
+    if a.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+    with socket.socket() as so:  # a free rendezvous port on the loopback
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def golden_summaries():
+    p = os.path.join(ROOT, "tests", "golden", "summaries.json")
+    try:
+        with open(p) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
 def main():
     a = parse()
+    rc = relaunch(a)
+    if rc is not None:
+        sys.exit(rc)
+    global torch, dist, _lib, Context, gen_zipf_lengths
+    import torch  # first: liblsmck must bind to the HIP runtime torch loaded (lsm_storage_engine_amd/_lib.py)
+    import torch.distributed as dist
+    from lsm_storage_engine_amd import _lib
+    from lsm_storage_engine_amd.device import Context, gen_zipf_lengths
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -106,12 +148,20 @@ def main():
     cfg = a.config
     seed = SEED[cfg]
     if cfg == 2:
-        nrec = a.blocks_per_gpu or (1 << 24)
+        # N > 1: BASELINE config 4, 2^26 blocks per GPU (256 GiB; 2^26/N per rank
+        # when the ranks share one GPU in a rehearsal, LSMCK_BENCH_SHARE_GPU)
+        c4 = world > 1 or a.blocks_per_gpu == (1 << 26)
+        share = os.environ.get("LSMCK_BENCH_SHARE_GPU") and world > 1
+        nrec = a.blocks_per_gpu or (((1 << 26) // world if share else (1 << 26)) if world > 1 else (1 << 24))
         rec_len = 4096
         nbytes = nrec * rec_len
         byte_off = rank * nbytes  # this rank's shard of the global block stream
-        cname = "config4 per-GPU shard" if nrec == (1 << 26) else "config2"
-        workload = f"{cname}: {nrec} fixed 4 KiB SSTable blocks per GPU ({nbytes / GIB:.0f} GiB), device-resident"
+        if c4:
+            cname = "config4" if nrec == (1 << 26) else f"config4 (reduced shard: {nrec} blocks per rank)"
+            workload = (f"{cname}: {nrec} fixed 4 KiB SSTable blocks per GPU ({nbytes / GIB:.0f} GiB), "
+                        f"rank r = blocks [r*{nrec}, (r+1)*{nrec}) of config 2's stream, device-resident")
+        else:
+            workload = f"config2: {nrec} fixed 4 KiB SSTable blocks per GPU ({nbytes / GIB:.0f} GiB), device-resident"
     elif cfg == 1:
         nrec = a.blocks_per_gpu or (1 << 20)
         rec_len = 256
@@ -243,7 +293,7 @@ def main():
     achieved_gbs = algo_bytes / (ev_ms * 1e-3) / 1e9
     # diagnostics have no committed traffic
     # (the committed traffic is per launch of the default record count only)
-    wkey = None if (a.desc or a.pack_align > 1 or a.blocks_per_gpu) else f"{'sha256_' if sha else ''}config{cfg}"
+    wkey = None if (a.desc or a.pack_align > 1 or a.blocks_per_gpu or world > 1) else f"{'sha256_' if sha else ''}config{cfg}"
     traffic = traffic_from_profiles(wkey)
 
     res = {
@@ -346,17 +396,28 @@ def main():
         pb.free()
 
     # summary digest: CRC-32 of the little-endian output array
-    # (CRCs, or the 32-B digests), for cross-run comparison
+    # (CRCs, or the 32-B digests), for cross-run comparison; every rank's, for N > 1
+    import zlib
+    mine = "%08x" % zlib.crc32(out.download(np.uint8, count=(32 if sha else 4) * nrec).tobytes())
+    if world > 1:
+        allsum = [None] * world
+        dist.all_gather_object(allsum, mine)
+    else:
+        allsum = [mine]
     if rank == 0:
-        import zlib
-        res["summary_crc32"] = "%08x" % zlib.crc32(out.download(np.uint8, count=(32 if sha else 4) * nrec).tobytes())
-        # against the oracle's full-size value (tests/golden/make_summaries.py; default layouts only)
-        gpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "summaries.json")
-        if not a.blocks_per_gpu and a.pack_align <= 1 and os.path.exists(gpath):
-            with open(gpath) as f:
-                gold = json.load(f).get(f"config{cfg}", {}).get("summary_sha256" if sha else "summary_crc32")
-            if gold:
-                res["summary_matches_oracle"] = res["summary_crc32"] == gold
+        res["summary_crc32"] = allsum[0]
+        gold = golden_summaries()
+        if world > 1 or (cfg == 2 and nrec == (1 << 26)):
+            res["rank_summaries_crc32"] = allsum
+            # config 4 shards against the oracle's (tests/golden/make_summaries.py config4)
+            g4 = gold.get("config4", {}).get("shard_summary_crc32", [])
+            if cfg == 2 and not sha and nrec == (1 << 26) and world <= len(g4):
+                res["summary_matches_oracle"] = allsum == g4[:world]
+        elif not a.blocks_per_gpu and a.pack_align <= 1:
+            # against the oracle's full-size value (default layouts only)
+            g = gold.get(f"config{cfg}", {}).get("summary_sha256" if sha else "summary_crc32")
+            if g:
+                res["summary_matches_oracle"] = res["summary_crc32"] == g
 
     # CPU baseline + parity of the same sample (rank 0, N = 1 only)
     if rank == 0 and world == 1 and not a.no_cpu_baseline and sha:

@@ -84,23 +84,44 @@ void lsmck_sha256(const uint8_t* p, size_t n, uint8_t out[32]);
  * Writes 4*ceil(n/3) chars plus a NUL; returns the char count. */
 size_t lsmck_base64_encode(const uint8_t* p, size_t n, char* out);
 
+/* Positive status codes mark the places where the reference PANICS; negative
+ * ones (-errno, LSMCK_EJSON) the places where it returns Err(io::Error).
+ *   LSMCK_PANIC_OPEN_FILE      calculate_checksum's .expect("Can't open file to
+ *                              calculate checksum") (src/checksums.rs:22-25), on the
+ *                              file given (lsmck_checksum_file) or on the data file
+ *                              (verify / write_checksums: it is hashed first, :41, :65)
+ *   LSMCK_PANIC_OPEN_INDEX     the same panic on the index file (:42, :66)
+ *   LSMCK_PANIC_OPEN_CHECKSUM  verify's .expect("Can't open checksum file") (:43-46)
+ * A read error after a successful open is -errno (the `?` at :30). */
+#define LSMCK_PANIC_OPEN_FILE 4
+#define LSMCK_PANIC_OPEN_INDEX 5
+#define LSMCK_PANIC_OPEN_CHECKSUM 6
+
 /* Replaces Checksums::calculate_checksum(path) (src/checksums.rs:20-38):
- * SHA-256 of the whole file, base64 -> out (44 chars + NUL).
- * The reference panics when the file cannot be opened (:25); this returns
- * -errno and the Rust shim re-raises the panic. */
+ * SHA-256 of the whole file, base64 -> out (44 chars + NUL).  Returns 0,
+ * LSMCK_PANIC_OPEN_FILE when the file cannot be opened (the reference panics,
+ * :25), or -errno on a read error (Err, :30). */
 int lsmck_checksum_file(const char* path, char out[45]);
 
 /* Replaces Checksums::write_checksums(&SsTableMetadata) (src/checksums.rs:64-80):
  * hashes the data and index files and writes
  * {"index_checksum":"<b64>","data_checksum":"<b64>"} to checksum_path, opened
- * write+create WITHOUT truncate exactly as the reference opens it (:75-78). */
+ * write+create WITHOUT truncate exactly as the reference opens it (:75-78).
+ * Returns 0, LSMCK_PANIC_OPEN_FILE / LSMCK_PANIC_OPEN_INDEX (a data / index
+ * file cannot be opened: panic), or -errno (a read error, or the checksum
+ * file cannot be opened or written: Err, :78-79). */
 int lsmck_checksums_write(const char* data_path, const char* index_path, const char* checksum_path);
 
 /* Replaces Checksums::verify(&SsTableMetadata) (src/checksums.rs:40-62).
- * Returns 0 when both digests match, LSMCK_DATA_MISMATCH / LSMCK_INDEX_MISMATCH
- * where the reference panics (:49-60; data is checked first), -errno when a
- * file cannot be read, LSMCK_EJSON when the checksum file is not valid JSON of
- * the Checksums shape (the reference's serde_json error, :48). */
+ * Returns, in the reference's order of checks:
+ *   LSMCK_PANIC_OPEN_FILE / -errno      data file: cannot be opened (panic) / read error (Err)
+ *   LSMCK_PANIC_OPEN_INDEX / -errno     index file: the same
+ *   LSMCK_PANIC_OPEN_CHECKSUM           checksum file cannot be opened (panic, :46)
+ *   LSMCK_EJSON / -errno                checksum file is not JSON of the Checksums
+ *                                       shape, or cannot be read (Err, :48)
+ *   LSMCK_DATA_MISMATCH / LSMCK_INDEX_MISMATCH   digest mismatch (panic, :49-60;
+ *                                       data is checked first)
+ *   0                                   both digests match */
 #define LSMCK_DATA_MISMATCH 1
 #define LSMCK_INDEX_MISMATCH 2
 #define LSMCK_EJSON (-74)
@@ -244,10 +265,11 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
  * Streams every data/index file in slices: 8192 files in flight, 128 KiB of
  * each per round, 16 reader threads filling one pinned slot while the GPU
  * hashes the previous round (per-file SHA-256 state carried on the device),
- * then compares with each checksum file.  status[i] gets 0 /
- * LSMCK_DATA_MISMATCH / LSMCK_INDEX_MISMATCH / -errno / LSMCK_EJSON for table
- * i (-EAGAIN: a file shrank while it was read).  Returns the number of tables
- * whose status is not 0. */
+ * then compares with each checksum file.  status[i] gets table i's
+ * lsmck_checksums_verify status (0, the LSMCK_PANIC_OPEN_* codes,
+ * LSMCK_DATA_MISMATCH / LSMCK_INDEX_MISMATCH, -errno, LSMCK_EJSON; -EAGAIN: a
+ * file shrank while it was read).  Returns the number of tables whose status
+ * is not 0. */
 int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, const char* const* index_paths,
                                 const char* const* checksum_paths, size_t n, int* status);
 

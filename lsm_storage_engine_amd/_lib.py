@@ -29,6 +29,9 @@ WAL_CORRUPTED = 1
 WAL_REMOVE_PANIC = 2
 WAL_BAD_TYPE = 3
 META_PANIC = 3  # lsmck_tree_verify status: metadata file unreadable / not SsTableMetadata JSON
+PANIC_OPEN_FILE = 4      # checksums.rs:25 "Can't open file to calculate checksum" (the data file in verify/write)
+PANIC_OPEN_INDEX = 5     # the same panic on the index file
+PANIC_OPEN_CHECKSUM = 6  # checksums.rs:46 "Can't open checksum file"
 SSTABLE_MAX_LEVEL = 5
 
 DEVICE = 0x1

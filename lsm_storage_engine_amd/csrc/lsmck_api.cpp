@@ -1045,12 +1045,14 @@ struct SlotFds {
     if (fd[k] >= 0) close(fd[k]);
     fd[k] = -1;
   }
-  // read one slice of `path` for slot k; `last` closes the file after it
+  // read one slice of `path` for slot k; `last` closes the file after it.
+  // An open failure returns kOpenFailed (a panic site of the reference, not -errno)
+  static constexpr int kOpenFailed = 1;
   int read(uint32_t k, const char* path, uint8_t* dst, uint64_t off, uint64_t n, bool last) {
     int f = fd[k];
     if (f < 0) {
       f = open(path, O_RDONLY | O_CLOEXEC);
-      if (f < 0) return -errno;
+      if (f < 0) return kOpenFailed;
     }
     int rc = pread_fd(f, dst, off, n);
     if (last || rc || k >= cached) {
@@ -1120,9 +1122,12 @@ static int verify_tables(lsmck_ctx* ctx, const char* const* data_paths, const ch
     paths[2 * i] = data_paths[i];
     paths[2 * i + 1] = index_paths[i];
   }
+  // a file that cannot be opened is calculate_checksum's panic (checksums.rs:25):
+  // LSMCK_PANIC_OPEN_FILE for the data file, _INDEX for the index file
+  auto open_panic = [](size_t f) { return (f & 1) ? LSMCK_PANIC_OPEN_INDEX : LSMCK_PANIC_OPEN_FILE; };
   host_parallel(nf, [&](size_t f) {
     struct stat st;
-    if (stat(paths[f], &st) != 0) ferr[f] = -errno;
+    if (stat(paths[f], &st) != 0) ferr[f] = open_panic(f);
     else fsize[f] = (uint64_t)st.st_size;
   });
   tm->stat += clk.lap();
@@ -1230,7 +1235,7 @@ static int verify_tables(lsmck_ctx* ctx, const char* const* data_paths, const ch
             continue;
           }
           int e = fds.read(d.slot, paths[d.msg], S.h_pay + d.off, rd_off[j], d.len, d.flags & SHA_SLICE_LAST);
-          if (e) ferr[d.msg] = e;
+          if (e) ferr[d.msg] = e == SlotFds::kOpenFailed ? open_panic(d.msg) : e;
         }
       };
       const unsigned nt = (unsigned)std::min<size_t>(kTreeReaders, cnt);

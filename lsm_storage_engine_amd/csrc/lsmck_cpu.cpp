@@ -359,7 +359,11 @@ size_t lsmck_base64_encode(const uint8_t* p, size_t n, char* out) {
 int lsmck_checksum_file(const char* path, char out[45]) {
   if (!path || !out) return lsmck_host::set_error(LSMCK_EINVAL, "null argument");
   int fd = open(path, O_RDONLY | O_CLOEXEC);
-  if (fd < 0) return lsmck_host::set_errno_error(errno, "open", path);
+  if (fd < 0) {  // the reference panics here (checksums.rs:25)
+    int e = errno;
+    std::string m = std::string("Can't open file to calculate checksum ") + path + ": " + strerror(e);
+    return lsmck_host::set_error(LSMCK_PANIC_OPEN_FILE, m.c_str());
+  }
   lsmck_sha256_ctx c;
   lsmck_sha256_init(&c);
   uint8_t buf[1 << 16];
@@ -381,11 +385,21 @@ int lsmck_checksum_file(const char* path, char out[45]) {
   return 0;
 }
 
+// the index file is hashed second: its open panic is LSMCK_PANIC_OPEN_INDEX
+static int checksum_index_file(const char* index_path, char out[45]) {
+  int rc = lsmck_checksum_file(index_path, out);
+  if (rc == LSMCK_PANIC_OPEN_FILE) {
+    std::string m = lsmck_last_error();
+    return lsmck_host::set_error(LSMCK_PANIC_OPEN_INDEX, m.c_str());
+  }
+  return rc;
+}
+
 int lsmck_checksums_write(const char* data_path, const char* index_path, const char* checksum_path) {
   char db[45], ib[45];
   int rc = lsmck_checksum_file(data_path, db);
   if (rc) return rc;
-  rc = lsmck_checksum_file(index_path, ib);
+  rc = checksum_index_file(index_path, ib);
   if (rc) return rc;
   return lsmck_host::write_checksum_json(checksum_path, ib, db);
 }
@@ -394,7 +408,7 @@ int lsmck_checksums_verify(const char* data_path, const char* index_path, const 
   char db[45], ib[45];
   int rc = lsmck_checksum_file(data_path, db);
   if (rc) return rc;
-  rc = lsmck_checksum_file(index_path, ib);
+  rc = checksum_index_file(index_path, ib);
   if (rc) return rc;
   std::string want_index, want_data;
   rc = lsmck_host::read_checksum_json(checksum_path, &want_index, &want_data);

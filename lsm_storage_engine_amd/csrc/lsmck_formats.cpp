@@ -166,9 +166,18 @@ struct P {
 // file's read does -- which saves the extra read(2) that would return 0: a
 // whole-tree verify opens ~230k such files, and the system calls are its cost
 // (DESIGN.md 7a).
-static int read_file(const char* path, std::string* buf) {
+// open_code != 0: the status when the file cannot be opened (a panic site of
+// the reference) instead of -errno
+static int read_file(const char* path, std::string* buf, int open_code = 0) {
   int fd = open(path, O_RDONLY | O_CLOEXEC);
-  if (fd < 0) return set_errno_error(errno, "open", path);
+  if (fd < 0) {
+    if (open_code) {
+      int e = errno;
+      std::string m = std::string("Can't open checksum file ") + path + ": " + strerror(e);
+      return set_error(open_code, m.c_str());
+    }
+    return set_errno_error(errno, "open", path);
+  }
   buf->clear();
   char tmp[16384];
   for (;;) {
@@ -188,7 +197,7 @@ static int read_file(const char* path, std::string* buf) {
 
 int read_checksum_json(const char* path, std::string* index_b64, std::string* data_b64) {
   std::string buf;
-  if (int rc = read_file(path, &buf)) return rc;
+  if (int rc = read_file(path, &buf, LSMCK_PANIC_OPEN_CHECKSUM)) return rc;  // checksums.rs:43-46
   P p{buf.data(), buf.size(), 0};
   bool have_i = false, have_d = false;
   if (!p.lit('{')) return set_error(LSMCK_EJSON, "checksum file: expected '{'");

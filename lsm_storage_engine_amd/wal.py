@@ -173,14 +173,17 @@ class CommandLog:
         if status == _lib.WAL_BAD_TYPE:
             raise InvalidCommandType(bad[1])
         out = []
+        consumed = 0
         for k0, kl, vl, t in zip(records.payload_off.tolist(), records.klen.tolist(), records.vlen.tolist(),
                                  records.type.tolist()):
-            key = img[k0:k0 + kl]
+            # the payload actually read: u32 data_len (wal.rs:129), short at EOF
+            # (read_to_end on take(), :132) -- the same bytes the CRC covered
+            data = img[k0:k0 + ((kl + vl) & 0xFFFFFFFF)]
             if t == INSERT:
-                out.append(Insert(key, img[k0 + kl:k0 + kl + vl]))
+                out.append(Insert(data[:kl], data[kl:]))  # data.split_off(key_len), wal.rs:142
             else:
-                out.append(Remove(key))
-        consumed = int(records[-1].payload_off + records[-1].klen + records[-1].vlen) if len(records) else 0
+                out.append(Remove(data))
+            consumed = k0 + len(data)
         self.file.seek(pos + consumed)
         return out
 

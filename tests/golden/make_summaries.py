@@ -15,8 +15,11 @@ with these values; bench.py prints the GPU's as "summary_crc32".
   config 2: 2^24 x 4096 B, seed 0x5EED0002
   config 3: 2^26 Zipf(1.5) records of 64 B - 64 KiB packed back to back,
             lengths from the seed, bytes from the same seed
+  config 4: 8 per-GPU shards of 2^26 x 4096 B (256 GiB each) of config 2's
+            block stream (seed 0x5EED0002): shard r = blocks [r*2^26, (r+1)*2^26),
+            CRC-32 only (bench.py --gpus N: rank r checksums shard r)
 
-Run:  python3 tests/golden/make_summaries.py [crc|sha|all]   (updates summaries.json here)
+Run:  python3 tests/golden/make_summaries.py [crc|sha|all|config4]   (updates summaries.json here)
 """
 import concurrent.futures as cf
 import json
@@ -52,11 +55,11 @@ def _chunks(offs, lens):
         r0 = r1
 
 
-def summary(seed, offs, lens, sha):
+def summary(seed, offs, lens, sha, byte_off=0):
     def job(rng):
         r0, r1 = rng
         base = int(offs[r0])
-        data = O.gen_stream(seed, base, int(offs[r1 - 1]) + int(lens[r1 - 1]) - base)
+        data = O.gen_stream(seed, byte_off + base, int(offs[r1 - 1]) + int(lens[r1 - 1]) - base)
         return _digest(data, offs[r0:r1] - np.uint64(base), lens[r0:r1], sha)
     crc = 0
     with cf.ThreadPoolExecutor(THREADS) as ex:  # ctypes calls release the GIL
@@ -84,6 +87,20 @@ def main():
     res["method"] = ("oracle digest per record (1 GiB chunks), zlib.crc32 of the output array "
                      "(LE u32 CRCs / 32-B SHA-256 digests)")
     t0 = time.time()
+    if what == "config4":
+        n, L = 1 << 26, 4096
+        offs, lens = np.arange(n, dtype=np.uint64) * np.uint64(L), np.full(n, L, dtype=np.uint32)
+        e = res.setdefault("config4", {})
+        e.update({"records_per_shard": n, "record_bytes": L, "seed": hex(0x5EED0002),
+                  "shard_byte_offset": "rank * 2^38 (shard r = blocks [r*2^26, (r+1)*2^26) of config 2's stream)"})
+        shards = e.setdefault("shard_summary_crc32", [])
+        for r in range(len(shards), 8):
+            shards.append(summary(0x5EED0002, offs, lens, False, byte_off=r * n * L))
+            print("config4 shard", r, shards[-1], round(time.time() - t0, 1), flush=True)
+            with open(OUT, "w") as f:
+                json.dump(res, f, indent=1)
+                f.write("\n")
+        return
     for cfg in (1, 2, 3):
         seed = 0x5EED0000 + cfg
         offs, lens = layout(cfg)

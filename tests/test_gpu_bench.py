@@ -1,0 +1,83 @@
+"""bench.py's N-rank path and BASELINE config 4 on the GPU.
+
+* `python bench.py --gpus 2` (no launcher) must start two ranks itself
+  (torch.distributed.run as a child process), report n_gpus 2 and the config-4
+  workload, and every rank's shard must match the oracle.  The two ranks share
+  the box's one GPU (LSMCK_BENCH_SHARE_GPU=1) on a reduced shard.
+* Config 4's per-GPU shard at full size (2^26 x 4 KiB = 256 GiB, rank 0's
+  blocks [0, 2^26) of config 2's stream) through the C ABI, against the
+  oracle's summary digest (tests/golden/make_summaries.py config4).
+"""
+import json
+import os
+import subprocess
+import sys
+import zlib
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SEED2 = 0x5EED0002
+
+
+def _oracle_shard_summary(rank, nrec, threads=16):
+    data = O.gen_stream(SEED2, rank * nrec * 4096, nrec * 4096)
+    crc = O.crc32_fixed(data, 4096, 4096, nrec, threads=threads)
+    return "%08x" % zlib.crc32(crc.astype("<u4").tobytes())
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_launches_two_ranks():
+    nrec = 1 << 18  # 1 GiB per rank
+    env = dict(os.environ, LSMCK_BENCH_SHARE_GPU="1")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--blocks-per-gpu",
+                        str(nrec), "--steps", "3", "--warmup", "1"], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
+    r = json.loads(line)
+    assert r["n_gpus"] == 2
+    assert r["config"]["workload"].startswith("config4")
+    assert r["config"]["records_per_gpu"] == nrec
+    assert r["scaling"] == "weak"
+    want = [_oracle_shard_summary(k, nrec) for k in range(2)]
+    assert r["rank_summaries_crc32"] == want
+    # value = both ranks' payload over the slowest rank's time
+    assert abs(r["value"] - 2 * nrec * 4096 / 2**30 / (r["ms_per_step"] * 1e-3)) / r["value"] < 0.01
+
+
+def test_bench_world_size_mismatch_fails():
+    """Under a launcher, WORLD_SIZE must equal --gpus (checked before any GPU call)."""
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2
+    assert "WORLD_SIZE=2" in p.stderr
+
+
+@pytest.mark.gpu
+def test_config4_rank0_shard_full_size(ctx):
+    """2^26 x 4 KiB = 256 GiB on one GPU, every CRC checked through the summary digest."""
+    with open(os.path.join(ROOT, "tests", "golden", "summaries.json")) as f:
+        want = json.load(f)["config4"]["shard_summary_crc32"][0]
+    n = 1 << 26
+    d = ctx.alloc(n * 4096)
+    out = ctx.alloc(4 * n)
+    try:
+        ctx.gen_stream(d.ptr, SEED2, 0, n * 4096)
+        ctx.crc32_fixed_device(d.ptr, 4096, 4096, n, out.ptr)
+        ctx.sync()
+        crc = out.download(np.uint32)
+        assert "%08x" % zlib.crc32(crc.astype("<u4").tobytes()) == want
+        # and a spread sample against the oracle record by record
+        idx = np.linspace(0, n - 1, 512).astype(np.int64)
+        for i in idx[::64]:
+            blk = O.gen_stream(SEED2, int(i) * 4096, 4096)
+            assert crc[i] == O.crc32(blk)
+    finally:
+        d.free()
+        out.free()

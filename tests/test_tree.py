@@ -9,7 +9,7 @@ import struct
 
 import pytest
 
-from lsm_storage_engine_amd import tree
+from lsm_storage_engine_amd import _lib, tree
 from lsm_storage_engine_amd.checksums import ChecksumPanic
 from lsm_storage_engine_amd.sstable_metadata import SsTableMetadata
 from lsm_storage_engine_amd.wal import CorruptedData
@@ -170,4 +170,20 @@ def test_tree_verify_empty_and_missing_files(ctx, tmp_path):
     m = SsTableMetadata.new(base, 2, timestamp_ms=1_700_000_000_999)
     m.write_to_file()  # a table whose data/index/checksum files are missing
     r = ctx.tree_verify(base)
-    assert r["tables"] == 1 and r["first_status"] == -2  # ENOENT
+    # the data file cannot be opened: calculate_checksum's panic (checksums.rs:25)
+    assert r["tables"] == 1 and r["first_status"] == _lib.PANIC_OPEN_FILE
+    with pytest.raises(ChecksumPanic, match="Can't open file to calculate checksum"):
+        tree.load_verify(ctx, base)
+    # data file present, index missing: the same panic on the index file
+    open(m.data_path(), "wb").close()
+    r = ctx.tree_verify(base)
+    assert r["first_status"] == _lib.PANIC_OPEN_INDEX
+    # both present, checksum file missing: "Can't open checksum file" (:46)
+    open(m.index_path(), "wb").close()
+    r = ctx.tree_verify(base)
+    assert r["first_status"] == _lib.PANIC_OPEN_CHECKSUM
+    with pytest.raises(ChecksumPanic, match="Can't open checksum file"):
+        tree.load_verify(ctx, base)
+    st = ctx.checksums_verify_many([(m.data_path(), m.index_path(), m.checksum_path()),
+                                    (m.data_path() + "x", m.index_path(), m.checksum_path())])
+    assert st == [_lib.PANIC_OPEN_CHECKSUM, _lib.PANIC_OPEN_FILE]
