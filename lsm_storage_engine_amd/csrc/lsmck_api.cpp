@@ -177,6 +177,21 @@ struct lsmck_ctx {
   uint64_t* h_total = nullptr;   // pinned
   unsigned long long* d_verify = nullptr;  // [n_bad, first_bad]
   unsigned long long* h_verify = nullptr;  // pinned
+  // device verify / device WAL replay (grow-only; part of the scratch, ordered by scratch_ev)
+  uint32_t* d_vcrc = nullptr;  // computed CRCs
+  size_t cap_vcrc = 0;
+  uint64_t* d_woff = nullptr;  // WAL payload descriptors and stored CRCs
+  size_t cap_woff = 0;
+  uint32_t* d_wlen = nullptr;
+  size_t cap_wlen = 0;
+  uint32_t* d_wexp = nullptr;
+  size_t cap_wexp = 0;
+  uint64_t* h_woff = nullptr;  // pinned staging of the same
+  size_t cap_hwoff = 0;
+  uint32_t* h_wlen = nullptr;
+  size_t cap_hwlen = 0;
+  uint32_t* h_wexp = nullptr;
+  size_t cap_hwexp = 0;
   Stage stage[2];
   int variant = 0;  // kernel variant for A/B timing (LSMCK_CRC_CHAINS=1|2|4); 0 = default
   uint32_t tree_active = 0;  // whole-tree verify: files in flight (0 = kTreeActive)
@@ -215,6 +230,18 @@ struct DevGuard {
 };
 
 hipStream_t pick_stream(lsmck_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream0; }
+
+// Every use of the context's device scratch (ctx->scratch, d_vcrc, d_verify,
+// the WAL descriptor buffers) is ordered across streams by scratch_ev: the
+// stream waits for the previous user's work, and the event is re-recorded
+// after this call's work is enqueued (the host mutex only orders the enqueue).
+struct ScratchOrder {
+  lsmck_ctx* ctx;
+  hipStream_t st;
+  hipError_t e;
+  ScratchOrder(lsmck_ctx* c, hipStream_t s) : ctx(c), st(s), e(hipStreamWaitEvent(s, c->scratch_ev, 0)) {}
+  ~ScratchOrder() { (void)hipEventRecord(ctx->scratch_ev, st); }
+};
 
 int ensure_scratch(DescScratch& sc, size_t nblocks) {
   int rc;
@@ -384,11 +411,37 @@ int stage_retire(Stage& S, const HostJob& J) {
   return 0;
 }
 
+// On any early return of run_host_job: wait for both staging streams (no DMA
+// from the caller's memory may still run after the call returns) and drop the
+// slots' bookkeeping, so that the next call never retires a stale chunk into
+// its own output.
+struct StageGuard {
+  lsmck_ctx* ctx;
+  bool ok = false;
+  ~StageGuard() {
+    if (ok) return;
+    for (auto& S : ctx->stage) {
+      if (S.s) (void)hipStreamSynchronize(S.s);
+      S.busy = false;
+    }
+  }
+};
+
 int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
   size_t esz = J.kind == CRC ? 4 : 32;
   int rc;
-  for (auto& S : ctx->stage)
+  StageGuard guard{ctx};
+  for (auto& S : ctx->stage) {
     if ((rc = stage_init(S))) return rc;
+    if (S.busy) {  // left by a call that failed before its guard existed: never retire it here
+      HIPCHK(hipStreamSynchronize(S.s));
+      S.busy = false;
+    }
+  }
+  // Fixed records far apart (stride well above len) are gathered into a packed
+  // layout instead of shipping their whole span: a span of cnt*stride bytes
+  // would cost stride/len times the PCIe traffic (and the staging memory).
+  const bool sparse = !J.off && (uint64_t)J.stride * 4 > (uint64_t)J.flen * 5 + 256;
   size_t r = 0;
   int slot = 0;
   while (r < J.n) {
@@ -411,8 +464,8 @@ int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
     }
     size_t cnt = r1 - r;
     if (span_lo == UINT64_MAX) span_lo = span_hi = 0;
-    // fixed-stride records always ship as their span (the kernel indexes by stride)
-    bool use_span = !J.off || (mono && (span_hi - span_lo) <= bytes + bytes / 4 + 4096);
+    // dense fixed-stride records ship as their span (the kernel indexes by stride)
+    bool use_span = !J.off ? !sparse : (mono && (span_hi - span_lo) <= bytes + bytes / 4 + 4096);
     Stage& S = ctx->stage[slot];
     if ((rc = stage_retire(S, J))) return rc;
     // descriptors (rebased) and payload
@@ -440,6 +493,16 @@ int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
       if ((rc = ensure_pinned(&S.h_pay, &S.cap_h_pay, pay_bytes + 16))) return rc;
       if (use_span) {
         stage_copy(S.h_pay, J.base + span_lo, pay_bytes, ctx->stage_threads);
+      } else if (!J.off) {
+        // sparse fixed records: record r+i lands at i*flen
+        const unsigned T = pay_bytes >= (8u << 20) ? std::max(1u, ctx->stage_threads) : 1u;
+        auto gather = [&](size_t i0, size_t i1) {
+          for (size_t i = i0; i < i1; ++i) memcpy(S.h_pay + i * J.flen, J.base + (r + i) * J.stride, J.flen);
+        };
+        std::vector<std::thread> pool;
+        for (unsigned t = 1; t < T; ++t) pool.emplace_back(gather, cnt * t / T, cnt * (t + 1) / T);
+        gather(0, cnt / T);
+        for (auto& th : pool) th.join();
       } else {
         // gather: record i lands at its packed position S.h_off[i]; large
         // chunks split the records over stage_threads threads
@@ -465,14 +528,15 @@ int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
         for (size_t i = 0; i < cnt; ++i) total += S.h_len[i] ? (S.h_len[i] + 127u) / 128u : 1u;
         rc = crc_desc_device(ctx, S.scratch, S.d_pay, S.d_off, S.d_len, cnt, (uint32_t*)S.d_out, S.s, total, nullptr);
       } else {
-        // fixed records: the span starts at record r
-        rc = crc_fixed_device(ctx, S.d_pay, J.stride, J.flen, cnt, (uint32_t*)S.d_out, S.s);
+        // fixed records: the span starts at record r (gathered: packed at stride flen)
+        rc = crc_fixed_device(ctx, S.d_pay, use_span ? J.stride : J.flen, J.flen, cnt, (uint32_t*)S.d_out, S.s);
       }
     } else {
       if (J.off)
         rc = sha_device(ctx, S.scratch, S.d_pay, S.d_off, S.d_len, 0, 0, cnt, S.d_out, S.s);
       else
-        rc = sha_device(ctx, S.scratch, S.d_pay, nullptr, nullptr, J.stride, J.flen, cnt, S.d_out, S.s);
+        rc = sha_device(ctx, S.scratch, S.d_pay, nullptr, nullptr, use_span ? J.stride : J.flen, J.flen, cnt,
+                        S.d_out, S.s);
     }
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(S.h_out, S.d_out, cnt * esz, hipMemcpyDeviceToHost, S.s));
@@ -485,12 +549,33 @@ int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
   }
   for (auto& S : ctx->stage)
     if ((rc = stage_retire(S, J))) return rc;
+  guard.ok = true;
   return 0;
 }
 
 int check_ctx(lsmck_ctx* ctx) {
   if (!ctx) return lsmck_host::set_error(LSMCK_EINVAL, "null context");
   return 0;
+}
+
+// CRC batch + GPU compare with expected[] (all device pointers) on st, into the
+// context's pooled buffers; synchronous (the counts come back to the host).
+// Caller holds ctx->mu and orders st on the scratch.
+int device_verify(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len,
+                  const uint32_t* expected, size_t n, hipStream_t st, uint64_t* n_bad, uint64_t* first_bad) {
+  int rc = ensure_dev(&ctx->d_vcrc, &ctx->cap_vcrc, std::max<size_t>(n, 1));
+  if (rc) return rc;
+  rc = crc_desc_device(ctx, ctx->scratch, base, off, len, n, ctx->d_vcrc, st, -1, ctx->h_total);
+  if (rc) return rc;
+  HIPCHK(hipMemsetAsync(ctx->d_verify, 0, 8, st));         // n_bad
+  HIPCHK(hipMemsetAsync(ctx->d_verify + 1, 0xFF, 8, st));  // first_bad = ~0
+  rc = lsmk_launch_crc32_compare(ctx->d_vcrc, expected, n, ctx->d_verify, ctx->d_verify + 1, st);
+  if (rc) return launch_rc(rc, "compare kernel");
+  HIPCHK(hipMemcpyAsync(ctx->h_verify, ctx->d_verify, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (n_bad) *n_bad = ctx->h_verify[0];
+  if (first_bad) *first_bad = ctx->h_verify[0] ? ctx->h_verify[1] : n;
+  return ctx->h_verify[0] ? 1 : 0;
 }
 
 }  // namespace
@@ -689,6 +774,10 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   if (ctx->d_tinit) (void)hipFree(ctx->d_tinit);
   if (ctx->d_zero) (void)hipFree(ctx->d_zero);
   if (ctx->d_verify) (void)hipFree(ctx->d_verify);
+  for (void* p : {(void*)ctx->d_vcrc, (void*)ctx->d_woff, (void*)ctx->d_wlen, (void*)ctx->d_wexp})
+    if (p) (void)hipFree(p);
+  for (void* p : {(void*)ctx->h_woff, (void*)ctx->h_wlen, (void*)ctx->h_wexp})
+    if (p) (void)hipHostFree(p);
   if (ctx->h_total) (void)hipHostFree(ctx->h_total);
   if (ctx->h_verify) (void)hipHostFree(ctx->h_verify);
   if (ctx->wal_host) (void)hipHostFree(ctx->wal_host);
@@ -705,11 +794,9 @@ int lsmck_crc32_batch(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, 
   std::lock_guard<std::mutex> lk(ctx->mu);
   DevGuard g(ctx->dev);
   if (flags & LSMCK_DEVICE) {
-    hipStream_t st = pick_stream(ctx, stream);
-    HIPCHK(hipStreamWaitEvent(st, ctx->scratch_ev, 0));
-    rc = crc_desc_device(ctx, ctx->scratch, base, off, len, n, out, st, -1, ctx->h_total);
-    HIPCHK(hipEventRecord(ctx->scratch_ev, st));
-    return rc;
+    ScratchOrder so(ctx, pick_stream(ctx, stream));
+    if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
+    return crc_desc_device(ctx, ctx->scratch, base, off, len, n, out, so.st, -1, ctx->h_total);
   }
   HostJob J{CRC, base, off, len, 0, 0, n, (uint8_t*)out, (flags & LSMCK_HOST_PINNED) != 0};
   return run_host_job(ctx, J);
@@ -734,31 +821,12 @@ int lsmck_crc32_verify_batch(lsmck_ctx* ctx, const uint8_t* base, const uint64_t
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if (flags & LSMCK_DEVICE) {
-    uint32_t* d_crc = nullptr;
-    {
-      DevGuard g(ctx->dev);
-      HIPCHK(hipMalloc((void**)&d_crc, std::max<size_t>(n, 1) * 4));
-    }
-    rc = lsmck_crc32_batch(ctx, base, off, len, n, d_crc, flags, stream);
-    if (!rc) {
-      std::lock_guard<std::mutex> lk(ctx->mu);
-      DevGuard g(ctx->dev);
-      hipStream_t st = pick_stream(ctx, stream);
-      unsigned long long init[2] = {0ull, ~0ull};
-      hipError_t e = hipMemcpyAsync(ctx->d_verify, init, 16, hipMemcpyHostToDevice, st);
-      if (e == hipSuccess) rc = lsmk_launch_crc32_compare(d_crc, expected, n, ctx->d_verify, ctx->d_verify + 1, st);
-      if (e == hipSuccess && !rc) e = hipMemcpyAsync(ctx->h_verify, ctx->d_verify, 16, hipMemcpyDeviceToHost, st);
-      if (e == hipSuccess && !rc) e = hipStreamSynchronize(st);
-      if (e != hipSuccess) rc = hip_error(e, "verify");
-      else if (rc) rc = launch_rc(rc, "compare kernel");
-      if (!rc) {
-        if (n_bad) *n_bad = ctx->h_verify[0];
-        if (first_bad) *first_bad = ctx->h_verify[0] ? ctx->h_verify[1] : n;
-        rc = ctx->h_verify[0] ? 1 : 0;
-      }
-    }
+    if (n && (!off || !len || !expected)) return lsmck_host::set_error(LSMCK_EINVAL, "null descriptor or expected");
+    std::lock_guard<std::mutex> lk(ctx->mu);
     DevGuard g(ctx->dev);
-    (void)hipFree(d_crc);
+    ScratchOrder so(ctx, pick_stream(ctx, stream));
+    if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
+    rc = device_verify(ctx, base, off, len, expected, n, so.st, n_bad, first_bad);
     return rc;
   }
   std::vector<uint32_t> crc(n);
@@ -782,8 +850,11 @@ int lsmck_sha256_batch(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off,
   if (n && (!off || !len || !out32)) return lsmck_host::set_error(LSMCK_EINVAL, "null descriptor or output");
   std::lock_guard<std::mutex> lk(ctx->mu);
   DevGuard g(ctx->dev);
-  if (flags & LSMCK_DEVICE)
-    return sha_device(ctx, ctx->scratch, base, off, len, 0, 0, n, out32, pick_stream(ctx, stream));
+  if (flags & LSMCK_DEVICE) {
+    ScratchOrder so(ctx, pick_stream(ctx, stream));
+    if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
+    return sha_device(ctx, ctx->scratch, base, off, len, 0, 0, n, out32, so.st);
+  }
   HostJob J{SHA, base, off, len, 0, 0, n, out32, (flags & LSMCK_HOST_PINNED) != 0};
   return run_host_job(ctx, J);
 }
@@ -795,8 +866,11 @@ int lsmck_sha256_batch_fixed(lsmck_ctx* ctx, const uint8_t* base, size_t stride,
   if (n && !out32) return lsmck_host::set_error(LSMCK_EINVAL, "null output");
   std::lock_guard<std::mutex> lk(ctx->mu);
   DevGuard g(ctx->dev);
-  if (flags & LSMCK_DEVICE)
-    return sha_device(ctx, ctx->scratch, base, nullptr, nullptr, stride, len, n, out32, pick_stream(ctx, stream));
+  if (flags & LSMCK_DEVICE) {
+    ScratchOrder so(ctx, pick_stream(ctx, stream));
+    if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
+    return sha_device(ctx, ctx->scratch, base, nullptr, nullptr, stride, len, n, out32, so.st);
+  }
   HostJob J{SHA, base, nullptr, nullptr, stride, len, n, out32, (flags & LSMCK_HOST_PINNED) != 0};
   return run_host_job(ctx, J);
 }
@@ -907,32 +981,25 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
   uint64_t nb = 0, first = m;
   if (m) {
     if (flags & LSMCK_DEVICE) {
+      // descriptors + stored CRCs through pinned staging into pooled device
+      // buffers, one CRC batch over the device image, and the GPU compare:
+      // only the two counts come back
       std::lock_guard<std::mutex> lk(ctx->mu);
       DevGuard g(ctx->dev);
-      uint64_t* d_off = nullptr;
-      uint32_t *d_len = nullptr, *d_exp = nullptr, *d_crc = nullptr;
-      hipError_t e = hipMalloc((void**)&d_off, m * 8);
-      if (e == hipSuccess) e = hipMalloc((void**)&d_len, m * 4);
-      if (e == hipSuccess) e = hipMalloc((void**)&d_crc, m * 4);
-      if (e == hipSuccess) e = hipMemcpy(d_off, poff.data(), m * 8, hipMemcpyHostToDevice);
-      if (e == hipSuccess) e = hipMemcpy(d_len, plen.data(), m * 4, hipMemcpyHostToDevice);
-      std::vector<uint32_t> crc(m);
-      if (e == hipSuccess) {
-        rc = crc_desc_device(ctx, ctx->scratch, wal, d_off, d_len, m, d_crc, ctx->stream0, -1, ctx->h_total);
-        if (!rc) e = hipMemcpyAsync(crc.data(), d_crc, m * 4, hipMemcpyDeviceToHost, ctx->stream0);
-        if (!rc && e == hipSuccess) e = hipStreamSynchronize(ctx->stream0);
-      }
-      (void)d_exp;
-      if (d_off) (void)hipFree(d_off);
-      if (d_len) (void)hipFree(d_len);
-      if (d_crc) (void)hipFree(d_crc);
-      if (e != hipSuccess) return hip_error(e, "wal replay verify");
-      if (rc) return rc;
-      for (size_t i = 0; i < m; ++i)
-        if (crc[i] != pcrc[i]) {
-          if (!nb) first = i;
-          ++nb;
-        }
+      if ((rc = ensure_pinned(&ctx->h_woff, &ctx->cap_hwoff, m)) || (rc = ensure_pinned(&ctx->h_wlen, &ctx->cap_hwlen, m)) ||
+          (rc = ensure_pinned(&ctx->h_wexp, &ctx->cap_hwexp, m)) || (rc = ensure_dev(&ctx->d_woff, &ctx->cap_woff, m)) ||
+          (rc = ensure_dev(&ctx->d_wlen, &ctx->cap_wlen, m)) || (rc = ensure_dev(&ctx->d_wexp, &ctx->cap_wexp, m)))
+        return rc;
+      ScratchOrder so(ctx, ctx->stream0);
+      if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
+      memcpy(ctx->h_woff, poff.data(), m * 8);
+      memcpy(ctx->h_wlen, plen.data(), m * 4);
+      memcpy(ctx->h_wexp, pcrc.data(), m * 4);
+      HIPCHK(hipMemcpyAsync(ctx->d_woff, ctx->h_woff, m * 8, hipMemcpyHostToDevice, so.st));
+      HIPCHK(hipMemcpyAsync(ctx->d_wlen, ctx->h_wlen, m * 4, hipMemcpyHostToDevice, so.st));
+      HIPCHK(hipMemcpyAsync(ctx->d_wexp, ctx->h_wexp, m * 4, hipMemcpyHostToDevice, so.st));
+      rc = device_verify(ctx, wal, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, m, so.st, &nb, &first);
+      if (rc < 0) return rc;
     } else if (overlap) {
       int prc = 0;
       std::string perr;

@@ -1,0 +1,140 @@
+"""Streams, scratch and staging of the batch entry points (include/lsmck.h
+section 3): device-pointer calls on different streams share the context's
+scratch in order, host batches of sparse fixed records ship only their
+records, and every result still matches the oracle."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from lsm_storage_engine_amd import _lib
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+class Hip:
+    """hipStreamCreate / Query / Destroy from the HIP runtime liblsmck runs on."""
+
+    def __init__(self):
+        _lib.load()
+        self.rt = C.CDLL(_lib._foreign_hip_runtime_loaded())
+        self.rt.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
+        self.rt.hipStreamQuery.argtypes = [C.c_void_p]
+        self.rt.hipStreamDestroy.argtypes = [C.c_void_p]
+
+    def stream(self):
+        s = C.c_void_p()
+        assert self.rt.hipStreamCreate(C.byref(s)) == 0
+        return s.value
+
+    def query(self, s):
+        return self.rt.hipStreamQuery(s)  # 0 = idle, 600 = hipErrorNotReady
+
+    def destroy(self, s):
+        self.rt.hipStreamDestroy(s)
+
+
+def _records(rng, n, total, lmax):
+    ln = rng.integers(0, lmax, n).astype(np.uint32)
+    off = rng.integers(0, total - lmax, n).astype(np.uint64)
+    return off, ln
+
+
+def test_scratch_ordered_across_streams(ctx):
+    """An async descriptor CRC batch on one stream, then a length-ordered SHA
+    batch on a second and a device WAL replay on the context's stream: they
+    share the descriptor scratch (prefix sums, tile map, sort keys), so each
+    must wait for the previous user (scratch_ev).  All three match the oracle."""
+    hip = Hip()
+    s1, s2 = hip.stream(), hip.stream()
+    rng = np.random.default_rng(11)
+    total = 96 << 20
+    data = O.gen_stream(0x77, 0, total)
+    d = ctx.alloc(total)
+    d.upload(data)
+    n1 = 1 << 20
+    off1, ln1 = _records(rng, n1, total, 2000)
+    n2 = 1 << 14
+    off2, ln2 = _records(rng, n2, total, 6000)
+    bufs = [ctx.alloc(x.nbytes) for x in (off1, ln1, off2, ln2)]
+    for b, x in zip(bufs, (off1, ln1, off2, ln2)):
+        b.upload(x)
+    o1, o2 = ctx.alloc(4 * n1), ctx.alloc(32 * n2)
+    # a WAL image in device memory
+    parts = [O.wal_insert(data[i:i + 7].tobytes(), data[i + 7:i + 7 + (i % 3000)].tobytes()) for i in range(0, 40000, 7)]
+    img = b"".join(parts)
+    dw = ctx.alloc(len(img))
+    dw.upload(np.frombuffer(img, np.uint8))
+    try:
+        for _ in range(3):
+            ctx.memset(o1.ptr, 0xAB, 4 * n1, s1)
+            ctx.crc32_device(d.ptr, bufs[0].ptr, bufs[1].ptr, n1, o1.ptr, s1)
+            ctx.sha256_device(d.ptr, bufs[2].ptr, bufs[3].ptr, n2, o2.ptr, s2)
+            recs, st, _ = ctx.wal_replay_verify(len(img), device_ptr=dw.ptr)
+            ctx.sync(s1)
+            ctx.sync(s2)
+            assert st == 0 and len(recs) == len(parts)
+            assert np.array_equal(o1.download(np.uint32), O.crc32_batch(data, off1, ln1, threads=8))
+            assert np.array_equal(o2.download(np.uint8).reshape(n2, 32),
+                                  np.asarray(O.sha256_batch(data, off2, ln2, threads=8)).reshape(n2, 32))
+    finally:
+        for b in bufs + [d, o1, o2, dw]:
+            b.free()
+        hip.destroy(s1)
+        hip.destroy(s2)
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_sparse_fixed_host_batches(ctx, pinned):
+    """Fixed records far apart (1 MiB stride, 16-200 B records): the host
+    path gathers the records instead of shipping a span of n*stride bytes."""
+    stride, n = 1 << 20, 300
+    src = O.gen_stream(0x99, 0, stride * n)
+    if pinned:
+        pb = ctx.alloc_pinned(src.nbytes)
+        pb.array[:] = src
+        buf = pb.array
+    else:
+        buf = src
+    try:
+        for length in (16, 200, 1000):
+            got = ctx.crc32_fixed(buf, stride, length, n, pinned=pinned)
+            assert np.array_equal(got, O.crc32_fixed(src, stride, length, n))
+        sh = ctx.sha256_fixed(src, stride, 100, n)
+        want = np.asarray(O.sha256_batch(src, np.arange(n, dtype=np.uint64) * np.uint64(stride),
+                                         np.full(n, 100, np.uint32))).reshape(n, 32)
+        assert np.array_equal(sh, want)
+    finally:
+        if pinned:
+            pb.free()
+
+
+def test_verify_batch_device_pooled(ctx):
+    """Device verify runs the CRC batch and the GPU compare in the context's
+    pooled buffers (no per-call allocation): repeated calls of growing and
+    shrinking sizes report the same first bad record as the oracle."""
+    rng = np.random.default_rng(5)
+    total = 8 << 20
+    data = O.gen_stream(0x55, 0, total)
+    d = ctx.alloc(total)
+    d.upload(data)
+    try:
+        for n in (1000, 100000, 10, 50000):
+            off, ln = _records(rng, n, total, 1500)
+            want = O.crc32_batch(data, off, ln, threads=8)
+            exp = want.copy()
+            bad = sorted(rng.choice(n, size=min(3, n), replace=False).tolist())
+            exp[bad] ^= 1
+            bo, bl, be = ctx.alloc(8 * n), ctx.alloc(4 * n), ctx.alloc(4 * n)
+            bo.upload(off)
+            bl.upload(ln)
+            be.upload(exp)
+            rc, nb, fb = ctx.crc32_verify_device(d.ptr, bo.ptr, bl.ptr, be.ptr, n)
+            assert (rc, nb, fb) == (1, len(bad), bad[0])
+            be.upload(want)
+            assert ctx.crc32_verify_device(d.ptr, bo.ptr, bl.ptr, be.ptr, n) == (0, 0, n)
+            for b in (bo, bl, be):
+                b.free()
+    finally:
+        d.free()

@@ -109,3 +109,24 @@ def test_overlapped_chunks(ctx, golden, chunk):
         assert same(ctx, bytes(b)) == 3
     finally:
         ctx.set_option("wal_chunk_bytes", 32 << 20)
+
+
+def test_truncated_payload_with_matching_crc(ctx):
+    """A last record whose payload is cut off at EOF but whose stored CRC
+    matches the bytes that are there: read_to_end on take() returns the short
+    payload (wal.rs:130-133) and the record is accepted.  The batch replay
+    yields the same records as the iterator and leaves the log at its end."""
+    good = O.wal_insert(b"alpha", b"one") + O.wal_remove(b"beta")
+    short = b"kkkkkvvvvv"  # klen 5 + vlen 95 announced, 10 bytes present
+    tail = bytes([1]) + O.crc32(short).to_bytes(4, "little") + (5).to_bytes(4, "little") + \
+        (95).to_bytes(4, "little") + short
+    img = good + tail
+    same(ctx, img)
+    cpu_log = wal.CommandLog.new_in_memory(img)
+    cpu = list(cpu_log)
+    gpu_log = wal.CommandLog.new_in_memory(img)
+    gpu = gpu_log.replay_verify(ctx)
+    assert [(type(r), r.key, getattr(r, "val", None)) for r in gpu] == \
+        [(type(r), r.key, getattr(r, "val", None)) for r in cpu]
+    assert gpu[-1].key == b"kkkkk" and gpu[-1].val == b"vvvvv"
+    assert gpu_log.file.tell() == len(img)
