@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--digest", default="crc32", choices=["crc32", "sha256"],
                     help="crc32 = the WAL record checksum (headline); sha256 = the SSTable digest "
                          "(checksums.rs) over the same records, reported against its int32 VALU roof")
+    ap.add_argument("--walk", type=int, default=1, choices=[0, 1],
+                    help="descriptor batches: 1 = walking kernel (default), 0 = r01 tile-map kernel (A/B)")
     ap.add_argument("--pack-align", type=int, default=1,
                     help="diagnostic: config 3 record offsets rounded up to this many bytes")
     return ap.parse_args()
@@ -144,6 +146,8 @@ def main():
     stream = torch.cuda.Stream(device=local)  # a real stream: the null stream's handle (0) means
     sptr = stream.cuda_stream                 # "the context's own stream" to liblsmck
     ctx = Context(local)
+    if a.walk != 1:
+        ctx.set_option("crc_walk", a.walk)
 
     cfg = a.config
     seed = SEED[cfg]
@@ -326,7 +330,8 @@ def main():
             "traffic": traffic,
             # fixed records whose segment count divides 64 (configs 1, 2) run the
             # whole-tile ring kernel by default (lsmck_crc32.hip, LSMCK_DEFAULT_RING)
-            "kernel": "crc32_desc_kernel" if (cfg == 3 or a.desc) else "crc32_wring_kernel",
+            "kernel": (("crc32_walk_kernel" if a.walk else "crc32_desc_kernel") if (cfg == 3 or a.desc)
+                       else "crc32_wring_kernel"),
             "algorithmic_bytes_per_launch": algo_bytes,
             "launch_ms_hip_events": round(ev_ms, 4),
         },

@@ -37,6 +37,7 @@ using lsmck::ShaParams;
 namespace {
 
 constexpr uint64_t kMaxSegsPerLaunch = (1ull << 32) - 64;  // 32-bit segment indices in the kernels
+constexpr int kVariantTileMap = 0x100000;  // descriptor batches: the r01 tile-map kernel instead of the walking one
 constexpr size_t kChunkBytes = 64ull << 20;                // host staging chunk (payload)
 constexpr size_t kChunkRecs = 1u << 20;                    // host staging chunk (records)
 
@@ -293,6 +294,22 @@ int crc_desc_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const 
                     size_t n, uint32_t* out, hipStream_t st, int64_t known_total, uint64_t* h_total) {
   if (n == 0) return 0;
   if (n >= (1ull << 32)) return lsmck_host::set_error(LSMCK_EINVAL, "more than 2^32-1 records in one batch");
+  if (!(ctx->variant & kVariantTileMap)) {
+    // walking kernel (default): scratch sized by the record count, nothing
+    // read back, every CRC stored once -- asynchronous on st
+    int rc = ensure_scratch(sc, (size_t)lsmk_walk_sb_count(n));
+    if (rc) return rc;
+    CrcParams P{};
+    P.base = base;
+    P.off = off;
+    P.len = len;
+    P.nrec = n;
+    P.total_segs = sc.total;
+    P.out = out;
+    fill_tables(ctx, &P);
+    rc = lsmk_launch_crc32_walk(&P, sc.block_sum, ctx->ncu, ctx->variant, st);
+    return rc ? launch_rc(rc, "crc32_walk kernel") : 0;
+  }
   size_t nb = (size_t)lsmk_scan_block_count(n);
   int rc = ensure_scratch(sc, nb);
   if (rc) return rc;
@@ -748,6 +765,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "sha_order must be 0 or 1");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->variant = (ctx->variant & ~0x10000) | (value ? 0 : 0x10000);
+    return 0;
+  }
+  if (!strcmp(key, "crc_walk")) {  // A/B: descriptor batches, 1 = walking kernel (default), 0 = r01 tile-map kernel
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_walk must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (ctx->variant & ~kVariantTileMap) | (value ? 0 : kVariantTileMap);
     return 0;
   }
   if (!strcmp(key, "crc_loads")) {  // A/B: payload load instruction, 0 default, 1 global, 2 raw buffer

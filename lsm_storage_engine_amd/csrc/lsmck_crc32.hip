@@ -357,7 +357,7 @@ __device__ __forceinline__ void seg_issue_pk(const CrcParams& P, const SegInfo& 
 // CHAINS independent register chains per lane (the segment's 128 bytes cut in
 // CHAINS pieces) hide the LDS lookup latency; they are recombined with the
 // shift-by-32m-bytes tables: raw(A||B) = shift_|B|(raw(A)) ^ raw(B).
-template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false>
+template <bool FAST, int CHAINS, int ABLATE = 0, bool PERCOL = false, bool RAW = false>
 __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const CrcParams& P, const SegLoad& L,
                                                uint32_t lo, uint32_t hi) {
   if (ABLATE == 1 || (ABLATE >= 3 && ABLATE <= 7) || ABLATE == 12 || ABLATE == 13) {  // diagnostic: loads only (results invalid)
@@ -427,6 +427,7 @@ __device__ __forceinline__ uint32_t seg_finish(const unsigned char* smem, const 
   // init term of a record's first segment: 0xFFFFFFFF (x) x^(8*len0), len0 = 128 - lead
   const uint32_t lead0 = FL_BST(L.fl) - FL_SH(L.fl);
   s ^= (L.fl & FL_FIRST) ? lds_ld(smem, LDS_TINIT_OFF + ((128u - lead0) << 2)) : 0u;
+  if constexpr (RAW) return s;  // walking kernel: shifted by the caller (Horner within the tile)
   if constexpr (PERCOL) {
     // s (x) K with the lane's 32 precomputed columns K*x^i: p ^= col_i if bit 31-i of s
     const uint32_t lane = threadIdx.x & 63u;
@@ -1063,6 +1064,272 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_phase3(const uint32_t* __rest
   }
 }
 
+
+// ===========================================================================
+// Walking descriptor kernel (the default for descriptor batches).
+//
+// Every wave owns ONE contiguous run of records -- whole superblocks of
+// WALK_SB records, cut so that every wave gets about the same number of
+// 128-byte segments (walk_phase1 + scan_phase2 give the segment prefix per
+// superblock; a wave binary-searches its cut points) -- and walks the run's
+// segments in order, 64 per tile.  So:
+//  * no record is split between waves: every CRC is stored once, with a plain
+//    store (no zeroing of `out`, no atomics);
+//  * a record spanning tiles carries its partial value to the next tile in a
+//    wave-uniform register (Horner: carry (x) x^(8*128*m) ^ the next tile's
+//    part), so a lane only shifts its segment to the record's last lane IN THE
+//    TILE, d < 64 segments: 32 precomputed LDS columns per d (8 ds_read_b128 +
+//    32 v_bitop3) instead of the 32-step generic GF(2) multiply;
+//  * the segment -> record map comes from windows of 64 records (one per lane:
+//    off, len, prefix of segment counts) held in registers, three windows deep
+//    (current, next, prefetched): no per-tile map in HBM.  The only scratch is
+//    one u64 per superblock, sized by the record count, so the host never has
+//    to read a device total back to size anything: the batch is asynchronous
+//    on its stream;
+//  * contiguous per-wave runs stream as fast as the strided tile order of the
+//    fixed kernels (tools/microbench_walk.hip: 6.56 against 6.42 TB/s over
+//    96 GiB, profiles/r02/mb/mb_walk96.log).
+#define WALK_SB 256u
+#define LDS_WCOLS_OFF LDS_COLS_OFF  // [8 groups][65 d][4 u32] columns of x^(8*128*d), d = 0..64 (8320 B)
+
+__global__ __launch_bounds__(1024) void walk_phase1(const uint32_t* __restrict__ len, uint64_t n,
+                                                     uint64_t* __restrict__ sb_sum) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t sb = (uint64_t)blockIdx.x * 16u + (threadIdx.x >> 6);
+  if (sb * WALK_SB >= n) return;  // wave-uniform
+  const uint64_t r0 = sb * WALK_SB + lane * 4u;
+  uint32_t l[4];
+  load_len4(len, n, r0, l);
+  uint64_t x = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) x += (r0 + j < n) ? rec_nseg(l[j]) : 0u;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  if (lane == 0) sb_sum[sb] = x;
+}
+
+// columns K*x^i (i = 0..31) of K = x^(8*128*d), d = 0..64, for the Horner shifts
+__device__ __forceinline__ void build_walk_cols(const CrcParams& P) {
+  if (threadIdx.x > 64) return;
+  const uint32_t d = threadIdx.x;
+  uint32_t b = P.kseg[d];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    *(__attribute__((address_space(3))) uint32_t*)(size_t)(LDS_WCOLS_OFF + ((i >> 2) * 65u + d) * 16u + (i & 3) * 4u) = b;
+    b = (b >> 1) ^ (0xEDB88320u & (0u - (b & 1u)));
+  }
+}
+
+// v (x) x^(8*128*d), d = 0..64, from the LDS columns
+__device__ __forceinline__ uint32_t walk_mulcol(uint32_t v, uint32_t d) {
+  uint32_t p = 0;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    const u32x4 c = lds_ld128(LDS_WCOLS_OFF + (g * 65u + d) * 16u);
+    p = __builtin_amdgcn_bitop3_b32(p, c.x, (uint32_t)((int32_t)(v << (4 * g + 0)) >> 31), 0x78);
+    p = __builtin_amdgcn_bitop3_b32(p, c.y, (uint32_t)((int32_t)(v << (4 * g + 1)) >> 31), 0x78);
+    p = __builtin_amdgcn_bitop3_b32(p, c.z, (uint32_t)((int32_t)(v << (4 * g + 2)) >> 31), 0x78);
+    p = __builtin_amdgcn_bitop3_b32(p, c.w, (uint32_t)((int32_t)(v << (4 * g + 3)) >> 31), 0x78);
+  }
+  return p;
+}
+
+// the same for a wave-uniform v and d = 1..64, spread over the lanes: lane i
+// < 32 contributes column i if bit 31-i of v is set; XOR over lanes 0..31
+__device__ __forceinline__ uint32_t walk_mulcol_uniform(uint32_t v, uint32_t d, uint32_t lane) {
+  const uint32_t i = lane & 31u;
+  const uint32_t col = lds_ld(nullptr, LDS_WCOLS_OFF + ((i >> 2) * 65u + d) * 16u + (i & 3u) * 4u);
+  const uint32_t t = (lane < 32u && ((v >> (31u - i)) & 1u)) ? col : 0u;
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_prefix_xor(t), 31);
+}
+
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t x) {  // OR over the wave (uniform)
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// a window: records w0 + lane of the run (lane-held), absent past the run's end
+struct WalkWin {
+  uint64_t off;
+  uint32_t len;
+  uint32_t p;    // exclusive prefix of the segment counts inside the window
+  uint32_t ok;   // the record exists (in the run)
+};
+__device__ __forceinline__ void walk_win_issue(const CrcParams& P, uint64_t w0, uint64_t r1, uint32_t lane, WalkWin& W) {
+  const uint64_t r = w0 + lane;
+  W.ok = r < r1;
+  const uint64_t rr = W.ok ? r : (r1 - 1u);  // r1 > 0 whenever a window is loaded
+  W.off = P.off[rr];
+  W.len = P.len[rr];
+}
+// segment prefix of a landed window; returns the window's segment total (uniform)
+__device__ __forceinline__ uint32_t walk_win_scan(WalkWin& W) {
+  const uint32_t ns = W.ok ? rec_nseg(W.len) : 0u;
+  const uint32_t inc = wave_prefix_add(ns);
+  W.p = inc - ns;
+  return (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+}
+__device__ __forceinline__ uint64_t start_bit(const WalkWin& W, int64_t rel) {
+  // rel = position of the window's first segment relative to the tile start
+  const int64_t s = rel + (int64_t)W.p;
+  return (W.ok && s >= 1 && s <= 63) ? (1ull << s) : 0ull;
+}
+
+template <int CHAINS, int ABLATE = 0>
+__global__ __launch_bounds__(1024) void crc32_walk_kernel(CrcParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  build_lds_tables(smem, P);
+  __syncthreads();  // the column table reuses the khi/klo area the table build fills
+  build_walk_cols(P);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lo = (lane & 31u) * 4u, hi = lo | 0x10000u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+  const uint64_t n = P.nrec;
+  const uint64_t nsb = (n + WALK_SB - 1u) / WALK_SB;
+  const uint64_t S = *P.total_segs;
+  // this wave's superblocks [b0, b1): the first superblock whose segment
+  // prefix reaches S*w/nw (lower bound), for w and w+1
+  auto cut = [&](uint32_t w) -> uint64_t {
+    if (w >= nw) return nsb;
+    const uint64_t target = (S / nw) * w + (S % nw) * w / nw;  // floor(S*w/nw) without overflow
+    uint64_t a = 0, b = nsb;
+    while (a < b) {
+      const uint64_t m = (a + b) >> 1;
+      if (P.sb_prefix[m] < target) a = m + 1; else b = m;
+    }
+    return a;
+  };
+  const uint64_t b0 = cut(wave), b1 = cut(wave + 1);
+  if (b0 >= b1) return;
+  const uint64_t r0 = b0 * WALK_SB, r1 = min(n, b1 * WALK_SB);
+  const uint64_t segs = (b1 < nsb ? P.sb_prefix[b1] : S) - P.sb_prefix[b0];
+  const uint64_t ntile = (segs + 63u) >> 6;
+  // windows: records [r0 + 64*wc, +64) (cur), the next (nxt), the one after (pre, in flight)
+  WalkWin cur, nxt, pre;
+  walk_win_issue(P, r0, r1, lane, cur);
+  walk_win_issue(P, r0 + 64u, r1, lane, nxt);
+  walk_win_issue(P, r0 + 128u, r1, lane, pre);
+  uint64_t wc0 = r0;                      // first record of cur
+  uint64_t Bc = 0;                         // run segment of cur's first segment
+  const uint32_t totc0 = walk_win_scan(cur);
+  uint64_t Bn = Bc + totc0;                // run segment of nxt's first segment
+  uint32_t totn = walk_win_scan(nxt);
+  uint64_t G = 0;                          // run segment at lane 0 of the tile being mapped
+  uint64_t rg = r0;                        // record holding segment G
+  uint32_t qg = 0;                         //   and its segment index there
+  uint32_t carry = 0;                      // partial value of the record continuing across tiles
+  SegLoad A, B;
+  A.fl = 0;  // virtual tile before the first: no valid lane, nothing stored
+  A.k = 0;
+  A.rec = 0;
+
+  // map the tile at G onto (record, segment) per lane, advance the cursor and the windows
+  auto map_tile = [&]() -> SegInfo {
+    const uint64_t m = start_bit(cur, (int64_t)(Bc - G)) | start_bit(nxt, (int64_t)(Bn - G));
+    const uint64_t M = (uint64_t)wave_or_u32((uint32_t)m) | ((uint64_t)wave_or_u32((uint32_t)(m >> 32)) << 32);
+    const uint64_t below = M & ((lane == 63u) ? ~0ull : ((2ull << lane) - 1ull));
+    SegInfo si;
+    const uint64_t rec = rg + (uint64_t)__builtin_popcountll(below);
+    si.q = below ? lane - (63u - (uint32_t)__builtin_clzll(below)) : qg + lane;
+    // pad lanes: past the run's last segment (no start bit marks the end of
+    // the run's last record, so the record index alone cannot tell)
+    si.valid = G + lane < segs;
+    const uint32_t idx = (uint32_t)(si.valid ? rec - wc0 : 0u);  // < 128
+    const int src = (int)((idx & 63u) << 2);
+    const uint32_t ol_c = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)cur.off);
+    const uint32_t oh_c = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(cur.off >> 32));
+    const uint32_t ln_c = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)cur.len);
+    const uint32_t ol_n = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)nxt.off);
+    const uint32_t oh_n = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(nxt.off >> 32));
+    const uint32_t ln_n = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)nxt.len);
+    const bool in_c = idx < 64u;
+    si.rec = (uint32_t)rec;
+    si.rec_off = in_c ? (((uint64_t)oh_c << 32) | ol_c) : (((uint64_t)oh_n << 32) | ol_n);
+    si.rec_len = in_c ? ln_c : ln_n;
+    si.k = 0;
+    // (defensive: a lane never addresses a segment its record does not have)
+    si.valid = si.valid && si.q < (si.rec_len ? (si.rec_len + 127u) >> 7 : 1u);
+    desc_map_complete(si);  // k; pad lanes become empty first segments
+    // cursor for the next tile: the record holding segment G + 64
+    const uint32_t rec63 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(rec - wc0), 63);
+    const uint32_t q63 = (uint32_t)__builtin_amdgcn_readlane((int)si.q, 63);
+    const uint32_t k63 = (uint32_t)__builtin_amdgcn_readlane((int)si.k, 63);
+    rg = wc0 + rec63 + (k63 ? 0u : 1u);
+    qg = k63 ? q63 + 1u : 0u;
+    G += 64u;
+    // one window step when the cursor left cur (at most one per tile: a full
+    // window holds >= 64 segments); branch-free, pre is reloaded every tile
+    const bool rot = rg >= wc0 + 64u;
+    cur.off = rot ? nxt.off : cur.off;
+    cur.len = rot ? nxt.len : cur.len;
+    cur.p = rot ? nxt.p : cur.p;
+    cur.ok = rot ? nxt.ok : cur.ok;
+    nxt.off = rot ? pre.off : nxt.off;
+    nxt.len = rot ? pre.len : nxt.len;
+    nxt.ok = rot ? pre.ok : nxt.ok;
+    wc0 = rot ? wc0 + 64u : wc0;
+    Bc = rot ? Bn : Bc;
+    const uint32_t tn = walk_win_scan(nxt);
+    Bn = Bc + (rot ? totn : (Bn - Bc));
+    totn = tn;
+    walk_win_issue(P, wc0 + 128u, r1, lane, pre);
+    return si;
+  };
+
+  auto finish = [&](const SegLoad& L) {
+    if (!__builtin_amdgcn_readfirstlane((int)(L.fl & FL_VALID))) return;  // virtual tile (lane 0 valid otherwise)
+    uint32_t v = seg_finish<false, CHAINS, ABLATE, false, true>(smem, P, L, lo, hi);
+    if (ABLATE == 3) {  // loads only (no reduction or store, unless a magic value keeps the loads alive)
+      if (v == 0x9E3779B1u) P.out[0] = v;
+      return;
+    }
+    const bool valid = (L.fl & FL_VALID) != 0;
+    v = valid ? v : 0u;
+    const uint32_t d = min(63u - lane, L.k);
+    v = walk_mulcol(v, d);
+    const uint32_t run_end = min(63u, lane + L.k);
+    const uint32_t X = wave_prefix_xor(v);
+    const uint32_t Xe = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(run_end << 2), (int)X);
+    uint32_t total = Xe ^ dpp0<0x138, 0xF>(X);  // lanes [lane, run_end]
+    const bool head = valid && (lane == 0u || (L.fl & FL_FIRST));
+    // lane 0 continuing a record from the previous tile: Horner step
+    const bool cont0 = !__builtin_amdgcn_readfirstlane((int)(L.fl & FL_FIRST));
+    const uint32_t re0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)run_end);
+    const uint32_t cm = cont0 ? walk_mulcol_uniform(carry, re0 + 1u, lane) : 0u;
+    total ^= (lane == 0u) ? cm : 0u;
+    const bool ends = head && (lane + L.k <= 63u);
+    if (ends) P.out[L.rec] = ~total;
+    const uint64_t cb = __ballot(head && lane + L.k > 63u);
+    carry = cb ? (uint32_t)__builtin_amdgcn_readlane((int)total, __builtin_ctzll(cb)) : 0u;
+  };
+
+  // half-steps: map + issue tile t, then finish tile t-1; one bottom exit with
+  // a precomputed trip count (see crc32_fixed_kernel)
+  uint64_t t = 0;
+  for (; t + 2 <= ntile; t += 2) {
+    seg_issue<false, ABLATE>(P, map_tile(), B);
+    __builtin_amdgcn_sched_barrier(0);
+    finish(A);
+    seg_issue<false, ABLATE>(P, map_tile(), A);
+    __builtin_amdgcn_sched_barrier(0);
+    finish(B);
+  }
+  if (t < ntile) {
+    seg_issue<false, ABLATE>(P, map_tile(), B);
+    __builtin_amdgcn_sched_barrier(0);
+    finish(A);
+    finish(B);
+  } else {
+    finish(A);
+  }
+}
 }  // namespace lsmck
 
 // ---------------------------------------------------------------------------
@@ -1198,6 +1465,36 @@ extern "C" int lsmk_launch_crc32_desc(const CrcParams* P, const uint64_t* block_
   if (e != hipSuccess) return -(int)e;
   void* args[] = {(void*)P};
   e = hipLaunchKernel(fn, dim3(ncu), dim3(block), args, lds, st);
+  if (e != hipSuccess) return -(int)e;
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : -(int)e;
+}
+
+
+extern "C" uint64_t lsmk_walk_sb_count(uint64_t n) { return (n + WALK_SB - 1) / WALK_SB; }
+
+// walking descriptor kernel: superblock sums, their scan (total at
+// P->total_segs), the kernel; sb_prefix holds lsmk_walk_sb_count(n) u64.
+// Nothing is read back: asynchronous on st.
+extern "C" int lsmk_launch_crc32_walk(const CrcParams* P, uint64_t* sb_prefix, int ncu, int variant,
+                                      hipStream_t st) {
+  const uint64_t n = P->nrec;
+  if (n == 0) return 0;
+  const uint64_t nsb = lsmk_walk_sb_count(n);
+  hipLaunchKernelGGL(walk_phase1, dim3((unsigned)((nsb + 15) / 16)), dim3(1024), 0, st, P->len, n, sb_prefix);
+  hipLaunchKernelGGL(scan_phase2, dim3(1), dim3(1024), 0, st, sb_prefix, (uint32_t)nsb, P->total_segs);
+  CrcParams Q = *P;
+  Q.sb_prefix = sb_prefix;
+  const int ch = (variant & 0xF) ? (variant & 0xF) : LSMCK_DEFAULT_DESC_CHAINS;
+  const int ablate = (variant >> 8) & 0xF;
+  const void* fn = ablate == 3 ? (const void*)crc32_walk_kernel<2, 3>
+                 : ch == 1 ? (const void*)crc32_walk_kernel<1>
+                 : ch == 4 ? (const void*)crc32_walk_kernel<4> : (const void*)crc32_walk_kernel<2>;
+  size_t lds = LDS_SCRATCH_OFF;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return -(int)e;
+  void* args[] = {(void*)&Q};
+  e = hipLaunchKernel(fn, dim3(ncu), dim3(1024), args, lds, st);
   if (e != hipSuccess) return -(int)e;
   e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;

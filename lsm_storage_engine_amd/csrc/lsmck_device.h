@@ -24,6 +24,7 @@ struct CrcParams {
   const uint32_t* tinit;      // 0xFFFFFFFF (x) x^(8*m) mod P, m = 0..128; [129] = 0
   const uint32_t* master;     // slicing-by-4 tables T0..T3 (4 x 256), then shift tables ST_1..ST_3 (3 x 4 x 256)
   const uint32_t* zero;       // 256 zero bytes (16-aligned): the load window of empty segments
+  const uint64_t* sb_prefix;  // walking descriptor kernel: exclusive segment prefix per WALK_SB-record superblock
 };
 
 // SHA-256 batch job (lane per message).
@@ -66,6 +67,8 @@ int lsmk_launch_crc32_scan(const lsmck::CrcParams* P, uint64_t* block_sum, hipSt
 int lsmk_launch_crc32_desc(const lsmck::CrcParams* P, const uint64_t* block_sum, int ncu, int variant, hipStream_t st);
 int lsmk_launch_sha256(const lsmck::ShaParams* P, hipStream_t st);
 int lsmk_launch_sha256_slices(const lsmck::ShaSliceParams* P, hipStream_t st);
+uint64_t lsmk_walk_sb_count(uint64_t n);
+int lsmk_launch_crc32_walk(const lsmck::CrcParams* P, uint64_t* sb_prefix, int ncu, int variant, hipStream_t st);
 int lsmk_launch_crc32_compare(const uint32_t* crc, const uint32_t* expected, uint64_t n,
                                unsigned long long* n_bad, unsigned long long* first_bad, hipStream_t st);
 int lsmk_sha_order(const uint32_t* len, size_t n, uint16_t* keys_out, uint32_t* order, void* tmp, size_t* tmp_bytes,

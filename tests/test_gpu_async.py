@@ -138,3 +138,75 @@ def test_verify_batch_device_pooled(ctx):
                 b.free()
     finally:
         d.free()
+
+
+def test_device_descriptor_batch_is_asynchronous(ctx):
+    """LSMCK_DEVICE descriptor batches read nothing back (the walking kernel's
+    scratch is sized by the record count): the call returns while the kernels
+    still run on the caller's stream, and the CRCs are unchanged."""
+    hip = Hip()
+    s = hip.stream()
+    from lsm_storage_engine_amd.device import gen_zipf_lengths
+    n = 1 << 22
+    ln = gen_zipf_lengths(0x5EED0003, n)
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum(ln[:-1].astype(np.uint64), out=off[1:])
+    total = int(off[-1]) + int(ln[-1])
+    d = ctx.alloc(total + 64)
+    bo, bl, o = ctx.alloc(8 * n), ctx.alloc(4 * n), ctx.alloc(4 * n)
+    try:
+        ctx.gen_stream(d.ptr, 0x5EED0003, 0, total, s)
+        bo.upload(off)
+        bl.upload(ln)
+        ctx.sync(s)
+        states = []
+        for _ in range(3):
+            ctx.crc32_device(d.ptr, bo.ptr, bl.ptr, n, o.ptr, s)
+            states.append(hip.query(s))
+            ctx.sync(s)
+        assert 600 in states, states  # hipErrorNotReady right after the call returned
+        got = o.download(np.uint32)
+        host = O.gen_stream(0x5EED0003, 0, total)
+        assert np.array_equal(got, O.crc32_batch(host, off, ln, threads=16))
+    finally:
+        for b in (d, bo, bl, o):
+            b.free()
+        hip.destroy(s)
+
+
+@pytest.mark.parametrize("walk", [0, 1])
+def test_walk_and_tile_map_kernels_agree(ctx, walk):
+    """The walking kernel (default) and the r01 tile-map kernel (crc_walk 0)
+    give the oracle's CRCs on records from empty to several MiB (records
+    spanning many tiles carry their value across tiles), packed, scattered
+    and overlapping."""
+    rng = np.random.default_rng(21)
+    total = 64 << 20
+    data = O.gen_stream(0x31, 0, total)
+    ctx.set_option("crc_walk", walk)
+    try:
+        for trial in range(4):
+            n = int(rng.integers(1, 30000))
+            kind = trial % 4
+            if kind == 0:    # packed, mixed small
+                ln = rng.integers(0, 700, n).astype(np.uint32)
+                off = np.zeros(n, np.uint64)
+                np.cumsum(ln[:-1].astype(np.uint64), out=off[1:])
+            elif kind == 1:  # a few huge records among small ones
+                ln = rng.integers(0, 300, n).astype(np.uint32)
+                ln[rng.integers(0, n, 3)] = rng.integers(1 << 20, 12 << 20, 3)
+                off = np.zeros(n, np.uint64)
+                np.cumsum(ln[:-1].astype(np.uint64), out=off[1:])
+                keep = off + ln <= total
+                off, ln = off[keep], ln[keep]
+            elif kind == 2:  # scattered, overlapping, unsorted
+                ln = rng.integers(0, 5000, n).astype(np.uint32)
+                off = rng.integers(0, total - 5000, n).astype(np.uint64)
+            else:            # one record per tile boundary region: lengths around multiples of 128*64
+                ln = (rng.integers(1, 4, n) * 8192 + rng.integers(-130, 130, n)).astype(np.uint32)
+                ln = np.minimum(ln, 40000).astype(np.uint32)
+                off = rng.integers(0, total - 40000, n).astype(np.uint64)
+            got = ctx.crc32(data, off, ln)
+            assert np.array_equal(got, O.crc32_batch(data, off, ln, threads=8)), (walk, kind)
+    finally:
+        ctx.set_option("crc_walk", 1)
