@@ -177,6 +177,7 @@ struct lsmck_ctx {
   hipEvent_t scratch_ev = nullptr;
   uint64_t* h_total = nullptr;   // pinned
   unsigned long long* d_verify = nullptr;  // [n_bad, first_bad]
+  uint32_t* d_work = nullptr;              // work counters of the claimed-block kernels, one per stage + 1
   unsigned long long* h_verify = nullptr;  // pinned
   // device verify / device WAL replay (grow-only; part of the scratch, ordered by scratch_ev)
   uint32_t* d_vcrc = nullptr;  // computed CRCs
@@ -252,6 +253,7 @@ int ensure_scratch(DescScratch& sc, size_t nblocks) {
 }
 
 void fill_tables(lsmck_ctx* ctx, CrcParams* P) {
+  P->work = ctx->d_work;
   P->kseg = ctx->d_kseg;
   P->khi = ctx->d_khi;
   P->tinit = ctx->d_tinit;
@@ -661,7 +663,8 @@ lsmck_ctx* lsmck_ctx_create(int device) {
             hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming) == hipSuccess &&
             hipHostMalloc((void**)&ctx->h_total, 64, hipHostMallocDefault) == hipSuccess &&
             hipHostMalloc((void**)&ctx->h_verify, 64, hipHostMallocDefault) == hipSuccess &&
-            hipMalloc((void**)&ctx->d_verify, 64) == hipSuccess;
+            hipMalloc((void**)&ctx->d_verify, 64) == hipSuccess &&
+            hipMalloc((void**)&ctx->d_work, 256) == hipSuccess;
   if (!ok) {
     lsmck_host::set_error(LSMCK_ENOMEM, "context allocation failed");
     lsmck_ctx_destroy(ctx);
@@ -767,6 +770,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->variant = (ctx->variant & ~0x10000) | (value ? 0 : 0x10000);
     return 0;
   }
+  if (!strcmp(key, "crc_order")) {  // A/B: fixed ring kernel tile order, 0 strided, 1 contiguous, 2 claimed blocks
+    if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_order must be 0, 1 or 2");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (ctx->variant & ~0x3000000) | ((int)value << 24);
+    return 0;
+  }
   if (!strcmp(key, "crc_walk")) {  // A/B: descriptor batches, 1 = walking kernel (default), 0 = r01 tile-map kernel
     if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_walk must be 0 or 1");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -797,6 +806,7 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   if (ctx->d_tinit) (void)hipFree(ctx->d_tinit);
   if (ctx->d_zero) (void)hipFree(ctx->d_zero);
   if (ctx->d_verify) (void)hipFree(ctx->d_verify);
+  if (ctx->d_work) (void)hipFree(ctx->d_work);
   for (void* p : {(void*)ctx->d_vcrc, (void*)ctx->d_woff, (void*)ctx->d_wlen, (void*)ctx->d_wexp})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)ctx->h_woff, (void*)ctx->h_wlen, (void*)ctx->h_wexp})

@@ -678,7 +678,13 @@ __device__ __forceinline__ void issue_whole(const CrcParams& P, const PercolMap&
   L.k = nsegr - 1u - q;
   L.fl = (gi < total ? FL_VALID : 0u) | (q == 0u ? FL_FIRST : 0u);
 }
-template <int R, int ABLATE = 0, int BLOCK = 1024>
+// ORDER: which tiles a wave walks.  0 = strided (tile t -> wave t mod nwaves);
+// 1 = one contiguous range per wave; 2 = blocks of WRING_BLOCK tiles claimed
+// from an atomic counter (P.work, zeroed by the host), each walked in order.
+// tools/microbench_walk.hip measured the load stream at 10.69 / 10.65 / 10.52
+// ms for 64 GiB in these orders (profiles/r02/mb/mb_walk64.log).
+#define WRING_BLOCK 16u
+template <int R, int ABLATE = 0, int BLOCK = 1024, int ORDER = 0>
 __global__ __launch_bounds__(BLOCK) void crc32_wring_kernel(CrcParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t nsegr = P.flen >> 7;
@@ -691,33 +697,51 @@ __global__ __launch_bounds__(BLOCK) void crc32_wring_kernel(CrcParams P) {
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   const uint32_t total = nsegr * (uint32_t)P.nrec;
   const uint32_t ntiles = (total + 63u) >> 6;
-  if (wave >= ntiles) return;
   PercolMap M;
   M.lsh = __builtin_ctz(nsegr);
   M.tstride = (uint64_t)(64u >> M.lsh) * P.stride;
   M.end = (uint64_t)(P.nrec - 1) * P.stride + P.flen;
   const uint32_t vo = (uint32_t)((lane >> M.lsh) * P.stride) + 128u * (lane & (nsegr - 1u));
-  const uint32_t mine = (ntiles - wave + nwaves - 1u) / nwaves;
-  const uint32_t iters = (mine + R - 1u) / R;
-  // tiles past the wave's last one reload its first tile (in bounds) and are
-  // marked invalid (no store)
-  auto tile_of = [&](uint32_t i) -> uint32_t { return i < mine ? wave + i * nwaves : wave; };
-  SegLoad S[R];
+  // walk tiles t0, t0 + step, ... (mine of them) through the R-slot ring
+  auto run = [&](uint32_t t0, uint32_t mine, uint32_t step) {
+    const uint32_t iters = (mine + R - 1u) / R;
+    // slots past the run's last tile reload its first tile (in bounds) and are
+    // marked invalid (no store)
+    auto tile_of = [&](uint32_t i) -> uint32_t { return i < mine ? t0 + i * step : t0; };
+    SegLoad S[R];
 #pragma unroll
-  for (int k = 0; k < R - 1; ++k) {
-    issue_whole(P, M, vo, tile_of(k), lane, nsegr, (k < (int)mine) ? total : 0u, S[k]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  uint32_t n0 = 0;
-  for (uint32_t it = 0; it < iters; ++it) {
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      const uint32_t ni = n0 + k + R - 1;
-      issue_whole(P, M, vo, tile_of(ni), lane, nsegr, ni < mine ? total : 0u, S[(k + R - 1) % R]);
+    for (int k = 0; k < R - 1; ++k) {
+      issue_whole(P, M, vo, tile_of(k), lane, nsegr, (k < (int)mine) ? total : 0u, S[k]);
       __builtin_amdgcn_sched_barrier(0);
-      finish_tile<true, 2, ABLATE, true>(smem, P, S[k % R], lane, lo, hi);
     }
-    n0 += R;
+    uint32_t n0 = 0;
+    for (uint32_t it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const uint32_t ni = n0 + k + R - 1;
+        issue_whole(P, M, vo, tile_of(ni), lane, nsegr, ni < mine ? total : 0u, S[(k + R - 1) % R]);
+        __builtin_amdgcn_sched_barrier(0);
+        finish_tile<true, 2, ABLATE, true>(smem, P, S[k % R], lane, lo, hi);
+      }
+      n0 += R;
+    }
+  };
+  if constexpr (ORDER == 0) {
+    if (wave >= ntiles) return;
+    run(wave, (ntiles - wave + nwaves - 1u) / nwaves, nwaves);
+  } else if constexpr (ORDER == 1) {
+    const uint32_t per = (ntiles + nwaves - 1u) / nwaves, t0 = wave * per;
+    if (t0 >= ntiles) return;
+    run(t0, min(per, ntiles - t0), 1u);
+  } else {
+    const uint32_t nb = (ntiles + WRING_BLOCK - 1u) / WRING_BLOCK;
+    for (;;) {
+      uint32_t b = 0;
+      if (lane == 0) b = atomicAdd(P.work, 1u);
+      b = __builtin_amdgcn_readfirstlane(b);
+      if (b >= nb) break;
+      run(b * WRING_BLOCK, min(WRING_BLOCK, ntiles - b * WRING_BLOCK), 1u);
+    }
   }
 }
 
@@ -1348,13 +1372,18 @@ static int launch_fixed(const CrcParams* P, int ncu, hipStream_t st) {
   return e == hipSuccess ? 0 : -(int)e;
 }
 
-template <int R, int ABLATE = 0, int BLOCK = 1024>
+template <int R, int ABLATE = 0, int BLOCK = 1024, int ORDER = 0>
 static int launch_wring(const CrcParams* P, int ncu, hipStream_t st) {
   size_t lds = LDS_SCRATCH_OFF;
-  hipError_t e = hipFuncSetAttribute((const void*)crc32_wring_kernel<R, ABLATE, BLOCK>,
+  hipError_t e = hipFuncSetAttribute((const void*)crc32_wring_kernel<R, ABLATE, BLOCK, ORDER>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return -(int)e;
-  hipLaunchKernelGGL((crc32_wring_kernel<R, ABLATE, BLOCK>), dim3(ncu), dim3(BLOCK), lds, st, *P);
+  if (ORDER == 2) {
+    if (!P->work) return -(int)hipErrorInvalidValue;
+    e = hipMemsetAsync(P->work, 0, 4, st);
+    if (e != hipSuccess) return -(int)e;
+  }
+  hipLaunchKernelGGL((crc32_wring_kernel<R, ABLATE, BLOCK, ORDER>), dim3(ncu), dim3(BLOCK), lds, st, *P);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
 }
@@ -1384,6 +1413,10 @@ extern "C" int lsmk_launch_crc32_fixed(const CrcParams* P, int ncu, int variant,
       if (ring == 2) return launch_wring<2, 0, 768>(P, ncu, st);
       return ablate ? launch_wring<3, 3, 768>(P, ncu, st) : launch_wring<3, 0, 768>(P, ncu, st);
     }
+    // tile order (variant bits 24-25): 0 strided, 1 contiguous per wave, 2 claimed blocks
+    const int order = (variant >> 24) & 3;
+    if (ring == 2 && order == 1) return ablate ? launch_wring<2, 3, 1024, 1>(P, ncu, st) : launch_wring<2, 0, 1024, 1>(P, ncu, st);
+    if (ring == 2 && order == 2) return ablate ? launch_wring<2, 3, 1024, 2>(P, ncu, st) : launch_wring<2, 0, 1024, 2>(P, ncu, st);
     if (ring == 2) return ablate ? launch_wring<2, 3>(P, ncu, st) : launch_wring<2, 0>(P, ncu, st);
     return ablate ? launch_wring<3, 3>(P, ncu, st) : launch_wring<3, 0>(P, ncu, st);
   }

@@ -25,6 +25,7 @@ struct CrcParams {
   const uint32_t* master;     // slicing-by-4 tables T0..T3 (4 x 256), then shift tables ST_1..ST_3 (3 x 4 x 256)
   const uint32_t* zero;       // 256 zero bytes (16-aligned): the load window of empty segments
   const uint64_t* sb_prefix;  // walking descriptor kernel: exclusive segment prefix per WALK_SB-record superblock
+  uint32_t* work;             // fixed ring kernel, claimed-block order: work counter (zeroed by the launcher)
 };
 
 // SHA-256 batch job (lane per message).

@@ -210,3 +210,26 @@ def test_walk_and_tile_map_kernels_agree(ctx, walk):
             assert np.array_equal(got, O.crc32_batch(data, off, ln, threads=8)), (walk, kind)
     finally:
         ctx.set_option("crc_walk", 1)
+
+
+@pytest.mark.parametrize("order", [0, 1, 2])
+def test_fixed_ring_tile_orders(ctx, order):
+    """The fixed-record ring kernel walks its tiles strided (0), as one
+    contiguous range per wave (1) or as claimed 16-tile blocks (2): the same
+    CRCs either way, including a last partial tile and fewer tiles than waves."""
+    ctx.set_option("crc_order", order)
+    try:
+        for length, nb in ((4096, 1 << 16), (4096, 77), (256, 100003), (1024, 5000)):
+            d = ctx.alloc(nb * length)
+            out = ctx.alloc(4 * nb)
+            try:
+                ctx.gen_stream(d.ptr, 0x44 + length, 0, nb * length)
+                ctx.crc32_fixed_device(d.ptr, length, length, nb, out.ptr)
+                ctx.sync()
+                host = O.gen_stream(0x44 + length, 0, nb * length)
+                assert np.array_equal(out.download(np.uint32), O.crc32_fixed(host, length, length, nb, threads=8))
+            finally:
+                d.free()
+                out.free()
+    finally:
+        ctx.set_option("crc_order", 0)
