@@ -1,0 +1,780 @@
+// lsmck_server -- the loopback line-protocol server of the reference
+// (src/server.rs, protocol src/command.rs), the front end that drives the
+// checksum path end to end (BASELINE config 5):
+//
+//   * start-up is Db::load (src/tokio/db.rs:37-73): every SSTable of the tree
+//     verified in one GPU batch (lsmck_tree_verify: Checksums::verify of every
+//     table, checksums.rs:40-62), then the WAL replayed with its payload CRCs
+//     checked in one GPU batch (lsmck_wal_replay_verify: CommandLog iterator +
+//     MemTable::from_log, wal.rs:68-163, memtable.rs:28-47);
+//   * every insert / update / delete is appended to the WAL with its CRC-32
+//     from lsmck_crc32_ieee (through lsmck_wal_encode_*: CommandLog::log,
+//     wal.rs:165-196), one write(2) per record as the reference's flushed
+//     BufWriter does;
+//   * a memtable over memtable_limit_bytes is flushed to a level-0 SSTable in
+//     the reference's on-disk layout, its checksum file written by
+//     lsmck_checksums_write (Checksums::write_checksums, checksums.rs:64-80)
+//     (db.rs:73-123).  One deliberate difference: the reference deletes and
+//     recreates the WAL after the flush completes (db.rs:109-114), so records
+//     appended between the memtable swap and the delete are lost from the log
+//     (a crash loses them).  Here the log is rotated AT the swap (wal.log ->
+//     wal.log.flushing, a fresh wal.log for the new memtable) and the rotated
+//     log is deleted when its table is written; a start-up that finds one
+//     replays it before wal.log and merges the two;
+//   * get reads the memtable, the memtable being flushed, then the SSTables
+//     (level 0 first, newest table first) through their sparse index and data
+//     file (tokio/sstable.rs:63-86, datafile.rs:70-112).  Bloom filters are not
+//     read (their probabilistic-collections encoding is not reproduced; the
+//     flush writes an empty bloom file); in their place a table is skipped when
+//     the key lies outside its key range (first index key .. last record's
+//     key, the latter read once per table on first use).
+//
+// Responses are the reference's: "ok", the value, "<key> not found",
+// "Supported commands: get, insert, update, delete" (server.rs:42-67).  A
+// command with a missing argument makes the reference's connection task panic
+// (command.rs:27 indexes args[1]); here the connection is closed.  At EOF the
+// reference's read_line loop spins on Ok(0) (server.rs:20); here the
+// connection is closed.  Compaction (db.rs:188-232) is not run: it is not on
+// the checksum path.
+//
+// Usage: lsmck_server [--base DIR] [--port P] [--bind ADDR] [--device D]
+//                     [--memtable-limit BYTES] [--exit-after-load]
+// Prints one JSON line when loaded ({"event":"loaded",...}) and one when it
+// listens ({"event":"listening","port":P}).
+#include <arpa/inet.h>
+#include <dirent.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "lsmck.h"
+
+namespace {
+
+constexpr int kMaxLevel = LSMCK_SSTABLE_MAX_LEVEL;  // db.rs:17
+constexpr size_t kIndexStep = 100;                  // tokio/sstable.rs:17
+
+double now_s() {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+[[noreturn]] void panic_exit(const std::string& msg) {
+  // a Rust panic in main: the message on stderr, exit status 101
+  fprintf(stderr, "thread 'main' panicked at '%s'\n", msg.c_str());
+  fflush(stderr);
+  _exit(101);
+}
+
+std::string join(const std::string& a, const std::string& b) {
+  if (a.empty()) return b;
+  return a.back() == '/' ? a + b : a + "/" + b;
+}
+
+int mkdir_p(const std::string& p) {
+  struct stat st;
+  if (stat(p.c_str(), &st) == 0) return S_ISDIR(st.st_mode) ? 0 : -EEXIST;
+  size_t cut = p.find_last_of('/');
+  if (cut != std::string::npos && cut > 0) {
+    int rc = mkdir_p(p.substr(0, cut));
+    if (rc) return rc;
+  }
+  if (mkdir(p.c_str(), 0777) != 0 && errno != EEXIST) return -errno;
+  return 0;
+}
+
+bool read_file(const std::string& path, std::string* out) {
+  int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return false;
+  out->clear();
+  char buf[1 << 16];
+  for (;;) {
+    ssize_t k = read(fd, buf, sizeof buf);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      close(fd);
+      return false;
+    }
+    if (k == 0) break;
+    out->append(buf, (size_t)k);
+  }
+  close(fd);
+  return true;
+}
+
+bool write_all(int fd, const void* p, size_t n) {
+  const char* c = (const char*)p;
+  while (n) {
+    ssize_t k = write(fd, c, n);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    c += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+
+void put_u32(std::string& s, uint32_t v) {
+  for (int i = 0; i < 4; ++i) s.push_back((char)(v >> (8 * i)));
+}
+void put_u64(std::string& s, uint64_t v) {
+  for (int i = 0; i < 8; ++i) s.push_back((char)(v >> (8 * i)));
+}
+uint32_t get_u32(const unsigned char* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+uint64_t get_u64(const unsigned char* p) { return (uint64_t)get_u32(p) | ((uint64_t)get_u32(p + 4) << 32); }
+
+// serde_json string escaping (the metadata's file names and base path)
+std::string json_str(const std::string& s) {
+  std::string o = "\"";
+  for (unsigned char c : s) {
+    if (c == '"' || c == '\\') {
+      o.push_back('\\');
+      o.push_back((char)c);
+    } else if (c < 0x20) {
+      char b[8];
+      snprintf(b, sizeof b, "\\u%04x", c);
+      o += b;
+    } else {
+      o.push_back((char)c);
+    }
+  }
+  return o + "\"";
+}
+
+// the few fields of a SsTableMetadata JSON record the read path needs
+// (sstable_metadata.rs:8-17); the file was verified by lsmck_tree_verify's
+// serde-rules parser already
+bool json_field(const std::string& j, const char* key, std::string* out) {
+  const std::string k = std::string("\"") + key + "\"";
+  size_t i = j.find(k);
+  if (i == std::string::npos) return false;
+  i = j.find(':', i + k.size());
+  if (i == std::string::npos) return false;
+  ++i;
+  while (i < j.size() && isspace((unsigned char)j[i])) ++i;
+  if (i < j.size() && j[i] == '"') {
+    std::string v;
+    for (++i; i < j.size() && j[i] != '"'; ++i) {
+      if (j[i] == '\\' && i + 1 < j.size()) ++i;
+      v.push_back(j[i]);
+    }
+    *out = v;
+    return true;
+  }
+  size_t e = i;
+  while (e < j.size() && (isdigit((unsigned char)j[e]) || j[e] == '-')) ++e;
+  *out = j.substr(i, e - i);
+  return e > i;
+}
+
+// ---------------------------------------------------------------------------
+// MemTable (src/memtable.rs): BTreeMap + byte count
+struct MemTable {
+  std::map<std::string, std::string> data;
+  size_t bytes = 0;
+  void insert(const std::string& k, const std::string& v) {  // memtable.rs:67-74
+    auto it = data.find(k);
+    size_t prev = it != data.end() ? it->second.size() + k.size() : 0;
+    bytes = bytes + k.size() + v.size() - prev;
+    data[k] = v;
+  }
+  void remove(const std::string& k) {  // memtable.rs:76-81
+    auto it = data.find(k);
+    if (it == data.end()) return;
+    bytes -= it->second.size() + k.size();
+    data.erase(it);
+  }
+  const std::string* get(const std::string& k) const {
+    auto it = data.find(k);
+    return it == data.end() ? nullptr : &it->second;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// SSTable read path: sparse index (bincode BTreeMap<Vec<u8>, u64>,
+// sstable_index.rs) + data file ([u32 klen][u32 vlen][key][val], datafile.rs)
+struct SsTable {
+  uint64_t id = 0;
+  int level = 0;
+  std::string data_path;
+  std::map<std::string, uint64_t> index;
+  uint64_t size = 0;
+  mutable std::once_flag last_once;
+  mutable std::string last_key;  // the table's largest key (read on first use)
+
+  bool load_index(const std::string& index_path) {
+    std::string b;
+    if (!read_file(index_path, &b) || b.size() < 8) return false;
+    const unsigned char* p = (const unsigned char*)b.data();
+    size_t n = b.size(), pos = 8;
+    const uint64_t cnt = get_u64(p);
+    for (uint64_t i = 0; i < cnt; ++i) {
+      if (pos + 8 > n) return false;
+      const uint64_t kl = get_u64(p + pos);
+      pos += 8;
+      if (pos + kl + 8 > n) return false;
+      std::string k((const char*)p + pos, (size_t)kl);
+      pos += kl;
+      index[k] = get_u64(p + pos);
+      pos += 8;
+    }
+    return true;
+  }
+
+  // read_record at pos: false at EOF (UnexpectedEof -> None, datafile.rs:59-67)
+  static bool read_record(int fd, uint64_t pos, std::string* k, std::string* v, uint64_t* len) {
+    unsigned char h[8];
+    if (pread(fd, h, 8, (off_t)pos) != 8) return false;
+    const uint32_t kl = get_u32(h), vl = get_u32(h + 4);
+    std::string buf((size_t)kl + vl, '\0');
+    if (kl + (size_t)vl && pread(fd, &buf[0], buf.size(), (off_t)(pos + 8)) != (ssize_t)buf.size()) return false;
+    *k = buf.substr(0, kl);
+    *v = buf.substr(kl);
+    *len = 8ull + kl + vl;
+    return true;
+  }
+
+  // tokio/sstable.rs:63-86: exact index hit -> read_record, else scan the
+  // index range that can hold the key
+  bool get(const std::string& key, std::string* val) const {
+    // key range filter (in place of the bloom filter, tokio/sstable.rs:64)
+    if (index.empty() || key < index.begin()->first) return false;
+    std::call_once(last_once, [this] {
+      int fd = open(data_path.c_str(), O_RDONLY | O_CLOEXEC);
+      if (fd < 0) return;
+      std::string k, v;
+      uint64_t len = 0;
+      for (uint64_t pos = index.rbegin()->second; read_record(fd, pos, &k, &v, &len); pos += len) last_key = k;
+      close(fd);
+    });
+    if (key > last_key) return false;
+    int fd = open(data_path.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return false;
+    std::string k, v;
+    uint64_t len = 0;
+    bool found = false;
+    auto hit = index.find(key);
+    if (hit != index.end()) {
+      found = read_record(fd, hit->second, &k, &v, &len) && k == key;
+    } else {
+      auto hi = index.lower_bound(key);  // first entry >= key
+      const uint64_t end = hi == index.end() ? size : hi->second;
+      uint64_t start = 0;
+      if (hi != index.begin()) start = std::prev(hi)->second;
+      for (uint64_t pos = start; read_record(fd, pos, &k, &v, &len);) {  // datafile.rs:87-106
+        if (k == key) {
+          found = true;
+          break;
+        }
+        pos += len;
+        if (pos >= end) break;
+      }
+    }
+    close(fd);
+    if (found) *val = v;
+    return found;
+  }
+};
+
+struct Config {
+  std::string base = "./data";
+  size_t memtable_limit = 4096;  // config/default: memtable_limit_bytes
+  int port = 3333;
+  std::string bind = "127.0.0.1";
+  int device = 0;
+  bool exit_after_load = false;
+};
+
+// ---------------------------------------------------------------------------
+struct Db {
+  Config cfg;
+  lsmck_ctx* ctx = nullptr;
+  std::mutex wal_mu;
+  int wal_fd = -1;
+  std::mutex mem_mu;
+  MemTable mem;
+  std::shared_ptr<const MemTable> old;  // being flushed (db.rs:28)
+  std::shared_mutex lv_mu;
+  std::vector<std::vector<std::shared_ptr<SsTable>>> levels{(size_t)kMaxLevel};
+  uint64_t last_id = 0;
+
+  std::string wal_path() const { return join(join(cfg.base, "wal"), "wal.log"); }
+  std::string flushing_path() const { return wal_path() + ".flushing"; }
+
+  int open_wal() {  // CommandLog::new (wal.rs:86-101): create dirs, read + append
+    mkdir_p(join(cfg.base, "wal"));
+    return open(wal_path().c_str(), O_RDWR | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+  }
+
+  // Db::load (db.rs:37-73)
+  void load() {
+    const double t0 = now_s();
+    lsmck_tree_report rep;
+    int rc = lsmck_tree_verify(ctx, cfg.base.c_str(), &rep);
+    if (rc < 0) {
+      fprintf(stderr, "lsmck_tree_verify: %s\n", lsmck_last_error());
+      exit(1);
+    }
+    if (rc == 1) {  // the reference panics at its first bad table (SsTable::load)
+      switch (rep.first_status) {
+        case LSMCK_META_PANIC: panic_exit("Can't read metadata file, file with unknown format");
+        case LSMCK_DATA_MISMATCH:
+        case LSMCK_INDEX_MISMATCH: {  // checksums.rs:49-60 names the data / index file
+          std::string j, fn;
+          read_file(rep.first_metadata_path, &j);
+          json_field(j, rep.first_status == LSMCK_DATA_MISMATCH ? "data_filename" : "index_filename", &fn);
+          panic_exit("Can't load SSTable from " + fn + ". Checksum is not correct");
+        }
+        case LSMCK_PANIC_OPEN_FILE:
+        case LSMCK_PANIC_OPEN_INDEX: panic_exit("Can't open file to calculate checksum");
+        case LSMCK_PANIC_OPEN_CHECKSUM: panic_exit("Can't open checksum file");
+        default:  // io::Error from SsTable::load -> `?` in Db::load -> .expect in main
+          panic_exit(std::string("unable run storage: ") + rep.first_metadata_path + " (" +
+                     std::to_string(rep.first_status) + ")");
+      }
+    }
+    const double t_tree = now_s() - t0;
+    // the tables' read-path state, in load order: per level, sorted by id
+    for (int lv = 0; lv < kMaxLevel; ++lv) {
+      const std::string dir = join(cfg.base, "level-" + std::to_string(lv));
+      DIR* d = opendir(dir.c_str());
+      if (!d) continue;
+      while (struct dirent* e = readdir(d)) {
+        if (!strstr(e->d_name, "metadata")) continue;
+        std::string j, id, level, base, data, index;
+        if (!read_file(join(dir, e->d_name), &j) || !json_field(j, "id", &id) || !json_field(j, "level", &level) ||
+            !json_field(j, "base_path", &base) || !json_field(j, "data_filename", &data) ||
+            !json_field(j, "index_filename", &index))
+          panic_exit("Can't read metadata file, file with unknown format");
+        auto t = std::make_shared<SsTable>();
+        t->id = strtoull(id.c_str(), nullptr, 10);
+        t->level = atoi(level.c_str());
+        const std::string ldir = join(base, "level-" + level);
+        t->data_path = join(ldir, data);
+        struct stat st;
+        if (stat(t->data_path.c_str(), &st) == 0) t->size = (uint64_t)st.st_size;
+        if (!t->load_index(join(ldir, index))) panic_exit("Can't open index file");
+        last_id = std::max(last_id, t->id);
+        levels[lv].push_back(t);
+      }
+      closedir(d);
+      std::sort(levels[lv].begin(), levels[lv].end(),
+                [](const std::shared_ptr<SsTable>& a, const std::shared_ptr<SsTable>& b) { return a->id < b->id; });
+    }
+    // WAL replay: every payload CRC in one GPU batch
+    const double t1 = now_s();
+    {
+      // a log rotated at a memtable swap whose flush did not complete: its
+      // records come first; merge it in front of wal.log (see the header)
+      std::string older, newer;
+      if (read_file(flushing_path(), &older)) {
+        read_file(wal_path(), &newer);
+        const std::string tmp = wal_path() + ".merge";
+        int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+        if (fd < 0 || !write_all(fd, older.data(), older.size()) || !write_all(fd, newer.data(), newer.size()) ||
+            fsync(fd) != 0 || close(fd) != 0 || rename(tmp.c_str(), wal_path().c_str()) != 0)
+          panic_exit("Can't merge the rotated WAL");
+        unlink(flushing_path().c_str());
+      }
+    }
+    wal_fd = open_wal();
+    if (wal_fd < 0) {
+      fprintf(stderr, "Can't create WAL file: %s\n", strerror(errno));
+      exit(1);
+    }
+    struct stat st;
+    fstat(wal_fd, &st);
+    const size_t n = (size_t)st.st_size;
+    const uint8_t* img = nullptr;
+    void* map = nullptr;
+    if (n) {
+      map = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, wal_fd, 0);
+      if (map == MAP_FAILED) {
+        fprintf(stderr, "mmap wal: %s\n", strerror(errno));
+        exit(1);
+      }
+      img = (const uint8_t*)map;
+    }
+    const size_t cap = n / 9 + 1;
+    std::vector<lsmck_wal_rec> recs(cap);
+    size_t nrec = 0;
+    uint64_t bad_index = 0;
+    uint32_t bad_crc = 0, bad_expected = 0;
+    rc = lsmck_wal_replay_verify(ctx, img, n, LSMCK_HOST, recs.data(), cap, &nrec, &bad_index, &bad_crc, &bad_expected);
+    if (rc < 0) {
+      fprintf(stderr, "lsmck_wal_replay_verify: %s\n", lsmck_last_error());
+      exit(1);
+    }
+    char msg[256];
+    if (rc == LSMCK_WAL_CORRUPTED) {  // MemTable::from_log(..).expect(..) on Err (db.rs:61-62)
+      snprintf(msg, sizeof msg,
+               "Can't restore memtable from a log: CorruptedData { checksum: %u, expected: %u }", bad_crc,
+               bad_expected);
+      panic_exit(msg);
+    }
+    if (rc == LSMCK_WAL_REMOVE_PANIC) {  // wal.rs:154-159
+      snprintf(msg, sizeof msg, "data corruption encountered (%08x) != %08x", bad_crc, bad_expected);
+      panic_exit(msg);
+    }
+    if (rc == LSMCK_WAL_BAD_TYPE) {
+      snprintf(msg, sizeof msg, "Can't restore memtable from a log: InvalidCommandType(%u)", bad_crc);
+      panic_exit(msg);
+    }
+    // MemTable::from_log (memtable.rs:28-47): the payload actually read (short at EOF)
+    for (size_t i = 0; i < nrec; ++i) {
+      const lsmck_wal_rec& r = recs[i];
+      const uint64_t want = (uint64_t)(uint32_t)(r.klen + r.vlen);
+      const uint64_t got = std::min<uint64_t>(want, n - r.payload_off);
+      const char* p = (const char*)img + r.payload_off;
+      if (r.type == 1) {
+        const uint64_t kl = std::min<uint64_t>(r.klen, got);
+        mem.insert(std::string(p, kl), std::string(p + kl, got - kl));
+      } else {
+        mem.remove(std::string(p, got));
+      }
+    }
+    if (map) munmap(map, n);
+    const double t_wal = now_s() - t1;
+    uint64_t ntab = 0;
+    for (auto& l : levels) ntab += l.size();
+    printf("{\"event\": \"loaded\", \"tables\": %llu, \"table_bytes\": %llu, \"tree_verify_s\": %.6f, "
+           "\"tree_list_s\": %.6f, \"wal_bytes\": %zu, \"wal_records\": %zu, \"wal_replay_s\": %.6f, "
+           "\"memtable_entries\": %zu, \"memtable_bytes\": %zu, \"load_s\": %.6f}\n",
+           (unsigned long long)ntab, (unsigned long long)rep.table_bytes, t_tree, rep.list_seconds, n, nrec, t_wal,
+           mem.data.size(), mem.bytes, now_s() - t0);
+    fflush(stdout);
+  }
+
+  int wal_append(const std::string& rec) {
+    std::lock_guard<std::mutex> lk(wal_mu);
+    return write_all(wal_fd, rec.data(), rec.size()) ? 0 : -errno;
+  }
+
+  // Db::insert (db.rs:76-124)
+  int insert(const std::string& k, const std::string& v) {
+    std::string rec(13 + k.size() + v.size(), '\0');
+    lsmck_wal_encode_insert((const uint8_t*)k.data(), (uint32_t)k.size(), (const uint8_t*)v.data(),
+                            (uint32_t)v.size(), (uint8_t*)&rec[0]);
+    std::shared_ptr<const MemTable> to_flush;
+    {
+      // the log record and the memtable entry change together with respect to
+      // a swap (a record never lands in one memtable's log and the other table)
+      std::lock_guard<std::mutex> lk(mem_mu);
+      int rc = wal_append(rec);
+      if (rc) return rc;
+      mem.insert(k, v);
+      if (mem.bytes > cfg.memtable_limit && !old) {
+        old = std::make_shared<const MemTable>(std::move(mem));
+        mem = MemTable();
+        to_flush = old;
+        // rotate the log with the memtable (the reference recreates it only
+        // after the flush, db.rs:109-114, and loses what came in between)
+        std::lock_guard<std::mutex> wl(wal_mu);
+        close(wal_fd);
+        if (rename(wal_path().c_str(), flushing_path().c_str()) != 0) panic_exit("Can't rotate WAL file");
+        wal_fd = open_wal();
+        if (wal_fd < 0) panic_exit("Can't create WAL file");
+      }
+    }
+    if (to_flush) std::thread([this, to_flush] { flush(to_flush); }).detach();
+    return 0;
+  }
+
+  // Db::delete (db.rs:131-143): WAL Remove, memtable tombstone vec![0]
+  int remove(const std::string& k) {
+    std::string rec(9 + k.size(), '\0');
+    lsmck_wal_encode_remove((const uint8_t*)k.data(), (uint32_t)k.size(), (uint8_t*)&rec[0]);
+    std::lock_guard<std::mutex> lk(mem_mu);
+    int rc = wal_append(rec);
+    if (rc) return rc;
+    mem.insert(k, std::string(1, '\0'));
+    return 0;
+  }
+
+  // Db::get (db.rs:144-186); a tombstone [0] reads as not found
+  bool get(const std::string& k, std::string* v) {
+    bool found = false;
+    {
+      std::lock_guard<std::mutex> lk(mem_mu);
+      if (const std::string* p = mem.get(k)) {
+        *v = *p;
+        found = true;
+      } else if (old) {
+        if (const std::string* q = old->get(k)) {
+          *v = *q;
+          found = true;
+        }
+      }
+    }
+    if (!found) {
+      std::shared_lock<std::shared_mutex> lk(lv_mu);
+      for (int lv = 0; lv < kMaxLevel && !found; ++lv)
+        for (auto it = levels[lv].rbegin(); it != levels[lv].rend() && !found; ++it) found = (*it)->get(k, v);
+    }
+    return found && !(v->size() == 1 && (*v)[0] == '\0');
+  }
+
+  // SsTable::from_memtable (tokio/sstable.rs:88-111) + the WAL swap (db.rs:100-121)
+  void flush(std::shared_ptr<const MemTable> m) {
+    uint64_t id;
+    {
+      std::unique_lock<std::shared_mutex> lk(lv_mu);
+      struct timespec ts;
+      clock_gettime(CLOCK_REALTIME, &ts);
+      id = (uint64_t)ts.tv_sec * 1000ull + (uint64_t)ts.tv_nsec / 1000000ull;  // ms ids (sstable_metadata.rs:21-27)
+      if (id <= last_id) id = last_id + 1;  // two flushes in one ms would share file names
+      last_id = id;
+    }
+    const std::string ids = std::to_string(id), dir = join(cfg.base, "level-0");
+    mkdir_p(dir);
+    const std::string data_fn = "data_" + ids + ".db", index_fn = "index_" + ids + ".db",
+                      checksum_fn = "checksum_" + ids + ".db", bloom_fn = "bloom_" + ids + ".db",
+                      meta_fn = "metadata_" + ids + ".db";
+    auto t = std::make_shared<SsTable>();
+    t->id = id;
+    t->data_path = join(dir, data_fn);
+    std::string data, index;
+    uint64_t i = 0;
+    for (const auto& kv : m->data) {  // write_data_file (tokio/sstable.rs:113-135)
+      if (i++ % kIndexStep == 0) t->index[kv.first] = data.size();
+      put_u32(data, (uint32_t)kv.first.size());
+      put_u32(data, (uint32_t)kv.second.size());
+      data += kv.first;
+      data += kv.second;
+    }
+    t->size = data.size();
+    put_u64(index, t->index.size());  // bincode 1.x fixint BTreeMap<Vec<u8>, u64>
+    for (const auto& e : t->index) {
+      put_u64(index, e.first.size());
+      index += e.first;
+      put_u64(index, e.second);
+    }
+    auto write_file = [](const std::string& p, const std::string& b) {
+      int fd = open(p.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
+      if (fd < 0) return false;
+      bool ok = write_all(fd, b.data(), b.size());
+      close(fd);
+      return ok;
+    };
+    std::string meta = "{\"base_path\":" + json_str(cfg.base) + ",\"id\":" + ids +
+                       ",\"level\":0,\"metadata_filename\":" + json_str(meta_fn) +
+                       ",\"checksum_filename\":" + json_str(checksum_fn) + ",\"data_filename\":" + json_str(data_fn) +
+                       ",\"index_filename\":" + json_str(index_fn) +
+                       ",\"bloom_filter_filename\":" + json_str(bloom_fn) + "}";
+    if (!write_file(t->data_path, data) || !write_file(join(dir, index_fn), index))
+      panic_exit("Can't create new sstable");
+    int rc = lsmck_checksums_write(t->data_path.c_str(), join(dir, index_fn).c_str(), join(dir, checksum_fn).c_str());
+    if (rc) panic_exit(std::string("Can't create new sstable: ") + lsmck_last_error());
+    if (!write_file(join(dir, bloom_fn), "") || !write_file(join(dir, meta_fn), meta))
+      panic_exit("Can't create new sstable");
+    {
+      std::unique_lock<std::shared_mutex> lk(lv_mu);
+      levels[0].push_back(t);
+    }
+    // the flushed memtable's log is no longer needed (wal.close(), db.rs:110)
+    unlink(flushing_path().c_str());
+    std::lock_guard<std::mutex> lk(mem_mu);
+    old.reset();
+  }
+};
+
+// String::from_utf8_lossy (server.rs:47): each maximal invalid subpart -> U+FFFD
+std::string utf8_lossy(const std::string& in) {
+  static const char kRep[] = "\xEF\xBF\xBD";
+  std::string o;
+  const unsigned char* s = (const unsigned char*)in.data();
+  const size_t n = in.size();
+  for (size_t i = 0; i < n;) {
+    const unsigned c = s[i];
+    if (c < 0x80) {
+      o.push_back((char)c);
+      ++i;
+      continue;
+    }
+    size_t need;
+    unsigned lo = 0x80, hi = 0xBF;  // bounds of the second byte
+    if (c >= 0xC2 && c <= 0xDF) need = 1;
+    else if (c == 0xE0) need = 2, lo = 0xA0;
+    else if ((c >= 0xE1 && c <= 0xEC) || c == 0xEE || c == 0xEF) need = 2;
+    else if (c == 0xED) need = 2, hi = 0x9F;
+    else if (c == 0xF0) need = 3, lo = 0x90;
+    else if (c >= 0xF1 && c <= 0xF3) need = 3;
+    else if (c == 0xF4) need = 3, hi = 0x8F;
+    else {
+      o += kRep;
+      ++i;
+      continue;
+    }
+    size_t k = 1;
+    for (; k <= need && i + k < n; ++k) {
+      const unsigned b = s[i + k];
+      if (k == 1 ? (b < lo || b > hi) : (b < 0x80 || b > 0xBF)) break;
+    }
+    if (k == need + 1) {
+      o.append((const char*)s + i, need + 1);
+      i += need + 1;
+    } else {
+      o += kRep;
+      i += k;  // the valid prefix of the sequence is one maximal subpart
+    }
+  }
+  return o;
+}
+
+// split_whitespace (command.rs:17)
+std::vector<std::string> split_ws(const std::string& s) {
+  std::vector<std::string> out;
+  size_t i = 0;
+  while (i < s.size()) {
+    while (i < s.size() && (isspace((unsigned char)s[i]) || s[i] == '\v')) ++i;
+    size_t j = i;
+    while (j < s.size() && !(isspace((unsigned char)s[j]) || s[j] == '\v')) ++j;
+    if (j > i) out.push_back(s.substr(i, j - i));
+    i = j;
+  }
+  return out;
+}
+
+// handle_client (server.rs:16-84); false ends the connection
+bool handle_line(Db& db, const std::string& line, std::string* resp) {
+  const std::vector<std::string> a = split_ws(line);
+  if (a.empty()) {
+    *resp = "Supported commands: get, insert, update, delete\n";
+    return true;
+  }
+  const std::string& c = a[0];
+  const bool known = c == "get" || c == "insert" || c == "update" || c == "delete";
+  if (!known) {
+    *resp = "Supported commands: get, insert, update, delete\n";
+    return true;
+  }
+  const size_t need = (c == "insert" || c == "update") ? 3 : 2;
+  if (a.size() < need) return false;  // the reference's args[i] panics its connection task
+  if (c == "get") {
+    std::string v;
+    if (db.get(a[1], &v)) *resp = utf8_lossy(v) + "\n";
+    else *resp = utf8_lossy(a[1]) + " not found\n";
+    return true;
+  }
+  int rc = c == "delete" ? db.remove(a[1]) : db.insert(a[1], a[2]);
+  if (rc) return false;  // db.*().await.unwrap() panics the task
+  *resp = "ok\n";
+  return true;
+}
+
+void serve_client(Db* db, int fd) {
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+  std::string buf, out;
+  char tmp[65536];
+  bool alive = true;
+  while (alive) {
+    ssize_t k = recv(fd, tmp, sizeof tmp, 0);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) break;
+    buf.append(tmp, (size_t)k);
+    size_t start = 0;
+    out.clear();
+    for (size_t nl; (nl = buf.find('\n', start)) != std::string::npos; start = nl + 1) {
+      std::string resp;
+      if (!handle_line(*db, buf.substr(start, nl + 1 - start), &resp)) {
+        alive = false;
+        break;
+      }
+      out += resp;
+    }
+    buf.erase(0, start);
+    if (!out.empty() && !write_all(fd, out.data(), out.size())) break;
+  }
+  close(fd);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  signal(SIGPIPE, SIG_IGN);
+  Config cfg;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto val = [&]() -> const char* {
+      if (i + 1 >= argc) {
+        fprintf(stderr, "missing value for %s\n", a.c_str());
+        exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--base") cfg.base = val();
+    else if (a == "--port") cfg.port = atoi(val());
+    else if (a == "--bind") cfg.bind = val();
+    else if (a == "--device") cfg.device = atoi(val());
+    else if (a == "--memtable-limit") cfg.memtable_limit = strtoull(val(), nullptr, 10);
+    else if (a == "--exit-after-load") cfg.exit_after_load = true;
+    else {
+      fprintf(stderr, "usage: %s [--base DIR] [--port P] [--bind ADDR] [--device D] [--memtable-limit B] "
+                      "[--exit-after-load]\n", argv[0]);
+      return 2;
+    }
+  }
+  Db db;
+  db.cfg = cfg;
+  db.ctx = lsmck_ctx_create(cfg.device);
+  if (!db.ctx) {  // the batch paths have no CPU fallback
+    fprintf(stderr, "lsmck_ctx_create(%d): %s\n", cfg.device, lsmck_last_error());
+    return 1;
+  }
+  db.load();
+  if (cfg.exit_after_load) {
+    lsmck_ctx_destroy(db.ctx);
+    return 0;
+  }
+  int ls = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  int one = 1;
+  setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  struct sockaddr_in sa;
+  memset(&sa, 0, sizeof sa);
+  sa.sin_family = AF_INET;
+  sa.sin_port = htons((uint16_t)cfg.port);
+  if (inet_pton(AF_INET, cfg.bind.c_str(), &sa.sin_addr) != 1 || bind(ls, (struct sockaddr*)&sa, sizeof sa) != 0 ||
+      listen(ls, 128) != 0) {
+    fprintf(stderr, "bind %s:%d: %s\n", cfg.bind.c_str(), cfg.port, strerror(errno));
+    return 1;
+  }
+  socklen_t sl = sizeof sa;
+  getsockname(ls, (struct sockaddr*)&sa, &sl);
+  printf("{\"event\": \"listening\", \"port\": %d}\n", ntohs(sa.sin_port));
+  fflush(stdout);
+  for (;;) {
+    int fd = accept4(ls, nullptr, nullptr, SOCK_CLOEXEC);
+    if (fd < 0) {
+      if (errno == EINTR || errno == ECONNABORTED) continue;
+      break;
+    }
+    std::thread(serve_client, &db, fd).detach();
+  }
+  return 0;
+}

@@ -1,0 +1,134 @@
+"""The loopback server (lsmck_server; src/server.rs, src/command.rs) driving the
+checksum path end to end: start-up verifies the tree and replays the WAL on the
+GPU (Db::load), inserts append CRC-framed WAL records (lsmck_crc32_ieee),
+memtable flushes write SSTables with checksum files, and after a SIGKILL the
+restart replays the log into the same state.  The WAL the server wrote is
+replayed by the oracle (oracle/lsmck_oracle.c, wal.rs semantics) as the
+reference; the server's own replay must agree with it."""
+import os
+import shutil
+
+import numpy as np
+import pytest
+
+from lsm_storage_engine_amd import tree
+from lsm_storage_engine_amd.server import Client, Server, ServerExited
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_state(base):
+    """The memtable the reference's MemTable::from_log builds from the server's
+    WAL (memtable.rs:28-47), from the oracle's replay."""
+    img = open(os.path.join(base, "wal", "wal.log"), "rb").read()
+    st, recs, _ = O.wal_replay(img)
+    assert st == 0
+    mem = {}
+    for r in recs:
+        p = img[r.payload_off:r.payload_off + ((r.klen + r.vlen) & 0xFFFFFFFF)]
+        if r.type == 1:
+            mem[p[:r.klen]] = p[r.klen:]
+        else:
+            mem.pop(p, None)
+    return len(recs), mem
+
+
+def test_insert_kill_restart_replay(tmp_path):
+    base = str(tmp_path / "db")
+    synth = tree.synthesize_tree(base, 2 << 20, wal_records=3000)
+    srv = Server(base, memtable_limit=1 << 16)
+    try:
+        assert srv.loaded["tables"] == synth["tables"]
+        assert srv.loaded["wal_records"] == 3000
+        n_wal0, mem0 = _oracle_state(base)
+        assert srv.loaded["memtable_entries"] == len(mem0)
+        c = srv.client()
+        rng = np.random.default_rng(3)
+        model = {k: v for k, v in mem0.items()}
+        cmds, want = [], []
+        for i in range(4000):
+            k = b"k%05d" % int(rng.integers(0, 1500))
+            if i % 7 == 3:
+                cmds.append(b"delete " + k)
+                want.append(b"ok")
+                model[k] = None
+            else:
+                v = b"v%d_%d" % (i, int(rng.integers(0, 1 << 30)))
+                cmds.append((b"update " if i % 5 == 0 else b"insert ") + k + b" " + v)
+                want.append(b"ok")
+                model[k] = v
+        assert c.pipeline(cmds) == want
+        # reads: memtable, the table being flushed, level-0 tables (flushes ran)
+        keys = sorted(k for k in model if len(k) == 6 and k[:1] == b"k" and k[1:].isdigit())  # the traffic's keys
+        got = c.pipeline([b"get " + k for k in keys])
+        exp = [model[k] if model[k] is not None else k + b" not found" for k in keys]
+        assert got == exp
+        # (the synthesized tables hold binary values, which can contain the
+        # protocol's newline -- as in the reference; the traffic's own keys,
+        # flushed to level-0 tables, exercise the table read path)
+        assert c.call(b"get", b"nosuchkey") == b"nosuchkey not found"
+        assert c.call(b"frobnicate") == b"Supported commands: get, insert, update, delete"
+        assert c.call(b"") == b"Supported commands: get, insert, update, delete"
+        c.close()
+        srv.kill()  # crash: no clean shutdown
+        n_wal, mem = _oracle_state(base)
+        srv = Server(base, memtable_limit=1 << 16)
+        assert srv.loaded["wal_records"] == n_wal
+        assert srv.loaded["memtable_entries"] == len(mem)
+        assert srv.loaded["tables"] > synth["tables"]  # the flushed memtables are tables of the tree now
+        assert len(mem) < len(model)  # so some reads below come from tables, not the replayed log
+        c = srv.client()
+        got = c.pipeline([b"get " + k for k in keys])
+        assert got == exp
+        # a missing argument ends the connection (the reference's task panics)
+        c2 = srv.client()
+        with pytest.raises(ConnectionError):
+            c2.call(b"get")
+        c.close()
+    finally:
+        srv.kill()
+
+
+def test_start_refuses_corrupt_tree_and_wal(tmp_path):
+    base = str(tmp_path / "db")
+    tree.synthesize_tree(base, 1 << 20, wal_records=500)
+    metas = tree.list_tables(base)
+    m = metas[len(metas) // 2]
+    shutil.copy(m.data_path(), str(tmp_path / "saved"))
+    with open(m.data_path(), "r+b") as f:
+        f.seek(10)
+        b = f.read(1)
+        f.seek(10)
+        f.write(bytes([b[0] ^ 0x20]))
+    with pytest.raises(ServerExited) as ei:
+        Server(base)
+    assert ei.value.rc == 101 and "Checksum is not correct" in ei.value.stderr
+    shutil.copy(str(tmp_path / "saved"), m.data_path())
+    # a bad Insert payload CRC: MemTable::from_log(..).expect panics
+    wal = os.path.join(base, "wal", "wal.log")
+    img = bytearray(open(wal, "rb").read())
+    st, recs, _ = O.wal_replay(bytes(img))
+    r = next(r for r in recs if r.type == 1 and r.klen + r.vlen > 0)
+    img[r.payload_off] ^= 1
+    open(wal, "wb").write(bytes(img))
+    with pytest.raises(ServerExited) as ei:
+        Server(base)
+    assert ei.value.rc == 101 and "CorruptedData" in ei.value.stderr
+
+
+def test_client_protocol_edges(tmp_path):
+    base = str(tmp_path / "db")
+    srv = Server(base)
+    try:
+        c = srv.client()
+        assert c.call(b"insert", b"a", b"\xc3\xa9t\xe9") == b"ok"  # value bytes from the wire
+        assert c.call(b"get", b"a") == "ét�".encode()  # String::from_utf8_lossy
+        assert c.call(b"insert  b\t c  extra") == b"ok"  # split_whitespace; extra args ignored
+        assert c.call(b"get", b"b") == b"c"
+        assert c.call(b"delete", b"b") == b"ok"
+        assert c.call(b"get", b"b") == b"b not found"
+        c.close()
+        assert Client(srv.port).call(b"get", b"a") == "ét�".encode()
+    finally:
+        srv.kill()
