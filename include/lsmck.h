@@ -188,6 +188,9 @@ int lsmck_device_count(void);
  *                 files in flight (0 = 8192) and bytes of a file per round
  *                 (0 = 128 KiB; a multiple of 64).  Tests use small values.
  *   "tree_list_threads"  lsmck_tree_verify's metadata parsing threads (0 = 8).
+ *   "tree_cpu_file_bytes"  whole-tree verify: files of at least this many
+ *                 bytes are hashed on 4 host threads (SHA-NI where present)
+ *                 instead of a GPU lane (0 = 16 MiB).
  *   "wal_prefetch"  bytes lsmck_wal_replay_verify's header walk prefetches
  *                 ahead of its position (default 4096; 0 = off).  A/B switch.
  *   "stage_threads"  host-memory batches: threads that copy a pageable chunk
@@ -262,10 +265,12 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
 
 /* Whole-tree SSTable verify: the batch form of Checksums::verify over many
  * tables (Db::load, src/tokio/db.rs:37-59 -> src/tokio/sstable.rs:34).
- * Streams every data/index file in slices: 8192 files in flight, 128 KiB of
- * each per round, 16 reader threads filling one pinned slot while the GPU
- * hashes the previous round (per-file SHA-256 state carried on the device),
- * then compares with each checksum file.  status[i] gets table i's
+ * Streams every data/index file in slices: 8192 files in flight (largest
+ * first), 128 KiB of each per round, 16 reader threads filling one pinned slot
+ * while the GPU hashes the previous round (per-file SHA-256 state carried on
+ * the device), then compares with each checksum file.  Files of 16 MiB and
+ * more are hashed on host threads meanwhile (one file is one sequential
+ * SHA-256: a GPU lane would take ~1 s per 16 MB).  status[i] gets table i's
  * lsmck_checksums_verify status (0, the LSMCK_PANIC_OPEN_* codes,
  * LSMCK_DATA_MISMATCH / LSMCK_INDEX_MISMATCH, -errno, LSMCK_EJSON; -EAGAIN: a
  * file shrank while it was read).  Returns the number of tables whose status

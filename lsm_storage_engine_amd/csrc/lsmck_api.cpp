@@ -199,6 +199,7 @@ struct lsmck_ctx {
   uint32_t tree_active = 0;  // whole-tree verify: files in flight (0 = kTreeActive)
   uint32_t tree_slice = 0;   // whole-tree verify: bytes of a file per round (0 = kTreeSlice)
   long tree_open = -1;       // whole-tree verify: files kept open between slices (-1 = RLIMIT_NOFILE budget)
+  uint64_t tree_cpu_file = 0;  // whole-tree verify: files of at least this many bytes go to host threads (0 = 16 MiB)
   int sha_bucket_shift = 2;  // SHA order key: 2^shift-block buckets for from..1023 blocks (0 = exact; A/B: DESIGN.md 3.2)
   int sha_bucket_from = 128;
   unsigned tree_list_threads = 0;  // lsmck_tree_verify: metadata parsing threads (0 = kListThreads)
@@ -728,6 +729,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->tree_open = value;
     return 0;
   }
+  if (!strcmp(key, "tree_cpu_file_bytes")) {  // whole-tree verify: host-thread SHA-256 for files >= this (0 = 16 MiB)
+    if (value < 0) return lsmck_host::set_error(LSMCK_EINVAL, "tree_cpu_file_bytes: >= 0");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->tree_cpu_file = (uint64_t)value;
+    return 0;
+  }
   if (!strcmp(key, "tree_list_threads")) {  // A/B: metadata parsing threads of lsmck_tree_verify (0 = 8)
     if (value < 0 || value > 256) return lsmck_host::set_error(LSMCK_EINVAL, "tree_list_threads: 0..256");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1104,6 +1111,8 @@ constexpr uint32_t kTreeActive = 8192;        // files in flight
 constexpr uint32_t kTreeSlice = 128u << 10;   // bytes of a file per round (multiple of 64; A/B: DESIGN.md 7a)
 constexpr unsigned kTreeReaders = 16;  // the GPU box gives a process 16 CPUs
 constexpr unsigned kListThreads = 8;   // lsmck_tree_verify's metadata parsing (A/B: DESIGN.md 7a)
+constexpr uint64_t kTreeCpuFile = 16ull << 20;  // files this large are hashed on host threads, not a GPU lane
+constexpr unsigned kTreeCpuThreads = 4;
 
 // pread exactly n bytes at offset off of fd into dst
 int pread_fd(int fd, uint8_t* dst, uint64_t off, uint64_t n) {
@@ -1251,6 +1260,54 @@ static int verify_tables(lsmck_ctx* ctx, const char* const* data_paths, const ch
   const uint32_t active_max = ctx->tree_active ? ctx->tree_active : kTreeActive;
   const uint32_t slice = ctx->tree_slice ? ctx->tree_slice : kTreeSlice;
   std::vector<uint8_t> dig(32 * std::max<size_t>(nf, 1), 0);
+  // Large files are hashed on host threads (SHA-NI where the CPU has it,
+  // ~1.5-2 GB/s per thread) while the GPU streams the rest: SHA-256 is
+  // sequential inside a file, so one file is one GPU lane at ~16 MB/s -- a
+  // 230 MB table alone would hold the stream open for 14 s.  The GPU admits
+  // the remaining files largest first, so no large file starts at the tail.
+  const uint64_t cpu_min = ctx->tree_cpu_file ? ctx->tree_cpu_file : kTreeCpuFile;
+  std::vector<size_t> gpu_order, cpu_files;
+  for (size_t f = 0; f < nf; ++f) {
+    if (ferr[f]) continue;
+    (fsize[f] >= cpu_min ? cpu_files : gpu_order).push_back(f);
+  }
+  std::stable_sort(gpu_order.begin(), gpu_order.end(), [&](size_t a, size_t b) { return fsize[a] > fsize[b]; });
+  std::atomic<size_t> cpu_next{0};
+  struct CpuJoiner {
+    std::vector<std::thread> t;
+    ~CpuJoiner() {
+      for (auto& x : t)
+        if (x.joinable()) x.join();
+    }
+  } cpu_th;
+  for (unsigned t = 0; t < std::min<size_t>(kTreeCpuThreads, cpu_files.size()); ++t)
+    cpu_th.t.emplace_back([&]() {
+      std::vector<uint8_t> buf(1u << 20);
+      for (size_t j; (j = cpu_next.fetch_add(1)) < cpu_files.size();) {
+        const size_t f = cpu_files[j];
+        int fd = open(paths[f], O_RDONLY | O_CLOEXEC);
+        if (fd < 0) {
+          ferr[f] = open_panic(f);
+          continue;
+        }
+        lsmck_sha256_ctx c;
+        lsmck_sha256_init(&c);
+        uint64_t off = 0;
+        for (;;) {
+          ssize_t k = pread(fd, buf.data(), buf.size(), (off_t)off);
+          if (k < 0 && errno == EINTR) continue;
+          if (k < 0) {
+            ferr[f] = -errno;
+            break;
+          }
+          if (k == 0) break;
+          lsmck_sha256_update(&c, buf.data(), (size_t)k);
+          off += (uint64_t)k;
+        }
+        close(fd);
+        if (!ferr[f]) lsmck_sha256_final(&c, &dig[32 * f]);
+      }
+    });
   {
     std::lock_guard<std::mutex> lk(ctx->mu);
     DevGuard g(ctx->dev);
@@ -1274,8 +1331,8 @@ static int verify_tables(lsmck_ctx* ctx, const char* const* data_paths, const ch
     tm->fds_cached = fds.cached;
     for (;;) {
       // admit files into free slots
-      while (!free_slots.empty() && next_file < nf) {
-        const size_t f = next_file++;
+      while (!free_slots.empty() && next_file < gpu_order.size()) {
+        const size_t f = gpu_order[next_file++];
         if (ferr[f]) continue;
         const uint32_t k = free_slots.back();
         free_slots.pop_back();
@@ -1366,11 +1423,17 @@ static int verify_tables(lsmck_ctx* ctx, const char* const* data_paths, const ch
     clk.lap();
     for (int k = 0; k < 2; ++k)
       if (busy[k]) HIPCHK(hipEventSynchronize(ctx->stage[k].done));
-    if (nf) HIPCHK(hipMemcpy(dig.data(), T.digests, 32 * nf, hipMemcpyDeviceToHost));
+    if (nf) {  // the GPU's digests land at their files' slots; the CPU threads write theirs in place
+      std::vector<uint8_t> gd(32 * nf);
+      HIPCHK(hipMemcpy(gd.data(), T.digests, 32 * nf, hipMemcpyDeviceToHost));
+      for (size_t f : gpu_order) memcpy(&dig[32 * f], &gd[32 * f], 32);
+    }
     tm->wait += clk.lap();
   }
   for (auto& x : want_th.t) x.join();
   want_th.t.clear();
+  for (auto& x : cpu_th.t) x.join();
+  cpu_th.t.clear();
   host_parallel(n, [&](size_t i) {
     status[i] = ferr[2 * i] ? ferr[2 * i] : ferr[2 * i + 1];
     if (status[i] == 0) {

@@ -187,3 +187,39 @@ def test_tree_verify_empty_and_missing_files(ctx, tmp_path):
     st = ctx.checksums_verify_many([(m.data_path(), m.index_path(), m.checksum_path()),
                                     (m.data_path() + "x", m.index_path(), m.checksum_path())])
     assert st == [_lib.PANIC_OPEN_CHECKSUM, _lib.PANIC_OPEN_FILE]
+
+
+@pytest.mark.gpu
+def test_tree_verify_large_files_on_host_threads(ctx, tmp_path):
+    """Files at or above tree_cpu_file_bytes are hashed on host threads while
+    the GPU streams the rest: same verdicts (clean, data mismatch, index
+    mismatch, missing file) whichever side hashes a file."""
+    base = str(tmp_path / "big")
+    tree.synthesize_tree(base, 6 << 20, wal_records=10)
+    metas = tree.list_tables(base)
+    trip = [(m.data_path(), m.index_path(), m.checksum_path()) for m in metas]
+    sizes = sorted(os.path.getsize(m.data_path()) for m in metas)
+    try:
+        for cut in (0, sizes[len(sizes) // 2], 1):  # default (all GPU), half and half, all on host threads
+            ctx.set_option("tree_cpu_file_bytes", cut)
+            assert ctx.checksums_verify_many(trip) == [0] * len(trip)
+            big = max(range(len(metas)), key=lambda i: os.path.getsize(metas[i].data_path()))
+            small = min(range(len(metas)), key=lambda i: os.path.getsize(metas[i].data_path()))
+            saved = {}
+            for i, which in ((big, 0), (small, 1)):
+                p = trip[i][which]
+                saved[p] = open(p, "rb").read()
+                b = bytearray(saved[p])
+                b[len(b) // 2] ^= 4
+                open(p, "wb").write(bytes(b))
+            st = ctx.checksums_verify_many(trip)
+            assert st[big] == _lib.DATA_MISMATCH and st[small] == _lib.INDEX_MISMATCH
+            assert sum(x != 0 for x in st) == 2
+            for p, b in saved.items():
+                open(p, "wb").write(b)
+            os.rename(trip[big][0], trip[big][0] + ".gone")
+            st = ctx.checksums_verify_many(trip)
+            assert st[big] == _lib.PANIC_OPEN_FILE and sum(x != 0 for x in st) == 1
+            os.rename(trip[big][0] + ".gone", trip[big][0])
+    finally:
+        ctx.set_option("tree_cpu_file_bytes", 0)
