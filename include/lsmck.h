@@ -312,6 +312,16 @@ typedef struct {
 } lsmck_tree_report;
 int lsmck_tree_verify(lsmck_ctx* ctx, const char* base, lsmck_tree_report* rep);
 
+/* The same over several devices of one node: the tables are split
+ * into contiguous runs balanced by bytes, one per context (one host thread,
+ * one set of pinned slots and one PCIe link each), verified concurrently; no
+ * data moves between devices.  Statuses and the report are those of the
+ * single-context call (timings: the slowest device's). */
+int lsmck_tree_verify_multi(lsmck_ctx* const* ctxs, size_t nctx, const char* base, lsmck_tree_report* rep);
+int lsmck_checksums_verify_many_multi(lsmck_ctx* const* ctxs, size_t nctx, const char* const* data_paths,
+                                      const char* const* index_paths, const char* const* checksum_paths, size_t n,
+                                      int* status);
+
 /* ======================================================================== */
 /* 4. Plumbing for hosts without their own HIP bindings (tests, bench)        */
 /* ======================================================================== */

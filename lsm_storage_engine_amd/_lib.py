@@ -93,6 +93,10 @@ SIGNATURES = [
     ("lsmck_checksums_verify_many", C.c_int,
      [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), sz, C.POINTER(C.c_int)]),
     ("lsmck_tree_verify", C.c_int, [vp, C.c_char_p, C.POINTER(TreeReport)]),
+    ("lsmck_tree_verify_multi", C.c_int, [C.POINTER(vp), sz, C.c_char_p, C.POINTER(TreeReport)]),
+    ("lsmck_checksums_verify_many_multi", C.c_int,
+     [C.POINTER(vp), sz, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), sz,
+      C.POINTER(C.c_int)]),
     ("lsmck_dev_alloc", vp, [vp, sz]),
     ("lsmck_dev_free", None, [vp, vp]),
     ("lsmck_host_alloc_pinned", vp, [vp, sz]),

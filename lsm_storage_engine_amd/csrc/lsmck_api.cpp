@@ -1457,6 +1457,77 @@ int lsmck_checksums_verify_many(lsmck_ctx* ctx, const char* const* data_paths, c
   return verify_tables(ctx, data_paths, index_paths, checksum_paths, n, status, nullptr);
 }
 
+}  // extern "C"
+
+// The tables split over several devices (one host thread, one
+// context and one set of pinned slots per device, no data exchange): contiguous
+// runs of tables balanced by bytes, each verified by its own context in its
+// own thread, so every device's PCIe link streams its share.  Statuses land in
+// place; the timing fields are the slowest device's, byte and round counts sum.
+static int verify_tables_multi(lsmck_ctx* const* ctxs, size_t nctx, const char* const* data_paths,
+                               const char* const* index_paths, const char* const* checksum_paths, size_t n,
+                               int* status, TreeTiming* tm) {
+  if (!ctxs || nctx == 0) return lsmck_host::set_error(LSMCK_EINVAL, "no contexts");
+  for (size_t k = 0; k < nctx; ++k)
+    if (!ctxs[k]) return lsmck_host::set_error(LSMCK_EINVAL, "null context");
+  if (nctx == 1 || n < 2) return verify_tables(ctxs[0], data_paths, index_paths, checksum_paths, n, status, tm);
+  std::vector<uint64_t> bytes(n, 0);
+  host_parallel(n, [&](size_t i) {
+    struct stat st;
+    if (stat(data_paths[i], &st) == 0) bytes[i] += (uint64_t)st.st_size;
+    if (stat(index_paths[i], &st) == 0) bytes[i] += (uint64_t)st.st_size;
+  });
+  uint64_t total = 0;
+  for (uint64_t b : bytes) total += b;
+  std::vector<size_t> cut(nctx + 1, n);
+  cut[0] = 0;
+  uint64_t acc = 0;
+  size_t k = 1;
+  for (size_t i = 0; i < n && k < nctx; ++i) {
+    acc += bytes[i];
+    while (k < nctx && acc * nctx >= total * k) cut[k++] = i + 1;
+  }
+  std::vector<int> rc(nctx, 0);
+  std::vector<TreeTiming> tms(nctx);
+  std::vector<std::string> errs(nctx);
+  std::vector<std::thread> th;
+  for (size_t j = 0; j < nctx; ++j)
+    th.emplace_back([&, j]() {
+      const size_t a = cut[j], b = cut[j + 1];
+      if (a >= b) return;
+      rc[j] = verify_tables(ctxs[j], data_paths + a, index_paths + a, checksum_paths + a, b - a, status + a, &tms[j]);
+      if (rc[j] < 0) errs[j] = lsmck_last_error();  // thread-local: carry it back
+    });
+  for (auto& t : th) t.join();
+  int bad = 0;
+  for (size_t j = 0; j < nctx; ++j) {
+    if (rc[j] < 0) return lsmck_host::set_error(rc[j], errs[j].c_str());
+    bad += rc[j];
+  }
+  if (tm) {
+    for (auto& x : tms) {
+      tm->stat = std::max(tm->stat, x.stat);
+      tm->read = std::max(tm->read, x.read);
+      tm->wait = std::max(tm->wait, x.wait);
+      tm->compare = std::max(tm->compare, x.compare);
+      tm->rounds += x.rounds;
+      tm->bytes += x.bytes;
+      tm->fds_cached += x.fds_cached;
+    }
+  }
+  return bad;
+}
+
+extern "C" {
+
+int lsmck_checksums_verify_many_multi(lsmck_ctx* const* ctxs, size_t nctx, const char* const* data_paths,
+                                      const char* const* index_paths, const char* const* checksum_paths, size_t n,
+                                      int* status) {
+  if (n && (!data_paths || !index_paths || !checksum_paths || !status))
+    return lsmck_host::set_error(LSMCK_EINVAL, "null path array or status");
+  return verify_tables_multi(ctxs, nctx, data_paths, index_paths, checksum_paths, n, status, nullptr);
+}
+
 // ---------------------------------------------------------------------------
 // Db::load's table scan (src/tokio/db.rs:37-59) in native code: per level
 // create_dir_all + read_dir, every entry whose (UTF-8) name contains
@@ -1504,9 +1575,26 @@ int mkdir_p(const std::string& path) {  // fs::create_dir_all
 
 }  // namespace
 
+static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* base, lsmck_tree_report* rep);
+
 int lsmck_tree_verify(lsmck_ctx* ctx, const char* base, lsmck_tree_report* rep) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
+  return tree_verify_impl(&ctx, 1, base, rep);
+}
+
+int lsmck_tree_verify_multi(lsmck_ctx* const* ctxs, size_t nctx, const char* base, lsmck_tree_report* rep) {
+  if (!ctxs || nctx == 0) return lsmck_host::set_error(LSMCK_EINVAL, "no contexts");
+  for (size_t k = 0; k < nctx; ++k)
+    if (!ctxs[k]) return lsmck_host::set_error(LSMCK_EINVAL, "null context");
+  return tree_verify_impl(ctxs, nctx, base, rep);
+}
+
+}  // extern "C"
+
+static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* base, lsmck_tree_report* rep) {
+  lsmck_ctx* ctx = ctxs[0];
+  int rc = 0;
   if (!base || !rep) return lsmck_host::set_error(LSMCK_EINVAL, "null base path or report");
   memset(rep, 0, sizeof *rep);
   rep->first_index = UINT64_MAX;
@@ -1561,7 +1649,7 @@ int lsmck_tree_verify(lsmck_ctx* ctx, const char* base, lsmck_tree_report* rep) 
   for (size_t j = 0; j < m; ++j) dpp[j] = dp[j].c_str(), ipp[j] = ip[j].c_str(), cpp[j] = cp[j].c_str();
   std::vector<int> vst(std::max<size_t>(m, 1), 0);
   TreeTiming tm;
-  rc = verify_tables(ctx, dpp.data(), ipp.data(), cpp.data(), m, vst.data(), &tm);
+  rc = verify_tables_multi(ctxs, nctx, dpp.data(), ipp.data(), cpp.data(), m, vst.data(), &tm);
   if (rc < 0) return rc;
   rep->table_bytes = tm.bytes;
   rep->rounds = tm.rounds;
@@ -1582,6 +1670,8 @@ int lsmck_tree_verify(lsmck_ctx* ctx, const char* base, lsmck_tree_report* rep) 
   }
   return rep->bad_tables ? 1 : 0;
 }
+
+extern "C" {
 
 // ---------------------------------------------------------------------------
 void* lsmck_dev_alloc(lsmck_ctx* ctx, size_t bytes) {

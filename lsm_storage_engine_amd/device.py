@@ -237,14 +237,26 @@ class Context:
         first failing table in load order, or are None)."""
         rep = _lib.TreeReport()
         rc = _lib.check(self.lib.lsmck_tree_verify(self.handle, str(base).encode(), C.byref(rep)), "tree_verify")
-        bad = rc != 0
-        return {"tables": rep.tables, "table_bytes": rep.table_bytes, "bad_tables": rep.bad_tables,
-                "first_index": rep.first_index if bad else None, "first_status": rep.first_status if bad else None,
-                "first_metadata_path": rep.first_metadata_path.decode(errors="surrogateescape") if bad else None,
-                "list_seconds": rep.list_seconds, "verify_seconds": rep.verify_seconds,
-                "stat_seconds": rep.stat_seconds, "read_seconds": rep.read_seconds,
-                "gpu_wait_seconds": rep.gpu_wait_seconds, "compare_seconds": rep.compare_seconds,
-                "rounds": rep.rounds, "fds_cached": rep.fds_cached}
+        return _tree_report(rep, rc)
+
+
+def _tree_report(rep, rc):
+    """lsmck_tree_report as a dict (first_* are None when every table verified)."""
+    bad = rc != 0
+    return {"tables": rep.tables, "table_bytes": rep.table_bytes, "bad_tables": rep.bad_tables,
+            "first_index": rep.first_index if bad else None, "first_status": rep.first_status if bad else None,
+            "first_metadata_path": rep.first_metadata_path.decode(errors="surrogateescape") if bad else None,
+            "list_seconds": rep.list_seconds, "verify_seconds": rep.verify_seconds,
+            "stat_seconds": rep.stat_seconds, "read_seconds": rep.read_seconds,
+            "gpu_wait_seconds": rep.gpu_wait_seconds, "compare_seconds": rep.compare_seconds,
+            "rounds": rep.rounds, "fds_cached": rep.fds_cached}
+
+
+def _path_arrays(triples):
+    n = len(triples)
+    arr = C.c_char_p * max(n, 1)
+    return (arr(*[str(t[0]).encode() for t in triples]), arr(*[str(t[1]).encode() for t in triples]),
+            arr(*[str(t[2]).encode() for t in triples]))
 
 
 class MultiContext:
@@ -304,6 +316,30 @@ class MultiContext:
 
     def sha256_fixed(self, data, stride, length, n):
         return self._fixed(data, stride, length, n, 32, Context.sha256_fixed)
+
+    # --- SSTable verify over every device's PCIe link (lsmck_*_multi) ---------
+    def _handles(self):
+        return (C.c_void_p * len(self.ctxs))(*[c.handle for c in self.ctxs])
+
+    def checksums_verify_many(self, triples):
+        n = len(triples)
+        d, i, c = _path_arrays(triples)
+        status = (C.c_int * max(n, 1))()
+        lib = _lib.load()
+        _lib.check(lib.lsmck_checksums_verify_many_multi(self._handles(), len(self.ctxs), d, i, c, n, status),
+                   "checksums_verify_many_multi")
+        return list(status[:n])
+
+    def tree_verify(self, base):
+        rep = _lib.TreeReport()
+        lib = _lib.load()
+        rc = _lib.check(lib.lsmck_tree_verify_multi(self._handles(), len(self.ctxs), str(base).encode(),
+                                                    C.byref(rep)), "tree_verify_multi")
+        return _tree_report(rep, rc)
+
+    def wal_replay_verify(self, image, device_ptr=None):
+        """The WAL is one log: replayed on the first device."""
+        return self.ctxs[0].wal_replay_verify(image, device_ptr)
 
 
 # include/lsmck.h lsmck_wal_rec (32 bytes, no padding)

@@ -223,3 +223,33 @@ def test_tree_verify_large_files_on_host_threads(ctx, tmp_path):
             os.rename(trip[big][0] + ".gone", trip[big][0])
     finally:
         ctx.set_option("tree_cpu_file_bytes", 0)
+
+
+@pytest.mark.gpu
+def test_multicontext_tree_verify(ctx, tmp_path):
+    """lsmck_tree_verify_multi / lsmck_checksums_verify_many_multi: the tables
+    split by bytes over three contexts (all on this box's one GPU; on a node,
+    one per device and PCIe link) give the single-context verdicts."""
+    from lsm_storage_engine_amd.device import MultiContext
+    base = str(tmp_path / "multi")
+    tree.synthesize_tree(base, 6 << 20, wal_records=200)
+    mc = MultiContext(devices=[0, 0, 0])
+    try:
+        mem1, r1 = tree.load_verify(ctx, base)
+        mem3, r3 = tree.load_verify(mc, base)
+        assert mem1.data == mem3.data and r1["tables"] == r3["tables"] and r1["table_bytes"] == r3["table_bytes"]
+        metas = tree.list_tables(base)
+        trip = [(m.data_path(), m.index_path(), m.checksum_path()) for m in metas]
+        for i, which in ((1, 0), (len(metas) // 2, 1), (len(metas) - 2, 0)):
+            p = trip[i][which]
+            b = bytearray(open(p, "rb").read())
+            b[3] ^= 1
+            open(p, "wb").write(bytes(b))
+        assert mc.checksums_verify_many(trip) == ctx.checksums_verify_many(trip)
+        assert sum(x != 0 for x in mc.checksums_verify_many(trip)) == 3
+        a, b = ctx.tree_verify(base), mc.tree_verify(base)
+        for k in ("tables", "table_bytes", "bad_tables", "first_index", "first_status", "first_metadata_path"):
+            assert a[k] == b[k], k
+    finally:
+        for c in mc.ctxs:
+            c.close()
