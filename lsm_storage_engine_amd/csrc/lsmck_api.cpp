@@ -188,6 +188,27 @@ struct lsmck_ctx {
   size_t cap_wlen = 0;
   uint32_t* d_wexp = nullptr;
   size_t cap_wexp = 0;
+  // device WAL walk (lsmck_wal.hip): candidate bitmap, ranks, successor levels, chain
+  struct {
+    uint64_t* bits = nullptr;
+    size_t cap_bits = 0;
+    uint32_t* pre = nullptr;
+    size_t cap_pre = 0;
+    uint32_t* bsum = nullptr;
+    size_t cap_bsum = 0;
+    uint64_t* pos = nullptr;
+    size_t cap_pos = 0;
+    uint32_t* J = nullptr;
+    size_t cap_J = 0;
+    uint64_t* badpos = nullptr;
+    size_t cap_badpos = 0;
+    uint32_t* chain = nullptr;
+    size_t cap_chain = 0;
+    lsmck_wal_rec* recs = nullptr;
+    size_t cap_recs = 0;
+    unsigned long long* info = nullptr;  // [records, terminal, bad position, candidates (u32 at info+3)]
+    unsigned long long* h_info = nullptr;  // pinned
+  } wd;
   uint64_t* h_woff = nullptr;  // pinned staging of the same
   size_t cap_hwoff = 0;
   uint32_t* h_wlen = nullptr;
@@ -208,6 +229,7 @@ struct lsmck_ctx {
   size_t wal_host_cap = 0;
   std::mutex wal_mu;  // guards wal_host for the duration of one device-image replay
   size_t wal_chunk = 32u << 20;
+  int wal_gpu_walk = 1;  // lsmck_wal_replay_verify of a device image: header walk on the GPU (0 = copy back, host walk)
   unsigned stage_threads = 8;  // host batches: threads copying a pageable chunk into its pinned slot (1 = memcpy)  // lsmck_wal_replay_verify, host image: payload bytes per overlapped CRC batch (0 = one batch)
   struct {
     uint32_t* state = nullptr;  // 8 u32 per active slot
@@ -753,6 +775,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->wal_chunk = (size_t)value;
     return 0;
   }
+  if (!strcmp(key, "wal_gpu_walk")) {  // A/B: device-image WAL replay, 1 = GPU header walk (default), 0 = host walk
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "wal_gpu_walk must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_gpu_walk = (int)value;
+    return 0;
+  }
   if (!strcmp(key, "wal_prefetch")) {  // A/B: bytes the WAL header walk prefetches ahead (0 = off)
     if (value < 0 || value > (1l << 24)) return lsmck_host::set_error(LSMCK_EINVAL, "wal_prefetch: 0..16 MiB");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -814,6 +842,10 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   if (ctx->d_zero) (void)hipFree(ctx->d_zero);
   if (ctx->d_verify) (void)hipFree(ctx->d_verify);
   if (ctx->d_work) (void)hipFree(ctx->d_work);
+  for (void* p : {(void*)ctx->wd.bits, (void*)ctx->wd.pre, (void*)ctx->wd.bsum, (void*)ctx->wd.pos, (void*)ctx->wd.J,
+                  (void*)ctx->wd.badpos, (void*)ctx->wd.chain, (void*)ctx->wd.recs, (void*)ctx->wd.info})
+    if (p) (void)hipFree(p);
+  if (ctx->wd.h_info) (void)hipHostFree(ctx->wd.h_info);
   for (void* p : {(void*)ctx->d_vcrc, (void*)ctx->d_woff, (void*)ctx->d_wlen, (void*)ctx->d_wexp})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)ctx->h_woff, (void*)ctx->h_wlen, (void*)ctx->h_wexp})
@@ -921,10 +953,91 @@ static uint32_t rd_u32(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
+}  // extern "C"
+
+// WAL replay of a device-resident image with the header walk on the GPU
+// (lsmck_wal.hip): nothing of the image comes back to the host, only the
+// accepted records (32 B each) and a few counters.
+static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck_wal_rec* recs, size_t cap,
+                             size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected) {
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DevGuard g(ctx->dev);
+  auto& W = ctx->wd;
+  int rc;
+  const size_t nw = (size_t)lsmk_wal_words(n), nb = (size_t)lsmk_wal_scan_blocks(n);
+  if ((rc = ensure_dev(&W.bits, &W.cap_bits, std::max<size_t>(nw, 1))) ||
+      (rc = ensure_dev(&W.pre, &W.cap_pre, std::max<size_t>(nw, 1))) ||
+      (rc = ensure_dev(&W.bsum, &W.cap_bsum, nb + 1)))
+    return rc;
+  if (!W.info) HIPCHK(hipMalloc((void**)&W.info, 64));
+  if (!W.h_info) HIPCHK(hipHostMalloc((void**)&W.h_info, 64, hipHostMallocDefault));
+  ScratchOrder so(ctx, ctx->stream0);
+  if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
+  hipStream_t st = so.st;
+  uint32_t* d_total = (uint32_t*)(W.info + 3);
+  HIPCHK(hipMemsetAsync(d_total, 0, 4, st));
+  rc = lsmk_wal_mark(img, n, W.bits, W.pre, W.bsum, d_total, st);
+  if (rc) return launch_rc(rc, "wal mark/scan kernels");
+  HIPCHK(hipMemcpyAsync(W.h_info + 3, d_total, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint32_t nc = (uint32_t)(W.h_info[3] & 0xFFFFFFFFull);
+  int levels = 0;
+  while (levels < 32 && (1ull << levels) <= nc) ++levels;  // 2^levels > nc
+  if ((rc = ensure_dev(&W.pos, &W.cap_pos, std::max<size_t>(nc, 1))) ||
+      (rc = ensure_dev(&W.J, &W.cap_J, std::max<size_t>((size_t)levels * nc, 1))) ||
+      (rc = ensure_dev(&W.badpos, &W.cap_badpos, std::max<size_t>(nc, 1))) ||
+      (rc = ensure_dev(&W.chain, &W.cap_chain, (size_t)1 << levels)))
+    return rc;
+  rc = lsmk_wal_chain(img, n, W.bits, W.pre, nc, levels, W.pos, W.J, W.badpos, W.chain, W.info, st);
+  if (rc) return launch_rc(rc, "wal chain kernels");
+  HIPCHK(hipMemcpyAsync(W.h_info, W.info, 24, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const size_t m = (size_t)W.h_info[0];
+  const uint32_t term = (uint32_t)W.h_info[1];
+  const uint64_t badq = W.h_info[2];
+  // records -> lsmck_wal_rec, payload descriptors, stored CRCs; one CRC batch + compare
+  uint64_t nbad = 0, first = m;
+  if (m) {
+    if ((rc = ensure_dev(&W.recs, &W.cap_recs, m)) || (rc = ensure_dev(&ctx->d_woff, &ctx->cap_woff, m)) ||
+        (rc = ensure_dev(&ctx->d_wlen, &ctx->cap_wlen, m)) || (rc = ensure_dev(&ctx->d_wexp, &ctx->cap_wexp, m)))
+      return rc;
+    rc = lsmk_wal_emit(img, n, W.chain, W.pos, W.info, (uint32_t)m, W.recs, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st);
+    if (rc) return launch_rc(rc, "wal emit kernel");
+    rc = device_verify(ctx, img, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, m, st, &nbad, &first);
+    if (rc < 0) return rc;
+  }
+  const size_t accepted = nbad ? (size_t)first : m;
+  if (recs && accepted) HIPCHK(hipMemcpy(recs, W.recs, std::min(accepted, cap) * sizeof(lsmck_wal_rec),
+                                         hipMemcpyDeviceToHost));
+  if (nrec) *nrec = accepted;
+  if (nbad) {
+    lsmck_wal_rec r;
+    uint32_t got = 0;
+    HIPCHK(hipMemcpy(&r, W.recs + first, sizeof r, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&got, ctx->d_vcrc + first, 4, hipMemcpyDeviceToHost));
+    if (bad_index) *bad_index = first;
+    if (bad_expected) *bad_expected = r.crc;
+    if (bad_crc) *bad_crc = got;
+    return r.type == 1 ? LSMCK_WAL_CORRUPTED : LSMCK_WAL_REMOVE_PANIC;
+  }
+  if (term == 0xFFFFFFFEu) {  // InvalidCommandType at the record after the last one
+    uint8_t t = 0;
+    HIPCHK(hipMemcpy(&t, img + badq, 1, hipMemcpyDeviceToHost));
+    if (bad_index) *bad_index = m;
+    if (bad_crc) *bad_crc = t;
+    return LSMCK_WAL_BAD_TYPE;
+  }
+  return 0;
+}
+
+extern "C" {
+
 int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsigned flags, lsmck_wal_rec* recs,
                             size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
+  if ((flags & LSMCK_DEVICE) && ctx->wal_gpu_walk)
+    return wal_replay_device(ctx, wal, n, recs, cap, nrec, bad_index, bad_crc, bad_expected);
   const uint8_t* h = wal;
   // Device image: the walk reads a host copy, made by DMA into a pinned
   // buffer the context keeps (grow-only).  Copying into fresh pageable memory

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "lsmck.h"
+
 namespace lsmck {
 
 // CRC-32 batch job.  Records are either fixed ([r*stride, r*stride+flen)) or
@@ -70,6 +72,16 @@ int lsmk_launch_sha256(const lsmck::ShaParams* P, hipStream_t st);
 int lsmk_launch_sha256_slices(const lsmck::ShaSliceParams* P, hipStream_t st);
 uint64_t lsmk_walk_sb_count(uint64_t n);
 int lsmk_launch_crc32_walk(const lsmck::CrcParams* P, uint64_t* sb_prefix, int ncu, int variant, hipStream_t st);
+uint64_t lsmk_wal_words(uint64_t n);
+uint64_t lsmk_wal_scan_blocks(uint64_t n);
+int lsmk_wal_mark(const uint8_t* img, uint64_t n, uint64_t* bits, uint32_t* pre, uint32_t* bsum, uint32_t* total,
+                  hipStream_t st);
+int lsmk_wal_chain(const uint8_t* img, uint64_t n, const uint64_t* bits, const uint32_t* pre, uint32_t nc, int levels,
+                   uint64_t* pos, uint32_t* J, uint64_t* badpos, uint32_t* chain, unsigned long long* info,
+                   hipStream_t st);
+int lsmk_wal_emit(const uint8_t* img, uint64_t n, const uint32_t* chain, const uint64_t* pos,
+                  const unsigned long long* info, uint32_t m, lsmck_wal_rec* recs, uint64_t* poff, uint32_t* plen,
+                  uint32_t* pcrc, hipStream_t st);
 int lsmk_launch_crc32_compare(const uint32_t* crc, const uint32_t* expected, uint64_t n,
                                unsigned long long* n_bad, unsigned long long* first_bad, hipStream_t st);
 int lsmk_sha_order(const uint32_t* len, size_t n, uint16_t* keys_out, uint32_t* order, void* tmp, size_t* tmp_bytes,

@@ -1,0 +1,338 @@
+// lsmck_wal.hip -- WAL replay header walk on the GPU (gfx950).
+//
+// The reference reads the log record by record (src/wal.rs:68-84, 122-163):
+// each header's position comes from the previous header's lengths, a serial
+// chain.  Here the chain is found in parallel, without reading the image back
+// to the host:
+//   1. every byte position p whose byte is a command type (1 Insert, 2 Remove)
+//      and whose header fits in the log is a CANDIDATE record start (a bitmap,
+//      one u64 per 64 bytes, and per-word candidate counts);
+//   2. an exclusive scan of the counts ranks the candidates;
+//   3. every candidate gets its successor -- the position after its header and
+//      payload (the payload cut at EOF as read_to_end on take() does) -- as a
+//      candidate rank, or a terminal: clean END (EOF at or inside the next
+//      header) or BAD (the next byte is not a command type, at position q);
+//   4. pointer doubling J_{k+1} = J_k o J_k (terminals absorb) over the
+//      candidates, every level kept;
+//   5. the chain from position 0 is unrolled by doubling too: knowing records
+//      0..L-1, records L..2L-1 are J_k of them (k = log2 L);
+//   6. the chain's records become payload descriptors for the CRC batch
+//      (crc32_walk_kernel) and the GPU compare.
+// Candidates are positions, so bogus ones (type bytes inside payloads) only
+// cost work: a chain that starts at position 0 follows real headers only.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lsmck.h"
+#include "lsmck_device.h"
+
+namespace lsmck {
+
+#define WAL_END 0xFFFFFFFFu  // chain ends cleanly (EOF at or inside the next header)
+#define WAL_BAD 0xFFFFFFFEu  // the next byte is not a command type
+
+__device__ __forceinline__ uint32_t rd32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+__device__ __forceinline__ uint32_t hdr_len(uint8_t t) { return t == 1 ? 13u : 9u; }
+
+// 1. candidate bitmap: thread per 64-byte word of positions (16-byte loads
+// when the image is 16-byte aligned, byte loads otherwise)
+__global__ __launch_bounds__(256) void wal_mark(const uint8_t* __restrict__ img, uint64_t n, int aligned,
+                                                 uint64_t* __restrict__ bits, uint32_t* __restrict__ cnt) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nw = (n + 63) >> 6;
+  if (w >= nw) return;
+  const uint64_t p0 = w << 6;
+  uint64_t m = 0;
+  if (aligned && p0 + 64 <= n) {
+    const uint4* q = (const uint4*)(img + p0);  // the image is 16-byte aligned by the caller
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const uint4 v = q[g];
+      const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t b = (d[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+        const uint64_t p = p0 + 16 * g + j;
+        if ((b == 1u || b == 2u) && p + hdr_len((uint8_t)b) <= n) m |= 1ull << (16 * g + j);
+      }
+    }
+  } else {
+    for (uint64_t p = p0; p < n; ++p) {
+      const uint8_t b = img[p];
+      if ((b == 1 || b == 2) && p + hdr_len(b) <= n) m |= 1ull << (p - p0);
+    }
+  }
+  bits[w] = m;
+  cnt[w] = (uint32_t)__popcll(m);
+}
+
+// 2. exclusive scan of cnt (u32) in place: per-block sums, one-block scan of
+// those, per-block rescan.  1024 threads x 4 words per block.
+#define WSCAN_ITEMS 4u
+#define WSCAN_BLOCK 1024u
+__global__ __launch_bounds__(WSCAN_BLOCK) void wal_scan_a(const uint32_t* __restrict__ cnt, uint64_t nw,
+                                                            uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t s[WSCAN_BLOCK / 64];
+  const uint64_t i0 = ((uint64_t)blockIdx.x * WSCAN_BLOCK + threadIdx.x) * WSCAN_ITEMS;
+  uint32_t x = 0;
+  for (uint32_t j = 0; j < WSCAN_ITEMS; ++j) x += (i0 + j < nw) ? cnt[i0 + j] : 0u;
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  if ((threadIdx.x & 63u) == 0) s[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t k = 0; k < WSCAN_BLOCK / 64; ++k) t += s[k];
+    bsum[blockIdx.x] = t;
+  }
+}
+__global__ __launch_bounds__(1024) void wal_scan_b(uint32_t* __restrict__ bsum, uint32_t nb,
+                                                     uint32_t* __restrict__ total) {
+  __shared__ uint32_t ws[16];
+  const uint32_t C = (nb + 1023u) / 1024u, b0 = threadIdx.x * C, b1 = min(nb, b0 + C);
+  uint32_t mine = 0;
+  for (uint32_t b = b0; b < b1; ++b) mine += bsum[b];
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t x = mine;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += o;
+  }
+  if (lane == 63u) ws[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t v = ws[i];
+      ws[i] = acc;
+      acc += v;
+    }
+    *total = acc;
+  }
+  __syncthreads();
+  uint32_t run = ws[threadIdx.x >> 6] + x - mine;
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t v = bsum[b];
+    bsum[b] = run;
+    run += v;
+  }
+}
+__global__ __launch_bounds__(WSCAN_BLOCK) void wal_scan_c(uint32_t* __restrict__ cnt, uint64_t nw,
+                                                            const uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t s[WSCAN_BLOCK / 64];
+  const uint64_t i0 = ((uint64_t)blockIdx.x * WSCAN_BLOCK + threadIdx.x) * WSCAN_ITEMS;
+  uint32_t v[WSCAN_ITEMS], x = 0;
+  for (uint32_t j = 0; j < WSCAN_ITEMS; ++j) {
+    v[j] = (i0 + j < nw) ? cnt[i0 + j] : 0u;
+    x += v[j];
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t inc = x;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += o;
+  }
+  if (lane == 63u) s[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < WSCAN_BLOCK / 64; ++k) {
+      const uint32_t t = s[k];
+      s[k] = acc;
+      acc += t;
+    }
+  }
+  __syncthreads();
+  uint32_t run = bsum[blockIdx.x] + s[threadIdx.x >> 6] + inc - x;
+  for (uint32_t j = 0; j < WSCAN_ITEMS; ++j)
+    if (i0 + j < nw) {
+      cnt[i0 + j] = run;  // now: candidates before word i0 + j
+      run += v[j];
+    }
+}
+
+// rank of candidate position q (q must be a candidate)
+__device__ __forceinline__ uint32_t cand_rank(const uint64_t* __restrict__ bits, const uint32_t* __restrict__ pre,
+                                              uint64_t q) {
+  const uint64_t w = q >> 6;
+  const uint32_t b = (uint32_t)(q & 63u);
+  return pre[w] + (uint32_t)__popcll(bits[w] & ((1ull << b) - 1ull));
+}
+
+// 3. positions and successors of the candidates: thread per 64-byte word
+__global__ __launch_bounds__(256) void wal_succ(const uint8_t* __restrict__ img, uint64_t n,
+                                                 const uint64_t* __restrict__ bits, const uint32_t* __restrict__ pre,
+                                                 uint64_t* __restrict__ pos, uint32_t* __restrict__ J0,
+                                                 uint64_t* __restrict__ badpos) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nw = (n + 63) >> 6;
+  if (w >= nw) return;
+  uint64_t m = bits[w];
+  uint32_t c = pre[w];
+  while (m) {
+    const uint32_t b = (uint32_t)__builtin_ctzll(m);
+    m &= m - 1;
+    const uint64_t p = (w << 6) + b;
+    const uint8_t t = img[p];
+    const uint32_t h = hdr_len(t);
+    const uint32_t klen = rd32(img + p + 5);
+    const uint32_t vlen = t == 1 ? rd32(img + p + 9) : 0u;
+    const uint32_t dlen = klen + vlen;  // u32, as wal.rs:129
+    const uint64_t avail = n - (p + h);
+    const uint64_t q = p + h + (dlen <= avail ? (uint64_t)dlen : avail);
+    uint32_t s;
+    if (q >= n) {
+      s = WAL_END;  // wal.rs:76-77: EOF on the next header's type byte
+    } else {
+      const uint8_t t2 = img[q];
+      if (t2 != 1 && t2 != 2) {
+        s = WAL_BAD;
+        badpos[c] = q;
+      } else if (q + hdr_len(t2) > n) {
+        s = WAL_END;  // UnexpectedEof inside the next header
+      } else {
+        s = cand_rank(bits, pre, q);
+      }
+    }
+    pos[c] = p;
+    J0[c] = s;
+    ++c;
+  }
+}
+
+// the chain's first entry: candidate 0 when position 0 is one; otherwise the
+// log ends before its first record: empty (END) or a bad type byte at 0
+__global__ void wal_chain_init(const uint8_t* __restrict__ img, uint64_t n, const uint64_t* __restrict__ bits,
+                               uint32_t* __restrict__ chain, unsigned long long* __restrict__ info) {
+  const bool cand = n && (bits[0] & 1ull);
+  const bool bad = n && img[0] != 1 && img[0] != 2;
+  chain[0] = cand ? 0u : (bad ? WAL_BAD : WAL_END);
+  info[0] = 0;
+  info[1] = bad ? WAL_BAD : WAL_END;
+  info[2] = 0;  // bad position
+}
+
+// 4. one doubling level: Jn[c] = J[J[c]] (terminals absorb)
+__global__ __launch_bounds__(256) void wal_double(const uint32_t* __restrict__ J, uint32_t* __restrict__ Jn,
+                                                   uint32_t nc) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  const uint32_t s = J[c];
+  Jn[c] = s >= WAL_BAD ? s : J[s];
+}
+
+// 5. chain unrolling, one level: chain[L + i] = J_k(chain[i]) for i < L = 2^k
+// (an entry is a candidate rank or a terminal; a terminal absorbs).
+__global__ __launch_bounds__(256) void wal_unroll(const uint32_t* __restrict__ Jk, uint32_t* __restrict__ chain,
+                                                   uint32_t L) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= L) return;
+  const uint32_t c = chain[i];
+  chain[L + i] = c >= WAL_BAD ? c : Jk[c];
+}
+
+// the chain's length and how it ends: the first terminal entry (entries are
+// ranks up to it, terminals after); out[0] = records, out[1] = terminal code,
+// out[2..3] = the BAD position (u64)
+__global__ __launch_bounds__(256) void wal_chain_end(const uint32_t* __restrict__ chain, uint32_t len,
+                                                      const uint32_t* __restrict__ J0, const uint64_t* __restrict__ badpos,
+                                                      unsigned long long* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= len) return;
+  const bool here = chain[i] < WAL_BAD && (i + 1 == len || chain[i + 1] >= WAL_BAD);
+  if (!here) return;  // exactly one entry: the chain's last record
+  const uint32_t c = chain[i];
+  out[0] = i + 1;
+  out[1] = J0[c];
+  out[2] = J0[c] == WAL_BAD ? badpos[c] : 0ull;
+}
+
+// 6. records -> lsmck_wal_rec entries, CRC descriptors and stored CRCs
+__global__ __launch_bounds__(256) void wal_emit(const uint8_t* __restrict__ img, uint64_t n,
+                                                 const uint32_t* __restrict__ chain, const uint64_t* __restrict__ pos,
+                                                 const unsigned long long* __restrict__ info,
+                                                 lsmck_wal_rec* __restrict__ recs, uint64_t* __restrict__ poff,
+                                                 uint32_t* __restrict__ plen, uint32_t* __restrict__ pcrc) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint32_t)info[0]) return;
+  const uint64_t p = pos[chain[i]];
+  const uint8_t t = img[p];
+  const uint32_t h = hdr_len(t);
+  const uint32_t klen = rd32(img + p + 5), vlen = t == 1 ? rd32(img + p + 9) : 0u;
+  const uint32_t dlen = klen + vlen;
+  const uint64_t avail = n - (p + h);
+  lsmck_wal_rec r;
+  r.rec_off = p;
+  r.payload_off = p + h;
+  r.klen = klen;
+  r.vlen = vlen;
+  r.crc = rd32(img + p + 1);
+  r.type = t;
+  recs[i] = r;
+  poff[i] = p + h;
+  plen[i] = dlen <= avail ? dlen : (uint32_t)avail;
+  pcrc[i] = r.crc;
+}
+
+}  // namespace lsmck
+
+using namespace lsmck;
+
+static int launch_err() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -(int)e;
+}
+
+extern "C" uint64_t lsmk_wal_words(uint64_t n) { return (n + 63) >> 6; }
+extern "C" uint64_t lsmk_wal_scan_blocks(uint64_t n) {
+  const uint64_t nw = lsmk_wal_words(n);
+  return (nw + WSCAN_BLOCK * WSCAN_ITEMS - 1) / (WSCAN_BLOCK * WSCAN_ITEMS);
+}
+
+// phase 1-2: bitmap, counts, their exclusive scan; *total = candidates
+extern "C" int lsmk_wal_mark(const uint8_t* img, uint64_t n, uint64_t* bits, uint32_t* pre, uint32_t* bsum,
+                             uint32_t* total, hipStream_t st) {
+  const uint64_t nw = lsmk_wal_words(n);
+  if (nw == 0) return 0;
+  const int aligned = ((uintptr_t)img & 15) == 0;
+  hipLaunchKernelGGL(wal_mark, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, img, n, aligned, bits, pre);
+  const uint64_t nb = lsmk_wal_scan_blocks(n);
+  hipLaunchKernelGGL(wal_scan_a, dim3((unsigned)nb), dim3(WSCAN_BLOCK), 0, st, pre, nw, bsum);
+  hipLaunchKernelGGL(wal_scan_b, dim3(1), dim3(1024), 0, st, bsum, (uint32_t)nb, total);
+  hipLaunchKernelGGL(wal_scan_c, dim3((unsigned)nb), dim3(WSCAN_BLOCK), 0, st, pre, nw, bsum);
+  return launch_err();
+}
+
+// phase 3-5 for nc candidates (read back by the host): levels = bit length of
+// nc (2^levels > nc >= the chain's length), J holds levels * nc u32, chain
+// 2^levels u32, info 4 u64 (device): records, terminal code, bad position
+extern "C" int lsmk_wal_chain(const uint8_t* img, uint64_t n, const uint64_t* bits, const uint32_t* pre, uint32_t nc,
+                              int levels, uint64_t* pos, uint32_t* J, uint64_t* badpos, uint32_t* chain,
+                              unsigned long long* info, hipStream_t st) {
+  const uint64_t nw = lsmk_wal_words(n);
+  hipLaunchKernelGGL(wal_chain_init, dim3(1), dim3(1), 0, st, img, n, bits, chain, info);
+  if (nc == 0) return launch_err();
+  hipLaunchKernelGGL(wal_succ, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, img, n, bits, pre, pos, J,
+                     badpos);
+  for (int k = 0; k + 1 < levels; ++k)
+    hipLaunchKernelGGL(wal_double, dim3((nc + 255) / 256), dim3(256), 0, st, J + (uint64_t)k * nc,
+                       J + (uint64_t)(k + 1) * nc, nc);
+  for (int k = 0; k < levels; ++k) {
+    const uint32_t L = 1u << k;
+    hipLaunchKernelGGL(wal_unroll, dim3((L + 255) / 256), dim3(256), 0, st, J + (uint64_t)k * nc, chain, L);
+  }
+  const uint32_t len = 1u << levels;
+  hipLaunchKernelGGL(wal_chain_end, dim3((len + 255) / 256), dim3(256), 0, st, chain, len, J, badpos, info);
+  return launch_err();
+}
+
+// records, descriptors and stored CRCs of the first info[0] chain entries
+extern "C" int lsmk_wal_emit(const uint8_t* img, uint64_t n, const uint32_t* chain, const uint64_t* pos,
+                             const unsigned long long* info, uint32_t m, lsmck_wal_rec* recs, uint64_t* poff,
+                             uint32_t* plen, uint32_t* pcrc, hipStream_t st) {
+  if (m == 0) return 0;
+  hipLaunchKernelGGL(wal_emit, dim3((m + 255) / 256), dim3(256), 0, st, img, n, chain, pos, info, recs, poff, plen,
+                     pcrc);
+  return launch_err();
+}

@@ -18,12 +18,12 @@ def load_img():
     return open(os.path.join(GOLDEN, "wal_2000.bin"), "rb").read()
 
 
-def same(ctx, img, device=False):
-    if device:
-        d = ctx.alloc(max(1, len(img)))
+def same(ctx, img, device=False, shift=0):
+    if device:  # shift: the image at an unaligned device address
+        d = ctx.alloc(max(1, len(img)) + shift)
         if img:
-            d.upload(np.frombuffer(img, np.uint8))
-        recs, st, bad = ctx.wal_replay_verify(len(img), device_ptr=d.ptr)
+            d.upload(np.frombuffer(img, np.uint8), offset=shift)
+        recs, st, bad = ctx.wal_replay_verify(len(img), device_ptr=d.ptr + shift)
     else:
         recs, st, bad = ctx.wal_replay_verify(img)
     ost, orecs, obad = O.wal_replay(img)
@@ -42,7 +42,11 @@ def test_clean_log(ctx, golden, device):
     assert same(ctx, b"", device) == 0
 
 
-def test_corruptions(ctx, golden):
+@pytest.mark.parametrize("device,shift", [(False, 0), (True, 0), (True, 3)])
+def test_corruptions(ctx, golden, device, shift):
+    """Bit flips, a bad type byte and truncations: the first failure in log
+    order, from the host walk (host image) and from the GPU header walk
+    (device image, lsmck_wal.hip; aligned and unaligned)."""
     img = load_img()
     recs = golden["wal_2000"]["records"]
     rng = np.random.default_rng(3)
@@ -54,13 +58,15 @@ def test_corruptions(ctx, golden):
         if r["klen"] + r["vlen"] == 0:
             continue
         b[r["off"] + hdr + int(rng.integers(0, r["klen"] + r["vlen"]))] ^= 1 << int(rng.integers(0, 8))
-        st = same(ctx, bytes(b))
+        st = same(ctx, bytes(b), device, shift)
         assert st == (1 if r["type"] == 1 else 2)
     b = bytearray(img)
     b[recs[77]["off"]] = 0
-    assert same(ctx, bytes(b)) == 3
-    for cut in (recs[300]["off"] + 1, recs[300]["off"] + 5, recs[300]["off"] + 12, len(img) - 1):
-        same(ctx, img[:cut])
+    assert same(ctx, bytes(b), device, shift) == 3
+    b[recs[0]["off"]] = 9  # bad type of the very first record
+    assert same(ctx, bytes(b), device, shift) == 3
+    for cut in (recs[300]["off"] + 1, recs[300]["off"] + 5, recs[300]["off"] + 12, len(img) - 1, 1, 5, 0):
+        same(ctx, img[:cut], device, shift)
 
 
 def test_memtable_from_log_gpu_equals_cpu(ctx):
@@ -130,3 +136,29 @@ def test_truncated_payload_with_matching_crc(ctx):
         [(type(r), r.key, getattr(r, "val", None)) for r in cpu]
     assert gpu[-1].key == b"kkkkk" and gpu[-1].val == b"vvvvv"
     assert gpu_log.file.tell() == len(img)
+
+
+def test_gpu_header_walk_big_binary_log(ctx):
+    """A log whose payloads are random bytes (so many bytes inside payloads look
+    like command types: bogus candidate starts for the GPU walk), device-resident:
+    the GPU header walk finds the real chain; the host walk agrees."""
+    rng = np.random.default_rng(12)
+    blob = O.gen_stream(77, 0, 1 << 21)
+    parts = []
+    for i in range(100000):
+        kl, vl = int(rng.integers(1, 40)), int(rng.integers(0, 600))
+        o = int(rng.integers(0, (1 << 21) - 700))
+        k = blob[o:o + kl].tobytes()
+        parts.append(O.wal_remove(k) if i % 9 == 0 else O.wal_insert(k, blob[o + 40:o + 40 + vl].tobytes()))
+    img = b"".join(parts)
+    assert same(ctx, img, device=True) == 0
+    ctx.set_option("wal_gpu_walk", 0)
+    try:
+        assert same(ctx, img, device=True) == 0
+    finally:
+        ctx.set_option("wal_gpu_walk", 1)
+    # a truncated payload at the end whose CRC matches what is there
+    short = b"abcdef"
+    tail = bytes([1]) + O.crc32(short).to_bytes(4, "little") + (3).to_bytes(4, "little") + \
+        (300).to_bytes(4, "little") + short
+    assert same(ctx, img + tail, device=True) == 0
