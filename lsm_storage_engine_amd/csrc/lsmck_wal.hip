@@ -59,7 +59,8 @@ __global__ __launch_bounds__(256) void wal_mark(const uint8_t* __restrict__ img,
       }
     }
   } else {
-    for (uint64_t p = p0; p < n; ++p) {
+    const uint64_t pe = p0 + 64 < n ? p0 + 64 : n;
+    for (uint64_t p = p0; p < pe; ++p) {
       const uint8_t b = img[p];
       if ((b == 1 || b == 2) && p + hdr_len(b) <= n) m |= 1ull << (p - p0);
     }
