@@ -259,12 +259,10 @@ struct SsTable {
     return true;
   }
 
-  // tokio/sstable.rs:63-86: exact index hit -> read_record, else scan the
-  // index range that can hold the key
-  bool get(const std::string& key, std::string* val) const {
-    // key range filter (in place of the bloom filter, tokio/sstable.rs:64)
-    if (index.empty() || key < index.begin()->first) return false;
+  // the largest key: the records after the last index entry, read once
+  const std::string& last() const {
     std::call_once(last_once, [this] {
+      if (index.empty()) return;
       int fd = open(data_path.c_str(), O_RDONLY | O_CLOEXEC);
       if (fd < 0) return;
       std::string k, v;
@@ -272,7 +270,18 @@ struct SsTable {
       for (uint64_t pos = index.rbegin()->second; read_record(fd, pos, &k, &v, &len); pos += len) last_key = k;
       close(fd);
     });
-    if (key > last_key) return false;
+    return last_key;
+  }
+  void set_last(const std::string& k) {  // a table written here: its last key is known
+    std::call_once(last_once, [&] { last_key = k; });
+  }
+  const std::string& first() const { return index.begin()->first; }
+
+  // tokio/sstable.rs:63-86: exact index hit -> read_record, else scan the
+  // index range that can hold the key
+  bool get(const std::string& key, std::string* val) const {
+    // key range filter (in place of the bloom filter, tokio/sstable.rs:64)
+    if (index.empty() || key < first() || key > last()) return false;
     int fd = open(data_path.c_str(), O_RDONLY | O_CLOEXEC);
     if (fd < 0) return false;
     std::string k, v;
@@ -301,6 +310,43 @@ struct SsTable {
   }
 };
 
+// One level's tables by key range, for Db::get: the reference asks every
+// table of a level (its bloom filter, tokio/db.rs:160-181); a 100 GiB tree has
+// ~230k tables, so the tables whose [first, last] key range can hold the key
+// are found by binary search over the first keys and a running maximum of the
+// last keys, then asked newest first as the reference does.
+struct LevelIndex {
+  bool built = false;
+  std::vector<std::shared_ptr<SsTable>> by_first;  // non-empty tables, ascending first key
+  std::vector<const std::string*> max_last;        // max_last[i] = max last key of by_first[0..i]
+
+  void build(const std::vector<std::shared_ptr<SsTable>>& tables) {
+    by_first.clear();
+    for (const auto& t : tables)
+      if (!t->index.empty()) by_first.push_back(t);
+    std::sort(by_first.begin(), by_first.end(),
+              [](const std::shared_ptr<SsTable>& a, const std::shared_ptr<SsTable>& b) { return a->first() < b->first(); });
+    max_last.resize(by_first.size());
+    for (size_t i = 0; i < by_first.size(); ++i) {
+      const std::string& l = by_first[i]->last();
+      max_last[i] = (i && *max_last[i - 1] > l) ? max_last[i - 1] : &l;
+    }
+    built = true;
+  }
+  // the tables that may hold k, newest (largest id) first
+  void candidates(const std::string& k, std::vector<SsTable*>* out) const {
+    out->clear();
+    size_t p = std::upper_bound(by_first.begin(), by_first.end(), k,
+                                [](const std::string& key, const std::shared_ptr<SsTable>& t) { return key < t->first(); }) -
+               by_first.begin();
+    while (p > 0 && !(*max_last[p - 1] < k)) {
+      --p;
+      if (!(by_first[p]->last() < k)) out->push_back(by_first[p].get());
+    }
+    std::sort(out->begin(), out->end(), [](const SsTable* a, const SsTable* b) { return a->id > b->id; });
+  }
+};
+
 struct Config {
   std::string base = "./data";
   size_t memtable_limit = 4096;  // config/default: memtable_limit_bytes
@@ -321,6 +367,7 @@ struct Db {
   std::shared_ptr<const MemTable> old;  // being flushed (db.rs:28)
   std::shared_mutex lv_mu;
   std::vector<std::vector<std::shared_ptr<SsTable>>> levels{(size_t)kMaxLevel};
+  std::vector<LevelIndex> lindex{(size_t)kMaxLevel};  // built at a level's first table read
   uint64_t last_id = 0;
 
   std::string wal_path() const { return join(join(cfg.base, "wal"), "wal.log"); }
@@ -534,10 +581,20 @@ struct Db {
         }
       }
     }
-    if (!found) {
+    for (int lv = 0; lv < kMaxLevel && !found; ++lv) {
       std::shared_lock<std::shared_mutex> lk(lv_mu);
-      for (int lv = 0; lv < kMaxLevel && !found; ++lv)
-        for (auto it = levels[lv].rbegin(); it != levels[lv].rend() && !found; ++it) found = (*it)->get(k, v);
+      if (!lindex[lv].built) {
+        lk.unlock();
+        {
+          std::unique_lock<std::shared_mutex> ul(lv_mu);
+          if (!lindex[lv].built) lindex[lv].build(levels[lv]);
+        }
+        lk.lock();
+      }
+      thread_local std::vector<SsTable*> cand;
+      lindex[lv].candidates(k, &cand);
+      for (SsTable* t : cand)
+        if ((found = t->get(k, v))) break;
     }
     return found && !(v->size() == 1 && (*v)[0] == '\0');
   }
@@ -563,6 +620,7 @@ struct Db {
     t->data_path = join(dir, data_fn);
     std::string data, index;
     uint64_t i = 0;
+    if (!m->data.empty()) t->set_last(m->data.rbegin()->first);
     for (const auto& kv : m->data) {  // write_data_file (tokio/sstable.rs:113-135)
       if (i++ % kIndexStep == 0) t->index[kv.first] = data.size();
       put_u32(data, (uint32_t)kv.first.size());
@@ -598,6 +656,7 @@ struct Db {
     {
       std::unique_lock<std::shared_mutex> lk(lv_mu);
       levels[0].push_back(t);
+      if (lindex[0].built) lindex[0].build(levels[0]);  // flushes are rare: rebuild
     }
     // the flushed memtable's log is no longer needed (wal.close(), db.rs:110)
     unlink(flushing_path().c_str());

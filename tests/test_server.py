@@ -132,3 +132,31 @@ def test_client_protocol_edges(tmp_path):
         assert Client(srv.port).call(b"get", b"a") == "ét�".encode()
     finally:
         srv.kill()
+
+
+def test_replayed_remove_drops_entry_like_the_reference(tmp_path):
+    """A live delete keeps the tombstone vec![0] (db.rs:131-143), but
+    MemTable::from_log drops a replayed Remove's entry (memtable.rs:40-43): after
+    a crash a key whose delete was only in the log reads as its flushed value."""
+    import time
+    base = str(tmp_path / "db")
+    srv = Server(base, memtable_limit=1 << 12)
+    try:
+        c = srv.client()
+        assert c.call(b"insert", b"victim", b"old") == b"ok"
+        cmds = [b"insert fill%04d %s" % (i, b"x" * 64) for i in range(80)]  # > 4 KiB: swap + flush
+        assert c.pipeline(cmds) == [b"ok"] * len(cmds)
+        lv0 = os.path.join(base, "level-0")
+        for _ in range(200):
+            if os.path.isdir(lv0) and any("metadata" in n for n in os.listdir(lv0)) and \
+                    not os.path.exists(os.path.join(base, "wal", "wal.log.flushing")):
+                break
+            time.sleep(0.05)
+        assert c.call(b"delete", b"victim") == b"ok"
+        assert c.call(b"get", b"victim") == b"victim not found"  # the tombstone, live
+        c.close()
+        srv.kill()
+        srv = Server(base, memtable_limit=1 << 12)
+        assert srv.client().call(b"get", b"victim") == b"old"
+    finally:
+        srv.kill()

@@ -41,6 +41,7 @@ def traffic(port, conn, ops, batch=512):
     """One connection's commands: inserts of its own keys, reads, deletes."""
     c = Client(port)
     model = {}
+    hist = {}  # every value a key held
     t0 = time.perf_counter()
     i = 0
     while i < ops:
@@ -60,6 +61,7 @@ def traffic(port, conn, ops, batch=512):
                 cmds.append(b"insert " + k + b" " + v)
                 want.append(b"ok")
                 model[k] = v
+                hist.setdefault(k, set()).add(v)
         got = c.pipeline(cmds)
         if conn == 0 and (i // batch) % 50 == 0:
             print(f"traffic: conn 0 at {i}/{ops}", file=sys.stderr, flush=True)
@@ -69,7 +71,27 @@ def traffic(port, conn, ops, batch=512):
         i += batch
     dt = time.perf_counter() - t0
     c.close()
-    return model, dt
+    return model, hist, dt
+
+
+def replayed_removes(base):
+    """Keys whose last record in the log the restart replays (a rotated
+    wal.log.flushing first, then wal.log) is a Remove (oracle replay)."""
+    from oracle import oracle as O
+    img = b""
+    for name in ("wal.log.flushing", "wal.log"):
+        p = os.path.join(base, "wal", name)
+        if os.path.exists(p):
+            img += open(p, "rb").read()
+    st, recs, _ = O.wal_replay(img)
+    last = {}
+    for r in recs:
+        p = img[r.payload_off:r.payload_off + ((r.klen + r.vlen) & 0xFFFFFFFF)]
+        if r.type == 1:
+            last[p[:r.klen]] = 1
+        else:
+            last[p] = 2
+    return {k for k, t in last.items() if t == 2}
 
 
 def main():
@@ -106,9 +128,11 @@ def main():
         outs = list(ex.map(lambda k: traffic(srv.port, k, a.ops), range(a.conns)))
     wall = time.perf_counter() - t1
     srv.kill()
-    model = {}
-    for m, _ in outs:
+    model, hist = {}, {}
+    for m, h, _ in outs:
         model.update(m)
+        hist.update(h)
+    removed = replayed_removes(a.dir)
     t0 = time.perf_counter()
     srv = Server(a.dir, memtable_limit=a.memtable_limit)
     start2 = time.perf_counter() - t0
@@ -120,7 +144,20 @@ def main():
     for i in range(0, len(keys), 4096):
         got += c.pipeline([b"get " + k for k in keys[i:i + 4096]])
     want = [model[k] if model[k] is not None else k + b" not found" for k in keys]
-    mismatches = sum(1 for x, y in zip(got, want) if x != y)
+    # The reference's MemTable::from_log drops the entry of a replayed Remove
+    # (memtable.rs:40-43) instead of keeping the tombstone vec![0] a live
+    # delete inserts (db.rs:131-143): after a crash, a key whose delete was
+    # only in the log reads as its value in the newest table holding it (or
+    # not found).  lsmck_server keeps that behaviour; such keys are counted
+    # apart and must read as "not found" or as a value the key once held.
+    mismatches = resurrected = 0
+    for k, x, y in zip(keys, got, want):
+        if x == y:
+            continue
+        if k in removed and (x == k + b" not found" or x in hist.get(k, ())):
+            resurrected += 1
+        else:
+            mismatches += 1
     c.close()
     srv.kill()
 
@@ -151,7 +188,8 @@ def main():
                     "commands_per_s": round(a.conns * a.ops / wall, 1),
                     "mix": "per connection: 80% insert, 10% get, 10% delete, pipelined 512 per round trip"},
         "restart": {**load2, "process_start_s": round(start2, 3)},
-        "readback": {"keys": len(keys), "mismatches": mismatches},
+        "readback": {"keys": len(keys), "mismatches": mismatches,
+                     "replayed_remove_reads_table_value": resurrected},
         "cpu_baseline": {"value": round(done / GIB / tc, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
                          "sample": f"first {done / GIB:.2f} GiB of data+index files, oracle FIPS SHA-256, 1 thread"},
         "synthesis_s": synth["seconds"],

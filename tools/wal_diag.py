@@ -8,7 +8,9 @@ values 0-999 B, 10% removes), then times, best of 5 each:
             batch after it)
   verify    lsmck_crc32_verify_batch on the same descriptors, pageable host image
   pinned    the same from a pinned copy of the image
-  device    the same on a device-resident copy
+  device    the same on a device-resident copy; replay of a device-resident
+            image with the GPU header walk (default) and with the copy-back
+            host walk (wal_gpu_walk 0)
 Prints one JSON line.
 """
 import json
@@ -84,6 +86,12 @@ def main():
     d.upload(img)
     ctx.sync()
     res["replay_device_image_s"] = best(lambda: ctx.wal_replay_verify(len(img), device_ptr=d.ptr))
+    ctx.set_option("wal_gpu_walk", 0)  # A/B: copy the device image back, host walk
+    res["replay_device_image_hostwalk_s"] = best(lambda: ctx.wal_replay_verify(len(img), device_ptr=d.ptr))
+    ctx.set_option("wal_gpu_walk", 1)
+    # a host image uploaded whole from pinned memory, then the GPU header walk
+    res["replay_pinned_upload_gpuwalk_s"] = best(
+        lambda: (d.upload(pin.array), ctx.wal_replay_verify(len(img), device_ptr=d.ptr)))
     for k in list(res):
         if k.endswith("_s"):
             res[k[:-2] + "_GiBps"] = round(len(img) / 2**30 / res[k], 2)
