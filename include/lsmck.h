@@ -195,6 +195,10 @@ int lsmck_device_count(void);
  *                 ahead of its position (default 4096; 0 = off).  A/B switch.
  *   "stage_threads"  host-memory batches: threads that copy a pageable chunk
  *                 into its pinned staging slot (default 8; 1 = one memcpy).
+ *   "wal_gpu_walk"  lsmck_wal_replay_verify of a device image: 1 = header walk
+ *                 on the GPU (default), 0 = read back and walk on the host.
+ *   "wal_upload_min"  host images of at least this many bytes are uploaded and
+ *                 walked on the GPU (default 1 MiB; 0 = always the host walk).
  *   "wal_chunk_bytes"  lsmck_wal_replay_verify of a host image: CRC batches
  *                 of this many payload bytes run on a helper thread while the
  *                 walk goes on (default 32 MiB; 0 = one batch after the walk).
@@ -237,8 +241,15 @@ int lsmck_sha256_batch_fixed(lsmck_ctx* ctx, const uint8_t* base, size_t stride,
 
 /* WAL replay verify: the batch form of the CommandLog iterator + MemTable::from_log
  * (src/wal.rs:68-84,122-163; src/memtable.rs:28-47) over an in-memory WAL image.
- * Headers are walked on the host (each record's length lives in the previous
- * header), every payload CRC is checked on the GPU in one batch.
+ * Each record's length lives in its own header, so the walk is a dependent
+ * chain.  On the GPU (lsmck_wal.hip) it is a speculative parallel parse: every
+ * byte that could start a header is a candidate, candidate -> successor links
+ * are followed by pointer doubling from offset 0, and the accepted chain's
+ * payload CRCs are checked in one batch with the GPU compare.  A device image
+ * never leaves the device; a host image of at least "wal_upload_min" bytes
+ * (default 1 MiB) is uploaded whole and walked there; smaller host images
+ * (and "wal_upload_min" 0) take the serial host walk with the CRC batches on
+ * the GPU.  Results are the same on every path.
  * recs (optional, cap entries) receives the parsed records in log order.
  * Returns
  *   0                      clean end of log (header EOF ends iteration, wal.rs:76-77)
@@ -246,9 +257,8 @@ int lsmck_sha256_batch_fixed(lsmck_ctx* ctx, const uint8_t* base, size_t stride,
  *                          {checksum=*bad_crc, expected=*bad_expected} (wal.rs:136-141)
  *   LSMCK_WAL_REMOVE_PANIC first bad record is a Remove: the reference panics (wal.rs:154-159)
  *   LSMCK_WAL_BAD_TYPE     InvalidCommandType(*bad_crc) at record *bad_index (wal.rs:36)
- * *nrec = records accepted before the stop.  flags: LSMCK_HOST or LSMCK_DEVICE
- * for `wal` (the header walk always needs a host copy: with LSMCK_DEVICE the
- * image is read back once). */
+ * *nrec = records accepted before the stop.  flags: LSMCK_HOST (optionally
+ * | LSMCK_HOST_PINNED) or LSMCK_DEVICE for `wal`.  Synchronous. */
 #define LSMCK_WAL_CORRUPTED 1
 #define LSMCK_WAL_REMOVE_PANIC 2
 #define LSMCK_WAL_BAD_TYPE 3

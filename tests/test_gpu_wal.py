@@ -42,11 +42,23 @@ def test_clean_log(ctx, golden, device):
     assert same(ctx, b"", device) == 0
 
 
-@pytest.mark.parametrize("device,shift", [(False, 0), (True, 0), (True, 3)])
-def test_corruptions(ctx, golden, device, shift):
+@pytest.fixture
+def upload_min(ctx):
+    """Sets wal_upload_min for one test (host images from that size are
+    uploaded and walked on the GPU; 0 = the host walk), then restores it."""
+    def set_(v):
+        ctx.set_option("wal_upload_min", v)
+    yield set_
+    ctx.set_option("wal_upload_min", 1 << 20)
+
+
+@pytest.mark.parametrize("device,shift,upload", [(False, 0, 0), (False, 0, 1), (True, 0, 0), (True, 3, 0)])
+def test_corruptions(ctx, golden, upload_min, device, shift, upload):
     """Bit flips, a bad type byte and truncations: the first failure in log
-    order, from the host walk (host image) and from the GPU header walk
-    (device image, lsmck_wal.hip; aligned and unaligned)."""
+    order, from the host walk (host image), from the GPU header walk of an
+    uploaded host image (upload=1), and from the GPU header walk of a device
+    image (lsmck_wal.hip; aligned and unaligned)."""
+    upload_min(upload)
     img = load_img()
     recs = golden["wal_2000"]["records"]
     rng = np.random.default_rng(3)
@@ -152,6 +164,7 @@ def test_gpu_header_walk_big_binary_log(ctx):
         parts.append(O.wal_remove(k) if i % 9 == 0 else O.wal_insert(k, blob[o + 40:o + 40 + vl].tobytes()))
     img = b"".join(parts)
     assert same(ctx, img, device=True) == 0
+    assert same(ctx, img) == 0  # host image over 1 MiB: uploaded, GPU walk
     ctx.set_option("wal_gpu_walk", 0)
     try:
         assert same(ctx, img, device=True) == 0

@@ -2,7 +2,8 @@
 
 Builds a WAL image like tree.synthesize_tree's (500k records, keys 1-39 B,
 values 0-999 B, 10% removes), then times, best of 5 each:
-  replay    lsmck_wal_replay_verify (header walk + CRC batch), and again
+  replay    lsmck_wal_replay_verify: by default a host image is uploaded and
+            walked on the GPU; the host walk (wal_upload_min 0) is timed too, and
             per wal_prefetch distance (A/B of the walk's prefetch) and per
             wal_chunk_bytes (CRC batches overlapped with the walk; 0 = one
             batch after it)
@@ -64,7 +65,9 @@ def main():
     res = {"wal_bytes": len(img), "records": n}
     recs, st, _ = ctx.wal_replay_verify(img)
     assert st == 0 and len(recs) == n
-    res["replay_total_s"] = best(lambda: ctx.wal_replay_verify(img))
+    res["replay_total_s"] = best(lambda: ctx.wal_replay_verify(img))  # default: uploaded, GPU header walk
+    ctx.set_option("wal_upload_min", 0)  # the host walk for the A/Bs below
+    res["replay_hostwalk_s"] = best(lambda: ctx.wal_replay_verify(img))
     for pf in (0, 1024, 4096, 16384, 65536):
         ctx.set_option("wal_prefetch", pf)
         res[f"replay_prefetch_{pf}_s"] = best(lambda: ctx.wal_replay_verify(img))
@@ -81,7 +84,9 @@ def main():
     res["verify_pageable_s"] = best(lambda: ctx.crc32_verify(img, off, ln, exp))
     pin = ctx.alloc_pinned(len(img))
     pin.array[:] = img
-    res["replay_pinned_image_s"] = best(lambda: ctx.wal_replay_verify(pin.array))
+    res["replay_pinned_image_hostwalk_s"] = best(lambda: ctx.wal_replay_verify(pin.array))
+    ctx.set_option("wal_upload_min", 1 << 20)
+    res["replay_pageable_upload_gpuwalk_s"] = best(lambda: ctx.wal_replay_verify(img))
     d = ctx.alloc(len(img))
     d.upload(img)
     ctx.sync()
