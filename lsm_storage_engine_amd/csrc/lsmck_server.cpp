@@ -514,9 +514,12 @@ struct Db {
     for (auto& l : levels) ntab += l.size();
     printf("{\"event\": \"loaded\", \"tables\": %llu, \"table_bytes\": %llu, \"tree_verify_s\": %.6f, "
            "\"tree_list_s\": %.6f, \"wal_bytes\": %zu, \"wal_records\": %zu, \"wal_replay_s\": %.6f, "
-           "\"wal_verify_s\": %.6f, \"memtable_entries\": %zu, \"memtable_bytes\": %zu, \"load_s\": %.6f}\n",
+           "\"wal_verify_s\": %.6f, \"memtable_entries\": %zu, \"memtable_bytes\": %zu, \"load_s\": %.6f, "
+           "\"tree_phases\": {\"stat_s\": %.6f, \"read_s\": %.6f, \"gpu_wait_s\": %.6f, \"compare_s\": %.6f, "
+           "\"rounds\": %llu}}\n",
            (unsigned long long)ntab, (unsigned long long)rep.table_bytes, t_tree, rep.list_seconds, n, nrec, t_wal,
-           t_verify, mem.data.size(), mem.bytes, now_s() - t0);
+           t_verify, mem.data.size(), mem.bytes, now_s() - t0, rep.stat_seconds, rep.read_seconds,
+           rep.gpu_wait_seconds, rep.compare_seconds, (unsigned long long)rep.rounds);
     fflush(stdout);
   }
 
