@@ -240,7 +240,8 @@ def main():
                 # "b<n>" = sha_bucket_shift n (SHA order: 2^n-block buckets for 128..1023 blocks)
                 # "f<n>" = sha_bucket_from n (first block count of the coarse buckets)
                 # "o<n>" = crc_order n (fixed ring kernel tile order)
-                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?(?:r(\d))?(?:b(\d))?(?:f(\d+))?(?:o(\d))?", v)
+                # "p<n>" = sha_pair n (SHA-256: two blocks per load window)
+                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?(?:r(\d))?(?:b(\d))?(?:f(\d+))?(?:o(\d))?(?:p(\d))?", v)
                 if not m:
                     raise SystemExit(f"bad variant {v!r}")
                 kind, num, waves = m.group(1), int(m.group(2)), int(m.group(3) or 0)
@@ -253,6 +254,7 @@ def main():
                 ctx.set_option("sha_bucket_shift", int(m.group(6)) if m.group(6) is not None else 2)
                 ctx.set_option("sha_bucket_from", int(m.group(7) or 128))
                 ctx.set_option("crc_order", int(m.group(8) or 0))
+                ctx.set_option("sha_pair", int(m.group(9)) if m.group(9) is not None else 1)
                 step()
                 e0.record(stream)
                 for _ in range(a.steps):
@@ -268,6 +270,7 @@ def main():
         ctx.set_option("crc_ring", 0)
         ctx.set_option("sha_bucket_shift", 2)
         ctx.set_option("sha_bucket_from", 128)
+        ctx.set_option("sha_pair", 1)
         ctx.set_option("crc_order", 0)
         ab = {str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                        "GiBps_median": payload / GIB / (float(np.median(t)) * 1e-3)} for v, t in ab.items()}

@@ -224,6 +224,7 @@ struct lsmck_ctx {
   uint64_t tree_cpu_file = 0;  // whole-tree verify: files of at least this many bytes go to host threads (0 = 16 MiB)
   int sha_bucket_shift = 2;  // SHA order key: 2^shift-block buckets for from..1023 blocks (0 = exact; A/B: DESIGN.md 3.2)
   int sha_bucket_from = 128;
+  int sha_pair = 1;  // SHA-256 batches: two blocks per load window (A/B: DESIGN.md 3.2)
   unsigned tree_list_threads = 0;  // lsmck_tree_verify: metadata parsing threads (0 = kListThreads)
   size_t wal_prefetch = 4096;  // lsmck_wal_replay_verify: host walk's prefetch distance in bytes (0 = off)
   uint8_t* wal_host = nullptr;  // lsmck_wal_replay_verify of a device image: pinned host copy (grow-only)
@@ -405,6 +406,7 @@ int sha_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const uint6
   P.nmsg = n;
   P.order = order;
   P.out = out32;
+  P.pair = (uint32_t)ctx->sha_pair;
   int rc = lsmk_launch_sha256(&P, st);
   return rc ? launch_rc(rc, "sha256 kernel") : 0;
 }
@@ -809,6 +811,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     if (value < 0 || value > 6) return lsmck_host::set_error(LSMCK_EINVAL, "sha_bucket_shift: 0..6");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->sha_bucket_shift = (int)value;
+    return 0;
+  }
+  if (!strcmp(key, "sha_pair")) {  // A/B: SHA-256 batch kernel loads two blocks (a 128-B line) per window
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "sha_pair must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->sha_pair = (int)value;
     return 0;
   }
   if (!strcmp(key, "sha_order")) {  // A/B: 1 = variable-length SHA batches in decreasing length order (default)
@@ -1529,6 +1537,7 @@ static int verify_tables(lsmck_ctx* ctx, const char* const* data_paths, const ch
         const uint64_t left = fsize[f] - slot_done[k];
         const uint32_t len = (uint32_t)std::min<uint64_t>(left, slice);
         lsmck::ShaSlice d{};
+        pay = (pay + 15) & ~(uint64_t)15;  // 16-B aligned slices: no funnel, no next-line dword (lsmck_sha256.hip)
         d.off = pay;
         d.total = fsize[f];
         d.len = len;
@@ -1809,7 +1818,7 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
       const uint32_t active = c->tree_active ? c->tree_active : kTreeActive;
       const uint32_t slice = c->tree_slice ? c->tree_slice : kTreeSlice;
       const size_t files = std::min<size_t>(active, 2 * n);
-      const size_t bytes = files * slice + 16;
+      const size_t bytes = files * ((size_t)slice + 16) + 16;  // slices are 16-B aligned in the slot
       std::lock_guard<std::mutex> lk(c->mu);
       DevGuard g(c->dev);
       for (auto& S : c->stage) {

@@ -40,6 +40,7 @@ struct ShaParams {
   uint64_t nmsg;
   const uint32_t* order;      // optional permutation (longest first), may be null
   unsigned char* out;         // 32 bytes per message
+  uint32_t pair;              // 1: two blocks per load window (A/B, lsmck_sha256.hip ShaWin2)
 };
 
 // One slice of a message streamed through sha256_slices_kernel.

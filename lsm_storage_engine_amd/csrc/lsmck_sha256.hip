@@ -135,7 +135,10 @@ __device__ __forceinline__ void issue_win(const unsigned char* base, uint64_t of
     W.d[4 * g + 2] = v.z;
     W.d[4 * g + 3] = v.w;
   }
-  W.d[16] = ld32(p + 64);
+  // the funnel dword only when the message is not dword aligned; otherwise a
+  // dword inside the window (unused): a load past the window pulls in the
+  // next line early, and it is fetched again when its own block comes
+  W.d[16] = ld32(p + (s != p ? 64 : 60));
   asm volatile("" ::"v"(p));  // keep the address live: no load overwrites it (lsmck_crc32.hip keep_live)
 }
 // Funnel shift by sh bytes and big-endian byte swap in one v_perm_b32 per
@@ -149,11 +152,45 @@ __device__ __forceinline__ void compress_win(uint32_t (&h)[8], const ShaWin& W, 
   sha256_compress(h, w);
 }
 
+// Two whole blocks per window (PAIR): 128 message bytes + the funnel dword,
+// [a4, a4 + 132).  A lane then reads each 128-B line of its message at once; a
+// 68-byte window per block reads half a line per block, and the other half is
+// fetched again when the line has left L2 in between (FETCH_SIZE 1.6x the
+// payload for config 2, profiles/pmc_traffic.json).  Costs 32 more VGPRs.
+struct ShaWin2 {
+  uint32_t d[33];
+};
+__device__ __forceinline__ void issue_win2(const unsigned char* base, uint64_t off, uint64_t p0, ShaWin2& W) {
+  const unsigned char* s = base + off + p0;
+  const unsigned char* p = s - ((uintptr_t)s & 3);
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    u32x4 v = ld128(p + 16 * g);
+    W.d[4 * g + 0] = v.x;
+    W.d[4 * g + 1] = v.y;
+    W.d[4 * g + 2] = v.z;
+    W.d[4 * g + 3] = v.w;
+  }
+  W.d[32] = ld32(p + (s != p ? 128 : 124));  // as issue_win: no next-line dword when aligned
+  asm volatile("" ::"v"(p));
+}
+__device__ __forceinline__ void compress_win2(uint32_t (&h)[8], const ShaWin2& W, uint32_t sh) {
+  const uint32_t sel = 0x00010203u + sh * 0x01010101u;
+  uint32_t w[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_perm(W.d[j + 1], W.d[j], sel);
+  sha256_compress(h, w);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_perm(W.d[j + 17], W.d[j + 16], sel);
+  sha256_compress(h, w);
+}
+
 // Runs the compression over `len` bytes at base + off into h.  last: these are
 // the message's final bytes -- pad and append the bit length `bits` of the
 // whole message (the slice starts on a 64-byte boundary of the message).  Not
 // last: len is a multiple of 64 and no padding is added (a slice of a message
 // streamed through sha256_slices_kernel).
+template <bool PAIR = false>
 __device__ __forceinline__ void sha256_run(uint32_t (&h)[8], const unsigned char* base, uint64_t off, uint64_t len,
                                            bool last, uint64_t bits) {
   const uintptr_t A = (uintptr_t)(base + off);
@@ -177,7 +214,24 @@ __device__ __forceinline__ void sha256_run(uint32_t (&h)[8], const unsigned char
     nmain = 0;
   }
   uint64_t b = 0;
-  if (nmain) {
+  if (PAIR && nmain >= 2) {
+    // pairs (2p, 2p+1), p < nmain/2: their 132-byte windows stay inside the
+    // message's dwords; an odd last main block goes through the loader below
+    const uint64_t npair = nmain >> 1;
+    ShaWin2 WA, WB;
+    issue_win2(base, off, 0, WA);
+    uint64_t p = 0;
+    for (; p + 1 < npair; p += 2) {
+      issue_win2(base, off, (p + 1) << 7, WB);
+      __builtin_amdgcn_sched_barrier(0);
+      compress_win2(h, WA, sh);
+      issue_win2(base, off, (p + 2 < npair ? p + 2 : p + 1) << 7, WA);
+      __builtin_amdgcn_sched_barrier(0);
+      compress_win2(h, WB, sh);
+    }
+    if (p < npair) compress_win2(h, WA, sh);
+    b = npair << 1;
+  } else if (!PAIR && nmain) {
     ShaWin WA, WB;
     issue_win(base, off, 0, WA);
     for (; b + 1 < nmain; b += 2) {
@@ -230,6 +284,7 @@ __device__ __forceinline__ void store_digest(unsigned char* out, const uint32_t 
   o[1] = o1;
 }
 
+template <bool PAIR>
 __global__ __launch_bounds__(256) void sha256_kernel(ShaParams P) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P.nmsg) return;
@@ -238,7 +293,7 @@ __global__ __launch_bounds__(256) void sha256_kernel(ShaParams P) {
   uint64_t len = P.len ? P.len[m] : P.flen;
   uint32_t h[8];
   sha256_iv(h);
-  sha256_run(h, P.base, off, len, true, len << 3);
+  sha256_run<PAIR>(h, P.base, off, len, true, len << 3);
   store_digest(P.out + 32 * m, h);
 }
 
@@ -311,7 +366,10 @@ using namespace lsmck;
 extern "C" int lsmk_launch_sha256(const ShaParams* P, hipStream_t st) {
   if (P->nmsg == 0) return 0;
   uint64_t blocks = (P->nmsg + 255) / 256;
-  hipLaunchKernelGGL(sha256_kernel, dim3((unsigned)blocks), dim3(256), 0, st, *P);
+  if (P->pair)
+    hipLaunchKernelGGL(sha256_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, *P);
+  else
+    hipLaunchKernelGGL(sha256_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, *P);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
 }

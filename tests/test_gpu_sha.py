@@ -31,9 +31,18 @@ def test_fips_and_golden_slices(ctx, golden, blob):
         assert got[i].tobytes().hex() == e["sha256"], e
 
 
+@pytest.fixture(params=[0, 1], ids=["win1", "win2"])
+def sha_pair(request, ctx):
+    """Both SHA-256 load windows: one block (68 B) or two blocks (132 B) per load."""
+    ctx.set_option("sha_pair", request.param)
+    yield request.param
+    ctx.set_option("sha_pair", 1)
+
+
 @pytest.mark.parametrize("length,stride,shift", [(4096, 4096, 0), (64, 64, 0), (55, 57, 1), (56, 59, 2),
-                                                 (1000, 1003, 3), (0, 8, 0), (100000, 100000, 0)])
-def test_fixed_vs_oracle(ctx, length, stride, shift):
+                                                 (1000, 1003, 3), (0, 8, 0), (100000, 100000, 0),
+                                                 (191, 193, 1), (192, 196, 2), (255, 257, 3), (256, 256, 0)])
+def test_fixed_vs_oracle(ctx, sha_pair, length, stride, shift):
     n = max(1, min(20000, (32 << 20) // max(stride, 1)))
     data = O.gen_stream(21, 0, n * stride + shift + 8)
     base = data[shift:]
@@ -43,7 +52,7 @@ def test_fixed_vs_oracle(ctx, length, stride, shift):
     assert np.array_equal(got, want)
 
 
-def test_random_lengths_vs_oracle(ctx):
+def test_random_lengths_vs_oracle(ctx, sha_pair):
     rng = np.random.default_rng(4)
     n = 20000
     ln = rng.integers(0, 3000, n).astype(np.uint32)
@@ -84,7 +93,8 @@ def test_verify_many_tree(ctx, tmp_path, golden):
         f.write(b"Z")
     os.remove(metas[9].checksum_path())
     st = Checksums.verify_many(ctx, metas)
-    assert st[3] == _lib.DATA_MISMATCH and st[7] == _lib.INDEX_MISMATCH and st[9] < 0
+    assert st[3] == _lib.DATA_MISMATCH and st[7] == _lib.INDEX_MISMATCH
+    assert st[9] == _lib.PANIC_OPEN_CHECKSUM  # verify's .expect("Can't open checksum file"), checksums.rs:46
     assert sum(1 for s in st if s) == 3
 
 
@@ -128,7 +138,8 @@ def test_verify_many_streaming(ctx, tmp_path, active, slice_bytes, open_files):
         ctx.set_option("tree_slice_bytes", 0)
         ctx.set_option("tree_open_files", -1)
     assert st[150] == _lib.DATA_MISMATCH and st[201] == _lib.INDEX_MISMATCH
-    assert st[77] < 0 and st[78] < 0
+    assert st[77] == _lib.PANIC_OPEN_FILE  # calculate_checksum's .expect on the data file, checksums.rs:25
+    assert st[78] == _lib.PANIC_OPEN_CHECKSUM  # checksums.rs:46
     assert sum(1 for s in st if s) == 4
 
 
