@@ -39,6 +39,7 @@ namespace {
 
 constexpr uint64_t kMaxSegsPerLaunch = (1ull << 32) - 64;  // 32-bit segment indices in the kernels
 constexpr int kVariantTileMap = 0x100000;  // descriptor batches: the r01 tile-map kernel instead of the walking one
+constexpr int kVariantNoStream = 0x200000;  // descriptor batches: no stream kernel for packed >= 64-byte records (A/B)
 constexpr size_t kChunkBytes = 64ull << 20;                // host staging chunk (payload)
 constexpr size_t kChunkRecs = 1u << 20;                    // host staging chunk (records)
 
@@ -102,7 +103,13 @@ struct DescScratch {
   size_t cap_order = 0;
   unsigned char* sort_tmp = nullptr;
   size_t cap_tmp = 0;
+  // stream kernel (lsmck_crc32.hip): eligibility flag, per-wave boundary cuts
+  uint32_t* sflag = nullptr;
+  uint64_t* scuts = nullptr;
+  size_t cap_cuts = 0;
   void release() {
+    if (sflag) (void)hipFree(sflag);
+    if (scuts) (void)hipFree(scuts);
     if (block_sum) (void)hipFree(block_sum);
     if (tile_info) (void)hipFree(tile_info);
     if (total) (void)hipFree(total);
@@ -339,6 +346,16 @@ int crc_desc_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const 
     P.total_segs = sc.total;
     P.out = out;
     fill_tables(ctx, &P);
+    if (!(ctx->variant & kVariantNoStream)) {
+      // packed batches of >= 64-byte records: the stream kernel (decided on
+      // the device; the walking kernel below then exits at once)
+      if (!sc.sflag) HIPCHK(hipMalloc((void**)&sc.sflag, 16));
+      if ((rc = ensure_dev(&sc.scuts, &sc.cap_cuts, (size_t)lsmk_stream_waves(ctx->ncu) + 1))) return rc;
+      P.sflag = sc.sflag;
+      P.scuts = sc.scuts;
+      rc = lsmk_launch_crc32_stream(&P, ctx->ncu, ctx->variant, st);
+      if (rc) return launch_rc(rc, "crc32_stream kernel");
+    }
     rc = lsmk_launch_crc32_walk(&P, sc.block_sum, ctx->ncu, ctx->variant, st);
     return rc ? launch_rc(rc, "crc32_walk kernel") : 0;
   }
@@ -829,6 +846,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_order must be 0, 1 or 2");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->variant = (ctx->variant & ~0x3000000) | ((int)value << 24);
+    return 0;
+  }
+  if (!strcmp(key, "crc_stream")) {  // A/B: descriptor batches, 1 = stream kernel for packed >= 64-byte records (default)
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (ctx->variant & ~kVariantNoStream) | (value ? 0 : kVariantNoStream);
     return 0;
   }
   if (!strcmp(key, "crc_walk")) {  // A/B: descriptor batches, 1 = walking kernel (default), 0 = r01 tile-map kernel

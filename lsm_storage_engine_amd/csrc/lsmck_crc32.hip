@@ -1206,6 +1206,7 @@ __device__ __forceinline__ uint64_t start_bit(const WalkWin& W, int64_t rel) {
 
 template <int CHAINS, int ABLATE = 0>
 __global__ __launch_bounds__(1024) void crc32_walk_kernel(CrcParams P) {
+  if (P.sflag && *P.sflag) return;  // a packed batch of >= 64-byte records: crc32_stream_kernel took it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   build_lds_tables(smem, P);
   __syncthreads();  // the column table reuses the khi/klo area the table build fills
@@ -1353,6 +1354,309 @@ __global__ __launch_bounds__(1024) void crc32_walk_kernel(CrcParams P) {
   } else {
     finish(A);
   }
+}
+
+// ===========================================================================
+// Stream kernel: packed batches (record r+1 starts where r ends) of records of
+// at least 64 bytes -- config 3's shape.  The lanes read the batch as ALIGNED
+// 128-byte chunks of the byte stream, the fixed ring kernel's load shape
+// (buffer loads from a wave-uniform tile base, no per-lane address from the
+// descriptors: tools/microbench_c3.hip, 16.2 against 18.2 ms for config 3's
+// per-record segment windows), and record boundaries inside a chunk are CRC
+// register resets.  tools/stream_sim.py is the lane-level model of the
+// algebra below, checked against zlib:
+//  * a chunk is 32 words in two chains of 16; a boundary at chunk byte j lies
+//    in chain h = j >= 64 (>= 64-byte records: at most one per chain).  At its
+//    word the chain computes A = F(c ^ (u & ~mlo)) -- the chain's bytes before
+//    j, zero-extended to the word end -- and xors A ^ I into its register,
+//    I = 0xFFFFFFFF (x) x^(8s), s = bytes from j to the word end: the register
+//    then holds the new record's bytes from j with the CRC's init folded in;
+//  * the chunk's tail T (the last piece, aligned to the chunk end) is carried
+//    Horner-wise to the chunk before the record's end chunk: T (x) x^(1024 d)
+//    from the LDS columns, a prefix XOR over the wave, a wave-uniform carry
+//    across tiles;
+//  * a record ending at byte j of chunk c: CRC = ~(P (x) x^(8m) ^ A (x)
+//    x^(-8s)), P = Hprev (chain 0) or shift64(Hprev) ^ R0 (chain 1), m = j -
+//    64h -- computed by the window lane of its end boundary, so every CRC is
+//    one plain, coalesced store.
+// Boundaries are read from off[] in windows of 128 (a tile holds at most 128:
+// records >= 64 bytes), one tile ahead.  Each wave owns the boundaries
+// [cut_w, cut_w+1] (stream_cuts: balanced by bytes) and the tiles that hold
+// them; a record belongs to the wave of its end boundary.  Eligibility is
+// decided on the device (stream_check); the walking kernel, launched after
+// this one, exits when the batch was taken here.
+#define STREAM_MIN_LEN 64u
+#define LDS_XM_OFF LDS_KLO_OFF  // x^(8m), m = 0..63, then x^(-8(4-t)), t = 0..3 (the descriptor kernels' klo
+                                // area, after the walk columns); from LDS, so that hipcc cannot fold a constant
+                                // factor into 32 hoisted shifted copies (70 spilled VGPRs)
+
+// gf2_mulmod evaluated step by step: the empty asm makes a, b and p opaque at
+// every step, so hipcc cannot compute the 32 masks and 32 shifted factors of
+// two multiplies up front (it did: 128 VGPRs and ~240 B/lane of spills)
+__device__ __forceinline__ uint32_t gf2_mulmod_seq(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    asm volatile("" : "+v"(a), "+v"(b), "+v"(p));
+    const uint32_t m = (uint32_t)((int32_t)(a << i) >> 31);
+    p = __builtin_amdgcn_bitop3_b32(p, b, m, 0x78);  // p ^ (b & m)
+    b = (b >> 1) ^ (0xEDB88320u & (0u - (b & 1u)));
+  }
+  return p;
+}
+
+__device__ __forceinline__ uint32_t stream_init(uint32_t t) {  // 0xFFFFFFFF (x) x^(8(4-t)), t = j & 3
+  return t == 0u ? 0xdebb20e3u : (t == 1u ? 0x00be26edu : (t == 2u ? 0xbe26ed00u : 0x2dfd1072u));
+}
+__device__ __forceinline__ uint32_t stream_xinv(uint32_t t) {  // x^(-8(4-t))
+  return t == 0u ? 0x5b358fd3u : (t == 1u ? 0x1f81b6e1u : (t == 2u ? 0xd7125358u : 0x6567cb95u));
+}
+
+__global__ __launch_bounds__(1024) void stream_check(const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
+                                                     uint64_t n, uint32_t* __restrict__ flag) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool bad = false;
+  if (i < n) {
+    const uint32_t l = len[i];
+    bad = l < STREAM_MIN_LEN || (i + 1 < n && off[i + 1] != off[i] + l);
+  }
+  if (__any(bad) && (threadIdx.x & 63u) == 0u) *flag = 0u;  // plain stores of one value: no atomic needed
+}
+
+// boundary b = 0..n: the start of record b (b = n: the end of the last record)
+__device__ __forceinline__ uint64_t stream_pos(const CrcParams& P, uint64_t b, uint64_t dend) {
+  return b < P.nrec ? P.off[b] : dend;
+}
+
+// cut w, w = 0..W: the first boundary at or after off[0] + total*w/W
+__global__ __launch_bounds__(256) void stream_cuts(CrcParams P, uint32_t W) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w > W || !*P.sflag) return;
+  const uint64_t n = P.nrec, o0 = P.off[0], dend = P.off[n - 1] + P.len[n - 1];
+  const uint64_t target = o0 + (dend - o0) * w / W;
+  uint64_t a = 0, b = n;
+  while (a < b) {
+    const uint64_t m = (a + b) >> 1;
+    if (stream_pos(P, m, dend) < target) a = m + 1; else b = m;
+  }
+  P.scuts[w] = a;
+}
+
+struct StreamWin {
+  uint64_t a, b;  // off[] of boundaries bt + lane and bt + 64 + lane (clamped to n - 1; fixed up at use)
+};
+__device__ __forceinline__ void stream_win_issue(const CrcParams& P, uint64_t bt, uint32_t lane, StreamWin& W) {
+  const uint64_t n = P.nrec, ia = bt + lane, ib = bt + 64u + lane;
+  W.a = P.off[ia < n ? ia : n - 1];
+  W.b = P.off[ib < n ? ib : n - 1];
+}
+
+// the tile's 64 chunks: bytes [tb, tb + 8192) from P.base (tb >= -127, the
+// chunk grid is 128-byte aligned in memory); the buffer range ends in the
+// dword holding the batch's last byte, so loads past it read zeros and touch
+// nothing
+template <int ABLATE>
+__device__ __forceinline__ void stream_issue(const CrcParams& P, int64_t tb, uintptr_t end4, uint32_t lane,
+                                             uint32_t (&u)[32]) {
+  const uintptr_t t0 = (uintptr_t)P.base + (uintptr_t)tb;
+  const uint64_t span = end4 - t0;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char*>(P.base + tb), (short)0, (int)(span < 0x7FFFFFFFull ? span : 0x7FFFFFFFull), 0x00020000);
+  const uint32_t vo = lane * 128u;
+  if (ABLATE == 2) {  // diagnostic: compute only (no payload loads; results invalid)
+#pragma unroll
+    for (int j = 0; j < 32; ++j) u[j] = (uint32_t)tb * 0x9E3779B1u + lane + j;
+    return;
+  }
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 16u * g, 0, 0);
+    u[4 * g + 0] = v[0];
+    u[4 * g + 1] = v[1];
+    u[4 * g + 2] = v[2];
+    u[4 * g + 3] = v[3];
+  }
+  keep_live(vo);
+}
+
+__device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
+  return (uint64_t)wave_or_u32((uint32_t)x) | ((uint64_t)wave_or_u32((uint32_t)(x >> 32)) << 32);
+}
+
+template <int ABLATE = 0>
+__global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
+  if (!*P.sflag) return;  // not a packed batch of >= 64-byte records: the walking kernel takes it
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  build_lds_tables(smem, P);
+  __syncthreads();  // the walk columns reuse the khi area, x^(8m) the klo area
+  build_walk_cols(P);
+  if (threadIdx.x < 64u) {  // x^(8m), m = threadIdx.x: m zero-byte steps of the register from x^0
+    uint32_t R = 0x80000000u;
+    for (uint32_t i = 0; i < threadIdx.x; ++i) R = (R >> 8) ^ P.master[R & 0xFFu];
+    *(__attribute__((address_space(3))) uint32_t*)(size_t)(LDS_XM_OFF + 4u * threadIdx.x) = R;
+  } else if (threadIdx.x < 68u) {
+    *(__attribute__((address_space(3))) uint32_t*)(size_t)(LDS_XM_OFF + 4u * threadIdx.x) =
+        stream_xinv(threadIdx.x - 64u);
+  }
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lo = (lane & 31u) * 4u, hi = lo | 0x10000u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const uint64_t n = P.nrec;
+  const uint64_t b_lo = P.scuts[wave], b_hi = P.scuts[wave + 1];
+  if (b_lo >= b_hi) return;  // no record ends in this wave's range
+  const uint64_t dend = P.off[n - 1] + P.len[n - 1];
+  const uintptr_t end4 = ((uintptr_t)P.base + dend + 3u) & ~(uintptr_t)3;
+  // chunk grid origin, relative to P.base (128-byte aligned in memory)
+  const int64_t a0 = (int64_t)((((uintptr_t)P.base + P.off[0]) & ~(uintptr_t)127) - (uintptr_t)P.base);
+  const uint64_t t_first = (uint64_t)((int64_t)stream_pos(P, b_lo, dend) - a0) >> 13;
+  const uint64_t t_last = (uint64_t)((int64_t)stream_pos(P, b_hi, dend) - a0) >> 13;
+  const uint64_t ntile = t_last - t_first + 1u;
+  auto tbase = [&](uint64_t t) -> int64_t { return a0 + (int64_t)(t << 13); };
+
+  StreamWin Wn;
+  uint64_t bt = b_lo;  // the first boundary of the tile being mapped
+  uint32_t carry = 0;  // the record crossing into the next tile, aligned to this tile's end
+  stream_win_issue(P, bt, lane, Wn);
+
+  auto process = [&](const uint32_t (&U)[32], uint64_t t) {
+    const int64_t tb = tbase(t);
+    // --- map: this tile's boundaries, bt .. bt+cnt-1 (window lanes); ra/rb:
+    // tile-relative byte of boundary bt+lane / bt+64+lane (chunk = r >> 7)
+    const uint64_t ia = bt + lane, ib = bt + 64u + lane;
+    const int64_t ra64 = (int64_t)(ia < n ? Wn.a : dend) - tb, rb64 = (int64_t)(ib < n ? Wn.b : dend) - tb;
+    const bool ina = ia <= b_hi && ra64 < 8192, inb = ib <= b_hi && rb64 < 8192;
+    const uint32_t ra = (uint32_t)ra64 & 8191u, rb = (uint32_t)rb64 & 8191u;
+    const uint64_t bal_a = __ballot(ina), bal_b = __ballot(inb);
+    const uint32_t na = (uint32_t)__builtin_popcountll(bal_a), nb = (uint32_t)__builtin_popcountll(bal_b);
+    const uint32_t cnt = na + nb;
+    const uint64_t bt0 = bt;
+    bt += cnt;
+    stream_win_issue(P, bt, lane, Wn);  // the next tile's window (lands while this tile is checksummed)
+    uint64_t M1, M2;
+    bool any2;
+    {
+      const uint32_t ca = ra >> 7, cb = rb >> 7;
+      const uint32_t ca63 = (uint32_t)__builtin_amdgcn_readlane((int)ca, 63);
+      const uint32_t pca = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ca, 0x138, 0xF, 0xF, false);  // wave_shr:1
+      const uint32_t pcb0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cb, 0x138, 0xF, 0xF, false);
+      const uint32_t pcb = lane ? pcb0 : ca63;
+      const bool seca = ina && lane > 0u && pca == ca;
+      const bool secb = inb && pcb == cb && (lane > 0u || (bal_a >> 63));
+      M1 = wave_or_u64(((ina && !seca) ? (1ull << ca) : 0ull) | ((inb && !secb) ? (1ull << cb) : 0ull));
+      any2 = __any(seca || secb);
+      M2 = any2 ? wave_or_u64((seca ? (1ull << ca) : 0ull) | (secb ? (1ull << cb) : 0ull)) : 0ull;
+    }
+    // --- chunk-lane view: this chunk's boundaries jc0 (chain 0), jc1 (chain 1); 128 = none
+    uint32_t jc0, jc1;
+    {
+      const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
+      const uint32_t k1 = (uint32_t)__builtin_popcountll(M1 & below) + (uint32_t)__builtin_popcountll(M2 & below);
+      const bool b1 = (M1 >> lane) & 1ull, b2 = (M2 >> lane) & 1ull;
+      const int s1 = (int)((k1 & 63u) << 2);
+      const uint32_t j1a = (uint32_t)__builtin_amdgcn_ds_bpermute(s1, (int)ra);
+      const uint32_t j1b = (uint32_t)__builtin_amdgcn_ds_bpermute(s1, (int)rb);
+      const uint32_t j1 = (k1 < 64u ? j1a : j1b) & 127u;
+      uint32_t j2 = 128u;
+      if (any2) {
+        const uint32_t k2 = k1 + 1u;
+        const int s2 = (int)((k2 & 63u) << 2);
+        const uint32_t j2a = (uint32_t)__builtin_amdgcn_ds_bpermute(s2, (int)ra);
+        const uint32_t j2b = (uint32_t)__builtin_amdgcn_ds_bpermute(s2, (int)rb);
+        j2 = b2 ? ((k2 < 64u ? j2a : j2b) & 127u) : 128u;
+      }
+      jc0 = (b1 && j1 < 64u) ? j1 : 128u;
+      jc1 = b2 ? j2 : ((b1 && j1 >= 64u) ? j1 : 128u);
+    }
+    const uint32_t Km0 = wave_or_u32(jc0 < 128u ? (1u << (jc0 >> 2)) : 0u);
+    const uint32_t Km1 = wave_or_u32(jc1 < 128u ? (1u << ((jc1 >> 2) - 16u)) : 0u);
+    if (ABLATE == 3) {  // diagnostic: payload loads only
+      uint32_t x = 0;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) x ^= U[k];
+      if (x == 0x9E3779B1u) P.out[0] = x ^ jc0 ^ jc1;
+      return;
+    }
+    // --- the chunk's two chains, with the register resets at its boundaries
+    // (mask and init term recomputed inside the rare boundary bodies: fewer
+    // registers live through the loop)
+    uint32_t c0 = U[0], c1 = U[16], cap0 = 0u, cap1 = 0u;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      uint32_t e0 = 0u, e1 = 0u;
+      if (Km0 & (1u << k)) {  // wave-uniform: some lane's chain-0 boundary is in word k
+        const uint32_t A = crc_word(smem, c0 ^ (U[k] & (0xFFFFFFFFu << (8u * (jc0 & 3u)))), 0u, lo, hi);
+        const bool mine = (jc0 >> 2) == (uint32_t)k;
+        cap0 = mine ? A : cap0;
+        e0 = mine ? (A ^ stream_init(jc0 & 3u)) : 0u;
+      }
+      if (Km1 & (1u << k)) {
+        const uint32_t A = crc_word(smem, c1 ^ (U[16 + k] & (0xFFFFFFFFu << (8u * (jc1 & 3u)))), 0u, lo, hi);
+        const bool mine = (jc1 >> 2) == (uint32_t)(16 + k);
+        cap1 = mine ? A : cap1;
+        e1 = mine ? (A ^ stream_init(jc1 & 3u)) : 0u;
+      }
+      c0 = crc_step_x(smem, c0, k + 1 < 16 ? U[k + 1] : 0u, lo, hi) ^ e0;
+      c1 = crc_step_x(smem, c1, k + 1 < 16 ? U[17 + k] : 0u, lo, hi) ^ e1;
+    }
+    const uint32_t R0 = c0;
+    const uint32_t T = (jc1 < 128u) ? c1 : (shift_bytes32<2>(smem, c0) ^ c1);
+    // --- Horner inside the tile: T to the chunk before the next boundary's chunk
+    const uint64_t above = lane == 63u ? 0ull : (M1 >> (lane + 1u)) << (lane + 1u);
+    const uint32_t cn = above ? (uint32_t)__builtin_ctzll(above) : 64u;
+    const uint32_t X = wave_prefix_xor(walk_mulcol(T, cn - 1u - lane));
+    // --- records: window lane i finishes the record that ends at boundary bt0 + i
+    const uint32_t ca = ra >> 7, cb = rb >> 7;
+    const uint32_t c00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ca);
+    const uint32_t cterm = na ? walk_mulcol_uniform(carry, c00, lane) : 0u;
+    auto finish = [&](bool in, uint32_t r, uint32_t ls, bool from_carry, uint64_t bidx) {
+      const uint32_t c = r >> 7, j = r & 127u;
+      const uint32_t Xc = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((c - 1u) & 63u) << 2), (int)X);
+      const uint32_t Xl = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((ls - 1u) & 63u) << 2), (int)X);
+      const uint32_t H = (c ? Xc : 0u) ^ (from_carry ? cterm : (ls ? Xl : 0u));
+      const int sc = (int)(c << 2);
+      const uint32_t R0c = (uint32_t)__builtin_amdgcn_ds_bpermute(sc, (int)R0);
+      const uint32_t A0c = (uint32_t)__builtin_amdgcn_ds_bpermute(sc, (int)cap0);
+      const uint32_t A1c = (uint32_t)__builtin_amdgcn_ds_bpermute(sc, (int)cap1);
+      const bool h = j >= 64u;
+      const uint32_t Pv = h ? (shift_bytes32<2>(smem, H) ^ R0c) : H;
+      const uint32_t K = lds_ld(smem, LDS_XM_OFF + ((j & 63u) << 2));
+      const uint32_t Ki = lds_ld(smem, LDS_XM_OFF + 256u + ((j & 3u) << 2));
+      const uint32_t v = gf2_mulmod_seq(Pv, K) ^ gf2_mulmod_seq(h ? A1c : A0c, Ki);
+      if (in && bidx > b_lo) P.out[bidx - 1u] = ~v;
+    };
+    {
+      const uint32_t ca63 = (uint32_t)__builtin_amdgcn_readlane((int)ca, 63);
+      const uint32_t pca = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ca, 0x138, 0xF, 0xF, false);
+      finish(ina, ra, pca, lane == 0u, bt0 + lane);
+      if (nb) {
+        const uint32_t pcb0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cb, 0x138, 0xF, 0xF, false);
+        finish(inb, rb, lane ? pcb0 : ca63, false, bt0 + 64u + lane);
+      }
+    }
+    // --- carry: the record active at the tile's end
+    const uint32_t X63 = (uint32_t)__builtin_amdgcn_readlane((int)X, 63);
+    if (cnt) {
+      const uint32_t cl = nb ? (uint32_t)__builtin_amdgcn_readlane((int)cb, (int)(nb - 1u))
+                             : (uint32_t)__builtin_amdgcn_readlane((int)ca, (int)(na - 1u));
+      carry = X63 ^ (cl ? (uint32_t)__builtin_amdgcn_readlane((int)X, (int)(cl - 1u)) : 0u);
+    } else {
+      carry = X63 ^ walk_mulcol_uniform(carry, 64u, lane);
+    }
+  };
+
+  uint32_t U0[32], U1[32];
+  stream_issue<ABLATE>(P, tbase(t_first), end4, lane, U0);
+  uint64_t i = 0;
+  for (; i + 2 <= ntile; i += 2) {
+    stream_issue<ABLATE>(P, tbase(t_first + i + 1), end4, lane, U1);
+    __builtin_amdgcn_sched_barrier(0);
+    process(U0, t_first + i);
+    stream_issue<ABLATE>(P, tbase(i + 2 < ntile ? t_first + i + 2 : t_last), end4, lane, U0);
+    __builtin_amdgcn_sched_barrier(0);
+    process(U1, t_first + i + 1);
+  }
+  if (i < ntile) process(U0, t_first + i);
 }
 }  // namespace lsmck
 
@@ -1503,6 +1807,31 @@ extern "C" int lsmk_launch_crc32_desc(const CrcParams* P, const uint64_t* block_
   return e == hipSuccess ? 0 : -(int)e;
 }
 
+
+extern "C" uint32_t lsmk_stream_waves(int ncu) { return (uint32_t)ncu * 16u; }
+
+// stream kernel: eligibility flag, per-wave cuts, the kernel.  The walking
+// kernel launched after it on the same stream exits when the flag is set.
+extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant, hipStream_t st) {
+  const uint64_t n = P->nrec;
+  if (n == 0) return 0;
+  hipError_t e = hipMemsetAsync(P->sflag, 1, 4, st);
+  if (e != hipSuccess) return -(int)e;
+  hipLaunchKernelGGL(stream_check, dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0, st, P->off, P->len, n, P->sflag);
+  const uint32_t W = lsmk_stream_waves(ncu);
+  hipLaunchKernelGGL(stream_cuts, dim3((W + 1u + 255u) / 256u), dim3(256), 0, st, *P, W);
+  const int ablate = (variant >> 8) & 0xF;
+  const void* fn = ablate == 3 ? (const void*)crc32_stream_kernel<3>
+                 : ablate == 2 ? (const void*)crc32_stream_kernel<2> : (const void*)crc32_stream_kernel<0>;
+  const size_t lds = LDS_SCRATCH_OFF;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return -(int)e;
+  void* args[] = {(void*)P};
+  e = hipLaunchKernel(fn, dim3(ncu), dim3(1024), args, lds, st);
+  if (e != hipSuccess) return -(int)e;
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : -(int)e;
+}
 
 extern "C" uint64_t lsmk_walk_sb_count(uint64_t n) { return (n + WALK_SB - 1) / WALK_SB; }
 

@@ -28,6 +28,8 @@ struct CrcParams {
   const uint32_t* zero;       // 256 zero bytes (16-aligned): the load window of empty segments
   const uint64_t* sb_prefix;  // walking descriptor kernel: exclusive segment prefix per WALK_SB-record superblock
   uint32_t* work;             // fixed ring kernel, claimed-block order: work counter (zeroed by the launcher)
+  uint32_t* sflag;            // stream kernel: nonzero = packed batch of >= 64-byte records (the walking kernel then exits)
+  uint64_t* scuts;            // stream kernel: first boundary of each wave's range (waves + 1 entries)
 };
 
 // SHA-256 batch job (lane per message).
@@ -73,6 +75,10 @@ int lsmk_launch_sha256(const lsmck::ShaParams* P, hipStream_t st);
 int lsmk_launch_sha256_slices(const lsmck::ShaSliceParams* P, hipStream_t st);
 uint64_t lsmk_walk_sb_count(uint64_t n);
 int lsmk_launch_crc32_walk(const lsmck::CrcParams* P, uint64_t* sb_prefix, int ncu, int variant, hipStream_t st);
+// stream kernel for packed batches of records >= 64 B (eligibility decided on
+// the device: P->sflag, P->scuts hold lsmk_stream_waves(ncu) + 1 entries)
+uint32_t lsmk_stream_waves(int ncu);
+int lsmk_launch_crc32_stream(const lsmck::CrcParams* P, int ncu, int variant, hipStream_t st);
 uint64_t lsmk_wal_words(uint64_t n);
 uint64_t lsmk_wal_scan_blocks(uint64_t n);
 int lsmk_wal_mark(const uint8_t* img, uint64_t n, uint64_t* bits, uint32_t* pre, uint32_t* bsum, uint32_t* total,
