@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--digest", default="crc32", choices=["crc32", "sha256"],
                     help="crc32 = the WAL record checksum (headline); sha256 = the SSTable digest "
                          "(checksums.rs) over the same records, reported against its int32 VALU roof")
+    ap.add_argument("--stream", type=int, default=1, choices=[0, 1],
+                    help="packed batches of >= 64-byte records (config 3): 1 = stream kernel (default), "
+                         "0 = walking kernel (A/B)")
     ap.add_argument("--walk", type=int, default=1, choices=[0, 1],
                     help="descriptor batches: 1 = walking kernel (default), 0 = r01 tile-map kernel (A/B)")
     ap.add_argument("--pack-align", type=int, default=1,
@@ -148,6 +151,8 @@ def main():
     ctx = Context(local)
     if a.walk != 1:
         ctx.set_option("crc_walk", a.walk)
+    if a.stream != 1:
+        ctx.set_option("crc_stream", a.stream)
 
     cfg = a.config
     seed = SEED[cfg]
@@ -241,7 +246,8 @@ def main():
                 # "f<n>" = sha_bucket_from n (first block count of the coarse buckets)
                 # "o<n>" = crc_order n (fixed ring kernel tile order)
                 # "p<n>" = sha_pair n (SHA-256: two blocks per load window)
-                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?(?:r(\d))?(?:b(\d))?(?:f(\d+))?(?:o(\d))?(?:p(\d))?", v)
+                # "s<n>" = crc_stream n (descriptor batches: 1 stream kernel where eligible, 0 walking kernel)
+                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?(?:r(\d))?(?:b(\d))?(?:f(\d+))?(?:o(\d))?(?:p(\d))?(?:s(\d))?", v)
                 if not m:
                     raise SystemExit(f"bad variant {v!r}")
                 kind, num, waves = m.group(1), int(m.group(2)), int(m.group(3) or 0)
@@ -255,6 +261,7 @@ def main():
                 ctx.set_option("sha_bucket_from", int(m.group(7) or 128))
                 ctx.set_option("crc_order", int(m.group(8) or 0))
                 ctx.set_option("sha_pair", int(m.group(9)) if m.group(9) is not None else 1)
+                ctx.set_option("crc_stream", int(m.group(10)) if m.group(10) is not None else 1)
                 step()
                 e0.record(stream)
                 for _ in range(a.steps):
@@ -271,6 +278,7 @@ def main():
         ctx.set_option("sha_bucket_shift", 2)
         ctx.set_option("sha_bucket_from", 128)
         ctx.set_option("sha_pair", 1)
+        ctx.set_option("crc_stream", 1)
         ctx.set_option("crc_order", 0)
         ab = {str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                        "GiBps_median": payload / GIB / (float(np.median(t)) * 1e-3)} for v, t in ab.items()}
@@ -336,7 +344,9 @@ def main():
             "traffic": traffic,
             # fixed records whose segment count divides 64 (configs 1, 2) run the
             # whole-tile ring kernel by default (lsmck_crc32.hip, LSMCK_DEFAULT_RING)
-            "kernel": (("crc32_walk_kernel" if a.walk else "crc32_desc_kernel") if (cfg == 3 or a.desc)
+            # config 3 is packed with records >= 64 B: the stream kernel takes it
+            "kernel": (("crc32_stream_kernel" if (cfg == 3 and a.walk and a.stream) else
+                        "crc32_walk_kernel" if a.walk else "crc32_desc_kernel") if (cfg == 3 or a.desc)
                        else "crc32_wring_kernel"),
             "algorithmic_bytes_per_launch": algo_bytes,
             "launch_ms_hip_events": round(ev_ms, 4),

@@ -40,6 +40,7 @@ namespace {
 constexpr uint64_t kMaxSegsPerLaunch = (1ull << 32) - 64;  // 32-bit segment indices in the kernels
 constexpr int kVariantTileMap = 0x100000;  // descriptor batches: the r01 tile-map kernel instead of the walking one
 constexpr int kVariantNoStream = 0x200000;  // descriptor batches: no stream kernel for packed >= 64-byte records (A/B)
+constexpr int kVariantStreamOnly = 0x400000;  // diagnostic: the stream kernel alone (ineligible batches get no CRCs)
 constexpr size_t kChunkBytes = 64ull << 20;                // host staging chunk (payload)
 constexpr size_t kChunkRecs = 1u << 20;                    // host staging chunk (records)
 
@@ -355,6 +356,7 @@ int crc_desc_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const 
       P.scuts = sc.scuts;
       rc = lsmk_launch_crc32_stream(&P, ctx->ncu, ctx->variant, st);
       if (rc) return launch_rc(rc, "crc32_stream kernel");
+      if (ctx->variant & kVariantStreamOnly) return 0;
     }
     rc = lsmk_launch_crc32_walk(&P, sc.block_sum, ctx->ncu, ctx->variant, st);
     return rc ? launch_rc(rc, "crc32_walk kernel") : 0;
@@ -848,10 +850,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->variant = (ctx->variant & ~0x3000000) | ((int)value << 24);
     return 0;
   }
-  if (!strcmp(key, "crc_stream")) {  // A/B: descriptor batches, 1 = stream kernel for packed >= 64-byte records (default)
-    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream must be 0 or 1");
+  if (!strcmp(key, "crc_stream")) {  // A/B: descriptor batches, 1 = stream kernel for packed >= 64-byte records
+                                     // (default), 0 = walking kernel only, 2 = stream kernel only (diagnostic)
+    if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream must be 0, 1 or 2");
     std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~kVariantNoStream) | (value ? 0 : kVariantNoStream);
+    ctx->variant = (ctx->variant & ~(kVariantNoStream | kVariantStreamOnly)) |
+                   (value == 0 ? kVariantNoStream : value == 2 ? kVariantStreamOnly : 0);
     return 0;
   }
   if (!strcmp(key, "crc_walk")) {  // A/B: descriptor batches, 1 = walking kernel (default), 0 = r01 tile-map kernel

@@ -30,6 +30,7 @@ def _device(ctx, data, off, ln, shift=0, exact=False):
     d = ctx.alloc(size + shift)
     d.upload(np.ascontiguousarray(data[:size]), offset=shift)
     d_o, d_l, out = ctx.alloc(8 * n), ctx.alloc(4 * n), ctx.alloc(4 * n)
+    out.upload(np.full(n, 0xA5A5A5A5, dtype=np.uint32))  # unwritten outputs show
     d_o.upload(off)
     d_l.upload(ln)
     ctx.crc32_device(d.ptr + shift, d_o.ptr, d_l.ptr, n, out.ptr)
@@ -42,9 +43,14 @@ def _device(ctx, data, off, ln, shift=0, exact=False):
 
 @pytest.fixture
 def stream_ab(ctx):
+    """(stream kernel alone, walking kernel alone) on the same records: the
+    first would leave the outputs unwritten if the batch were declined."""
     def run(*args, **kw):
-        ctx.set_option("crc_stream", 1)
-        a = _device(ctx, *args, **kw)
+        ctx.set_option("crc_stream", 2)
+        try:
+            a = _device(ctx, *args, **kw)
+        finally:
+            ctx.set_option("crc_stream", 1)
         ctx.set_option("crc_stream", 0)
         try:
             b = _device(ctx, *args, **kw)
@@ -121,6 +127,11 @@ def test_ineligible_batches_take_the_walking_kernel(ctx, case):
     data = O.gen_stream(0x57AE0300, 0, int(off.max()) + 4000)
     got = _device(ctx, data, off, ln)
     assert np.array_equal(got, O.crc32_batch(data, off, ln, threads=8))
+    ctx.set_option("crc_stream", 2)  # the stream kernel alone declines: nothing written
+    try:
+        assert (_device(ctx, data, off, ln) == 0xA5A5A5A5).all()
+    finally:
+        ctx.set_option("crc_stream", 1)
 
 
 def test_host_batches_use_it_too(ctx):
