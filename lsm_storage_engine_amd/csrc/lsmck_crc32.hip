@@ -1386,21 +1386,28 @@ __global__ __launch_bounds__(1024) void crc32_walk_kernel(CrcParams P) {
 // decided on the device (stream_check); the walking kernel, launched after
 // this one, exits when the batch was taken here.
 #define STREAM_MIN_LEN 64u
-#define LDS_XM_OFF LDS_KLO_OFF  // x^(8m), m = 0..63, then x^(-8(4-t)), t = 0..3 (the descriptor kernels' klo
-                                // area, after the walk columns); from LDS, so that hipcc cannot fold a constant
-                                // factor into 32 hoisted shifted copies (70 spilled VGPRs)
+// LDS columns K (x) x^i, i = 0..31 (128 B per factor K) of the finish factors,
+// in areas this kernel does not otherwise use: x^(8m) for m = 0..31 over the
+// shift-by-32-bytes table, m = 32..63 over the shift-by-96-bytes table (only
+// shift-by-64 is used here), x^(-8(4-t)) for t = 0..3 in the klo area
+#define LDS_XMC_OFF(m) ((m) < 32u ? LDS_SHIFT_OFF + (m) * 128u : LDS_SHIFT_OFF + 8192u + ((m) - 32u) * 128u)
+#define LDS_XIC_OFF(t) (LDS_KLO_OFF + (t) * 128u)
 
-// gf2_mulmod evaluated step by step: the empty asm makes a, b and p opaque at
-// every step, so hipcc cannot compute the 32 masks and 32 shifted factors of
-// two multiplies up front (it did: 128 VGPRs and ~240 B/lane of spills)
-__device__ __forceinline__ uint32_t gf2_mulmod_seq(uint32_t a, uint32_t b) {
+// v (x) K from K's 32 LDS columns at `base` (8 ds_read_b128 + 32 v_bitop3), in
+// two halves: hipcc otherwise loads the columns of both finish multiplies at
+// once (64 VGPRs) next to the next tile's payload in flight, and spills.  (The
+// generic gf2_mulmod here had its constant factor folded into 32 hoisted
+// shifted copies: ~70 spilled VGPRs.)
+__device__ __forceinline__ uint32_t stream_mulcol(uint32_t v, uint32_t base) {
   uint32_t p = 0;
 #pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    asm volatile("" : "+v"(a), "+v"(b), "+v"(p));
-    const uint32_t m = (uint32_t)((int32_t)(a << i) >> 31);
-    p = __builtin_amdgcn_bitop3_b32(p, b, m, 0x78);  // p ^ (b & m)
-    b = (b >> 1) ^ (0xEDB88320u & (0u - (b & 1u)));
+  for (int g = 0; g < 8; ++g) {
+    if (g == 4) __builtin_amdgcn_sched_barrier(0);
+    const u32x4 c = lds_ld128(base + g * 16u);
+    p = __builtin_amdgcn_bitop3_b32(p, c.x, (uint32_t)((int32_t)(v << (4 * g + 0)) >> 31), 0x78);
+    p = __builtin_amdgcn_bitop3_b32(p, c.y, (uint32_t)((int32_t)(v << (4 * g + 1)) >> 31), 0x78);
+    p = __builtin_amdgcn_bitop3_b32(p, c.z, (uint32_t)((int32_t)(v << (4 * g + 2)) >> 31), 0x78);
+    p = __builtin_amdgcn_bitop3_b32(p, c.w, (uint32_t)((int32_t)(v << (4 * g + 3)) >> 31), 0x78);
   }
   return p;
 }
@@ -1490,13 +1497,21 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
   build_lds_tables(smem, P);
   __syncthreads();  // the walk columns reuse the khi area, x^(8m) the klo area
   build_walk_cols(P);
-  if (threadIdx.x < 64u) {  // x^(8m), m = threadIdx.x: m zero-byte steps of the register from x^0
-    uint32_t R = 0x80000000u;
-    for (uint32_t i = 0; i < threadIdx.x; ++i) R = (R >> 8) ^ P.master[R & 0xFFu];
-    *(__attribute__((address_space(3))) uint32_t*)(size_t)(LDS_XM_OFF + 4u * threadIdx.x) = R;
-  } else if (threadIdx.x < 68u) {
-    *(__attribute__((address_space(3))) uint32_t*)(size_t)(LDS_XM_OFF + 4u * threadIdx.x) =
-        stream_xinv(threadIdx.x - 64u);
+  if (threadIdx.x >= 128u && threadIdx.x < 196u) {  // the finish factors' columns
+    const uint32_t f = threadIdx.x - 128u;
+    uint32_t K, base;
+    if (f < 64u) {  // x^(8m): m zero-byte steps of the register from x^0
+      K = 0x80000000u;
+      for (uint32_t i = 0; i < f; ++i) K = (K >> 8) ^ P.master[K & 0xFFu];
+      base = LDS_XMC_OFF(f);
+    } else {
+      K = stream_xinv(f - 64u);
+      base = LDS_XIC_OFF(f - 64u);
+    }
+    for (uint32_t i = 0; i < 32u; ++i) {
+      *(__attribute__((address_space(3))) uint32_t*)(size_t)(base + 4u * i) = K;
+      K = (K >> 1) ^ (0xEDB88320u & (0u - (K & 1u)));
+    }
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
@@ -1585,16 +1600,20 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     for (int k = 0; k < 16; ++k) {
       uint32_t e0 = 0u, e1 = 0u;
       if (Km0 & (1u << k)) {  // wave-uniform: some lane's chain-0 boundary is in word k
-        const uint32_t A = crc_word(smem, c0 ^ (U[k] & (0xFFFFFFFFu << (8u * (jc0 & 3u)))), 0u, lo, hi);
-        const bool mine = (jc0 >> 2) == (uint32_t)k;
+        uint32_t jj = jc0;
+        asm volatile("" : "+v"(jj));  // mask and init term here, not hoisted: 4 VGPRs fewer through the loop
+        const uint32_t A = crc_word(smem, c0 ^ (U[k] & (0xFFFFFFFFu << (8u * (jj & 3u)))), 0u, lo, hi);
+        const bool mine = (jj >> 2) == (uint32_t)k;
         cap0 = mine ? A : cap0;
-        e0 = mine ? (A ^ stream_init(jc0 & 3u)) : 0u;
+        e0 = mine ? (A ^ stream_init(jj & 3u)) : 0u;
       }
       if (Km1 & (1u << k)) {
-        const uint32_t A = crc_word(smem, c1 ^ (U[16 + k] & (0xFFFFFFFFu << (8u * (jc1 & 3u)))), 0u, lo, hi);
-        const bool mine = (jc1 >> 2) == (uint32_t)(16 + k);
+        uint32_t jj = jc1;
+        asm volatile("" : "+v"(jj));
+        const uint32_t A = crc_word(smem, c1 ^ (U[16 + k] & (0xFFFFFFFFu << (8u * (jj & 3u)))), 0u, lo, hi);
+        const bool mine = (jj >> 2) == (uint32_t)(16 + k);
         cap1 = mine ? A : cap1;
-        e1 = mine ? (A ^ stream_init(jc1 & 3u)) : 0u;
+        e1 = mine ? (A ^ stream_init(jj & 3u)) : 0u;
       }
       c0 = crc_step_x(smem, c0, k + 1 < 16 ? U[k + 1] : 0u, lo, hi) ^ e0;
       c1 = crc_step_x(smem, c1, k + 1 < 16 ? U[17 + k] : 0u, lo, hi) ^ e1;
@@ -1620,9 +1639,9 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
       const uint32_t A1c = (uint32_t)__builtin_amdgcn_ds_bpermute(sc, (int)cap1);
       const bool h = j >= 64u;
       const uint32_t Pv = h ? (shift_bytes32<2>(smem, H) ^ R0c) : H;
-      const uint32_t K = lds_ld(smem, LDS_XM_OFF + ((j & 63u) << 2));
-      const uint32_t Ki = lds_ld(smem, LDS_XM_OFF + 256u + ((j & 3u) << 2));
-      const uint32_t v = gf2_mulmod_seq(Pv, K) ^ gf2_mulmod_seq(h ? A1c : A0c, Ki);
+      const uint32_t v1 = stream_mulcol(Pv, LDS_XMC_OFF(j & 63u));
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t v = v1 ^ stream_mulcol(h ? A1c : A0c, LDS_XIC_OFF(j & 3u));
       if (in && bidx > b_lo) P.out[bidx - 1u] = ~v;
     };
     {
