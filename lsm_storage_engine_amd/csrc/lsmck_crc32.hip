@@ -1490,8 +1490,8 @@ __device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
   return (uint64_t)wave_or_u32((uint32_t)x) | ((uint64_t)wave_or_u32((uint32_t)(x >> 32)) << 32);
 }
 
-template <int ABLATE = 0>
-__global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
+template <int ABLATE = 0, int BLOCK = 1024>
+__global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
   if (!*P.sflag) return;  // not a packed batch of >= 64-byte records: the walking kernel takes it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   build_lds_tables(smem, P);
@@ -1583,8 +1583,9 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
       jc0 = (b1 && j1 < 64u) ? j1 : 128u;
       jc1 = b2 ? j2 : ((b1 && j1 >= 64u) ? j1 : 128u);
     }
-    const uint32_t Km0 = wave_or_u32(jc0 < 128u ? (1u << (jc0 >> 2)) : 0u);
-    const uint32_t Km1 = wave_or_u32(jc1 < 128u ? (1u << ((jc1 >> 2) - 16u)) : 0u);
+    // (ABLATE 4, diagnostic: no boundary bodies; results invalid)
+    const uint32_t Km0 = ABLATE == 4 ? 0u : wave_or_u32(jc0 < 128u ? (1u << (jc0 >> 2)) : 0u);
+    const uint32_t Km1 = ABLATE == 4 ? 0u : wave_or_u32(jc1 < 128u ? (1u << ((jc1 >> 2) - 16u)) : 0u);
     if (ABLATE == 3) {  // diagnostic: payload loads only
       uint32_t x = 0;
 #pragma unroll
@@ -1623,7 +1624,8 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     // --- Horner inside the tile: T to the chunk before the next boundary's chunk
     const uint64_t above = lane == 63u ? 0ull : (M1 >> (lane + 1u)) << (lane + 1u);
     const uint32_t cn = above ? (uint32_t)__builtin_ctzll(above) : 64u;
-    const uint32_t X = wave_prefix_xor(walk_mulcol(T, cn - 1u - lane));
+    // (ABLATE 6, diagnostic: no per-lane Horner shift)
+    const uint32_t X = wave_prefix_xor(ABLATE == 6 ? (T ^ cn) : walk_mulcol(T, cn - 1u - lane));
     // --- records: window lane i finishes the record that ends at boundary bt0 + i
     const uint32_t ca = ra >> 7, cb = rb >> 7;
     const uint32_t c00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ca);
@@ -1637,18 +1639,32 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
       const uint32_t R0c = (uint32_t)__builtin_amdgcn_ds_bpermute(sc, (int)R0);
       const uint32_t A0c = (uint32_t)__builtin_amdgcn_ds_bpermute(sc, (int)cap0);
       const uint32_t A1c = (uint32_t)__builtin_amdgcn_ds_bpermute(sc, (int)cap1);
-      const bool h = j >= 64u;
-      const uint32_t Pv = h ? (shift_bytes32<2>(smem, H) ^ R0c) : H;
-      const uint32_t v1 = stream_mulcol(Pv, LDS_XMC_OFF(j & 63u));
-      __builtin_amdgcn_sched_barrier(0);
-      const uint32_t v = v1 ^ stream_mulcol(h ? A1c : A0c, LDS_XIC_OFF(j & 3u));
-      if (in && bidx > b_lo) P.out[bidx - 1u] = ~v;
+      // only the lanes holding a record from here on (a few per tile): the LDS
+      // reads below cost per active lane, and all 64 lanes doing them cost
+      // 4.8 of 25.6 ms (crc_ablate 5); the bpermutes above need every lane
+      if (in && bidx > b_lo) {
+        const bool h = j >= 64u;
+        const uint32_t Pv = h ? (shift_bytes32<2>(smem, H) ^ R0c) : H;
+        uint32_t v;
+        if (ABLATE == 7) {  // A/B: the multiplies on the VALU (factors from LDS column 0)
+          v = gf2_mulmod(Pv, lds_ld(smem, LDS_XMC_OFF(j & 63u))) ^ gf2_mulmod(h ? A1c : A0c, lds_ld(smem, LDS_XIC_OFF(j & 3u)));
+        } else {
+          const uint32_t v1 = stream_mulcol(Pv, LDS_XMC_OFF(j & 63u));
+          __builtin_amdgcn_sched_barrier(0);
+          v = v1 ^ stream_mulcol(h ? A1c : A0c, LDS_XIC_OFF(j & 3u));
+        }
+        P.out[bidx - 1u] = ~v;
+      }
     };
     {
       const uint32_t ca63 = (uint32_t)__builtin_amdgcn_readlane((int)ca, 63);
       const uint32_t pca = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ca, 0x138, 0xF, 0xF, false);
-      finish(ina, ra, pca, lane == 0u, bt0 + lane);
-      if (nb) {
+      if (ABLATE == 5) {  // diagnostic: no record finish (one store keeps the tile's work alive)
+        if (X == 0x9E3779B1u) P.out[0] = X ^ R0 ^ cap0 ^ cap1;
+      } else {
+        finish(ina, ra, pca, lane == 0u, bt0 + lane);
+      }
+      if (ABLATE != 5 && nb) {
         const uint32_t pcb0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cb, 0x138, 0xF, 0xF, false);
         finish(inb, rb, lane ? pcb0 : ca63, false, bt0 + 64u + lane);
       }
@@ -1837,16 +1853,25 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   hipError_t e = hipMemsetAsync(P->sflag, 1, 4, st);
   if (e != hipSuccess) return -(int)e;
   hipLaunchKernelGGL(stream_check, dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0, st, P->off, P->len, n, P->sflag);
-  const uint32_t W = lsmk_stream_waves(ncu);
+  // 0x20: 12-wave workgroups (168 VGPRs per lane instead of 128)
+  const bool w12 = (variant & 0x20) != 0;
+  const int block = w12 ? 768 : 1024;
+  const uint32_t W = (uint32_t)ncu * (uint32_t)(block / 64);
   hipLaunchKernelGGL(stream_cuts, dim3((W + 1u + 255u) / 256u), dim3(256), 0, st, *P, W);
   const int ablate = (variant >> 8) & 0xF;
-  const void* fn = ablate == 3 ? (const void*)crc32_stream_kernel<3>
-                 : ablate == 2 ? (const void*)crc32_stream_kernel<2> : (const void*)crc32_stream_kernel<0>;
+  const void* fn = (ablate >= 4 && ablate <= 7 && !w12)
+                       ? (ablate == 4 ? (const void*)crc32_stream_kernel<4>
+                          : ablate == 5 ? (const void*)crc32_stream_kernel<5>
+                          : ablate == 6 ? (const void*)crc32_stream_kernel<6> : (const void*)crc32_stream_kernel<7>)
+                 : w12 ? (ablate == 3 ? (const void*)crc32_stream_kernel<3, 768>
+                          : ablate == 2 ? (const void*)crc32_stream_kernel<2, 768> : (const void*)crc32_stream_kernel<0, 768>)
+                       : (ablate == 3 ? (const void*)crc32_stream_kernel<3>
+                          : ablate == 2 ? (const void*)crc32_stream_kernel<2> : (const void*)crc32_stream_kernel<0>);
   const size_t lds = LDS_SCRATCH_OFF;
   e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return -(int)e;
   void* args[] = {(void*)P};
-  e = hipLaunchKernel(fn, dim3(ncu), dim3(1024), args, lds, st);
+  e = hipLaunchKernel(fn, dim3(ncu), dim3(block), args, lds, st);
   if (e != hipSuccess) return -(int)e;
   e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
