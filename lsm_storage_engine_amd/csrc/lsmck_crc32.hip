@@ -1393,16 +1393,13 @@ __global__ __launch_bounds__(1024) void crc32_walk_kernel(CrcParams P) {
 #define LDS_XMC_OFF(m) ((m) < 32u ? LDS_SHIFT_OFF + (m) * 128u : LDS_SHIFT_OFF + 8192u + ((m) - 32u) * 128u)
 #define LDS_XIC_OFF(t) (LDS_KLO_OFF + (t) * 128u)
 
-// v (x) K from K's 32 LDS columns at `base` (8 ds_read_b128 + 32 v_bitop3), in
-// two halves: hipcc otherwise loads the columns of both finish multiplies at
-// once (64 VGPRs) next to the next tile's payload in flight, and spills.  (The
-// generic gf2_mulmod here had its constant factor folded into 32 hoisted
-// shifted copies: ~70 spilled VGPRs.)
+// v (x) K from K's 32 LDS columns at `base` (8 ds_read_b128 + 32 v_bitop3).
+// (The generic gf2_mulmod here had its factor folded into 32 hoisted shifted
+// copies: ~70 spilled VGPRs.)
 __device__ __forceinline__ uint32_t stream_mulcol(uint32_t v, uint32_t base) {
   uint32_t p = 0;
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
-    if (g == 4) __builtin_amdgcn_sched_barrier(0);
     const u32x4 c = lds_ld128(base + g * 16u);
     p = __builtin_amdgcn_bitop3_b32(p, c.x, (uint32_t)((int32_t)(v << (4 * g + 0)) >> 31), 0x78);
     p = __builtin_amdgcn_bitop3_b32(p, c.y, (uint32_t)((int32_t)(v << (4 * g + 1)) >> 31), 0x78);
@@ -1649,9 +1646,7 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
         if (ABLATE == 7) {  // A/B: the multiplies on the VALU (factors from LDS column 0)
           v = gf2_mulmod(Pv, lds_ld(smem, LDS_XMC_OFF(j & 63u))) ^ gf2_mulmod(h ? A1c : A0c, lds_ld(smem, LDS_XIC_OFF(j & 3u)));
         } else {
-          const uint32_t v1 = stream_mulcol(Pv, LDS_XMC_OFF(j & 63u));
-          __builtin_amdgcn_sched_barrier(0);
-          v = v1 ^ stream_mulcol(h ? A1c : A0c, LDS_XIC_OFF(j & 3u));
+          v = stream_mulcol(Pv, LDS_XMC_OFF(j & 63u)) ^ stream_mulcol(h ? A1c : A0c, LDS_XIC_OFF(j & 3u));
         }
         P.out[bidx - 1u] = ~v;
       }
