@@ -1487,7 +1487,7 @@ __device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
   return (uint64_t)wave_or_u32((uint32_t)x) | ((uint64_t)wave_or_u32((uint32_t)(x >> 32)) << 32);
 }
 
-template <int ABLATE = 0, int BLOCK = 1024>
+template <int ABLATE = 0, int BLOCK = 1024, int SLOTS = 2>
 __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
   if (!*P.sflag) return;  // not a packed batch of >= 64-byte records: the walking kernel takes it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1531,7 +1531,7 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
   uint32_t carry = 0;  // the record crossing into the next tile, aligned to this tile's end
   stream_win_issue(P, bt, lane, Wn);
 
-  auto process = [&](const uint32_t (&U)[32], uint64_t t) {
+  auto process = [&](const uint32_t (&U)[32], uint64_t t, auto&& issue_next) {
     const int64_t tb = tbase(t);
     // --- map: this tile's boundaries, bt .. bt+cnt-1 (window lanes); ra/rb:
     // tile-relative byte of boundary bt+lane / bt+64+lane (chunk = r >> 7)
@@ -1545,6 +1545,10 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     const uint64_t bt0 = bt;
     bt += cnt;
     stream_win_issue(P, bt, lane, Wn);  // the next tile's window (lands while this tile is checksummed)
+    // then the payload SLOTS-1 tiles ahead: after the window, so that waiting
+    // for the window at the next tile never waits for that payload
+    issue_next();
+    __builtin_amdgcn_sched_barrier(0);
     uint64_t M1, M2;
     bool any2;
     {
@@ -1675,18 +1679,30 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     }
   };
 
+  // payload slots: SLOTS - 1 tiles in flight while one is checksummed; tiles
+  // past the run reload its last tile (in bounds, unused)
+  auto tcl = [&](uint64_t x) -> int64_t { return tbase(x < ntile ? t_first + x : t_last); };
+  auto none = [] {};
   uint32_t U0[32], U1[32];
-  stream_issue<ABLATE>(P, tbase(t_first), end4, lane, U0);
+  stream_issue<ABLATE>(P, tcl(0), end4, lane, U0);
   uint64_t i = 0;
-  for (; i + 2 <= ntile; i += 2) {
-    stream_issue<ABLATE>(P, tbase(t_first + i + 1), end4, lane, U1);
-    __builtin_amdgcn_sched_barrier(0);
-    process(U0, t_first + i);
-    stream_issue<ABLATE>(P, tbase(i + 2 < ntile ? t_first + i + 2 : t_last), end4, lane, U0);
-    __builtin_amdgcn_sched_barrier(0);
-    process(U1, t_first + i + 1);
+  if constexpr (SLOTS == 3) {
+    uint32_t U2[32];
+    stream_issue<ABLATE>(P, tcl(1), end4, lane, U1);
+    for (; i + 3 <= ntile; i += 3) {
+      process(U0, t_first + i, [&] { stream_issue<ABLATE>(P, tcl(i + 2), end4, lane, U2); });
+      process(U1, t_first + i + 1, [&] { stream_issue<ABLATE>(P, tcl(i + 3), end4, lane, U0); });
+      process(U2, t_first + i + 2, [&] { stream_issue<ABLATE>(P, tcl(i + 4), end4, lane, U1); });
+    }
+    if (i < ntile) process(U0, t_first + i, none);
+    if (i + 1 < ntile) process(U1, t_first + i + 1, none);
+  } else {
+    for (; i + 2 <= ntile; i += 2) {
+      process(U0, t_first + i, [&] { stream_issue<ABLATE>(P, tcl(i + 1), end4, lane, U1); });
+      process(U1, t_first + i + 1, [&] { stream_issue<ABLATE>(P, tcl(i + 2), end4, lane, U0); });
+    }
+    if (i < ntile) process(U0, t_first + i, none);
   }
-  if (i < ntile) process(U0, t_first + i);
 }
 }  // namespace lsmck
 
@@ -1858,6 +1874,7 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
                        ? (ablate == 4 ? (const void*)crc32_stream_kernel<4>
                           : ablate == 5 ? (const void*)crc32_stream_kernel<5>
                           : ablate == 6 ? (const void*)crc32_stream_kernel<6> : (const void*)crc32_stream_kernel<7>)
+                 : (w12 && ((variant >> 12) & 0xF) == 3) ? (const void*)crc32_stream_kernel<0, 768, 3>  // crc_ring 3
                  : w12 ? (ablate == 3 ? (const void*)crc32_stream_kernel<3, 768>
                           : ablate == 2 ? (const void*)crc32_stream_kernel<2, 768> : (const void*)crc32_stream_kernel<0, 768>)
                        : (ablate == 3 ? (const void*)crc32_stream_kernel<3>

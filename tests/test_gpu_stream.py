@@ -141,3 +141,24 @@ def test_host_batches_use_it_too(ctx):
     off, ln = _packed(rng.integers(64, 5000, 60000), 11)
     data = O.gen_stream(0x57AE0400, 0, int(off[-1]) + int(ln[-1]) + 8)
     assert np.array_equal(ctx.crc32(data, off, ln), O.crc32_batch(data, off, ln, threads=8))
+
+
+@pytest.mark.parametrize("waves,ring", [(12, 0), (12, 3)])
+def test_workgroup_and_slot_variants(ctx, waves, ring):
+    """The 12-wave workgroup form (168 VGPRs) with two and three payload slots
+    in flight: same CRCs as the oracle."""
+    rng = np.random.default_rng(8)
+    lens = rng.choice([64, 65, 100, 127, 128, 129, 300, 1000, 4096, 20000], 50000)
+    off, ln = _packed(lens, 13)
+    data = O.gen_stream(0x57AE0500, 0, int(off[-1]) + int(ln[-1]) + 8)
+    want = O.crc32_batch(data, off, ln, threads=8)
+    ctx.set_option("crc_wg_waves", waves)
+    ctx.set_option("crc_ring", ring)
+    ctx.set_option("crc_stream", 2)
+    try:
+        got = _device(ctx, data, off, ln)
+    finally:
+        ctx.set_option("crc_wg_waves", 0)
+        ctx.set_option("crc_ring", 0)
+        ctx.set_option("crc_stream", 1)
+    assert np.array_equal(got, want)
