@@ -29,7 +29,8 @@ def main():
     write = per_kernel(wd, "WRITE_SIZE")
     res = {}
     for k in sorted(set(fetch) | set(write)):
-        if not any(n in k for n in ("crc32_fixed_kernel", "crc32_wring_kernel", "crc32_desc_kernel", "sha256_kernel")):
+        if not any(n in k for n in ("crc32_fixed_kernel", "crc32_wring_kernel", "crc32_desc_kernel", "crc32_walk_kernel",
+                                    "crc32_stream_kernel", "sha256_kernel")):
             continue
         f = fetch.get(k, [])
         w = write.get(k, [])
