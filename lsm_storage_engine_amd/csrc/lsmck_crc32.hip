@@ -1409,6 +1409,25 @@ __device__ __forceinline__ uint32_t stream_mulcol(uint32_t v, uint32_t base) {
   return p;
 }
 
+// A boundary at byte t (0..3) of word u, the chain's x-form register c = s ^ u
+// before it (s: the register before the word): four byte steps of the
+// register from s, the first t over the word's bytes before the boundary, the
+// rest over zeros.  Ax = the register after the t data steps (the chain's bytes
+// before the boundary, exactly); returns the register after all four (the same
+// bytes zero-extended to the word end, = F(s ^ (u & mlo))).
+__device__ __forceinline__ uint32_t stream_boundary_word(const unsigned char* smem, uint32_t c, uint32_t u, uint32_t t,
+                                                         uint32_t lo, uint32_t& Ax) {
+  uint32_t r = c ^ u;  // s
+  Ax = r;
+#pragma unroll
+  for (uint32_t b = 0; b < 4u; ++b) {
+    const uint32_t in = b < t ? (u >> (8u * b)) & 0xFFu : 0u;
+    r = (r >> 8) ^ lds_ld(smem, (((r ^ in) & 0xFFu) << 8) | lo);  // T0 (replica lane % 32)
+    Ax = (b + 1u == t) ? r : Ax;
+  }
+  return r;
+}
+
 __device__ __forceinline__ uint32_t stream_init(uint32_t t) {  // 0xFFFFFFFF (x) x^(8(4-t)), t = j & 3
   return t == 0u ? 0xdebb20e3u : (t == 1u ? 0x00be26edu : (t == 2u ? 0xbe26ed00u : 0x2dfd1072u));
 }
@@ -1604,17 +1623,19 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
       if (Km0 & (1u << k)) {  // wave-uniform: some lane's chain-0 boundary is in word k
         uint32_t jj = jc0;
         asm volatile("" : "+v"(jj));  // mask and init term here, not hoisted: 4 VGPRs fewer through the loop
-        const uint32_t A = crc_word(smem, c0 ^ (U[k] & (0xFFFFFFFFu << (8u * (jj & 3u)))), 0u, lo, hi);
+        uint32_t Ax;
+        const uint32_t A = stream_boundary_word(smem, c0, U[k], jj & 3u, lo, Ax);
         const bool mine = (jj >> 2) == (uint32_t)k;
-        cap0 = mine ? A : cap0;
+        cap0 = mine ? Ax : cap0;
         e0 = mine ? (A ^ stream_init(jj & 3u)) : 0u;
       }
       if (Km1 & (1u << k)) {
         uint32_t jj = jc1;
         asm volatile("" : "+v"(jj));
-        const uint32_t A = crc_word(smem, c1 ^ (U[16 + k] & (0xFFFFFFFFu << (8u * (jj & 3u)))), 0u, lo, hi);
+        uint32_t Ax;
+        const uint32_t A = stream_boundary_word(smem, c1, U[16 + k], jj & 3u, lo, Ax);
         const bool mine = (jj >> 2) == (uint32_t)(16 + k);
-        cap1 = mine ? A : cap1;
+        cap1 = mine ? Ax : cap1;
         e1 = mine ? (A ^ stream_init(jj & 3u)) : 0u;
       }
       c0 = crc_step_x(smem, c0, k + 1 < 16 ? U[k + 1] : 0u, lo, hi) ^ e0;
@@ -1650,7 +1671,8 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
         if (ABLATE == 7) {  // A/B: the multiplies on the VALU (factors from LDS column 0)
           v = gf2_mulmod(Pv, lds_ld(smem, LDS_XMC_OFF(j & 63u))) ^ gf2_mulmod(h ? A1c : A0c, lds_ld(smem, LDS_XIC_OFF(j & 3u)));
         } else {
-          v = stream_mulcol(Pv, LDS_XMC_OFF(j & 63u)) ^ stream_mulcol(h ? A1c : A0c, LDS_XIC_OFF(j & 3u));
+          // the capture is exact (the chain's bytes before j): one multiply
+          v = stream_mulcol(Pv, LDS_XMC_OFF(j & 63u)) ^ (h ? A1c : A0c);
         }
         P.out[bidx - 1u] = ~v;
       }

@@ -20,7 +20,8 @@ Model (all values are raw CRC registers; (x) is the product mod P):
     lane; X = prefix XOR of G over the wave; the record ending at chunk c
     (started at chunk ls in this tile, or before it) has Hprev = X[c-1] ^
     X[ls-1] (or ^ carry (x) x^(1024 c)).
-  * its CRC = ~(P (x) x^(8m) ^ A (x) x^(-8s)), P = Hprev for a chain-0 end,
+  * its CRC = ~(P (x) x^(8m) ^ A'), A' = the exact capture A (x) x^(-8s) (byte
+    steps in the kernel), P = Hprev for a chain-0 end,
     shift64(Hprev) ^ R0 for a chain-1 end, m = j - 64h.
 """
 import argparse
@@ -82,7 +83,7 @@ def chunk_lane(words, bounds):
                 t = jc[h] & 3
                 mlo = (1 << (8 * t)) - 1  # keep the low t bytes (little endian)
                 A = F(x ^ (u & ~mlo & 0xFFFFFFFF))
-                cap[h] = A
+                cap[h] = mul(A, XINV[4 - t])  # exact: the chain's bytes before j (byte steps in the kernel)
                 corr = A ^ INIT[4 - t]
             c = F(x) ^ corr
         R[h] = c
@@ -139,8 +140,8 @@ def simulate(data, starts, dend, tiles_per_wave=3):
             R0, R1, cap0, cap1, _ = L[c]
             A = cap1 if h else cap0
             P = mul(H, X512) ^ R0 if h else H
-            m, s = j - 64 * h, 4 - (j & 3)
-            v = mul(P, xpow(8 * m)) ^ mul(A, XINV[s])
+            m = j - 64 * h
+            v = mul(P, xpow(8 * m)) ^ A
             if 0 <= r < n:
                 out[r] = (~v) & 0xFFFFFFFF
         # carry out: the record active at the tile's end
