@@ -1006,10 +1006,7 @@ static uint32_t rd_u32(const uint8_t* p) {
 // WAL replay of a device-resident image with the header walk on the GPU
 // (lsmck_wal.hip): nothing of the image comes back to the host, only the
 // accepted records (32 B each) and a few counters.
-static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck_wal_rec* recs, size_t cap,
-                             size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected) {
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  DevGuard g(ctx->dev);
+static int wal_bitmap_ensure(lsmck_ctx* ctx, size_t n) {
   auto& W = ctx->wd;
   int rc;
   const size_t nw = (size_t)lsmk_wal_words(n), nb = (size_t)lsmk_wal_scan_blocks(n);
@@ -1017,6 +1014,19 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
       (rc = ensure_dev(&W.pre, &W.cap_pre, std::max<size_t>(nw, 1))) ||
       (rc = ensure_dev(&W.bsum, &W.cap_bsum, nb + 1)))
     return rc;
+  return 0;
+}
+
+// marked: the candidate bitmap of img is already in ctx->wd (wal_upload marks
+// each chunk behind its copy)
+static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck_wal_rec* recs, size_t cap,
+                             size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected,
+                             bool marked = false) {
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DevGuard g(ctx->dev);
+  auto& W = ctx->wd;
+  int rc;
+  if ((rc = wal_bitmap_ensure(ctx, n))) return rc;
   if (!W.info) HIPCHK(hipMalloc((void**)&W.info, 64));
   if (!W.h_info) HIPCHK(hipHostMalloc((void**)&W.h_info, 64, hipHostMallocDefault));
   ScratchOrder so(ctx, ctx->stream0);
@@ -1024,7 +1034,7 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
   hipStream_t st = so.st;
   uint32_t* d_total = (uint32_t*)(W.info + 3);
   HIPCHK(hipMemsetAsync(d_total, 0, 4, st));
-  rc = lsmk_wal_mark(img, n, W.bits, W.pre, W.bsum, d_total, st);
+  rc = lsmk_wal_mark(img, n, W.bits, W.pre, W.bsum, d_total, marked ? 1 : 0, st);
   if (rc) return launch_rc(rc, "wal mark/scan kernels");
   HIPCHK(hipMemcpyAsync(W.h_info + 3, d_total, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
@@ -1085,9 +1095,14 @@ static int wal_upload(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned)
   std::lock_guard<std::mutex> lk(ctx->mu);
   DevGuard g(ctx->dev);
   int rc;
-  if ((rc = ensure_dev(&ctx->d_wimg, &ctx->cap_wimg, n + 16))) return rc;
+  if ((rc = ensure_dev(&ctx->d_wimg, &ctx->cap_wimg, n + 16)) || (rc = wal_bitmap_ensure(ctx, n))) return rc;
+  // the candidate bitmap of each chunk is marked right behind its copy (the
+  // marking then overlaps the rest of the upload)
+  auto& W = ctx->wd;
   if (pinned) {
     HIPCHK(hipMemcpyAsync(ctx->d_wimg, img, n, hipMemcpyHostToDevice, ctx->stream0));
+    rc = lsmk_wal_mark_range(ctx->d_wimg, n, 0, n, W.bits, W.pre, ctx->stream0);
+    if (rc) return launch_rc(rc, "wal mark kernel");
     HIPCHK(hipStreamSynchronize(ctx->stream0));
     return 0;
   }
@@ -1108,6 +1123,8 @@ static int wal_upload(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned)
     stage_copy(S.h_pay, img + o, c, ctx->stage_threads);
     HIPCHK(hipMemcpyAsync(ctx->d_wimg + o, S.h_pay, c, hipMemcpyHostToDevice, S.s));
     HIPCHK(hipEventRecord(S.done, S.s));
+    rc = lsmk_wal_mark_range(ctx->d_wimg, n, o, o + c, W.bits, W.pre, S.s);  // kChunkBytes: a multiple of 64
+    if (rc) return launch_rc(rc, "wal mark kernel");
   }
   for (auto& S : ctx->stage) HIPCHK(hipStreamSynchronize(S.s));
   guard.ok = true;
@@ -1120,15 +1137,17 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
                             size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
-  if ((flags & LSMCK_DEVICE) && ctx->wal_gpu_walk)
+  if ((flags & LSMCK_DEVICE) && ctx->wal_gpu_walk) {
+    std::lock_guard<std::mutex> wl(ctx->wal_mu);  // the walk's bitmap (ctx->wd) is shared with the upload path
     return wal_replay_device(ctx, wal, n, recs, cap, nrec, bad_index, bad_crc, bad_expected);
+  }
   if (!(flags & LSMCK_DEVICE) && ctx->wal_upload_min && n >= ctx->wal_upload_min) {
     // Host image: one upload (~36 GiB/s through the staging slots) and the GPU
     // header walk, instead of the serial host walk (~12 GiB/s) -- the records
     // and offsets are the same, they index the caller's image
     std::lock_guard<std::mutex> wl(ctx->wal_mu);
     if ((rc = wal_upload(ctx, wal, n, (flags & LSMCK_HOST_PINNED) != 0))) return rc;
-    return wal_replay_device(ctx, ctx->d_wimg, n, recs, cap, nrec, bad_index, bad_crc, bad_expected);
+    return wal_replay_device(ctx, ctx->d_wimg, n, recs, cap, nrec, bad_index, bad_crc, bad_expected, true);
   }
   const uint8_t* h = wal;
   // Device image: the walk reads a host copy, made by DMA into a pinned

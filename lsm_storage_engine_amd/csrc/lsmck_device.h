@@ -81,8 +81,10 @@ uint32_t lsmk_stream_waves(int ncu);
 int lsmk_launch_crc32_stream(const lsmck::CrcParams* P, int ncu, int variant, hipStream_t st);
 uint64_t lsmk_wal_words(uint64_t n);
 uint64_t lsmk_wal_scan_blocks(uint64_t n);
+int lsmk_wal_mark_range(const uint8_t* img, uint64_t n, uint64_t b0, uint64_t b1, uint64_t* bits, uint32_t* pre,
+                        hipStream_t st);
 int lsmk_wal_mark(const uint8_t* img, uint64_t n, uint64_t* bits, uint32_t* pre, uint32_t* bsum, uint32_t* total,
-                  hipStream_t st);
+                  int marked, hipStream_t st);
 int lsmk_wal_chain(const uint8_t* img, uint64_t n, const uint64_t* bits, const uint32_t* pre, uint32_t nc, int levels,
                    uint64_t* pos, uint32_t* J, uint64_t* badpos, uint32_t* chain, unsigned long long* info,
                    hipStream_t st);

@@ -39,10 +39,10 @@ __device__ __forceinline__ uint32_t hdr_len(uint8_t t) { return t == 1 ? 13u : 9
 // 1. candidate bitmap: thread per 64-byte word of positions (16-byte loads
 // when the image is 16-byte aligned, byte loads otherwise)
 __global__ __launch_bounds__(256) void wal_mark(const uint8_t* __restrict__ img, uint64_t n, int aligned,
-                                                 uint64_t* __restrict__ bits, uint32_t* __restrict__ cnt) {
-  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t nw = (n + 63) >> 6;
-  if (w >= nw) return;
+                                                 uint64_t* __restrict__ bits, uint32_t* __restrict__ cnt, uint64_t w0,
+                                                 uint64_t w1) {
+  const uint64_t w = w0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // words [w0, w1)
+  if (w >= w1) return;
   const uint64_t p0 = w << 6;
   uint64_t m = 0;
   if (aligned && p0 + 64 <= n) {
@@ -291,13 +291,29 @@ extern "C" uint64_t lsmk_wal_scan_blocks(uint64_t n) {
   return (nw + WSCAN_BLOCK * WSCAN_ITEMS - 1) / (WSCAN_BLOCK * WSCAN_ITEMS);
 }
 
-// phase 1-2: bitmap, counts, their exclusive scan; *total = candidates
+// phase 1 over the words of bytes [b0, b1) (b0 a multiple of 64): candidate
+// bitmap and counts.  A word reads only its own 64 bytes, so an image uploaded
+// in 64-byte-aligned chunks is marked chunk by chunk behind its copies.
+extern "C" int lsmk_wal_mark_range(const uint8_t* img, uint64_t n, uint64_t b0, uint64_t b1, uint64_t* bits,
+                                   uint32_t* pre, hipStream_t st) {
+  const uint64_t w0 = b0 >> 6, w1 = lsmk_wal_words(b1 < n ? b1 : n);
+  if (w1 <= w0) return 0;
+  const int aligned = ((uintptr_t)img & 15) == 0;
+  hipLaunchKernelGGL(wal_mark, dim3((unsigned)((w1 - w0 + 255) / 256)), dim3(256), 0, st, img, n, aligned, bits, pre,
+                     w0, w1);
+  return launch_err();
+}
+
+// phase 1-2: bitmap, counts (unless `marked`: lsmk_wal_mark_range ran over the
+// whole image), their exclusive scan; *total = candidates
 extern "C" int lsmk_wal_mark(const uint8_t* img, uint64_t n, uint64_t* bits, uint32_t* pre, uint32_t* bsum,
-                             uint32_t* total, hipStream_t st) {
+                             uint32_t* total, int marked, hipStream_t st) {
   const uint64_t nw = lsmk_wal_words(n);
   if (nw == 0) return 0;
-  const int aligned = ((uintptr_t)img & 15) == 0;
-  hipLaunchKernelGGL(wal_mark, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, img, n, aligned, bits, pre);
+  if (!marked) {
+    const int rc = lsmk_wal_mark_range(img, n, 0, n, bits, pre, st);
+    if (rc) return rc;
+  }
   const uint64_t nb = lsmk_wal_scan_blocks(n);
   hipLaunchKernelGGL(wal_scan_a, dim3((unsigned)nb), dim3(WSCAN_BLOCK), 0, st, pre, nw, bsum);
   hipLaunchKernelGGL(wal_scan_b, dim3(1), dim3(1024), 0, st, bsum, (uint32_t)nb, total);
