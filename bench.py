@@ -247,7 +247,8 @@ def main():
                 # "o<n>" = crc_order n (fixed ring kernel tile order)
                 # "p<n>" = sha_pair n (SHA-256: two blocks per load window)
                 # "s<n>" = crc_stream n (descriptor batches: 1 stream kernel where eligible, 0 walking kernel)
-                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?(?:r(\d))?(?:b(\d))?(?:f(\d+))?(?:o(\d))?(?:p(\d))?(?:s(\d))?", v)
+                # "q<n>" = crc_stream_batch n (stream kernel: records finished in batches of 64)
+                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?(?:r(\d))?(?:b(\d))?(?:f(\d+))?(?:o(\d))?(?:p(\d))?(?:s(\d))?(?:q(\d))?", v)
                 if not m:
                     raise SystemExit(f"bad variant {v!r}")
                 kind, num, waves = m.group(1), int(m.group(2)), int(m.group(3) or 0)
@@ -262,6 +263,7 @@ def main():
                 ctx.set_option("crc_order", int(m.group(8) or 0))
                 ctx.set_option("sha_pair", int(m.group(9)) if m.group(9) is not None else 1)
                 ctx.set_option("crc_stream", int(m.group(10)) if m.group(10) is not None else 1)
+                ctx.set_option("crc_stream_batch", int(m.group(11) or 0))
                 step()
                 e0.record(stream)
                 for _ in range(a.steps):
@@ -279,6 +281,7 @@ def main():
         ctx.set_option("sha_bucket_from", 128)
         ctx.set_option("sha_pair", 1)
         ctx.set_option("crc_stream", 1)
+        ctx.set_option("crc_stream_batch", 0)
         ctx.set_option("crc_order", 0)
         ab = {str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                        "GiBps_median": payload / GIB / (float(np.median(t)) * 1e-3)} for v, t in ab.items()}

@@ -850,6 +850,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->variant = (ctx->variant & ~0x3000000) | ((int)value << 24);
     return 0;
   }
+  if (!strcmp(key, "crc_stream_batch")) {  // A/B: stream kernel, records finished in batches of 64 (1) or per tile (0)
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_batch must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (ctx->variant & ~0x800000) | (value ? 0x800000 : 0);
+    return 0;
+  }
   if (!strcmp(key, "crc_stream")) {  // A/B: descriptor batches, 1 = stream kernel for packed >= 64-byte records
                                      // (default), 0 = walking kernel only, 2 = stream kernel only (diagnostic)
     if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream must be 0, 1 or 2");

@@ -1506,7 +1506,7 @@ __device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
   return (uint64_t)wave_or_u32((uint32_t)x) | ((uint64_t)wave_or_u32((uint32_t)(x >> 32)) << 32);
 }
 
-template <int ABLATE = 0, int BLOCK = 1024, int SLOTS = 2>
+template <int ABLATE = 0, int BLOCK = 1024, int SLOTS = 2, bool BATCH = false>
 __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
   if (!*P.sflag) return;  // not a packed batch of >= 64-byte records: the walking kernel takes it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1548,6 +1548,17 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
   StreamWin Wn;
   uint64_t bt = b_lo;  // the first boundary of the tile being mapped
   uint32_t carry = 0;  // the record crossing into the next tile, aligned to this tile's end
+  // BATCH: records finished in batches of up to 64 (one per lane) instead of
+  // per tile: H, R0 of the end chunk, the exact capture, j, the output index
+  uint32_t qH = 0, qR = 0, qA = 0, qJ = 0, qI = 0xFFFFFFFFu, qn = 0;
+  auto flush = [&]() {
+    if (lane < qn && qI != 0xFFFFFFFFu) {  // per active lane: LDS reads in the record lanes only
+      const bool h = qJ >= 64u;
+      const uint32_t Pv = h ? (shift_bytes32<2>(smem, qH) ^ qR) : qH;
+      P.out[qI] = ~(stream_mulcol(Pv, LDS_XMC_OFF(qJ & 63u)) ^ qA);
+    }
+    qn = 0;
+  };
   stream_win_issue(P, bt, lane, Wn);
 
   auto process = [&](const uint32_t (&U)[32], uint64_t t, auto&& issue_next) {
@@ -1661,6 +1672,26 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
       const uint32_t R0c = (uint32_t)__builtin_amdgcn_ds_bpermute(sc, (int)R0);
       const uint32_t A0c = (uint32_t)__builtin_amdgcn_ds_bpermute(sc, (int)cap0);
       const uint32_t A1c = (uint32_t)__builtin_amdgcn_ds_bpermute(sc, (int)cap1);
+      if constexpr (BATCH) {
+        // append this half's record lanes (window lanes 0..m-1) to the queue
+        const uint32_t m = (uint32_t)__builtin_popcountll(__ballot(in));
+        if (qn + m > 64u) flush();
+        const int sh = (int)(((lane - qn) & 63u) << 2);
+        const uint32_t sH = (uint32_t)__builtin_amdgcn_ds_bpermute(sh, (int)H);
+        const uint32_t sR = (uint32_t)__builtin_amdgcn_ds_bpermute(sh, (int)R0c);
+        const uint32_t sA = (uint32_t)__builtin_amdgcn_ds_bpermute(sh, (int)(j >= 64u ? A1c : A0c));
+        const uint32_t sJ = (uint32_t)__builtin_amdgcn_ds_bpermute(sh, (int)j);
+        const uint32_t sI = (uint32_t)__builtin_amdgcn_ds_bpermute(
+            sh, (int)((in && bidx > b_lo) ? (uint32_t)(bidx - 1u) : 0xFFFFFFFFu));
+        const bool take = lane >= qn && lane < qn + m;
+        qH = take ? sH : qH;
+        qR = take ? sR : qR;
+        qA = take ? sA : qA;
+        qJ = take ? sJ : qJ;
+        qI = take ? sI : qI;
+        qn += m;
+        return;
+      }
       // only the lanes holding a record from here on (a few per tile): the LDS
       // reads below cost per active lane, and all 64 lanes doing them cost
       // 4.8 of 25.6 ms (crc_ablate 5); the bpermutes above need every lane
@@ -1725,6 +1756,7 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     }
     if (i < ntile) process(U0, t_first + i, none);
   }
+  if constexpr (BATCH) flush();
 }
 }  // namespace lsmck
 
@@ -1892,7 +1924,10 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   const uint32_t W = (uint32_t)ncu * (uint32_t)(block / 64);
   hipLaunchKernelGGL(stream_cuts, dim3((W + 1u + 255u) / 256u), dim3(256), 0, st, *P, W);
   const int ablate = (variant >> 8) & 0xF;
-  const void* fn = (ablate >= 4 && ablate <= 7 && !w12)
+  const bool batch = (variant & 0x800000) != 0;  // A/B: batched record finish
+  const void* fn = batch ? (w12 ? (const void*)crc32_stream_kernel<0, 768, 2, true>
+                                : (const void*)crc32_stream_kernel<0, 1024, 2, true>)
+                 : (ablate >= 4 && ablate <= 7 && !w12)
                        ? (ablate == 4 ? (const void*)crc32_stream_kernel<4>
                           : ablate == 5 ? (const void*)crc32_stream_kernel<5>
                           : ablate == 6 ? (const void*)crc32_stream_kernel<6> : (const void*)crc32_stream_kernel<7>)
