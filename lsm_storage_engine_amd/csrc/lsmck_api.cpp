@@ -1631,7 +1631,13 @@ static int verify_tables(lsmck_ctx* ctx, const char* const* data_paths, const ch
       for (unsigned t = 1; t < nt; ++t) th.emplace_back(work);
       work();
       for (auto& t : th) t.join();
-      tm->read += clk.lap();
+      {
+        const double dt = clk.lap();
+        tm->read += dt;
+        static const bool trace = getenv("LSMCK_TREE_TRACE") != nullptr;  // diagnostic: per-round read times
+        if (trace) fprintf(stderr, "tree round %llu slot %d: %zu slices, %.1f MB, read %.2f ms\n",
+                           (unsigned long long)tm->rounds, sl, cnt, pay / 1e6, dt * 1e3);
+      }
       ++tm->rounds;
       HIPCHK(hipMemcpyAsync(S.d_pay, S.h_pay, pay, hipMemcpyHostToDevice, S.s));
       HIPCHK(hipMemcpyAsync(S.d_slices, S.h_slices, cnt * sizeof(lsmck::ShaSlice), hipMemcpyHostToDevice, S.s));
@@ -1865,6 +1871,24 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
         if (x.joinable()) x.join();
     }
   } prewarm;
+  if (n) {
+    // Grow the process's descriptor table now, in one step: the verify keeps
+    // up to 8192 files open, and a table grown descriptor by descriptor under
+    // 16 reader threads is resized ~8 times, each resize waiting for an RCU
+    // grace period (a process's first verify read its first round in 1.1 s
+    // instead of 12 ms; LSMCK_TREE_TRACE).  Tables never shrink.
+    prewarm.t.emplace_back([c = ctxs[0]]() {
+      struct rlimit rl;
+      if (getrlimit(RLIMIT_NOFILE, &rl) != 0 || rl.rlim_cur == RLIM_INFINITY) return;
+      const uint32_t active = c->tree_active ? c->tree_active : kTreeActive;
+      const uint64_t want = std::min<uint64_t>((uint64_t)rl.rlim_cur - 1, (uint64_t)active + 512u);
+      const int fd = open("/dev/null", O_RDONLY | O_CLOEXEC);
+      if (fd < 0) return;
+      const int hi = fcntl(fd, F_DUPFD_CLOEXEC, (int)want);
+      if (hi >= 0) close(hi);
+      close(fd);
+    });
+  }
   for (size_t k = 0; k < nctx && n; ++k)
     prewarm.t.emplace_back([c = ctxs[k], n]() {
       const uint32_t active = c->tree_active ? c->tree_active : kTreeActive;
