@@ -24,13 +24,16 @@ def _oracle_state(base):
     img = open(os.path.join(base, "wal", "wal.log"), "rb").read()
     st, recs, _ = O.wal_replay(img)
     assert st == 0
-    mem = {}
+    mem, size = {}, 0
     for r in recs:
         p = img[r.payload_off:r.payload_off + ((r.klen + r.vlen) & 0xFFFFFFFF)]
         if r.type == 1:
             mem[p[:r.klen]] = p[r.klen:]
+            size += len(p)  # from_log adds key + value even over an existing key
         else:
-            mem.pop(p, None)
+            v = mem.pop(p, None)
+            size -= len(v) + len(p) if v is not None else 0
+    _oracle_state.size = size
     return len(recs), mem
 
 
@@ -43,6 +46,7 @@ def test_insert_kill_restart_replay(tmp_path):
         assert srv.loaded["wal_records"] == 3000
         n_wal0, mem0 = _oracle_state(base)
         assert srv.loaded["memtable_entries"] == len(mem0)
+        assert srv.loaded["memtable_bytes"] == _oracle_state.size  # MemTable::from_log's count
         c = srv.client()
         rng = np.random.default_rng(3)
         model = {k: v for k, v in mem0.items()}
@@ -76,6 +80,7 @@ def test_insert_kill_restart_replay(tmp_path):
         srv = Server(base, memtable_limit=1 << 16)
         assert srv.loaded["wal_records"] == n_wal
         assert srv.loaded["memtable_entries"] == len(mem)
+        assert srv.loaded["memtable_bytes"] == _oracle_state.size
         assert srv.loaded["tables"] > synth["tables"]  # the flushed memtables are tables of the tree now
         assert len(mem) < len(model)  # so some reads below come from tables, not the replayed log
         c = srv.client()
