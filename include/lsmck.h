@@ -322,6 +322,26 @@ typedef struct {
 } lsmck_tree_report;
 int lsmck_tree_verify(lsmck_ctx* ctx, const char* base, lsmck_tree_report* rep);
 
+/* The same verify, handing the caller the listing it made: `fn` is called once,
+ * after every metadata file is parsed and before the tables are hashed, with
+ * the tables in load order (per level, read_dir order).  The entries live until
+ * lsmck_tree_verify_listed returns, so the caller can load the tables' read
+ * path (their sparse indexes) beside the verify instead of opening every
+ * metadata file again -- Db::load's other half (src/tokio/db.rs:40-55 ->
+ * SsTable::load).  fn may be NULL. */
+typedef struct {
+  const char* metadata_path;
+  const char* data_path;     /* construct_path: base_path/level-<level>/data_filename (sstable_metadata.rs:43-48) */
+  const char* index_path;
+  const char* checksum_path;
+  const char* id;            /* the metadata's u128 id, decimal */
+  unsigned level;
+  int status;                /* 0, or LSMCK_META_PANIC: not SsTableMetadata JSON (no paths) */
+} lsmck_table_entry;
+typedef void (*lsmck_tree_listed_fn)(void* user, const lsmck_table_entry* tables, size_t n);
+int lsmck_tree_verify_listed(lsmck_ctx* ctx, const char* base, lsmck_tree_report* rep, lsmck_tree_listed_fn fn,
+                             void* user);
+
 /* The same over several devices of one node: the tables are split
  * into contiguous runs balanced by bytes, one per context (one host thread,
  * one set of pinned slots and one PCIe link each), verified concurrently; no

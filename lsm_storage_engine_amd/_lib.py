@@ -63,6 +63,14 @@ class TreeReport(C.Structure):
                 ("first_metadata_path", C.c_char * 4096)]
 
 
+class TableEntry(C.Structure):
+    _fields_ = [("metadata_path", C.c_char_p), ("data_path", C.c_char_p), ("index_path", C.c_char_p),
+                ("checksum_path", C.c_char_p), ("id", C.c_char_p), ("level", C.c_uint), ("status", C.c_int)]
+
+
+LISTED_FN = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(TableEntry), C.c_size_t)
+
+
 # (name, restype, argtypes) for every symbol of include/lsmck.h
 SIGNATURES = [
     ("lsmck_crc32_ieee", C.c_uint32, [vp, sz]),
@@ -93,6 +101,7 @@ SIGNATURES = [
     ("lsmck_checksums_verify_many", C.c_int,
      [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), sz, C.POINTER(C.c_int)]),
     ("lsmck_tree_verify", C.c_int, [vp, C.c_char_p, C.POINTER(TreeReport)]),
+    ("lsmck_tree_verify_listed", C.c_int, [vp, C.c_char_p, C.POINTER(TreeReport), LISTED_FN, vp]),
     ("lsmck_tree_verify_multi", C.c_int, [C.POINTER(vp), sz, C.c_char_p, C.POINTER(TreeReport)]),
     ("lsmck_checksums_verify_many_multi", C.c_int,
      [C.POINTER(vp), sz, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), sz,

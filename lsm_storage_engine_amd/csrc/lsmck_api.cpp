@@ -1812,7 +1812,16 @@ int mkdir_p(const std::string& path) {  // fs::create_dir_all
 
 }  // namespace
 
-static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* base, lsmck_tree_report* rep);
+static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* base, lsmck_tree_report* rep,
+                            lsmck_tree_listed_fn fn = nullptr, void* user = nullptr);
+
+int lsmck_tree_verify_listed(lsmck_ctx* ctx, const char* base, lsmck_tree_report* rep, lsmck_tree_listed_fn fn,
+                             void* user) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  lsmck_ctx* one[1] = {ctx};
+  return tree_verify_impl(one, 1, base, rep, fn, user);
+}
 
 int lsmck_tree_verify(lsmck_ctx* ctx, const char* base, lsmck_tree_report* rep) {
   int rc = check_ctx(ctx);
@@ -1829,7 +1838,8 @@ int lsmck_tree_verify_multi(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
 
 }  // extern "C"
 
-static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* base, lsmck_tree_report* rep) {
+static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* base, lsmck_tree_report* rep,
+                            lsmck_tree_listed_fn fn, void* user) {
   lsmck_ctx* ctx = ctxs[0];
   int rc = 0;
   if (!base || !rep) return lsmck_host::set_error(LSMCK_EINVAL, "null base path or report");
@@ -1838,6 +1848,10 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
   struct timespec t0;
   clock_gettime(CLOCK_MONOTONIC, &t0);
   std::vector<std::string> mpath;
+  struct {
+    std::vector<lsmck_table_entry> ents;
+    std::vector<std::string> dps, ips, cps;
+  } listed;  // lives until the verify returns (lsmck_tree_verify_listed's contract)
   for (int lv = 0; lv < LSMCK_SSTABLE_MAX_LEVEL; ++lv) {
     const std::string dir = lsmck_host::path_push(base, "level-" + std::to_string(lv));
     if ((rc = mkdir_p(dir))) return lsmck_host::set_errno_error(-rc, "create_dir_all", dir.c_str());
@@ -1930,6 +1944,31 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
   }
   rep->tables = n;
   rep->list_seconds = seconds_since(t0);
+  if (fn) {  // the caller's half of Db::load starts from this listing
+    std::vector<lsmck_table_entry> ents(n);
+    std::vector<std::string> dps(n), ips(n), cps(n);
+    for (size_t i = 0; i < n; ++i) {
+      lsmck_table_entry& e = ents[i];
+      e.metadata_path = mpath[i].c_str();
+      e.status = st[i];
+      e.level = meta[i].level;
+      e.id = meta[i].id.c_str();
+      if (!st[i]) {
+        const std::string lvdir = lsmck_host::path_push(meta[i].base_path, "level-" + std::to_string(meta[i].level));
+        dps[i] = lsmck_host::path_push(lvdir, meta[i].data_filename);
+        ips[i] = lsmck_host::path_push(lvdir, meta[i].index_filename);
+        cps[i] = lsmck_host::path_push(lvdir, meta[i].checksum_filename);
+      }
+      e.data_path = dps[i].c_str();
+      e.index_path = ips[i].c_str();
+      e.checksum_path = cps[i].c_str();
+    }
+    listed.ents.swap(ents);
+    listed.dps.swap(dps);
+    listed.ips.swap(ips);
+    listed.cps.swap(cps);
+    fn(user, listed.ents.data(), n);
+  }
   for (auto& x : prewarm.t) x.join();
   const size_t m = which.size();
   std::vector<const char*> dpp(m), ipp(m), cpp(m);

@@ -295,8 +295,11 @@ int read_metadata_json(const char* path, TableMeta* m) {
         if (key == kNames[k]) f = k;
       if (f >= 0 && have[f]) return set_error(LSMCK_EJSON, "metadata file: duplicate field");
       if (f == 1) {
+        p.ws();
+        const size_t st = p.i;
         if (!parse_uint(p, 39, "340282366920938463463374607431768211455"))
           return set_error(LSMCK_EJSON, "metadata file: id is not a u128");
+        m->id.assign(p.s + st, p.i - st);
       } else if (f == 2) {
         p.ws();
         size_t st = p.i;

@@ -23,6 +23,7 @@ int read_checksum_json(const char* path, std::string* index_b64, std::string* da
 // metadata_<ts>.db JSON (src/sstable_metadata.rs:7-17, 76-83); id is validated, not kept
 struct TableMeta {
   std::string base_path, metadata_filename, checksum_filename, data_filename, index_filename, bloom_filter_filename;
+  std::string id;  // decimal u128
   unsigned level = 0;
 };
 int read_metadata_json(const char* path, TableMeta* m);

@@ -383,66 +383,69 @@ struct Db {
   void load() {
     const double t0 = now_s();
     // The tables' read-path state (their sparse indexes) is loaded on its own
-    // threads while the tree is verified: independent file reads, and the
+    // threads while the tree is verified, from the verify's own listing
+    // (lsmck_tree_verify_listed): every metadata file is opened once.  The
     // server serves nothing before both are done.
     int idx_err = 0;
     double t_index = 0;
-    std::thread idx_thread([&]() {
+    struct Listed {
+      Db* db;
+      std::vector<std::string> data, index;
+      std::vector<uint64_t> id;
+      std::vector<int> level;
+      std::thread th;
+      int* err;
+      double* secs;
+    } L{this, {}, {}, {}, {}, {}, &idx_err, &t_index};
+    auto on_listed = [](void* user, const lsmck_table_entry* e, size_t n) {
+      Listed& L = *(Listed*)user;
       const double t_idx0 = now_s();
-      // per level, in load order (sorted by id); the metadata and index files
-      // on 8 threads (229k tables: 2.0 s on one thread, small-file system calls)
-      for (int lv = 0; lv < kMaxLevel && !idx_err; ++lv) {
-        const std::string dir = join(cfg.base, "level-" + std::to_string(lv));
-        DIR* d = opendir(dir.c_str());
-        if (!d) continue;
-        std::vector<std::string> names;
-        while (struct dirent* e = readdir(d))
-          if (strstr(e->d_name, "metadata")) names.push_back(e->d_name);
-        closedir(d);
-        std::vector<std::shared_ptr<SsTable>> tabs(names.size());
+      for (size_t i = 0; i < n; ++i) {  // copies: the entries die with the verify call
+        if (e[i].status) continue;  // a bad metadata file: the verify reports it (the reference panics)
+        L.data.emplace_back(e[i].data_path);
+        L.index.emplace_back(e[i].index_path);
+        L.id.push_back(strtoull(e[i].id, nullptr, 10));
+        L.level.push_back((int)e[i].level);
+      }
+      L.th = std::thread([&L, t_idx0]() {
+        const size_t m = L.data.size();
+        std::vector<std::shared_ptr<SsTable>> tabs(m);
         std::atomic<size_t> next{0};
-        std::atomic<bool> bad_meta{false}, bad_index{false};
+        std::atomic<bool> bad{false};
         auto work = [&]() {
-          for (size_t i; (i = next.fetch_add(1)) < names.size();) {
-            std::string j, id, level, base, data, index;
-            if (!read_file(join(dir, names[i]), &j) || !json_field(j, "id", &id) || !json_field(j, "level", &level) ||
-                !json_field(j, "base_path", &base) || !json_field(j, "data_filename", &data) ||
-                !json_field(j, "index_filename", &index)) {
-              bad_meta = true;
-              continue;
-            }
+          for (size_t i; (i = next.fetch_add(1)) < m;) {
             auto t = std::make_shared<SsTable>();
-            t->id = strtoull(id.c_str(), nullptr, 10);
-            t->level = atoi(level.c_str());
-            const std::string ldir = join(base, "level-" + level);
-            t->data_path = join(ldir, data);
+            t->id = L.id[i];
+            t->level = L.level[i];
+            t->data_path = L.data[i];
             struct stat st;
             if (stat(t->data_path.c_str(), &st) == 0) t->size = (uint64_t)st.st_size;
-            if (!t->load_index(join(ldir, index))) bad_index = true;
+            if (!t->load_index(L.index[i])) bad = true;
             tabs[i] = t;
           }
         };
         std::vector<std::thread> th;
-        const size_t nt = std::min<size_t>(8, names.size());
-        for (size_t k = 1; k < nt; ++k) th.emplace_back(work);
+        for (size_t k = 1; k < std::min<size_t>(8, m); ++k) th.emplace_back(work);
         work();
         for (auto& x : th) x.join();
-        if (bad_meta || bad_index) {
-          idx_err = bad_meta ? 1 : 2;
-          break;
+        if (bad) {
+          *L.err = 2;
+          return;
         }
         for (auto& t : tabs) {
-          last_id = std::max(last_id, t->id);
-          levels[lv].push_back(t);
+          if (t->level < 0 || t->level >= kMaxLevel) continue;
+          L.db->last_id = std::max(L.db->last_id, t->id);
+          L.db->levels[t->level].push_back(t);
         }
-        std::sort(levels[lv].begin(), levels[lv].end(),
-                  [](const std::shared_ptr<SsTable>& a, const std::shared_ptr<SsTable>& b) { return a->id < b->id; });
-      }
-      t_index = now_s() - t_idx0;
-    });
+        for (auto& lv : L.db->levels)  // load order: per level, sorted by id
+          std::sort(lv.begin(), lv.end(),
+                    [](const std::shared_ptr<SsTable>& a, const std::shared_ptr<SsTable>& b) { return a->id < b->id; });
+        *L.secs = now_s() - t_idx0;
+      });
+    };
     lsmck_tree_report rep;
-    int rc = lsmck_tree_verify(ctx, cfg.base.c_str(), &rep);
-    idx_thread.join();
+    int rc = lsmck_tree_verify_listed(ctx, cfg.base.c_str(), &rep, on_listed, &L);
+    if (L.th.joinable()) L.th.join();
     if (rc < 0) {
       fprintf(stderr, "lsmck_tree_verify: %s\n", lsmck_last_error());
       exit(1);
@@ -466,7 +469,6 @@ struct Db {
       }
     }
     const double t_tree = now_s() - t0;
-    if (idx_err == 1) panic_exit("Can't read metadata file, file with unknown format");
     if (idx_err == 2) panic_exit("Can't open index file");
     // WAL replay: every payload CRC in one GPU batch
     const double t1 = now_s();

@@ -231,13 +231,26 @@ class Context:
         _lib.check(self.lib.lsmck_checksums_verify_many(self.handle, d, i, c, n, status), "checksums_verify_many")
         return list(status[:n])
 
-    def tree_verify(self, base):
+    def tree_verify(self, base, listed=None):
         """lsmck_tree_verify: Db::load's table scan + batch verify of the tree
         under ``base``.  Returns a dict of the report (first_* describe the
-        first failing table in load order, or are None)."""
+        first failing table in load order, or are None).  ``listed``: a list
+        that receives the verify's listing (lsmck_tree_verify_listed), one
+        dict per table in load order, before the tables are hashed."""
         rep = _lib.TreeReport()
-        rc = _lib.check(self.lib.lsmck_tree_verify(self.handle, str(base).encode(), C.byref(rep)), "tree_verify")
-        return _tree_report(rep, rc)
+        if listed is None:
+            rc = self.lib.lsmck_tree_verify(self.handle, str(base).encode(), C.byref(rep))
+        else:
+            def on_listed(_user, e, n):
+                for i in range(n):
+                    t = e[i]
+                    dec = lambda b: b.decode(errors="surrogateescape") if b is not None else None  # noqa: E731
+                    listed.append({"metadata_path": dec(t.metadata_path), "data_path": dec(t.data_path),
+                                   "index_path": dec(t.index_path), "checksum_path": dec(t.checksum_path),
+                                   "id": dec(t.id), "level": t.level, "status": t.status})
+            fn = _lib.LISTED_FN(on_listed)
+            rc = self.lib.lsmck_tree_verify_listed(self.handle, str(base).encode(), C.byref(rep), fn, None)
+        return _tree_report(rep, _lib.check(rc, "tree_verify"))
 
 
 def _tree_report(rep, rc):

@@ -80,6 +80,15 @@ def test_load_verify_clean_and_corrupted(ctx, small_tree, tmp_path):
     _, recs, _ = O.wal_replay(open(os.path.join(base, "wal", "wal.log"), "rb").read())
     assert mem.size() <= 3000 and mem.size() > 0
     assert rep["table_bytes"] == small_tree[1]["table_bytes"]
+    # lsmck_tree_verify_listed: the verify's own listing, in load order, as the metadata files say
+    listed = []
+    ctx.tree_verify(base, listed=listed)
+    assert [e["metadata_path"] for e in listed] == tree.scan_order(base)
+    for e in listed:
+        m = SsTableMetadata.load(e["metadata_path"])
+        assert e["status"] == 0 and (e["data_path"], e["index_path"], e["checksum_path"]) == (
+            m.data_path(), m.index_path(), m.checksum_path())
+        assert (int(e["id"]), e["level"]) == (m.id, m.level)
     # the second table (load order) has its index file corrupted: panic naming the index file
     paths = tree.scan_order(base)
     order = [SsTableMetadata.load(p) for p in paths]
@@ -151,8 +160,13 @@ def test_tree_verify_metadata_json(ctx, tmp_path, case):
     checksums.Checksums.write_checksums(m)
     open(m.metadata_path(), "w").write(text.replace("BASE", base).replace("TS", str(m.id)))
     open(os.path.join(base, "level-0", "not-a-table.db"), "w").write("{}")  # name lacks "metadata": skipped
-    r = ctx.tree_verify(base)
-    assert r["tables"] == 1
+    listed = []
+    r = ctx.tree_verify(base, listed=listed)
+    assert r["tables"] == 1 and len(listed) == 1
+    assert listed[0]["status"] == (0 if want == "ok" else _lib.META_PANIC)
+    if want == "ok":
+        assert listed[0]["id"] == (str(m.id) if "340282" not in text else "340282366920938463463374607431768211455")
+        assert listed[0]["data_path"] == m.data_path()  # escapes decoded
     assert all(os.path.isdir(os.path.join(base, f"level-{lv}")) for lv in range(5))  # create_dir_all
     if want == "ok":
         assert r["bad_tables"] == 0 and r["table_bytes"] == 705
