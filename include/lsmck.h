@@ -336,7 +336,7 @@ typedef struct {
   const char* checksum_path;
   const char* id;            /* the metadata's u128 id, decimal */
   unsigned level;
-  int status;                /* 0, or LSMCK_META_PANIC: not SsTableMetadata JSON (no paths) */
+  int status;                /* 0, or LSMCK_META_PANIC: not SsTableMetadata JSON (paths and id "") */
 } lsmck_table_entry;
 typedef void (*lsmck_tree_listed_fn)(void* user, const lsmck_table_entry* tables, size_t n);
 int lsmck_tree_verify_listed(lsmck_ctx* ctx, const char* base, lsmck_tree_report* rep, lsmck_tree_listed_fn fn,

@@ -1952,7 +1952,7 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
       e.metadata_path = mpath[i].c_str();
       e.status = st[i];
       e.level = meta[i].level;
-      e.id = meta[i].id.c_str();
+      e.id = st[i] ? "" : meta[i].id.c_str();
       if (!st[i]) {
         const std::string lvdir = lsmck_host::path_push(meta[i].base_path, "level-" + std::to_string(meta[i].level));
         dps[i] = lsmck_host::path_push(lvdir, meta[i].data_filename);

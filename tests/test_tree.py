@@ -164,6 +164,8 @@ def test_tree_verify_metadata_json(ctx, tmp_path, case):
     r = ctx.tree_verify(base, listed=listed)
     assert r["tables"] == 1 and len(listed) == 1
     assert listed[0]["status"] == (0 if want == "ok" else _lib.META_PANIC)
+    if want != "ok":
+        assert listed[0]["id"] == listed[0]["data_path"] == ""
     if want == "ok":
         assert listed[0]["id"] == (str(m.id) if "340282" not in text else "340282366920938463463374607431768211455")
         assert listed[0]["data_path"] == m.data_path()  # escapes decoded
