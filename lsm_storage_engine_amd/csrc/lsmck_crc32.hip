@@ -1409,28 +1409,21 @@ __device__ __forceinline__ uint32_t stream_mulcol(uint32_t v, uint32_t base) {
   return p;
 }
 
-// A boundary at byte t (0..3) of word u, the chain's x-form register c = s ^ u
-// before it (s: the register before the word): four byte steps of the
-// register from s, the first t over the word's bytes before the boundary, the
-// rest over zeros.  Ax = the register after the t data steps (the chain's bytes
-// before the boundary, exactly); returns the register after all four (the same
-// bytes zero-extended to the word end, = F(s ^ (u & mlo))).
-__device__ __forceinline__ uint32_t stream_boundary_word(const unsigned char* smem, uint32_t c, uint32_t u, uint32_t t,
-                                                         uint32_t lo, uint32_t& Ax) {
-  uint32_t r = c ^ u;  // s
-  Ax = r;
-#pragma unroll
-  for (uint32_t b = 0; b < 4u; ++b) {
-    const uint32_t in = b < t ? (u >> (8u * b)) & 0xFFu : 0u;
-    r = (r >> 8) ^ lds_ld(smem, (((r ^ in) & 0xFFu) << 8) | lo);  // T0 (replica lane % 32)
-    Ax = (b + 1u == t) ? r : Ax;
-  }
-  return r;
+// The exact capture at a boundary at byte t of word u: the register s before
+// the word advanced over the word's t bytes before the boundary (the ending
+// record's last bytes), slicing-by-t from cx = s ^ u:
+// (s >> 8t) ^ XOR_{i<t} T_{t-1-i}[cx byte i].  Run once per chunk after the
+// chains, off their dependency path.
+__device__ __forceinline__ uint32_t stream_capture(const unsigned char* smem, uint32_t cx, uint32_t u, uint32_t t,
+                                                   uint32_t lo) {
+  const uint32_t b0 = t == 1u ? lo : (t == 2u ? lo + 128u : (lo | 0x10000u));  // T_{t-1}
+  const uint32_t b1 = t == 2u ? lo : lo + 128u;                                // T_{t-2}
+  const uint32_t l0 = lds_ld(smem, __builtin_amdgcn_perm(cx, b0, 0x0c020400u));  // byte 0
+  const uint32_t l1 = lds_ld(smem, __builtin_amdgcn_perm(cx, b1, 0x0c020500u));  // byte 1
+  const uint32_t l2 = lds_ld(smem, __builtin_amdgcn_perm(cx, lo, 0x0c020600u));  // byte 2 (T0)
+  return ((cx ^ u) >> (t << 3)) ^ (t >= 1u ? l0 : 0u) ^ (t >= 2u ? l1 : 0u) ^ (t >= 3u ? l2 : 0u);
 }
 
-__device__ __forceinline__ uint32_t stream_init(uint32_t t) {  // 0xFFFFFFFF (x) x^(8(4-t)), t = j & 3
-  return t == 0u ? 0xdebb20e3u : (t == 1u ? 0x00be26edu : (t == 2u ? 0xbe26ed00u : 0x2dfd1072u));
-}
 __device__ __forceinline__ uint32_t stream_xinv(uint32_t t) {  // x^(-8(4-t))
   return t == 0u ? 0x5b358fd3u : (t == 1u ? 0x1f81b6e1u : (t == 2u ? 0xd7125358u : 0x6567cb95u));
 }
@@ -1615,8 +1608,10 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
       jc1 = b2 ? j2 : ((b1 && j1 >= 64u) ? j1 : 128u);
     }
     // (ABLATE 4, diagnostic: no boundary bodies; results invalid)
-    const uint32_t Km0 = ABLATE == 4 ? 0u : wave_or_u32(jc0 < 128u ? (1u << (jc0 >> 2)) : 0u);
-    const uint32_t Km1 = ABLATE == 4 ? 0u : wave_or_u32(jc1 < 128u ? (1u << ((jc1 >> 2) - 16u)) : 0u);
+    // (ABLATE 9, diagnostic: the boundary branches kept, never taken; results invalid)
+    const uint32_t kz = ABLATE == 9 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(P.nrec >> 62)) : 0u;
+    const uint32_t Km0 = ABLATE == 4 ? 0u : ABLATE == 9 ? kz : wave_or_u32(jc0 < 128u ? (1u << (jc0 >> 2)) : 0u);
+    const uint32_t Km1 = ABLATE == 4 ? 0u : ABLATE == 9 ? kz : wave_or_u32(jc1 < 128u ? (1u << ((jc1 >> 2) - 16u)) : 0u);
     if (ABLATE == 3) {  // diagnostic: payload loads only
       uint32_t x = 0;
 #pragma unroll
@@ -1624,34 +1619,35 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
       if (x == 0x9E3779B1u) P.out[0] = x ^ jc0 ^ jc1;
       return;
     }
-    // --- the chunk's two chains, with the register resets at its boundaries
-    // (mask and init term recomputed inside the rare boundary bodies: fewer
-    // registers live through the loop)
-    uint32_t c0 = U[0], c1 = U[16], cap0 = 0u, cap1 = 0u;
+    // --- the chunk's two chains, with the register resets at its boundaries.
+    // A record starting at byte t of word u resets the chain: the register
+    // after the word is F(~(u | mlo)) ^ mlo (mlo: the t bytes before the
+    // boundary; the 0xFFFFFFFF init folded in), so the boundary lane only
+    // swaps the input of its ordinary word step -- no extra lookups -- and
+    // keeps c ^ u and u of that word for its capture.
+    uint32_t c0 = U[0], c1 = U[16], x0 = 0u, x1 = 0u, ub0 = 0u, ub1 = 0u;
+    const uint32_t Km = Km0 | Km1;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      uint32_t e0 = 0u, e1 = 0u;
-      if (Km0 & (1u << k)) {  // wave-uniform: some lane's chain-0 boundary is in word k
-        uint32_t jj = jc0;
-        asm volatile("" : "+v"(jj));  // mask and init term here, not hoisted: 4 VGPRs fewer through the loop
-        uint32_t Ax;
-        const uint32_t A = stream_boundary_word(smem, c0, U[k], jj & 3u, lo, Ax);
-        const bool mine = (jj >> 2) == (uint32_t)k;
-        cap0 = mine ? Ax : cap0;
-        e0 = mine ? (A ^ stream_init(jj & 3u)) : 0u;
+      const uint32_t w0 = k + 1 < 16 ? U[k + 1] : 0u, w1 = k + 1 < 16 ? U[17 + k] : 0u;
+      if (Km & (1u << k)) {  // wave-uniform: some lane's chain has a boundary in word k
+        uint32_t j0 = jc0, j1 = jc1;
+        asm volatile("" : "+v"(j0), "+v"(j1));  // recomputed here, not hoisted: fewer VGPRs through the loop
+        const bool m0 = (j0 >> 2) == (uint32_t)k, m1 = (j1 >> 2) == (uint32_t)(16 + k);
+        const uint32_t mlo0 = (1u << ((j0 & 3u) << 3)) - 1u, mlo1 = (1u << ((j1 & 3u) << 3)) - 1u;
+        x0 = m0 ? c0 : x0;
+        ub0 = m0 ? U[k] : ub0;
+        x1 = m1 ? c1 : x1;
+        ub1 = m1 ? U[16 + k] : ub1;
+        c0 = crc_step_x(smem, m0 ? ~(U[k] | mlo0) : c0, m0 ? (w0 ^ mlo0) : w0, lo, hi);
+        c1 = crc_step_x(smem, m1 ? ~(U[16 + k] | mlo1) : c1, m1 ? (w1 ^ mlo1) : w1, lo, hi);
+      } else {
+        c0 = crc_step_x(smem, c0, w0, lo, hi);
+        c1 = crc_step_x(smem, c1, w1, lo, hi);
       }
-      if (Km1 & (1u << k)) {
-        uint32_t jj = jc1;
-        asm volatile("" : "+v"(jj));
-        uint32_t Ax;
-        const uint32_t A = stream_boundary_word(smem, c1, U[16 + k], jj & 3u, lo, Ax);
-        const bool mine = (jj >> 2) == (uint32_t)(16 + k);
-        cap1 = mine ? Ax : cap1;
-        e1 = mine ? (A ^ stream_init(jj & 3u)) : 0u;
-      }
-      c0 = crc_step_x(smem, c0, k + 1 < 16 ? U[k + 1] : 0u, lo, hi) ^ e0;
-      c1 = crc_step_x(smem, c1, k + 1 < 16 ? U[17 + k] : 0u, lo, hi) ^ e1;
     }
+    const uint32_t cap0 = Km0 ? stream_capture(smem, x0, ub0, jc0 & 3u, lo) : 0u;
+    const uint32_t cap1 = Km1 ? stream_capture(smem, x1, ub1, jc1 & 3u, lo) : 0u;
     const uint32_t R0 = c0;
     const uint32_t T = (jc1 < 128u) ? c1 : (shift_bytes32<2>(smem, c0) ^ c1);
     // --- Horner inside the tile: T to the chunk before the next boundary's chunk
@@ -1699,7 +1695,9 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
         const bool h = j >= 64u;
         const uint32_t Pv = h ? (shift_bytes32<2>(smem, H) ^ R0c) : H;
         uint32_t v;
-        if (ABLATE == 7) {  // A/B: the multiplies on the VALU (factors from LDS column 0)
+        if (ABLATE == 8) {  // diagnostic: no finish multiply (results invalid)
+          v = Pv ^ (h ? A1c : A0c);
+        } else if (ABLATE == 7) {  // A/B: the multiplies on the VALU (factors from LDS column 0)
           v = gf2_mulmod(Pv, lds_ld(smem, LDS_XMC_OFF(j & 63u))) ^ gf2_mulmod(h ? A1c : A0c, lds_ld(smem, LDS_XIC_OFF(j & 3u)));
         } else {
           // the capture is exact (the chain's bytes before j): one multiply
@@ -1927,10 +1925,12 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   const bool batch = (variant & 0x800000) != 0;  // A/B: batched record finish
   const void* fn = batch ? (w12 ? (const void*)crc32_stream_kernel<0, 768, 2, true>
                                 : (const void*)crc32_stream_kernel<0, 1024, 2, true>)
-                 : (ablate >= 4 && ablate <= 7 && !w12)
+                 : (ablate >= 4 && ablate <= 9 && !w12)
                        ? (ablate == 4 ? (const void*)crc32_stream_kernel<4>
                           : ablate == 5 ? (const void*)crc32_stream_kernel<5>
-                          : ablate == 6 ? (const void*)crc32_stream_kernel<6> : (const void*)crc32_stream_kernel<7>)
+                          : ablate == 6 ? (const void*)crc32_stream_kernel<6>
+                          : ablate == 7 ? (const void*)crc32_stream_kernel<7>
+                          : ablate == 8 ? (const void*)crc32_stream_kernel<8> : (const void*)crc32_stream_kernel<9>)
                  : (w12 && ((variant >> 12) & 0xF) == 3) ? (const void*)crc32_stream_kernel<0, 768, 3>  // crc_ring 3
                  : w12 ? (ablate == 3 ? (const void*)crc32_stream_kernel<3, 768>
                           : ablate == 2 ? (const void*)crc32_stream_kernel<2, 768> : (const void*)crc32_stream_kernel<0, 768>)

@@ -10,18 +10,20 @@ Model (all values are raw CRC registers; (x) is the product mod P):
   * chunk = 32 little-endian words in two chains of 16; a chain's register
     starts at 0; F(v) = v (x) x^32 is one word step.
   * a record boundary at chunk byte j lies in chain h = j >= 64, word w = j/4,
-    t = j % 4, s = 4 - t.  At that word, A = F(c ^ (u_w & ~mlo)) is the chain's
-    value of the bytes before j (zero-extended to the word end); the chain's
-    register after the word is xored with A ^ I[s], I[s] = 0xFFFFFFFF (x)
-    x^(8s): it then holds the new record's bytes from j, init included.
+    t = j % 4, mlo = the mask of the word's t bytes before j.  The chain's
+    register after that word is RESET to F(~(u_w | mlo)) ^ mlo: the new
+    record's bytes from j with the 0xFFFFFFFF init folded in (no dependency on
+    the chain's register).  The capture A' = the register c advanced over the
+    t bytes before j, = (c >> 8t) ^ XOR_{i<t} T_{t-1-i}[(c ^ u_w) byte i]
+    (slicing-by-t; the kernel saves c ^ u_w and u_w at the boundary word and
+    runs the t lookups once after the chunk).
   * a chunk's tail T = the register of its last piece aligned to the chunk end
     (chain 1 alone if it holds a boundary, else shift64(R0) ^ R1).
   * per lane G = T (x) x^(1024 d), d = (next boundary chunk in the tile) - 1 -
     lane; X = prefix XOR of G over the wave; the record ending at chunk c
     (started at chunk ls in this tile, or before it) has Hprev = X[c-1] ^
     X[ls-1] (or ^ carry (x) x^(1024 c)).
-  * its CRC = ~(P (x) x^(8m) ^ A'), A' = the exact capture A (x) x^(-8s) (byte
-    steps in the kernel), P = Hprev for a chain-0 end,
+  * its CRC = ~(P (x) x^(8m) ^ A'), P = Hprev for a chain-0 end,
     shift64(Hprev) ^ R0 for a chain-1 end, m = j - 64h.
 """
 import argparse
@@ -55,14 +57,29 @@ def xpow(k):
 
 
 ORD = (1 << 32) - 1
-XINV = {s: xpow(ORD - 8 * s) for s in range(1, 5)}
-INIT = {s: mul(0xFFFFFFFF, xpow(8 * s)) for s in range(1, 5)}
 X32 = xpow(32)
 X512 = xpow(512)
 
 
 def F(v):
     return mul(v, X32)
+
+
+def _tables():
+    t0 = []
+    for n in range(256):
+        c = n
+        for _ in range(8):
+            c = (c >> 1) ^ POLY if c & 1 else c >> 1
+        t0.append(c)
+    tabs = [t0]
+    for _ in range(3):
+        prev = tabs[-1]
+        tabs.append([(v >> 8) ^ t0[v & 0xFF] for v in prev])
+    return tabs
+
+
+TAB = _tables()  # slicing-by-4 tables: T_k[n] = T0[n] advanced over k zero bytes
 
 
 def chunk_lane(words, bounds):
@@ -78,14 +95,20 @@ def chunk_lane(words, bounds):
             w = 16 * h + k
             u = words[w]
             x = c ^ u
-            corr = 0
             if jc[h] is not None and (jc[h] >> 2) == w:
                 t = jc[h] & 3
                 mlo = (1 << (8 * t)) - 1  # keep the low t bytes (little endian)
-                A = F(x ^ (u & ~mlo & 0xFFFFFFFF))
-                cap[h] = mul(A, XINV[4 - t])  # exact: the chain's bytes before j (byte steps in the kernel)
-                corr = A ^ INIT[4 - t]
-            c = F(x) ^ corr
+                # the capture: t byte steps of the register c over the word's
+                # bytes before j, as slicing-by-t from the saved x = c ^ u
+                ax = c >> (8 * t)
+                for i in range(t):
+                    ax ^= TAB[t - 1 - i][(x >> (8 * i)) & 0xFF]
+                cap[h] = ax
+                # the reset: the register after the word for a record starting
+                # at byte t, init included, = F(~(u | mlo)) ^ mlo (no c in it)
+                c = F(~(u | mlo) & 0xFFFFFFFF) ^ mlo
+                continue
+            c = F(x)
         R[h] = c
     tail = R[1] if jc[1] is not None else (mul(R[0], X512) ^ R[1])
     return R[0], R[1], cap[0], cap[1], tail
