@@ -1659,11 +1659,15 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     const uint32_t ca = ra >> 7, cb = rb >> 7;
     const uint32_t c00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ca);
     const uint32_t cterm = na ? walk_mulcol_uniform(carry, c00, lane) : 0u;
-    auto finish = [&](bool in, uint32_t r, uint32_t ls, bool from_carry, uint64_t bidx) {
+    // Y = X[c-1] of the window lane's end chunk c; the record began at the
+    // previous window lane's chunk, whose Y is one DPP shift away (lane 0:
+    // `first`, the carry term or the other half's last Y)
+    auto finish = [&](bool in, uint32_t r, uint32_t first, uint64_t bidx) -> uint32_t {
       const uint32_t c = r >> 7, j = r & 127u;
       const uint32_t Xc = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((c - 1u) & 63u) << 2), (int)X);
-      const uint32_t Xl = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((ls - 1u) & 63u) << 2), (int)X);
-      const uint32_t H = (c ? Xc : 0u) ^ (from_carry ? cterm : (ls ? Xl : 0u));
+      const uint32_t Y = c ? Xc : 0u;
+      const uint32_t Yp = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)Y, 0x138, 0xF, 0xF, false);  // wave_shr:1
+      const uint32_t H = Y ^ (lane ? Yp : first);
       const int sc = (int)(c << 2);
       const uint32_t R0c = (uint32_t)__builtin_amdgcn_ds_bpermute(sc, (int)R0);
       const uint32_t A0c = (uint32_t)__builtin_amdgcn_ds_bpermute(sc, (int)cap0);
@@ -1686,7 +1690,7 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
         qJ = take ? sJ : qJ;
         qI = take ? sI : qI;
         qn += m;
-        return;
+        return Y;
       }
       // only the lanes holding a record from here on (a few per tile): the LDS
       // reads below cost per active lane, and all 64 lanes doing them cost
@@ -1705,19 +1709,13 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
         }
         P.out[bidx - 1u] = ~v;
       }
+      return Y;
     };
-    {
-      const uint32_t ca63 = (uint32_t)__builtin_amdgcn_readlane((int)ca, 63);
-      const uint32_t pca = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ca, 0x138, 0xF, 0xF, false);
-      if (ABLATE == 5) {  // diagnostic: no record finish (one store keeps the tile's work alive)
-        if (X == 0x9E3779B1u) P.out[0] = X ^ R0 ^ cap0 ^ cap1;
-      } else {
-        finish(ina, ra, pca, lane == 0u, bt0 + lane);
-      }
-      if (ABLATE != 5 && nb) {
-        const uint32_t pcb0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cb, 0x138, 0xF, 0xF, false);
-        finish(inb, rb, lane ? pcb0 : ca63, false, bt0 + 64u + lane);
-      }
+    if (ABLATE == 5) {  // diagnostic: no record finish (one store keeps the tile's work alive)
+      if (X == 0x9E3779B1u) P.out[0] = X ^ R0 ^ cap0 ^ cap1;
+    } else {
+      const uint32_t Ya = finish(ina, ra, cterm, bt0 + lane);
+      if (nb) finish(inb, rb, (uint32_t)__builtin_amdgcn_readlane((int)Ya, 63), bt0 + 64u + lane);
     }
     // --- carry: the record active at the tile's end
     const uint32_t X63 = (uint32_t)__builtin_amdgcn_readlane((int)X, 63);
