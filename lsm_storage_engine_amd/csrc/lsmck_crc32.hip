@@ -953,8 +953,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_phase1(const uint32_t* __rest
 
 // single workgroup: exclusive scan of the block sums in place, total in *total.
 // Thread i owns the contiguous chunk [i*C, (i+1)*C).
+// skip: the stream kernel's flag -- set when it took the batch, so the walking
+// kernel's segment prefix is not needed (nullptr: always run)
 __global__ __launch_bounds__(1024) void scan_phase2(uint64_t* __restrict__ block_sum, uint32_t nblocks,
-                                                     uint64_t* __restrict__ total) {
+                                                     uint64_t* __restrict__ total, const uint32_t* skip = nullptr) {
+  if (skip && *skip) return;
   __shared__ uint64_t wsum[16];
   const uint32_t C = (nblocks + 1023u) / 1024u;
   const uint32_t b0 = threadIdx.x * C, b1 = min(nblocks, b0 + C);
@@ -1117,7 +1120,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_phase3(const uint32_t* __rest
 #define LDS_WCOLS_OFF LDS_COLS_OFF  // [8 groups][65 d][4 u32] columns of x^(8*128*d), d = 0..64 (8320 B)
 
 __global__ __launch_bounds__(1024) void walk_phase1(const uint32_t* __restrict__ len, uint64_t n,
-                                                     uint64_t* __restrict__ sb_sum) {
+                                                     uint64_t* __restrict__ sb_sum, const uint32_t* skip) {
+  if (skip && *skip) return;  // the stream kernel took the batch
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t sb = (uint64_t)blockIdx.x * 16u + (threadIdx.x >> 6);
   if (sb * WALK_SB >= n) return;  // wave-uniform
@@ -1855,7 +1859,7 @@ extern "C" int lsmk_launch_crc32_scan(const CrcParams* P, uint64_t* block_sum, h
   uint64_t n = P->nrec;
   uint32_t nb = (uint32_t)lsmk_scan_block_count(n);
   hipLaunchKernelGGL(scan_phase1, dim3(nb), dim3(SCAN_BLOCK), 0, st, P->len, n, block_sum);
-  hipLaunchKernelGGL(scan_phase2, dim3(1), dim3(1024), 0, st, block_sum, nb, P->total_segs);
+  hipLaunchKernelGGL(scan_phase2, dim3(1), dim3(1024), 0, st, block_sum, nb, P->total_segs, (const uint32_t*)nullptr);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
 }
@@ -1954,8 +1958,10 @@ extern "C" int lsmk_launch_crc32_walk(const CrcParams* P, uint64_t* sb_prefix, i
   const uint64_t n = P->nrec;
   if (n == 0) return 0;
   const uint64_t nsb = lsmk_walk_sb_count(n);
-  hipLaunchKernelGGL(walk_phase1, dim3((unsigned)((nsb + 15) / 16)), dim3(1024), 0, st, P->len, n, sb_prefix);
-  hipLaunchKernelGGL(scan_phase2, dim3(1), dim3(1024), 0, st, sb_prefix, (uint32_t)nsb, P->total_segs);
+  hipLaunchKernelGGL(walk_phase1, dim3((unsigned)((nsb + 15) / 16)), dim3(1024), 0, st, P->len, n, sb_prefix,
+                     (const uint32_t*)P->sflag);
+  hipLaunchKernelGGL(scan_phase2, dim3(1), dim3(1024), 0, st, sb_prefix, (uint32_t)nsb, P->total_segs,
+                     (const uint32_t*)P->sflag);
   CrcParams Q = *P;
   Q.sb_prefix = sb_prefix;
   const int ch = (variant & 0xF) ? (variant & 0xF) : LSMCK_DEFAULT_DESC_CHAINS;
