@@ -856,6 +856,20 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->variant = (ctx->variant & ~0x800000) | (value ? 0x800000 : 0);
     return 0;
   }
+  if (!strcmp(key, "crc_stream_window")) {  // A/B: stream kernel boundary window, 2 = sliding (default),
+                                            // 1 = reloaded, second half on demand, 0 = both halves reloaded
+    if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_window must be 0, 1 or 2");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (ctx->variant & ~0x18000000) | ((int)(2 - value) << 27);
+    return 0;
+  }
+  if (!strcmp(key, "crc_stream_qstore")) {  // A/B: stream kernel CRCs stored as queued 256-B blocks (1, default)
+                                            // or per tile (0)
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_qstore must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (ctx->variant & ~0x4000000) | (value ? 0 : 0x4000000);
+    return 0;
+  }
   if (!strcmp(key, "crc_stream")) {  // A/B: descriptor batches, 1 = stream kernel for packed >= 64-byte records
                                      // (default), 0 = walking kernel only, 2 = stream kernel only (diagnostic)
     if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream must be 0, 1 or 2");

@@ -1465,10 +1465,11 @@ __global__ __launch_bounds__(256) void stream_cuts(CrcParams P, uint32_t W) {
 struct StreamWin {
   uint64_t a, b;  // off[] of boundaries bt + lane and bt + 64 + lane (clamped to n - 1; fixed up at use)
 };
+template <int WIN>
 __device__ __forceinline__ void stream_win_issue(const CrcParams& P, uint64_t bt, uint32_t lane, StreamWin& W) {
   const uint64_t n = P.nrec, ia = bt + lane, ib = bt + 64u + lane;
   W.a = P.off[ia < n ? ia : n - 1];
-  W.b = P.off[ib < n ? ib : n - 1];
+  if (WIN == 0) W.b = P.off[ib < n ? ib : n - 1];
 }
 
 // the tile's 64 chunks: bytes [tb, tb + 8192) from P.base (tb >= -127, the
@@ -1503,7 +1504,13 @@ __device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
   return (uint64_t)wave_or_u32((uint32_t)x) | ((uint64_t)wave_or_u32((uint32_t)(x >> 32)) << 32);
 }
 
-template <int ABLATE = 0, int BLOCK = 1024, int SLOTS = 2, bool BATCH = false>
+// WIN: how the boundary window is read.  0: both halves (boundaries bt..bt+127)
+// reloaded every tile; 1: the second half only for a tile whose 64 first
+// boundaries all lie in it (no tile of config 3: at most 58); 2 (default): as
+// 1, and the first half slides -- the next tile's window is this one shifted by
+// the tile's boundary count (ds_bpermute), only the new entries loaded.  A tile
+// of config 3 ends ~5 records, so 0 requested 1 KiB of off[] per 8 KiB tile.
+template <int ABLATE = 0, int BLOCK = 1024, int SLOTS = 2, bool BATCH = false, bool QST = true, int WIN = 2>
 __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
   if (!*P.sflag) return;  // not a packed batch of >= 64-byte records: the walking kernel takes it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1556,22 +1563,75 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     }
     qn = 0;
   };
-  stream_win_issue(P, bt, lane, Wn);
+  // QST: the CRCs are queued in one VGPR (lane p: record qb + p, qb a
+  // multiple of 64) and stored as whole 256-byte blocks.  A wave's records are
+  // consecutive, so only its first and last blocks are partial.  Per-tile
+  // stores of the ~5 records a tile ends wrote partial 128-byte lines: the
+  // config-3 PMC counted 5.9 GB of fetches (and 2x the output's bytes written)
+  // for the 0.27 GB output (profiles/r02/official_b, a3 against c0).
+  uint32_t qv = 0;
+  uint64_t qb = b_lo & ~63ull;
+  uint32_t qs = (uint32_t)(b_lo & 63u), qf = qs;  // first valid lane of the block, next lane to fill
+  auto qstore = [&](uint32_t v, bool on) {  // block qb from a uniform base: no 64-bit lane address to keep
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(P.out + qb), (short)0, 256, 0x00020000);
+    if (on) __builtin_amdgcn_raw_buffer_store_b32(v, r, lane << 2, 0, 0);
+  };
+  auto qpush = [&](uint32_t v, uint32_t i0, uint32_t cnt) {  // window lanes i0 .. i0+cnt-1: the next cnt records
+    const uint32_t src = (lane - qf + i0) & 63u;
+    const uint32_t val = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+    const uint32_t end = qf + cnt;  // cnt <= 64 - i0: at most one block completes
+    qv = (lane >= qf && lane < end) ? val : qv;
+    if (end >= 64u) {
+      qstore(qv, lane >= qs);
+      qb += 64u;
+      qs = 0u;
+      qf = end - 64u;
+      qv = lane < qf ? val : qv;
+    } else {
+      qf = end;
+    }
+  };
+  stream_win_issue<WIN>(P, bt, lane, Wn);
 
   auto process = [&](const uint32_t (&U)[32], uint64_t t, auto&& issue_next) {
     const int64_t tb = tbase(t);
     // --- map: this tile's boundaries, bt .. bt+cnt-1 (window lanes); ra/rb:
     // tile-relative byte of boundary bt+lane / bt+64+lane (chunk = r >> 7)
     const uint64_t ia = bt + lane, ib = bt + 64u + lane;
-    const int64_t ra64 = (int64_t)(ia < n ? Wn.a : dend) - tb, rb64 = (int64_t)(ib < n ? Wn.b : dend) - tb;
-    const bool ina = ia <= b_hi && ra64 < 8192, inb = ib <= b_hi && rb64 < 8192;
+    const int64_t ra64 = (int64_t)(ia < n ? Wn.a : dend) - tb;
+    const bool ina = ia <= b_hi && ra64 < 8192;
+    const uint64_t bal_a = __ballot(ina);
+    int64_t rb64 = 8192;
+    bool inb = false;
+    if constexpr (WIN == 0) {
+      rb64 = (int64_t)(ib < n ? Wn.b : dend) - tb;
+      inb = ib <= b_hi && rb64 < 8192;
+    } else if (bal_a == ~0ull) {  // the first 64 boundaries all end here: the next 64 may too
+      const uint64_t wb = P.off[ib < n ? ib : n - 1];
+      rb64 = (int64_t)(ib < n ? wb : dend) - tb;
+      inb = ib <= b_hi && rb64 < 8192;
+    }
     const uint32_t ra = (uint32_t)ra64 & 8191u, rb = (uint32_t)rb64 & 8191u;
-    const uint64_t bal_a = __ballot(ina), bal_b = __ballot(inb);
+    const uint64_t bal_b = __ballot(inb);
     const uint32_t na = (uint32_t)__builtin_popcountll(bal_a), nb = (uint32_t)__builtin_popcountll(bal_b);
     const uint32_t cnt = na + nb;
     const uint64_t bt0 = bt;
     bt += cnt;
-    stream_win_issue(P, bt, lane, Wn);  // the next tile's window (lands while this tile is checksummed)
+    // the next tile's window (lands while this tile is checksummed)
+    if constexpr (WIN == 2) {
+      const uint32_t src = lane + cnt;  // lanes whose entry this window holds take it from there
+      const int sp = (int)((src & 63u) << 2);
+      const uint32_t wlo = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)(uint32_t)Wn.a);
+      const uint32_t whi = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)(uint32_t)(Wn.a >> 32));
+      Wn.a = ((uint64_t)whi << 32) | wlo;
+      if (src >= 64u) {  // the new entries only
+        const uint64_t i2 = bt + lane;
+        Wn.a = P.off[i2 < n ? i2 : n - 1];
+      }
+    } else {
+      stream_win_issue<WIN>(P, bt, lane, Wn);
+    }
     // then the payload SLOTS-1 tiles ahead: after the window, so that waiting
     // for the window at the next tile never waits for that payload
     issue_next();
@@ -1666,7 +1726,7 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     // Y = X[c-1] of the window lane's end chunk c; the record began at the
     // previous window lane's chunk, whose Y is one DPP shift away (lane 0:
     // `first`, the carry term or the other half's last Y)
-    auto finish = [&](bool in, uint32_t r, uint32_t first, uint64_t bidx) -> uint32_t {
+    auto finish = [&](bool in, uint32_t r, uint32_t first, uint64_t bidx, uint32_t i0, uint32_t cnt) -> uint32_t {
       const uint32_t c = r >> 7, j = r & 127u;
       const uint32_t Xc = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((c - 1u) & 63u) << 2), (int)X);
       const uint32_t Y = c ? Xc : 0u;
@@ -1699,6 +1759,7 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
       // only the lanes holding a record from here on (a few per tile): the LDS
       // reads below cost per active lane, and all 64 lanes doing them cost
       // 4.8 of 25.6 ms (crc_ablate 5); the bpermutes above need every lane
+      uint32_t fv = 0u;
       if (in && bidx > b_lo) {
         const bool h = j >= 64u;
         const uint32_t Pv = h ? (shift_bytes32<2>(smem, H) ^ R0c) : H;
@@ -1711,15 +1772,22 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
           // the capture is exact (the chain's bytes before j): one multiply
           v = stream_mulcol(Pv, LDS_XMC_OFF(j & 63u)) ^ (h ? A1c : A0c);
         }
-        P.out[bidx - 1u] = ~v;
+        fv = ~v;
+        if constexpr (!QST) P.out[bidx - 1u] = fv;
+      }
+      if constexpr (QST) {
+        if (cnt) qpush(fv, i0, cnt);
       }
       return Y;
     };
     if (ABLATE == 5) {  // diagnostic: no record finish (one store keeps the tile's work alive)
       if (X == 0x9E3779B1u) P.out[0] = X ^ R0 ^ cap0 ^ cap1;
     } else {
-      const uint32_t Ya = finish(ina, ra, cterm, bt0 + lane);
-      if (nb) finish(inb, rb, (uint32_t)__builtin_amdgcn_readlane((int)Ya, 63), bt0 + 64u + lane);
+      // record lanes: window lanes with a boundary after b_lo (only lane 0 of
+      // the wave's first tile is not one)
+      const uint32_t i0 = bt0 == b_lo ? 1u : 0u;
+      const uint32_t Ya = finish(ina, ra, cterm, bt0 + lane, i0, na > i0 ? na - i0 : 0u);
+      if (nb) finish(inb, rb, (uint32_t)__builtin_amdgcn_readlane((int)Ya, 63), bt0 + 64u + lane, 0u, nb);
     }
     // --- carry: the record active at the tile's end
     const uint32_t X63 = (uint32_t)__builtin_amdgcn_readlane((int)X, 63);
@@ -1757,6 +1825,9 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     if (i < ntile) process(U0, t_first + i, none);
   }
   if constexpr (BATCH) flush();
+  if constexpr (QST && !BATCH) {
+    qstore(qv, lane >= qs && lane < qf);
+  }
 }
 }  // namespace lsmck
 
@@ -1925,8 +1996,13 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   hipLaunchKernelGGL(stream_cuts, dim3((W + 1u + 255u) / 256u), dim3(256), 0, st, *P, W);
   const int ablate = (variant >> 8) & 0xF;
   const bool batch = (variant & 0x800000) != 0;  // A/B: batched record finish
+  const bool tstore = (variant & 0x4000000) != 0;  // A/B: per-tile stores instead of queued 256-B blocks
+  const int win = 2 - (int)((variant >> 27) & 3u);  // A/B: boundary window form (crc_stream_window)
   const void* fn = batch ? (w12 ? (const void*)crc32_stream_kernel<0, 768, 2, true>
                                 : (const void*)crc32_stream_kernel<0, 1024, 2, true>)
+                 : (tstore && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, false>
+                 : (win == 1 && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 1>
+                 : (win == 0 && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 0>
                  : (ablate >= 4 && ablate <= 9 && !w12)
                        ? (ablate == 4 ? (const void*)crc32_stream_kernel<4>
                           : ablate == 5 ? (const void*)crc32_stream_kernel<5>

@@ -143,10 +143,13 @@ def test_host_batches_use_it_too(ctx):
     assert np.array_equal(ctx.crc32(data, off, ln), O.crc32_batch(data, off, ln, threads=8))
 
 
-@pytest.mark.parametrize("waves,ring,batch", [(12, 0, 0), (12, 3, 0), (0, 0, 1), (12, 0, 1)])
-def test_workgroup_and_slot_variants(ctx, waves, ring, batch):
+@pytest.mark.parametrize("waves,ring,batch,qstore,window", [(12, 0, 0, 1, 2), (12, 3, 0, 1, 2), (0, 0, 1, 1, 2),
+                                                           (12, 0, 1, 1, 2), (0, 0, 0, 0, 2), (0, 0, 0, 1, 1),
+                                                           (0, 0, 0, 1, 0)])
+def test_workgroup_and_slot_variants(ctx, waves, ring, batch, qstore, window):
     """The 12-wave workgroup form (168 VGPRs) with two and three payload slots
-    in flight, and the records finished in batches of 64: same CRCs as the
+    in flight, the records finished in batches of 64, per-tile stores instead
+    of queued 256-B blocks, and the reloaded boundary windows: same CRCs as the
     oracle."""
     rng = np.random.default_rng(8)
     lens = rng.choice([64, 65, 100, 127, 128, 129, 300, 1000, 4096, 20000], 50000)
@@ -156,6 +159,8 @@ def test_workgroup_and_slot_variants(ctx, waves, ring, batch):
     ctx.set_option("crc_wg_waves", waves)
     ctx.set_option("crc_ring", ring)
     ctx.set_option("crc_stream_batch", batch)
+    ctx.set_option("crc_stream_qstore", qstore)
+    ctx.set_option("crc_stream_window", window)
     ctx.set_option("crc_stream", 2)
     try:
         got = _device(ctx, data, off, ln)
@@ -163,5 +168,7 @@ def test_workgroup_and_slot_variants(ctx, waves, ring, batch):
         ctx.set_option("crc_wg_waves", 0)
         ctx.set_option("crc_ring", 0)
         ctx.set_option("crc_stream_batch", 0)
+        ctx.set_option("crc_stream_qstore", 1)
+        ctx.set_option("crc_stream_window", 2)
         ctx.set_option("crc_stream", 1)
     assert np.array_equal(got, want)
