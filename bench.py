@@ -244,7 +244,7 @@ def main():
                 # (1 global, 2 raw buffer); "r<n>" = crc_ring n (1 = two-slot kernel)
                 # "b<n>" = sha_bucket_shift n (SHA order: 2^n-block buckets for 128..1023 blocks)
                 # "f<n>" = sha_bucket_from n (first block count of the coarse buckets)
-                # "o<n>" = crc_order n (fixed ring kernel tile order)
+                # "o<n>" = crc_order n (fixed ring kernel tile order; 3 = default)
                 # "p<n>" = sha_pair n (SHA-256: two blocks per load window)
                 # "s<n>" = crc_stream n (descriptor batches: 1 stream kernel where eligible, 0 walking kernel)
                 # "q<n>" = crc_stream_batch n (stream kernel: records finished in batches of 64)
@@ -262,7 +262,7 @@ def main():
                 ctx.set_option("crc_ring", int(m.group(5) or 0))
                 ctx.set_option("sha_bucket_shift", int(m.group(6)) if m.group(6) is not None else 2)
                 ctx.set_option("sha_bucket_from", int(m.group(7) or 128))
-                ctx.set_option("crc_order", int(m.group(8) or 0))
+                ctx.set_option("crc_order", int(m.group(8)) if m.group(8) is not None else 3)
                 ctx.set_option("sha_pair", int(m.group(9)) if m.group(9) is not None else 1)
                 ctx.set_option("crc_stream", int(m.group(10)) if m.group(10) is not None else 1)
                 ctx.set_option("crc_stream_batch", int(m.group(11) or 0))
@@ -288,7 +288,7 @@ def main():
         ctx.set_option("crc_stream_batch", 0)
         ctx.set_option("crc_stream_qstore", 1)
         ctx.set_option("crc_stream_window", 2)
-        ctx.set_option("crc_order", 0)
+        ctx.set_option("crc_order", 3)
         ab = {str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                        "GiBps_median": payload / GIB / (float(np.median(t)) * 1e-3)} for v, t in ab.items()}
 

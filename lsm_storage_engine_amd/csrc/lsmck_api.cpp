@@ -741,7 +741,7 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     return 0;
   }
   if (!strcmp(key, "crc_ablate")) {  // diagnostic only: timing ablations, results are garbage
-    if (value < 0 || value > 14) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0..14");
+    if (value < 0 || value > 15) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0..15");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->variant = (ctx->variant & ~0xF00) | ((int)value << 8);
     return 0;
@@ -844,10 +844,14 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->variant = (ctx->variant & ~0x10000) | (value ? 0 : 0x10000);
     return 0;
   }
-  if (!strcmp(key, "crc_order")) {  // A/B: fixed ring kernel tile order, 0 strided, 1 contiguous, 2 claimed blocks
-    if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_order must be 0, 1 or 2");
+  if (!strcmp(key, "crc_order")) {  // A/B: fixed ring kernel tile order, 0 strided, 1 contiguous, 2 claimed blocks,
+                                    // 3 contiguous with the CRCs stored as queued 256-B blocks (default), 4
+                                    // strided with the CRCs of 16 tiles gathered in LDS (<= 4 records per tile),
+                                    // 5 strided with each tile's store after the next tile's loads
+    if (value < 0 || value > 5) return lsmck_host::set_error(LSMCK_EINVAL, "crc_order must be 0..5");
     std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~0x3000000) | ((int)value << 24);
+    // stored as order + 1 (0 = the default)
+    ctx->variant = (ctx->variant & ~0x7000000) | ((value == LSMCK_DEFAULT_ORDER ? 0 : (int)value + 1) << 24);
     return 0;
   }
   if (!strcmp(key, "crc_stream_batch")) {  // A/B: stream kernel, records finished in batches of 64 (1) or per tile (0)
@@ -867,7 +871,7 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
                                             // or per tile (0)
     if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_qstore must be 0 or 1");
     std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~0x4000000) | (value ? 0 : 0x4000000);
+    ctx->variant = (ctx->variant & ~0x20000000) | (value ? 0 : 0x20000000);
     return 0;
   }
   if (!strcmp(key, "crc_stream")) {  // A/B: descriptor batches, 1 = stream kernel for packed >= 64-byte records

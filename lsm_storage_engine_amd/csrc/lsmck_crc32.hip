@@ -55,6 +55,10 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #define LDS_TINIT_OFF (LDS_KMID_OFF + 512u)
 #define LDS_SCRATCH_OFF (LDS_TINIT_OFF + 544u)
 #define WAVE_SCRATCH_BYTES 256u
+// ring kernel, ORDER 4: each wave's CRCs of 16 tiles (<= 4 records per tile)
+// gathered in LDS behind the kernel's tables, then stored by one instruction
+#define LDS_WOUT_OFF LDS_SCRATCH_OFF
+#define LDS_WOUT_BYTES 4096u
 #ifndef LSMCK_DEFAULT_CHAINS
 #define LSMCK_DEFAULT_CHAINS 2       // fixed records (A/B: profiles/r01)
 #endif
@@ -515,6 +519,14 @@ __device__ __forceinline__ void finish_tile(const unsigned char* smem, const Crc
   }
   v = (L.fl & FL_VALID) ? v : 0u;
   v = run_xor(v, min(63u, lane + L.k));
+  if (ABLATE == 14) {  // diagnostic: everything but the output store (results invalid)
+    if (v == 0x9E3779B1u) P.out[0] = v;
+    return;
+  }
+  if (ABLATE == 15) {  // diagnostic: the store, but every tile of a wave to the same 8 bytes (an L2 hit)
+    if ((L.fl & FL_VALID) && (L.fl & FL_FIRST)) P.out[((blockIdx.x * 16u + (threadIdx.x >> 6)) * 2u + (lane >> 5)) & 1023u] = ~v;
+    return;
+  }
   emit_record(P, v, L, lane, lane == 0 || (L.fl & FL_FIRST));
 }
 
@@ -684,7 +696,12 @@ __device__ __forceinline__ void issue_whole(const CrcParams& P, const PercolMap&
 // tools/microbench_walk.hip measured the load stream at 10.69 / 10.65 / 10.52
 // ms for 64 GiB in these orders (profiles/r02/mb/mb_walk64.log).
 #define WRING_BLOCK 16u
-template <int R, int ABLATE = 0, int BLOCK = 1024, int ORDER = 0>
+// QST (ORDER 1 only: a wave's records are consecutive): the CRCs are queued in
+// one VGPR (lane p: record qb + p) and stored as whole 256-byte blocks, as in
+// the stream kernel.  The per-tile store of a tile's two 4 KiB records (8
+// bytes) cost 0.68 of 11.96 ms on config 2 (crc_ablate 14:
+// profiles/r02/q/ab_r02c2s.log) and 0.94 GB of fetches per launch.
+template <int R, int ABLATE = 0, int BLOCK = 1024, int ORDER = 0, bool QST = false>
 __global__ __launch_bounds__(BLOCK) void crc32_wring_kernel(CrcParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t nsegr = P.flen >> 7;
@@ -702,6 +719,31 @@ __global__ __launch_bounds__(BLOCK) void crc32_wring_kernel(CrcParams P) {
   M.tstride = (uint64_t)(64u >> M.lsh) * P.stride;
   M.end = (uint64_t)(P.nrec - 1) * P.stride + P.flen;
   const uint32_t vo = (uint32_t)((lane >> M.lsh) * P.stride) + 128u * (lane & (nsegr - 1u));
+  const uint32_t m = 64u >> M.lsh;  // records per tile
+  uint32_t qv = 0, qs = 0, qf = 0;
+  uint64_t qb = 0;
+  auto qstore = [&](bool on) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(P.out + qb), (short)0, 256, 0x00020000);
+    if (ABLATE == 14) on = on && qv == 0x9E3779B1u;  // diagnostic: no output store
+    if (on) __builtin_amdgcn_raw_buffer_store_b32(qv, r, lane << 2, 0, 0);
+  };
+  // the tile's records (head lanes 0, nsegr, ...; cnt of them valid) onto the queue
+  auto qpush = [&](uint32_t v, uint32_t cnt) {
+    const uint32_t k = (lane - qf) & 63u;  // the queue lane's record within the tile
+    const uint32_t val = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((k << M.lsh) & 63u) << 2), (int)v);
+    const uint32_t end = qf + cnt;  // cnt <= 64: at most one block completes
+    qv = (lane >= qf && lane < end) ? val : qv;
+    if (end >= 64u) {
+      qstore(lane >= qs);
+      qb += 64u;
+      qs = 0u;
+      qf = end - 64u;
+      qv = lane < qf ? val : qv;
+    } else {
+      qf = end;
+    }
+  };
   // walk tiles t0, t0 + step, ... (mine of them) through the R-slot ring
   auto run = [&](uint32_t t0, uint32_t mine, uint32_t step) {
     const uint32_t iters = (mine + R - 1u) / R;
@@ -709,6 +751,12 @@ __global__ __launch_bounds__(BLOCK) void crc32_wring_kernel(CrcParams P) {
     // marked invalid (no store)
     auto tile_of = [&](uint32_t i) -> uint32_t { return i < mine ? t0 + i * step : t0; };
     SegLoad S[R];
+    // ORDER 5 / QST: the previous tile's CRCs, stored (pushed) only after the
+    // next tile's loads are issued -- no work between a tile's checksum and
+    // the next issue (profiles/r02/q: a store or queue push there cost
+    // 1.2-1.5 ms of 12.2 on config 2, whatever its address)
+    uint32_t dv = 0, drec = 0, dcnt = 0;
+    bool dst = false;
 #pragma unroll
     for (int k = 0; k < R - 1; ++k) {
       issue_whole(P, M, vo, tile_of(k), lane, nsegr, (k < (int)mine) ? total : 0u, S[k]);
@@ -721,18 +769,63 @@ __global__ __launch_bounds__(BLOCK) void crc32_wring_kernel(CrcParams P) {
         const uint32_t ni = n0 + k + R - 1;
         issue_whole(P, M, vo, tile_of(ni), lane, nsegr, ni < mine ? total : 0u, S[(k + R - 1) % R]);
         __builtin_amdgcn_sched_barrier(0);
-        finish_tile<true, 2, ABLATE, true>(smem, P, S[k % R], lane, lo, hi);
+        if constexpr (ORDER == 5) {
+          if (dst) P.out[drec] = dv;
+          uint32_t v = seg_finish<true, 2, ABLATE, true>(smem, P, S[k % R], lo, hi);
+          v = (S[k % R].fl & FL_VALID) ? v : 0u;
+          v = run_xor(v, min(63u, lane + S[k % R].k));
+          dv = ~v;
+          drec = S[k % R].rec;
+          dst = (S[k % R].fl & FL_VALID) && (S[k % R].fl & FL_FIRST);  // tiles start on records: heads end in the tile
+        } else if constexpr (ORDER == 4) {
+          // the tile's head lanes write their CRCs to the wave's LDS rows; every
+          // 16 tiles the rows go out in one store (lane l: tile l / m, record l % m)
+          const uint32_t ti = n0 + k;
+          uint32_t v = seg_finish<true, 2, ABLATE, true>(smem, P, S[k % R], lo, hi);
+          v = (S[k % R].fl & FL_VALID) ? v : 0u;
+          v = ~run_xor(v, min(63u, lane + S[k % R].k));
+          const uint32_t wb = LDS_WOUT_OFF + (threadIdx.x >> 6) * 256u;
+          if ((lane & (nsegr - 1u)) == 0u)
+            *(__attribute__((address_space(3))) uint32_t*)(size_t)(wb + (((ti & 15u) * m + (lane >> M.lsh)) << 2)) = v;
+          if (ti < mine && ((ti & 15u) == 15u || ti + 1u == mine)) {
+            const uint32_t j = lane >> __builtin_ctz(m), tj = (ti & ~15u) + j;
+            const uint32_t w = *(__attribute__((address_space(3))) const uint32_t*)(size_t)(wb + (lane << 2));
+            const uint64_t rec = (uint64_t)(t0 + tj * step) * m + (lane & (m - 1u));
+            if (lane < 16u * m && tj <= ti && rec < P.nrec) P.out[rec] = w;  // tj <= ti < mine
+          }
+        } else if constexpr (QST) {
+          if (dcnt) qpush(dv, dcnt);
+          const uint32_t ti = n0 + k;  // this slot's tile, valid if ti < mine
+          uint32_t v = seg_finish<true, 2, ABLATE, true>(smem, P, S[k % R], lo, hi);
+          v = (S[k % R].fl & FL_VALID) ? v : 0u;
+          dv = ~run_xor(v, min(63u, lane + S[k % R].k));
+          const uint64_t r0 = (uint64_t)(t0 + ti) * m;  // the tile's first record
+          dcnt = ti < mine ? (uint32_t)min((uint64_t)m, (uint64_t)P.nrec - r0) : 0u;
+        } else {
+          finish_tile<true, 2, ABLATE, true>(smem, P, S[k % R], lane, lo, hi);
+        }
       }
       n0 += R;
     }
+    if constexpr (ORDER == 5) {
+      if (dst) P.out[drec] = dv;
+    }
+    if constexpr (QST) {
+      if (dcnt) qpush(dv, dcnt);
+    }
   };
-  if constexpr (ORDER == 0) {
+  if constexpr (ORDER == 0 || ORDER == 4 || ORDER == 5) {
     if (wave >= ntiles) return;
     run(wave, (ntiles - wave + nwaves - 1u) / nwaves, nwaves);
   } else if constexpr (ORDER == 1) {
     const uint32_t per = (ntiles + nwaves - 1u) / nwaves, t0 = wave * per;
     if (t0 >= ntiles) return;
+    if constexpr (QST) {
+      qb = ((uint64_t)t0 * m) & ~63ull;
+      qs = qf = (uint32_t)(((uint64_t)t0 * m) & 63u);
+    }
     run(t0, min(per, ntiles - t0), 1u);
+    if constexpr (QST) qstore(lane >= qs && lane < qf);
   } else {
     const uint32_t nb = (ntiles + WRING_BLOCK - 1u) / WRING_BLOCK;
     for (;;) {
@@ -1847,10 +1940,10 @@ static int launch_fixed(const CrcParams* P, int ncu, hipStream_t st) {
   return e == hipSuccess ? 0 : -(int)e;
 }
 
-template <int R, int ABLATE = 0, int BLOCK = 1024, int ORDER = 0>
+template <int R, int ABLATE = 0, int BLOCK = 1024, int ORDER = 0, bool QST = false>
 static int launch_wring(const CrcParams* P, int ncu, hipStream_t st) {
-  size_t lds = LDS_SCRATCH_OFF;
-  hipError_t e = hipFuncSetAttribute((const void*)crc32_wring_kernel<R, ABLATE, BLOCK, ORDER>,
+  size_t lds = LDS_SCRATCH_OFF + (ORDER == 4 ? LDS_WOUT_BYTES : 0u);
+  hipError_t e = hipFuncSetAttribute((const void*)crc32_wring_kernel<R, ABLATE, BLOCK, ORDER, QST>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return -(int)e;
   if (ORDER == 2) {
@@ -1858,7 +1951,7 @@ static int launch_wring(const CrcParams* P, int ncu, hipStream_t st) {
     e = hipMemsetAsync(P->work, 0, 4, st);
     if (e != hipSuccess) return -(int)e;
   }
-  hipLaunchKernelGGL((crc32_wring_kernel<R, ABLATE, BLOCK, ORDER>), dim3(ncu), dim3(BLOCK), lds, st, *P);
+  hipLaunchKernelGGL((crc32_wring_kernel<R, ABLATE, BLOCK, ORDER, QST>), dim3(ncu), dim3(BLOCK), lds, st, *P);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
 }
@@ -1883,14 +1976,23 @@ extern "C" int lsmk_launch_crc32_fixed(const CrcParams* P, int ncu, int variant,
   // ring kernel (variant bits 12-15: 1 = the two-slot kernel below, 2 or 3 =
   // whole-tile ring of that many slots; 0 = LSMCK_DEFAULT_RING)
   const int ring = ((variant >> 12) & 0xF) ? ((variant >> 12) & 0xF) : LSMCK_DEFAULT_RING;
-  if (fast && percol && buf && ring >= 2 && (ablate == 0 || ablate == 3)) {
+  if (fast && percol && buf && ring >= 2 && (ablate == 0 || ablate == 3 || ablate == 14 || ablate == 15)) {
+    const int osel14 = (variant >> 24) & 7, order14 = osel14 ? osel14 - 1 : LSMCK_DEFAULT_ORDER;
+    if (ablate == 14 && order14 == 0) return launch_wring<2, 14>(P, ncu, st);  // diagnostic: no output store
+    if (ablate == 15 && order14 == 0) return launch_wring<2, 15>(P, ncu, st);  // diagnostic: L2-hit stores
+    if (ablate == 14 && order14 == 3) return launch_wring<2, 14, 1024, 1, true>(P, ncu, st);
     if (variant & 0x20) {  // 12-wave workgroups (168 VGPRs per lane): A/B of the 3-slot ring
       if (ring == 2) return launch_wring<2, 0, 768>(P, ncu, st);
       return ablate ? launch_wring<3, 3, 768>(P, ncu, st) : launch_wring<3, 0, 768>(P, ncu, st);
     }
     // tile order (variant bits 24-25): 0 strided, 1 contiguous per wave, 2 claimed blocks
-    const int order = (variant >> 24) & 3;
+    const int osel = (variant >> 24) & 7, order = osel ? osel - 1 : LSMCK_DEFAULT_ORDER;
+    if (ring == 2 && order == 1 && ablate == 14) return launch_wring<2, 14, 1024, 1>(P, ncu, st);
     if (ring == 2 && order == 1) return ablate ? launch_wring<2, 3, 1024, 1>(P, ncu, st) : launch_wring<2, 0, 1024, 1>(P, ncu, st);
+    if (ring == 2 && order == 5) return ablate ? launch_wring<2, 3>(P, ncu, st) : launch_wring<2, 0, 1024, 5>(P, ncu, st);
+    if (ring == 2 && order == 4 && (P->flen >> 7) >= 16u)  // <= 4 records per tile
+      return ablate ? launch_wring<2, 3, 1024, 4>(P, ncu, st) : launch_wring<2, 0, 1024, 4>(P, ncu, st);
+    if (ring == 2 && order == 3) return ablate ? launch_wring<2, 3, 1024, 1>(P, ncu, st) : launch_wring<2, 0, 1024, 1, true>(P, ncu, st);
     if (ring == 2 && order == 2) return ablate ? launch_wring<2, 3, 1024, 2>(P, ncu, st) : launch_wring<2, 0, 1024, 2>(P, ncu, st);
     if (ring == 2) return ablate ? launch_wring<2, 3>(P, ncu, st) : launch_wring<2, 0>(P, ncu, st);
     return ablate ? launch_wring<3, 3>(P, ncu, st) : launch_wring<3, 0>(P, ncu, st);
@@ -1996,7 +2098,7 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   hipLaunchKernelGGL(stream_cuts, dim3((W + 1u + 255u) / 256u), dim3(256), 0, st, *P, W);
   const int ablate = (variant >> 8) & 0xF;
   const bool batch = (variant & 0x800000) != 0;  // A/B: batched record finish
-  const bool tstore = (variant & 0x4000000) != 0;  // A/B: per-tile stores instead of queued 256-B blocks
+  const bool tstore = (variant & 0x20000000) != 0;  // A/B: per-tile stores instead of queued 256-B blocks
   const int win = 2 - (int)((variant >> 27) & 3u);  // A/B: boundary window form (crc_stream_window)
   const void* fn = batch ? (w12 ? (const void*)crc32_stream_kernel<0, 768, 2, true>
                                 : (const void*)crc32_stream_kernel<0, 1024, 2, true>)

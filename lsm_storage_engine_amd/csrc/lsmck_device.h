@@ -7,6 +7,10 @@
 
 #include "lsmck.h"
 
+// fixed-record ring kernel tile order (crc_order): 3 = one contiguous tile
+// range per wave, CRCs stored as queued 256-byte blocks (A/B: profiles/r02/q)
+#define LSMCK_DEFAULT_ORDER 3
+
 namespace lsmck {
 
 // CRC-32 batch job.  Records are either fixed ([r*stride, r*stride+flen)) or

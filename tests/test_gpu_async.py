@@ -212,14 +212,16 @@ def test_walk_and_tile_map_kernels_agree(ctx, walk):
         ctx.set_option("crc_walk", 1)
 
 
-@pytest.mark.parametrize("order", [0, 1, 2])
+@pytest.mark.parametrize("order", [0, 1, 2, 3, 4, 5])
 def test_fixed_ring_tile_orders(ctx, order):
     """The fixed-record ring kernel walks its tiles strided (0), as one
-    contiguous range per wave (1) or as claimed 16-tile blocks (2): the same
-    CRCs either way, including a last partial tile and fewer tiles than waves."""
+    contiguous range per wave (1, and 3 with the CRCs stored as queued 256-B
+    blocks) or as claimed 16-tile blocks (2): the same CRCs either way,
+    including a last partial tile and fewer tiles than waves."""
     ctx.set_option("crc_order", order)
     try:
-        for length, nb in ((4096, 1 << 16), (4096, 77), (256, 100003), (1024, 5000)):
+        for length, nb in ((4096, 1 << 16), (4096, 77), (256, 100003), (1024, 5000), (128, 777777), (8192, 9999),
+                           (2048, 1 << 20)):
             d = ctx.alloc(nb * length)
             out = ctx.alloc(4 * nb)
             try:
@@ -232,4 +234,4 @@ def test_fixed_ring_tile_orders(ctx, order):
                 d.free()
                 out.free()
     finally:
-        ctx.set_option("crc_order", 0)
+        ctx.set_option("crc_order", 3)
