@@ -248,7 +248,8 @@ def main():
                 # "p<n>" = sha_pair n (SHA-256: two blocks per load window)
                 # "s<n>" = crc_stream n (descriptor batches: 1 stream kernel where eligible, 0 walking kernel)
                 # "q<n>" = crc_stream_batch n (stream kernel: records finished in batches of 64)
-                # "t<n>" = crc_stream_qstore n (stream kernel: 1 queued 256-B output blocks, 0 per-tile stores)
+                # "t<n>" = crc_stream_qstore n (stream kernel: 1 queued 256-B output blocks, 0 per-tile stores,
+                #          2 queued with the push deferred to the next tile)
                 # "v<n>" = crc_stream_window n (stream kernel: 2 sliding, 1 second half on demand, 0 reloaded)
                 m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?(?:r(\d))?(?:b(\d))?(?:f(\d+))?(?:o(\d))?(?:p(\d))?(?:s(\d))?(?:q(\d))?(?:t(\d))?(?:v(\d))?", v)
                 if not m:

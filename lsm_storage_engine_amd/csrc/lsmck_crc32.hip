@@ -1603,7 +1603,10 @@ __device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
 // 1, and the first half slides -- the next tile's window is this one shifted by
 // the tile's boundary count (ds_bpermute), only the new entries loaded.  A tile
 // of config 3 ends ~5 records, so 0 requested 1 KiB of off[] per 8 KiB tile.
-template <int ABLATE = 0, int BLOCK = 1024, int SLOTS = 2, bool BATCH = false, bool QST = true, int WIN = 2>
+// DQ (with QST): a tile's first-half records are pushed onto the queue at the
+// next tile, after its payload loads are issued (as the ring kernel's order 3).
+template <int ABLATE = 0, int BLOCK = 1024, int SLOTS = 2, bool BATCH = false, bool QST = true, int WIN = 2,
+          bool DQ = false>
 __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
   if (!*P.sflag) return;  // not a packed batch of >= 64-byte records: the walking kernel takes it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1685,6 +1688,7 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
       qf = end;
     }
   };
+  uint32_t dqv = 0, dqi0 = 0, dqcnt = 0;  // DQ: the deferred push
   stream_win_issue<WIN>(P, bt, lane, Wn);
 
   auto process = [&](const uint32_t (&U)[32], uint64_t t, auto&& issue_next) {
@@ -1729,6 +1733,10 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     // for the window at the next tile never waits for that payload
     issue_next();
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (QST && DQ) {
+      if (dqcnt) qpush(dqv, dqi0, dqcnt);
+      dqcnt = 0;
+    }
     uint64_t M1, M2;
     bool any2;
     {
@@ -1819,7 +1827,8 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     // Y = X[c-1] of the window lane's end chunk c; the record began at the
     // previous window lane's chunk, whose Y is one DPP shift away (lane 0:
     // `first`, the carry term or the other half's last Y)
-    auto finish = [&](bool in, uint32_t r, uint32_t first, uint64_t bidx, uint32_t i0, uint32_t cnt) -> uint32_t {
+    auto finish = [&](bool in, uint32_t r, uint32_t first, uint64_t bidx, uint32_t i0, uint32_t cnt,
+                      bool half_b) -> uint32_t {
       const uint32_t c = r >> 7, j = r & 127u;
       const uint32_t Xc = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((c - 1u) & 63u) << 2), (int)X);
       const uint32_t Y = c ? Xc : 0u;
@@ -1868,7 +1877,17 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
         fv = ~v;
         if constexpr (!QST) P.out[bidx - 1u] = fv;
       }
-      if constexpr (QST) {
+      if constexpr (QST && DQ) {
+        if (half_b) {  // (rare) the first half's records go first
+          if (dqcnt) qpush(dqv, dqi0, dqcnt);
+          dqcnt = 0;
+          if (cnt) qpush(fv, i0, cnt);
+        } else {
+          dqv = fv;
+          dqi0 = i0;
+          dqcnt = cnt;
+        }
+      } else if constexpr (QST) {
         if (cnt) qpush(fv, i0, cnt);
       }
       return Y;
@@ -1879,8 +1898,8 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
       // record lanes: window lanes with a boundary after b_lo (only lane 0 of
       // the wave's first tile is not one)
       const uint32_t i0 = bt0 == b_lo ? 1u : 0u;
-      const uint32_t Ya = finish(ina, ra, cterm, bt0 + lane, i0, na > i0 ? na - i0 : 0u);
-      if (nb) finish(inb, rb, (uint32_t)__builtin_amdgcn_readlane((int)Ya, 63), bt0 + 64u + lane, 0u, nb);
+      const uint32_t Ya = finish(ina, ra, cterm, bt0 + lane, i0, na > i0 ? na - i0 : 0u, false);
+      if (nb) finish(inb, rb, (uint32_t)__builtin_amdgcn_readlane((int)Ya, 63), bt0 + 64u + lane, 0u, nb, true);
     }
     // --- carry: the record active at the tile's end
     const uint32_t X63 = (uint32_t)__builtin_amdgcn_readlane((int)X, 63);
@@ -1919,6 +1938,9 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
   }
   if constexpr (BATCH) flush();
   if constexpr (QST && !BATCH) {
+    if constexpr (DQ) {
+      if (dqcnt) qpush(dqv, dqi0, dqcnt);
+    }
     qstore(qv, lane >= qs && lane < qf);
   }
 }
@@ -2100,9 +2122,11 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   const bool batch = (variant & 0x800000) != 0;  // A/B: batched record finish
   const bool tstore = (variant & 0x20000000) != 0;  // A/B: per-tile stores instead of queued 256-B blocks
   const int win = 2 - (int)((variant >> 27) & 3u);  // A/B: boundary window form (crc_stream_window)
+  const bool dq = (variant & 0x40000000) != 0;       // A/B: deferred queue push (crc_stream_qstore 2)
   const void* fn = batch ? (w12 ? (const void*)crc32_stream_kernel<0, 768, 2, true>
                                 : (const void*)crc32_stream_kernel<0, 1024, 2, true>)
                  : (tstore && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, false>
+                 : (dq && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true>
                  : (win == 1 && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 1>
                  : (win == 0 && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 0>
                  : (ablate >= 4 && ablate <= 9 && !w12)

@@ -145,7 +145,7 @@ def test_host_batches_use_it_too(ctx):
 
 @pytest.mark.parametrize("waves,ring,batch,qstore,window", [(12, 0, 0, 1, 2), (12, 3, 0, 1, 2), (0, 0, 1, 1, 2),
                                                            (12, 0, 1, 1, 2), (0, 0, 0, 0, 2), (0, 0, 0, 1, 1),
-                                                           (0, 0, 0, 1, 0)])
+                                                           (0, 0, 0, 1, 0), (0, 0, 0, 2, 2)])
 def test_workgroup_and_slot_variants(ctx, waves, ring, batch, qstore, window):
     """The 12-wave workgroup form (168 VGPRs) with two and three payload slots
     in flight, the records finished in batches of 64, per-tile stores instead
