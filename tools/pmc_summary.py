@@ -7,6 +7,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 
@@ -38,7 +39,15 @@ def main():
         wb = 1024 * sum(w) / len(w) if w else None
         res[k] = {"dispatches": max(len(f), len(w)), "fetch_bytes_corrected": fb, "write_bytes": wb,
                   "hbm_bytes_per_launch": (fb or 0) + (wb or 0)}
-    dom = max(res.values(), key=lambda x: x["hbm_bytes_per_launch"]) if res else None
+    # the dominant kernel among the non-diagnostic ones (crc_ablate variants
+    # carry a nonzero ABLATE template argument)
+    def diagnostic(k):
+        m = re.search(r"crc32_(stream|wring|walk)_kernel<(\d+), (\d+)", k)
+        if not m:
+            return False
+        return int(m.group(2) if m.group(1) == "stream" else m.group(3)) != 0
+    real = {k: v for k, v in res.items() if not diagnostic(k)} or res
+    dom = max(real.values(), key=lambda x: x["hbm_bytes_per_launch"]) if real else None
     print(json.dumps({workload: {"hbm_bytes_per_launch": dom["hbm_bytes_per_launch"] if dom else None,
                                  "kernels": res,
                                  "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes; "
