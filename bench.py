@@ -248,8 +248,8 @@ def main():
                 # "p<n>" = sha_pair n (SHA-256: two blocks per load window)
                 # "s<n>" = crc_stream n (descriptor batches: 1 stream kernel where eligible, 0 walking kernel)
                 # "q<n>" = crc_stream_batch n (stream kernel: records finished in batches of 64)
-                # "t<n>" = crc_stream_qstore n (stream kernel: 1 queued 256-B output blocks, 0 per-tile stores,
-                #          2 queued with the push deferred to the next tile)
+                # "t<n>" = crc_stream_qstore n (stream kernel: 2 queued 256-B output blocks pushed at the next
+                #          tile (default), 1 pushed at once, 0 per-tile stores)
                 # "v<n>" = crc_stream_window n (stream kernel: 2 sliding, 1 second half on demand, 0 reloaded)
                 m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?(?:r(\d))?(?:b(\d))?(?:f(\d+))?(?:o(\d))?(?:p(\d))?(?:s(\d))?(?:q(\d))?(?:t(\d))?(?:v(\d))?", v)
                 if not m:
@@ -267,7 +267,7 @@ def main():
                 ctx.set_option("sha_pair", int(m.group(9)) if m.group(9) is not None else 1)
                 ctx.set_option("crc_stream", int(m.group(10)) if m.group(10) is not None else 1)
                 ctx.set_option("crc_stream_batch", int(m.group(11) or 0))
-                ctx.set_option("crc_stream_qstore", int(m.group(12)) if m.group(12) is not None else 1)
+                ctx.set_option("crc_stream_qstore", int(m.group(12)) if m.group(12) is not None else 2)
                 ctx.set_option("crc_stream_window", int(m.group(13)) if m.group(13) is not None else 2)
                 step()
                 e0.record(stream)
@@ -287,7 +287,7 @@ def main():
         ctx.set_option("sha_pair", 1)
         ctx.set_option("crc_stream", 1)
         ctx.set_option("crc_stream_batch", 0)
-        ctx.set_option("crc_stream_qstore", 1)
+        ctx.set_option("crc_stream_qstore", 2)
         ctx.set_option("crc_stream_window", 2)
         ctx.set_option("crc_order", 3)
         ab = {str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),

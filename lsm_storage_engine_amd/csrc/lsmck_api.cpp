@@ -867,12 +867,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->variant = (ctx->variant & ~0x18000000) | ((int)(2 - value) << 27);
     return 0;
   }
-  if (!strcmp(key, "crc_stream_qstore")) {  // A/B: stream kernel CRCs stored as queued 256-B blocks (1, default)
-                                            // or per tile (0)
+  if (!strcmp(key, "crc_stream_qstore")) {  // A/B: stream kernel CRCs stored as queued 256-B blocks, pushed
+                                            // at the next tile (2, default) or at once (1); or per tile (0)
     // or the queue's push deferred to the next tile (2)
     if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_qstore must be 0, 1 or 2");
     std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~0x60000000) | (value == 0 ? 0x20000000 : value == 2 ? 0x40000000 : 0);
+    ctx->variant = (ctx->variant & ~0x60000000) | (value == 0 ? 0x20000000 : value == 1 ? 0x40000000 : 0);
     return 0;
   }
   if (!strcmp(key, "crc_stream")) {  // A/B: descriptor batches, 1 = stream kernel for packed >= 64-byte records

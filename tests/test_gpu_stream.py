@@ -145,7 +145,7 @@ def test_host_batches_use_it_too(ctx):
 
 @pytest.mark.parametrize("waves,ring,batch,qstore,window", [(12, 0, 0, 1, 2), (12, 3, 0, 1, 2), (0, 0, 1, 1, 2),
                                                            (12, 0, 1, 1, 2), (0, 0, 0, 0, 2), (0, 0, 0, 1, 1),
-                                                           (0, 0, 0, 1, 0), (0, 0, 0, 2, 2)])
+                                                           (0, 0, 0, 1, 0), (0, 0, 0, 2, 2), (0, 0, 0, 1, 2)])
 def test_workgroup_and_slot_variants(ctx, waves, ring, batch, qstore, window):
     """The 12-wave workgroup form (168 VGPRs) with two and three payload slots
     in flight, the records finished in batches of 64, per-tile stores instead
@@ -168,7 +168,7 @@ def test_workgroup_and_slot_variants(ctx, waves, ring, batch, qstore, window):
         ctx.set_option("crc_wg_waves", 0)
         ctx.set_option("crc_ring", 0)
         ctx.set_option("crc_stream_batch", 0)
-        ctx.set_option("crc_stream_qstore", 1)
+        ctx.set_option("crc_stream_qstore", 2)
         ctx.set_option("crc_stream_window", 2)
         ctx.set_option("crc_stream", 1)
     assert np.array_equal(got, want)
