@@ -867,6 +867,13 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->variant = (ctx->variant & ~0x18000000) | ((int)(2 - value) << 27);
     return 0;
   }
+  if (!strcmp(key, "crc_stream_sel")) {  // A/B: stream kernel word steps after the boundary branch (1, default) or
+                                         // in it (0)
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_sel must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (ctx->variant & ~0x40000) | (value ? 0 : 0x40000);
+    return 0;
+  }
   if (!strcmp(key, "crc_stream_qstore")) {  // A/B: stream kernel CRCs stored as queued 256-B blocks, pushed
                                             // at the next tile (2, default) or at once (1); or per tile (0)
     // or the queue's push deferred to the next tile (2)

@@ -1605,8 +1605,12 @@ __device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
 // of config 3 ends ~5 records, so 0 requested 1 KiB of off[] per 8 KiB tile.
 // DQ (with QST): a tile's first-half records are pushed onto the queue at the
 // next tile, after its payload loads are issued (as the ring kernel's order 3).
+// SEL: a word's boundary branch only selects the two chains' step inputs; both
+// steps follow the branch, so their eight lookups issue together (else the
+// compiler split them over the branch's blocks: 1.9 ms of 21 on config 3,
+// crc_ablate 9 against 4 in profiles/r02/q).
 template <int ABLATE = 0, int BLOCK = 1024, int SLOTS = 2, bool BATCH = false, bool QST = true, int WIN = 2,
-          bool DQ = false>
+          bool DQ = false, bool SEL = false>
 __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
   if (!*P.sflag) return;  // not a packed batch of >= 64-byte records: the walking kernel takes it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1795,6 +1799,26 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const uint32_t w0 = k + 1 < 16 ? U[k + 1] : 0u, w1 = k + 1 < 16 ? U[17 + k] : 0u;
+      if constexpr (SEL) {
+        uint32_t i0 = c0, i1 = c1, n0 = w0, n1 = w1;
+        if (Km & (1u << k)) {  // wave-uniform: some lane's chain has a boundary in word k
+          uint32_t j0 = jc0, j1 = jc1;
+          asm volatile("" : "+v"(j0), "+v"(j1));
+          const bool m0 = (j0 >> 2) == (uint32_t)k, m1 = (j1 >> 2) == (uint32_t)(16 + k);
+          const uint32_t mlo0 = (1u << ((j0 & 3u) << 3)) - 1u, mlo1 = (1u << ((j1 & 3u) << 3)) - 1u;
+          x0 = m0 ? c0 : x0;
+          ub0 = m0 ? U[k] : ub0;
+          x1 = m1 ? c1 : x1;
+          ub1 = m1 ? U[16 + k] : ub1;
+          i0 = m0 ? ~(U[k] | mlo0) : c0;
+          n0 = m0 ? (w0 ^ mlo0) : w0;
+          i1 = m1 ? ~(U[16 + k] | mlo1) : c1;
+          n1 = m1 ? (w1 ^ mlo1) : w1;
+        }
+        c0 = crc_step_x(smem, i0, n0, lo, hi);
+        c1 = crc_step_x(smem, i1, n1, lo, hi);
+        continue;
+      }
       if (Km & (1u << k)) {  // wave-uniform: some lane's chain has a boundary in word k
         uint32_t j0 = jc0, j1 = jc1;
         asm volatile("" : "+v"(j0), "+v"(j1));  // recomputed here, not hoisted: fewer VGPRs through the loop
@@ -2123,11 +2147,13 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   const bool tstore = (variant & 0x20000000) != 0;  // A/B: per-tile stores instead of queued 256-B blocks
   const int win = 2 - (int)((variant >> 27) & 3u);  // A/B: boundary window form (crc_stream_window)
   const bool dq = (variant & 0x40000000) == 0;       // deferred queue push (A/B: crc_stream_qstore 1 = at once)
+  const bool sel = (variant & 0x40000) == 0;          // boundary branches select the step inputs (A/B: crc_stream_sel 0)
   const void* fn = batch ? (w12 ? (const void*)crc32_stream_kernel<0, 768, 2, true>
                                 : (const void*)crc32_stream_kernel<0, 1024, 2, true>)
                  : (tstore && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, false>
                  : (win == 1 && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 1>
                  : (win == 0 && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 0>
+                 : (dq && !w12 && ablate == 0 && sel) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, true>
                  : (dq && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true>
                  : (ablate >= 4 && ablate <= 9 && !w12)
                        ? (ablate == 4 ? (const void*)crc32_stream_kernel<4>

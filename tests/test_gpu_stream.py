@@ -62,7 +62,7 @@ def stream_ab(ctx):
 
 @pytest.mark.parametrize("dist,shift", [("min", 0), ("min", 3), ("short", 1), ("mixed", 0), ("mixed", 2),
                                         ("long", 0), ("zipf", 3)])
-def test_packed_vs_oracle(ctx, stream_ab, dist, shift):
+def test_packed_vs_oracle(ctx, stream_ab, sel, dist, shift):
     rng = np.random.default_rng(zlib.crc32(f"{dist}{shift}".encode()))
     n = 40000 if dist != "long" else 1500
     if dist == "min":  # 64-byte records: two boundaries in half the chunks
@@ -85,9 +85,18 @@ def test_packed_vs_oracle(ctx, stream_ab, dist, shift):
     assert np.array_equal(b, want)
 
 
+@pytest.fixture(params=[0, 1], ids=["branch_steps", "select_steps"])
+def sel(ctx, request):
+    """The stream kernel's boundary words: steps inside the branch (0) or the
+    branch selecting the step inputs (1, the default)."""
+    ctx.set_option("crc_stream_sel", request.param)
+    yield request.param
+    ctx.set_option("crc_stream_sel", 1)
+
+
 @pytest.mark.parametrize("lens,lead", [([64], 0), ([64], 77), ([1 << 20], 5), ([128] * 700, 0), ([128] * 700, 64),
                                        ([192, 64] * 500, 0), ([64] * 129 + [8192] * 3, 0), ([100] * 3, 127)])
-def test_boundary_positions(ctx, stream_ab, lens, lead):
+def test_boundary_positions(ctx, stream_ab, sel, lens, lead):
     """One record; records on the 128-byte grid (every boundary at chunk byte
     0, or at byte 64: a chain start); 64-byte records over a whole tile."""
     off, ln = _packed(lens, lead)
