@@ -867,11 +867,11 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->variant = (ctx->variant & ~0x18000000) | ((int)(2 - value) << 27);
     return 0;
   }
-  if (!strcmp(key, "crc_stream_sel")) {  // A/B: stream kernel word steps after the boundary branch (1, default) or
-                                         // in it (0)
-    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_sel must be 0 or 1");
+  if (!strcmp(key, "crc_stream_sel")) {  // A/B: stream kernel word steps after the boundary branch (1, default),
+                                         // in it (0), or no branch: inputs selected per step (2)
+    if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_sel must be 0, 1 or 2");
     std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~0x40000) | (value ? 0 : 0x40000);
+    ctx->variant = (ctx->variant & ~0xC0000) | (value == 0 ? 0x40000 : value == 2 ? 0x80000 : 0);
     return 0;
   }
   if (!strcmp(key, "crc_stream_qstore")) {  // A/B: stream kernel CRCs stored as queued 256-B blocks, pushed

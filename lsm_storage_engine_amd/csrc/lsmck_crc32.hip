@@ -1609,8 +1609,13 @@ __device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
 // steps follow the branch, so their eight lookups issue together (else the
 // compiler split them over the branch's blocks: 1.9 ms of 21 on config 3,
 // crc_ablate 9 against 4 in profiles/r02/q).
+// SEL 2: no branch at all.  The boundary word's step input is known before
+// the chain runs: ~(u | mlo) ^ Finv(mlo) (Finv(mlo): the word step's inverse
+// of the t-byte mask, so that F of it is the step's F(~(u | mlo)) ^ mlo), with
+// u the lane's word kb picked by a 16-way select; each step then selects its
+// input (and the capture) on kb == k, 3 VALU per chain step.
 template <int ABLATE = 0, int BLOCK = 1024, int SLOTS = 2, bool BATCH = false, bool QST = true, int WIN = 2,
-          bool DQ = false, bool SEL = false>
+          bool DQ = false, int SEL = 0>
 __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
   if (!*P.sflag) return;  // not a packed batch of >= 64-byte records: the walking kernel takes it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1779,8 +1784,12 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     // (ABLATE 4, diagnostic: no boundary bodies; results invalid)
     // (ABLATE 9, diagnostic: the boundary branches kept, never taken; results invalid)
     const uint32_t kz = ABLATE == 9 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(P.nrec >> 62)) : 0u;
-    const uint32_t Km0 = ABLATE == 4 ? 0u : ABLATE == 9 ? kz : wave_or_u32(jc0 < 128u ? (1u << (jc0 >> 2)) : 0u);
-    const uint32_t Km1 = ABLATE == 4 ? 0u : ABLATE == 9 ? kz : wave_or_u32(jc1 < 128u ? (1u << ((jc1 >> 2) - 16u)) : 0u);
+    const uint32_t Km0 = ABLATE == 4 ? 0u : ABLATE == 9 ? kz
+                         : SEL == 2 ? (uint32_t)(__ballot(jc0 < 128u) != 0ull)
+                                    : wave_or_u32(jc0 < 128u ? (1u << (jc0 >> 2)) : 0u);
+    const uint32_t Km1 = ABLATE == 4 ? 0u : ABLATE == 9 ? kz
+                         : SEL == 2 ? (uint32_t)(__ballot(jc1 < 128u) != 0ull)
+                                    : wave_or_u32(jc1 < 128u ? (1u << ((jc1 >> 2) - 16u)) : 0u);
     if (ABLATE == 3) {  // diagnostic: payload loads only
       uint32_t x = 0;
 #pragma unroll
@@ -1796,10 +1805,47 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     // keeps c ^ u and u of that word for its capture.
     uint32_t c0 = U[0], c1 = U[16], x0 = 0u, x1 = 0u, ub0 = 0u, ub1 = 0u;
     const uint32_t Km = Km0 | Km1;
+    uint32_t kb0 = 32u, kb1 = 32u, s0 = 0u, s1 = 0u;
+    if constexpr (SEL == 2) {
+      // U[base + kb], kb < 16, as a tree of bitwise selects (v_bitop3 0xCA:
+      // m ? a : b per bit): written as ?: selects, hipcc turned the tree into
+      // an indexed scratch array of the payload registers
+      auto pick16 = [&](uint32_t kb, int base) -> uint32_t {
+        auto bsel = [](uint32_t m, uint32_t a, uint32_t b) { return __builtin_amdgcn_bitop3_b32(m, a, b, 0xCA); };
+        const uint32_t m1 = 0u - (kb & 1u), m2 = 0u - ((kb >> 1) & 1u), m4 = 0u - ((kb >> 2) & 1u),
+                       m8 = 0u - ((kb >> 3) & 1u);
+        uint32_t a[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a[q] = bsel(m1, U[base + 2 * q + 1], U[base + 2 * q]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] = bsel(m2, a[2 * q + 1], a[2 * q]);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) a[q] = bsel(m4, a[2 * q + 1], a[2 * q]);
+        return bsel(m8, a[1], a[0]);
+      };
+      auto finv = [](uint32_t t) -> uint32_t {  // Finv of the t-byte mask (1 << 8t) - 1
+        return t == 1u ? 0x0f6a70d9u : (t == 2u ? 0x65e39d90u : (t == 3u ? 0x5c2e2681u : 0u));
+      };
+      kb0 = jc0 >> 2;          // 32: no boundary in chain 0
+      kb1 = (jc1 >> 2) - 16u;  // 16: none in chain 1
+      ub0 = pick16(kb0 & 15u, 0);
+      ub1 = pick16(kb1 & 15u, 16);
+      const uint32_t t0 = jc0 & 3u, t1 = jc1 & 3u;
+      s0 = ~(ub0 | ((1u << (t0 << 3)) - 1u)) ^ finv(t0);
+      s1 = ~(ub1 | ((1u << (t1 << 3)) - 1u)) ^ finv(t1);
+    }
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const uint32_t w0 = k + 1 < 16 ? U[k + 1] : 0u, w1 = k + 1 < 16 ? U[17 + k] : 0u;
-      if constexpr (SEL) {
+      if constexpr (SEL == 2) {
+        const bool m0 = kb0 == (uint32_t)k, m1 = kb1 == (uint32_t)k;
+        x0 = m0 ? c0 : x0;
+        x1 = m1 ? c1 : x1;
+        c0 = crc_step_x(smem, m0 ? s0 : c0, w0, lo, hi);
+        c1 = crc_step_x(smem, m1 ? s1 : c1, w1, lo, hi);
+        continue;
+      }
+      if constexpr (SEL == 1) {
         uint32_t i0 = c0, i1 = c1, n0 = w0, n1 = w1;
         if (Km & (1u << k)) {  // wave-uniform: some lane's chain has a boundary in word k
           uint32_t j0 = jc0, j1 = jc1;
@@ -2148,12 +2194,14 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   const int win = 2 - (int)((variant >> 27) & 3u);  // A/B: boundary window form (crc_stream_window)
   const bool dq = (variant & 0x40000000) == 0;       // deferred queue push (A/B: crc_stream_qstore 1 = at once)
   const bool sel = (variant & 0x40000) == 0;          // boundary branches select the step inputs (A/B: crc_stream_sel 0)
+  const bool sel2 = (variant & 0x80000) != 0;         // A/B: branch-free boundary steps (crc_stream_sel 2)
   const void* fn = batch ? (w12 ? (const void*)crc32_stream_kernel<0, 768, 2, true>
                                 : (const void*)crc32_stream_kernel<0, 1024, 2, true>)
                  : (tstore && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, false>
                  : (win == 1 && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 1>
                  : (win == 0 && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 0>
-                 : (dq && !w12 && ablate == 0 && sel) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, true>
+                 : (dq && !w12 && ablate == 0 && sel2) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, 2>
+                 : (dq && !w12 && ablate == 0 && sel) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, 1>
                  : (dq && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true>
                  : (ablate >= 4 && ablate <= 9 && !w12)
                        ? (ablate == 4 ? (const void*)crc32_stream_kernel<4>

@@ -85,10 +85,10 @@ def test_packed_vs_oracle(ctx, stream_ab, sel, dist, shift):
     assert np.array_equal(b, want)
 
 
-@pytest.fixture(params=[0, 1], ids=["branch_steps", "select_steps"])
+@pytest.fixture(params=[0, 1, 2], ids=["branch_steps", "select_steps", "branch_free"])
 def sel(ctx, request):
-    """The stream kernel's boundary words: steps inside the branch (0) or the
-    branch selecting the step inputs (1, the default)."""
+    """The stream kernel's boundary words: steps inside the branch (0), the
+    branch selecting the step inputs (1, the default), or no branch (2)."""
     ctx.set_option("crc_stream_sel", request.param)
     yield request.param
     ctx.set_option("crc_stream_sel", 1)
