@@ -208,6 +208,17 @@ int lsmck_device_count(void);
  *   "crc_ring"    fixed records whose segment count divides 64 (4 KiB, 256 B ...):
  *                 1 = two-slot kernel, 2 or 3 = whole-tile ring kernel with that
  *                 many load slots (0 = built-in default).  A/B switch.
+ *   "crc_order"   ring kernel tile order: 3 = one contiguous tile range per
+ *                 wave, CRCs stored as 256-byte blocks (default); 0 strided,
+ *                 1 contiguous, 2 claimed blocks, 4 strided with the CRCs
+ *                 gathered in LDS, 5 strided with deferred stores.  A/B switch.
+ *   "crc_stream_window"  stream kernel boundary window: 2 sliding (default),
+ *                 1 reloaded with the second half on demand, 0 reloaded.
+ *   "crc_stream_qstore"  stream kernel CRC stores: 2 queued 256-byte blocks
+ *                 pushed at the next tile (default), 1 pushed at once, 0 per tile.
+ *   "crc_stream_sel"  stream kernel boundary words: 1 = the branch selects the
+ *                 step inputs (default), 0 = steps inside the branch, 2 = no
+ *                 branch.  A/B switches; results are identical in every form.
  * Returns 0, or LSMCK_EINVAL for an unknown key / value. */
 int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
 
