@@ -218,7 +218,10 @@ int lsmck_device_count(void);
  *                 pushed at the next tile (default), 1 pushed at once, 0 per tile.
  *   "crc_stream_sel"  stream kernel boundary words: 1 = the branch selects the
  *                 step inputs (default), 0 = steps inside the branch, 2 = no
- *                 branch.  A/B switches; results are identical in every form.
+ *                 branch.
+ *   "crc_stream_z0"  stream kernel short path for tiles in which no record
+ *                 ends: 1 (default) or 0.  A/B switches; results are identical
+ *                 in every form.
  * Returns 0, or LSMCK_EINVAL for an unknown key / value. */
 int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
 

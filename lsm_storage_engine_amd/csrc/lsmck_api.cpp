@@ -867,6 +867,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->variant = (ctx->variant & ~0x18000000) | ((int)(2 - value) << 27);
     return 0;
   }
+  if (!strcmp(key, "crc_stream_z0")) {  // A/B: stream kernel short path for tiles where no record ends (1, default)
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_z0 must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (ctx->variant & ~0x20000) | (value ? 0 : 0x20000);
+    return 0;
+  }
   if (!strcmp(key, "crc_stream_sel")) {  // A/B: stream kernel word steps after the boundary branch (1, default),
                                          // in it (0), or no branch: inputs selected per step (2)
     if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_sel must be 0, 1 or 2");

@@ -1257,8 +1257,12 @@ __device__ __forceinline__ uint32_t walk_mulcol(uint32_t v, uint32_t d) {
 
 // the same for a wave-uniform v and d = 1..64, spread over the lanes: lane i
 // < 32 contributes column i if bit 31-i of v is set; XOR over lanes 0..31
+// OPQ: the lane's column offset is recomputed at each use rather than held
+// across the tile loop (in the stream kernel's short-path form it spilled)
+template <bool OPQ = false>
 __device__ __forceinline__ uint32_t walk_mulcol_uniform(uint32_t v, uint32_t d, uint32_t lane) {
-  const uint32_t i = lane & 31u;
+  uint32_t i = lane & 31u;
+  if (OPQ) asm volatile("" : "+v"(i));
   const uint32_t col = lds_ld(nullptr, LDS_WCOLS_OFF + ((i >> 2) * 65u + d) * 16u + (i & 3u) * 4u);
   const uint32_t t = (lane < 32u && ((v >> (31u - i)) & 1u)) ? col : 0u;
   return (uint32_t)__builtin_amdgcn_readlane((int)wave_prefix_xor(t), 31);
@@ -1614,8 +1618,12 @@ __device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
 // of the t-byte mask, so that F of it is the step's F(~(u | mlo)) ^ mlo), with
 // u the lane's word kb picked by a 16-way select; each step then selects its
 // input (and the capture) on kb == k, 3 VALU per chain step.
+// Z0: a tile in which no record ends (43% of config 3's tiles: records of
+// 8 KiB and more) takes a short path -- straight chains, the Horner shift to
+// the tile end, the carry -- without the boundary map, the word branches and
+// the finish.
 template <int ABLATE = 0, int BLOCK = 1024, int SLOTS = 2, bool BATCH = false, bool QST = true, int WIN = 2,
-          bool DQ = false, int SEL = 0>
+          bool DQ = false, int SEL = 0, bool Z0 = false>
 __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
   if (!*P.sflag) return;  // not a packed batch of >= 64-byte records: the walking kernel takes it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1745,6 +1753,21 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     if constexpr (QST && DQ) {
       if (dqcnt) qpush(dqv, dqi0, dqcnt);
       dqcnt = 0;
+    }
+    if constexpr (Z0 && ABLATE == 0 && !BATCH) {
+      if (cnt == 0u) {  // (uniform) no boundary in the tile
+        uint32_t z0 = U[0], z1 = U[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          z0 = crc_step_x(smem, z0, k + 1 < 16 ? U[k + 1] : 0u, lo, hi);
+          z1 = crc_step_x(smem, z1, k + 1 < 16 ? U[17 + k] : 0u, lo, hi);
+        }
+        uint32_t dz = 63u - lane;
+        asm volatile("" : "+v"(dz));  // not hoisted: eight loop-invariant column addresses spilled
+        const uint32_t XZ = wave_prefix_xor(walk_mulcol(shift_bytes32<2>(smem, z0) ^ z1, dz));
+        carry = (uint32_t)__builtin_amdgcn_readlane((int)XZ, 63) ^ walk_mulcol_uniform<Z0>(carry, 64u, lane);
+        return;
+      }
     }
     uint64_t M1, M2;
     bool any2;
@@ -1893,7 +1916,7 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     // --- records: window lane i finishes the record that ends at boundary bt0 + i
     const uint32_t ca = ra >> 7, cb = rb >> 7;
     const uint32_t c00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ca);
-    const uint32_t cterm = na ? walk_mulcol_uniform(carry, c00, lane) : 0u;
+    const uint32_t cterm = na ? walk_mulcol_uniform<Z0>(carry, c00, lane) : 0u;
     // Y = X[c-1] of the window lane's end chunk c; the record began at the
     // previous window lane's chunk, whose Y is one DPP shift away (lane 0:
     // `first`, the carry term or the other half's last Y)
@@ -1978,7 +2001,7 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
                              : (uint32_t)__builtin_amdgcn_readlane((int)ca, (int)(na - 1u));
       carry = X63 ^ (cl ? (uint32_t)__builtin_amdgcn_readlane((int)X, (int)(cl - 1u)) : 0u);
     } else {
-      carry = X63 ^ walk_mulcol_uniform(carry, 64u, lane);
+      carry = X63 ^ walk_mulcol_uniform<Z0>(carry, 64u, lane);
     }
   };
 
@@ -2195,12 +2218,14 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   const bool dq = (variant & 0x40000000) == 0;       // deferred queue push (A/B: crc_stream_qstore 1 = at once)
   const bool sel = (variant & 0x40000) == 0;          // boundary branches select the step inputs (A/B: crc_stream_sel 0)
   const bool sel2 = (variant & 0x80000) != 0;         // A/B: branch-free boundary steps (crc_stream_sel 2)
+  const bool z0 = (variant & 0x20000) == 0;           // short path for tiles without a boundary (A/B: crc_stream_z0 0)
   const void* fn = batch ? (w12 ? (const void*)crc32_stream_kernel<0, 768, 2, true>
                                 : (const void*)crc32_stream_kernel<0, 1024, 2, true>)
                  : (tstore && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, false>
                  : (win == 1 && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 1>
                  : (win == 0 && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 0>
                  : (dq && !w12 && ablate == 0 && sel2) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, 2>
+                 : (dq && !w12 && ablate == 0 && sel && z0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, 1, true>
                  : (dq && !w12 && ablate == 0 && sel) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, 1>
                  : (dq && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true>
                  : (ablate >= 4 && ablate <= 9 && !w12)
