@@ -867,6 +867,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->variant = (ctx->variant & ~0x18000000) | ((int)(2 - value) << 27);
     return 0;
   }
+  if (!strcmp(key, "crc_walk_opq")) {  // A/B: walking kernel, the carry multiply's lane offsets recomputed (1)
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_walk_opq must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant = (int)(((unsigned)ctx->variant & ~0x80000000u) | (value ? 0x80000000u : 0u));
+    return 0;
+  }
   if (!strcmp(key, "crc_stream_z0")) {  // A/B: stream kernel short path for tiles where no record ends (1, default)
     if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_z0 must be 0 or 1");
     std::lock_guard<std::mutex> lk(ctx->mu);

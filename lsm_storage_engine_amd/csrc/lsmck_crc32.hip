@@ -1305,7 +1305,10 @@ __device__ __forceinline__ uint64_t start_bit(const WalkWin& W, int64_t rel) {
   return (W.ok && s >= 1 && s <= 63) ? (1ull << s) : 0ull;
 }
 
-template <int CHAINS, int ABLATE = 0>
+// OPQ: the continuing record's uniform multiply recomputes its lane column
+// offset (else hipcc kept it in two VGPRs that spilled, reloaded in the tile
+// loop behind an s_waitcnt vmcnt(0) on the payload prefetch)
+template <int CHAINS, int ABLATE = 0, bool OPQ = false>
 __global__ __launch_bounds__(1024) void crc32_walk_kernel(CrcParams P) {
   if (P.sflag && *P.sflag) return;  // a packed batch of >= 64-byte records: crc32_stream_kernel took it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1428,7 +1431,7 @@ __global__ __launch_bounds__(1024) void crc32_walk_kernel(CrcParams P) {
     // lane 0 continuing a record from the previous tile: Horner step
     const bool cont0 = !__builtin_amdgcn_readfirstlane((int)(L.fl & FL_FIRST));
     const uint32_t re0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)run_end);
-    const uint32_t cm = cont0 ? walk_mulcol_uniform(carry, re0 + 1u, lane) : 0u;
+    const uint32_t cm = cont0 ? walk_mulcol_uniform<OPQ>(carry, re0 + 1u, lane) : 0u;
     total ^= (lane == 0u) ? cm : 0u;
     const bool ends = head && (lane + L.k <= 63u);
     if (ends) P.out[L.rec] = ~total;
@@ -2269,7 +2272,9 @@ extern "C" int lsmk_launch_crc32_walk(const CrcParams* P, uint64_t* sb_prefix, i
   const int ablate = (variant >> 8) & 0xF;
   const void* fn = ablate == 3 ? (const void*)crc32_walk_kernel<2, 3>
                  : ch == 1 ? (const void*)crc32_walk_kernel<1>
-                 : ch == 4 ? (const void*)crc32_walk_kernel<4> : (const void*)crc32_walk_kernel<2>;
+                 : ch == 4 ? (const void*)crc32_walk_kernel<4>
+                 : (variant & (int)0x80000000u) ? (const void*)crc32_walk_kernel<2, 0, true>  // A/B: crc_walk_opq 1
+                                                : (const void*)crc32_walk_kernel<2>;
   size_t lds = LDS_SCRATCH_OFF;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return -(int)e;
