@@ -1810,12 +1810,16 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     // (ABLATE 4, diagnostic: no boundary bodies; results invalid)
     // (ABLATE 9, diagnostic: the boundary branches kept, never taken; results invalid)
     const uint32_t kz = ABLATE == 9 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(P.nrec >> 62)) : 0u;
+    // the words holding a boundary, chain 0 in bits 0-15 and chain 1 in bits
+    // 16-31: one OR over the window's boundaries (at most one per chain and
+    // chunk) instead of one per chain over the chunk lanes
+    const uint32_t Kw = (ABLATE == 4 || ABLATE == 9 || SEL == 2)
+                            ? 0u
+                            : wave_or_u32((ina ? (1u << ((ra & 127u) >> 2)) : 0u) | (inb ? (1u << ((rb & 127u) >> 2)) : 0u));
     const uint32_t Km0 = ABLATE == 4 ? 0u : ABLATE == 9 ? kz
-                         : SEL == 2 ? (uint32_t)(__ballot(jc0 < 128u) != 0ull)
-                                    : wave_or_u32(jc0 < 128u ? (1u << (jc0 >> 2)) : 0u);
+                         : SEL == 2 ? (uint32_t)(__ballot(jc0 < 128u) != 0ull) : (Kw & 0xFFFFu);
     const uint32_t Km1 = ABLATE == 4 ? 0u : ABLATE == 9 ? kz
-                         : SEL == 2 ? (uint32_t)(__ballot(jc1 < 128u) != 0ull)
-                                    : wave_or_u32(jc1 < 128u ? (1u << ((jc1 >> 2) - 16u)) : 0u);
+                         : SEL == 2 ? (uint32_t)(__ballot(jc1 < 128u) != 0ull) : (Kw >> 16);
     if (ABLATE == 3) {  // diagnostic: payload loads only
       uint32_t x = 0;
 #pragma unroll
