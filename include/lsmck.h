@@ -220,8 +220,10 @@ int lsmck_device_count(void);
  *                 step inputs (default), 0 = steps inside the branch, 2 = no
  *                 branch.
  *   "crc_stream_z0"  stream kernel short path for tiles in which no record
- *                 ends: 1 (default) or 0.  A/B switches; results are identical
- *                 in every form.
+ *                 ends: 1 (default) or 0.
+ *   "crc_stream_lm"  stream kernel chunk boundaries through LDS bytes (1,
+ *                 default) or DPP reductions (0).  A/B switches; results are
+ *                 identical in every form.
  * Returns 0, or LSMCK_EINVAL for an unknown key / value. */
 int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
 

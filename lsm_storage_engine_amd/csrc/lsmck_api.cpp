@@ -226,6 +226,7 @@ struct lsmck_ctx {
   size_t cap_hwexp = 0;
   Stage stage[2];
   int variant = 0;  // kernel variant for A/B timing (LSMCK_CRC_CHAINS=1|2|4); 0 = default
+  int variant2 = 0;  // more A/B bits (0x1: crc_stream_lm 0); 0 = default
   uint32_t tree_active = 0;  // whole-tree verify: files in flight (0 = kTreeActive)
   uint32_t tree_slice = 0;   // whole-tree verify: bytes of a file per round (0 = kTreeSlice)
   long tree_open = -1;       // whole-tree verify: files kept open between slices (-1 = RLIMIT_NOFILE budget)
@@ -354,7 +355,7 @@ int crc_desc_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const 
       if ((rc = ensure_dev(&sc.scuts, &sc.cap_cuts, (size_t)lsmk_stream_waves(ctx->ncu) + 1))) return rc;
       P.sflag = sc.sflag;
       P.scuts = sc.scuts;
-      rc = lsmk_launch_crc32_stream(&P, ctx->ncu, ctx->variant, st);
+      rc = lsmk_launch_crc32_stream(&P, ctx->ncu, ctx->variant, ctx->variant2, st);
       if (rc) return launch_rc(rc, "crc32_stream kernel");
       if (ctx->variant & kVariantStreamOnly) return 0;
     }
@@ -865,6 +866,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_window must be 0, 1 or 2");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->variant = (ctx->variant & ~0x18000000) | ((int)(2 - value) << 27);
+    return 0;
+  }
+  if (!strcmp(key, "crc_stream_lm")) {  // A/B: stream kernel chunk boundaries through LDS bytes (1, default)
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_lm must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant2 = (ctx->variant2 & ~0x1) | (value ? 0 : 0x1);
     return 0;
   }
   if (!strcmp(key, "crc_walk_opq")) {  // A/B: walking kernel, the carry multiply's lane offsets recomputed (1)

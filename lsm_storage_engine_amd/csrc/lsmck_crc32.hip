@@ -59,6 +59,10 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // gathered in LDS behind the kernel's tables, then stored by one instruction
 #define LDS_WOUT_OFF LDS_SCRATCH_OFF
 #define LDS_WOUT_BYTES 4096u
+// stream kernel, LM: per wave 64 chunks x {first, second} boundary byte + 1
+// (0 = none), written by the window lanes, read and cleared by the chunk lanes
+#define LDS_SMAP_OFF LDS_SCRATCH_OFF
+#define LDS_SMAP_BYTES 2048u
 #ifndef LSMCK_DEFAULT_CHAINS
 #define LSMCK_DEFAULT_CHAINS 2       // fixed records (A/B: profiles/r01)
 #endif
@@ -1625,8 +1629,11 @@ __device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
 // 8 KiB and more) takes a short path -- straight chains, the Horner shift to
 // the tile end, the carry -- without the boundary map, the word branches and
 // the finish.
+// LM: the chunk lanes' boundaries through LDS bytes (window lanes write, chunk
+// lanes read and clear) instead of four DPP OR reductions, popcounts and
+// bpermutes.
 template <int ABLATE = 0, int BLOCK = 1024, int SLOTS = 2, bool BATCH = false, bool QST = true, int WIN = 2,
-          bool DQ = false, int SEL = 0, bool Z0 = false>
+          bool DQ = false, int SEL = 0, bool Z0 = false, bool LM = false>
 __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
   if (!*P.sflag) return;  // not a packed batch of >= 64-byte records: the walking kernel takes it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1653,6 +1660,8 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t lo = (lane & 31u) * 4u, hi = lo | 0x10000u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const uint32_t smap = LDS_SMAP_OFF + (threadIdx.x >> 6) * 128u;  // LM: this wave's boundary bytes
+  if (LM && lane < 32u) *(__attribute__((address_space(3))) uint32_t*)(size_t)(smap + 4u * lane) = 0u;
   const uint64_t n = P.nrec;
   const uint64_t b_lo = P.scuts[wave], b_hi = P.scuts[wave + 1];
   if (b_lo >= b_hi) return;  // no record ends in this wave's range
@@ -1774,7 +1783,29 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     }
     uint64_t M1, M2;
     bool any2;
-    {
+    uint32_t jc0, jc1;
+    if constexpr (LM) {
+      const uint32_t ca = ra >> 7, cb = rb >> 7;
+      const uint32_t ca63 = (uint32_t)__builtin_amdgcn_readlane((int)ca, 63);
+      const uint32_t pca = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ca, 0x138, 0xF, 0xF, false);  // wave_shr:1
+      const uint32_t pcb0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cb, 0x138, 0xF, 0xF, false);
+      const uint32_t pcb = lane ? pcb0 : ca63;
+      const bool seca = ina && lane > 0u && pca == ca;
+      const bool secb = inb && pcb == cb && (lane > 0u || (bal_a >> 63));
+      typedef __attribute__((address_space(3))) unsigned char lds_u8w_t;
+      typedef __attribute__((address_space(3))) unsigned short lds_u16w_t;
+      if (ina) *(lds_u8w_t*)(size_t)(smap + 2u * ca + (seca ? 1u : 0u)) = (unsigned char)((ra & 127u) + 1u);
+      if (inb) *(lds_u8w_t*)(size_t)(smap + 2u * cb + (secb ? 1u : 0u)) = (unsigned char)((rb & 127u) + 1u);
+      const uint32_t e = *(lds_u16w_t*)(size_t)(smap + 2u * lane);
+      if (e) *(lds_u16w_t*)(size_t)(smap + 2u * lane) = (unsigned short)0;
+      const uint32_t e1 = e & 0xFFu, e2 = e >> 8;
+      M1 = __ballot(e1 != 0u);
+      M2 = __ballot(e2 != 0u);
+      any2 = M2 != 0ull;
+      const uint32_t j1 = e1 - 1u;
+      jc0 = (e1 && j1 < 64u) ? j1 : 128u;
+      jc1 = e2 ? e2 - 1u : ((e1 && j1 >= 64u) ? j1 : 128u);
+    } else {
       const uint32_t ca = ra >> 7, cb = rb >> 7;
       const uint32_t ca63 = (uint32_t)__builtin_amdgcn_readlane((int)ca, 63);
       const uint32_t pca = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ca, 0x138, 0xF, 0xF, false);  // wave_shr:1
@@ -1787,8 +1818,7 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
       M2 = any2 ? wave_or_u64((seca ? (1ull << ca) : 0ull) | (secb ? (1ull << cb) : 0ull)) : 0ull;
     }
     // --- chunk-lane view: this chunk's boundaries jc0 (chain 0), jc1 (chain 1); 128 = none
-    uint32_t jc0, jc1;
-    {
+    if constexpr (!LM) {
       const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
       const uint32_t k1 = (uint32_t)__builtin_popcountll(M1 & below) + (uint32_t)__builtin_popcountll(M2 & below);
       const bool b1 = (M1 >> lane) & 1ull, b2 = (M2 >> lane) & 1ull;
@@ -2207,7 +2237,7 @@ extern "C" uint32_t lsmk_stream_waves(int ncu) { return (uint32_t)ncu * 16u; }
 
 // stream kernel: eligibility flag, per-wave cuts, the kernel.  The walking
 // kernel launched after it on the same stream exits when the flag is set.
-extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant, hipStream_t st) {
+extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant, int variant2, hipStream_t st) {
   const uint64_t n = P->nrec;
   if (n == 0) return 0;
   hipError_t e = hipMemsetAsync(P->sflag, 1, 4, st);
@@ -2226,12 +2256,14 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   const bool sel = (variant & 0x40000) == 0;          // boundary branches select the step inputs (A/B: crc_stream_sel 0)
   const bool sel2 = (variant & 0x80000) != 0;         // A/B: branch-free boundary steps (crc_stream_sel 2)
   const bool z0 = (variant & 0x20000) == 0;           // short path for tiles without a boundary (A/B: crc_stream_z0 0)
+  const bool lm = (variant2 & 0x1) == 0;              // chunk boundaries through LDS bytes (A/B: crc_stream_lm 0)
   const void* fn = batch ? (w12 ? (const void*)crc32_stream_kernel<0, 768, 2, true>
                                 : (const void*)crc32_stream_kernel<0, 1024, 2, true>)
                  : (tstore && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, false>
                  : (win == 1 && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 1>
                  : (win == 0 && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 0>
                  : (dq && !w12 && ablate == 0 && sel2) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, 2>
+                 : (dq && !w12 && ablate == 0 && sel && z0 && lm) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, 1, true, true>
                  : (dq && !w12 && ablate == 0 && sel && z0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, 1, true>
                  : (dq && !w12 && ablate == 0 && sel) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, 1>
                  : (dq && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true>
@@ -2246,7 +2278,7 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
                           : ablate == 2 ? (const void*)crc32_stream_kernel<2, 768> : (const void*)crc32_stream_kernel<0, 768>)
                        : (ablate == 3 ? (const void*)crc32_stream_kernel<3>
                           : ablate == 2 ? (const void*)crc32_stream_kernel<2> : (const void*)crc32_stream_kernel<0>);
-  const size_t lds = LDS_SCRATCH_OFF;
+  const size_t lds = LDS_SCRATCH_OFF + (lm ? LDS_SMAP_BYTES : 0u);
   e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return -(int)e;
   void* args[] = {(void*)P};

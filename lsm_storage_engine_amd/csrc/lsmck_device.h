@@ -82,7 +82,7 @@ int lsmk_launch_crc32_walk(const lsmck::CrcParams* P, uint64_t* sb_prefix, int n
 // stream kernel for packed batches of records >= 64 B (eligibility decided on
 // the device: P->sflag, P->scuts hold lsmk_stream_waves(ncu) + 1 entries)
 uint32_t lsmk_stream_waves(int ncu);
-int lsmk_launch_crc32_stream(const lsmck::CrcParams* P, int ncu, int variant, hipStream_t st);
+int lsmk_launch_crc32_stream(const lsmck::CrcParams* P, int ncu, int variant, int variant2, hipStream_t st);
 uint64_t lsmk_wal_words(uint64_t n);
 uint64_t lsmk_wal_scan_blocks(uint64_t n);
 int lsmk_wal_mark_range(const uint8_t* img, uint64_t n, uint64_t b0, uint64_t b1, uint64_t* bits, uint32_t* pre,
