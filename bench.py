@@ -250,12 +250,13 @@ def main():
                 # "q<n>" = crc_stream_batch n (stream kernel: records finished in batches of 64)
                 # "t<n>" = crc_stream_qstore n (stream kernel: 2 queued 256-B output blocks pushed at the next
                 #          tile (default), 1 pushed at once, 0 per-tile stores)
+                # "y<n>" = crc_stream_fsp n (stream kernel: finish multiplies spread over 8 lanes)
                 # "m<n>" = crc_stream_lm n (stream kernel: 1 chunk boundaries through LDS bytes, default)
                 # "k<n>" = crc_walk_opq n (walking kernel: carry multiply offsets recomputed)
                 # "z<n>" = crc_stream_z0 n (stream kernel: 1 short path for tiles without a boundary, default)
                 # "e<n>" = crc_stream_sel n (stream kernel: 1 boundary branches only select the step inputs, default)
                 # "v<n>" = crc_stream_window n (stream kernel: 2 sliding, 1 second half on demand, 0 reloaded)
-                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?(?:r(\d))?(?:b(\d))?(?:f(\d+))?(?:o(\d))?(?:p(\d))?(?:s(\d))?(?:q(\d))?(?:t(\d))?(?:v(\d))?(?:e(\d))?(?:z(\d))?(?:k(\d))?(?:m(\d))?", v)
+                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?(?:r(\d))?(?:b(\d))?(?:f(\d+))?(?:o(\d))?(?:p(\d))?(?:s(\d))?(?:q(\d))?(?:t(\d))?(?:v(\d))?(?:e(\d))?(?:z(\d))?(?:k(\d))?(?:m(\d))?(?:y(\d))?", v)
                 if not m:
                     raise SystemExit(f"bad variant {v!r}")
                 kind, num, waves = m.group(1), int(m.group(2)), int(m.group(3) or 0)
@@ -277,6 +278,7 @@ def main():
                 ctx.set_option("crc_stream_z0", int(m.group(15)) if m.group(15) is not None else 1)
                 ctx.set_option("crc_walk_opq", int(m.group(16) or 0))
                 ctx.set_option("crc_stream_lm", int(m.group(17)) if m.group(17) is not None else 1)
+                ctx.set_option("crc_stream_fsp", int(m.group(18) or 0))
                 step()
                 e0.record(stream)
                 for _ in range(a.steps):
@@ -301,6 +303,7 @@ def main():
         ctx.set_option("crc_stream_z0", 1)
         ctx.set_option("crc_walk_opq", 0)
         ctx.set_option("crc_stream_lm", 1)
+        ctx.set_option("crc_stream_fsp", 0)
         ctx.set_option("crc_order", 3)
         ab = {str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                        "GiBps_median": payload / GIB / (float(np.median(t)) * 1e-3)} for v, t in ab.items()}

@@ -222,8 +222,10 @@ int lsmck_device_count(void);
  *   "crc_stream_z0"  stream kernel short path for tiles in which no record
  *                 ends: 1 (default) or 0.
  *   "crc_stream_lm"  stream kernel chunk boundaries through LDS bytes (1,
- *                 default) or DPP reductions (0).  A/B switches; results are
- *                 identical in every form.
+ *                 default) or DPP reductions (0).
+ *   "crc_stream_fsp"  stream kernel finish multiplies spread over 8 lanes per
+ *                 record (1) or one per record lane (0, default).  A/B
+ *                 switches; results are identical in every form.
  * Returns 0, or LSMCK_EINVAL for an unknown key / value. */
 int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
 

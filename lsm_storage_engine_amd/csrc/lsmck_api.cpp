@@ -868,6 +868,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->variant = (ctx->variant & ~0x18000000) | ((int)(2 - value) << 27);
     return 0;
   }
+  if (!strcmp(key, "crc_stream_fsp")) {  // A/B: stream kernel finish multiplies spread over 8 lanes per record (1)
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_fsp must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->variant2 = (ctx->variant2 & ~0x2) | (value ? 0x2 : 0);
+    return 0;
+  }
   if (!strcmp(key, "crc_stream_lm")) {  // A/B: stream kernel chunk boundaries through LDS bytes (1, default)
     if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_lm must be 0 or 1");
     std::lock_guard<std::mutex> lk(ctx->mu);

@@ -1632,8 +1632,11 @@ __device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
 // LM: the chunk lanes' boundaries through LDS bytes (window lanes write, chunk
 // lanes read and clear) instead of four DPP OR reductions, popcounts and
 // bpermutes.
+// FSP: a half with at most 16 records spreads each record's finish multiply
+// over 8 lanes (4 LDS columns each, then a 3-step DPP XOR), 8 records per
+// round, instead of one 32-column multiply issued for the whole wave.
 template <int ABLATE = 0, int BLOCK = 1024, int SLOTS = 2, bool BATCH = false, bool QST = true, int WIN = 2,
-          bool DQ = false, int SEL = 0, bool Z0 = false, bool LM = false>
+          bool DQ = false, int SEL = 0, bool Z0 = false, bool LM = false, bool FSP = false>
 __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
   if (!*P.sflag) return;  // not a packed batch of >= 64-byte records: the walking kernel takes it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1992,7 +1995,36 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
       // reads below cost per active lane, and all 64 lanes doing them cost
       // 4.8 of 25.6 ms (crc_ablate 5); the bpermutes above need every lane
       uint32_t fv = 0u;
-      if (in && bidx > b_lo) {
+      if (FSP && ABLATE == 0 && cnt <= 16u) {  // (uniform)
+        uint32_t pv = 0u, av = 0u, mf = 0u;
+        if (in && bidx > b_lo) {
+          const bool h = j >= 64u;
+          pv = h ? (shift_bytes32<2>(smem, H) ^ R0c) : H;
+          av = h ? A1c : A0c;
+          mf = LDS_XMC_OFF(j & 63u);  // the factor x^(8m)'s 32 columns
+        }
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));  // lane-derived offsets recomputed here, not held across the tile loop (spilled)
+        for (uint32_t q = 0; q < cnt; q += 8u) {
+          // lane L works on record lane i0 + q + L/8, columns 4(L%8) .. +3
+          const int src = (int)(((i0 + q + (ln >> 3)) & 63u) << 2);
+          const uint32_t p = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pv);
+          const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)mf);
+          const uint32_t g = ln & 7u;
+          const u32x4 c = lds_ld128(b + g * 16u);
+          const uint32_t ps = p << (g << 2);
+          uint32_t x = c.x & (uint32_t)((int32_t)ps >> 31);
+          x = __builtin_amdgcn_bitop3_b32(x, c.y, (uint32_t)((int32_t)(ps << 1) >> 31), 0x78);
+          x = __builtin_amdgcn_bitop3_b32(x, c.z, (uint32_t)((int32_t)(ps << 2) >> 31), 0x78);
+          x = __builtin_amdgcn_bitop3_b32(x, c.w, (uint32_t)((int32_t)(ps << 3) >> 31), 0x78);
+          x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+          x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+          x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4: group total at L%8 >= 4
+          const uint32_t d = ln - i0 - q;  // this round's record lanes: d < 8
+          const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((((d << 3) + 4u) & 63u) << 2), (int)x);
+          fv = (d < 8u && d < cnt - q) ? ~(got ^ av) : fv;
+        }
+      } else if (in && bidx > b_lo) {
         const bool h = j >= 64u;
         const uint32_t Pv = h ? (shift_bytes32<2>(smem, H) ^ R0c) : H;
         uint32_t v;
@@ -2257,12 +2289,14 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   const bool sel2 = (variant & 0x80000) != 0;         // A/B: branch-free boundary steps (crc_stream_sel 2)
   const bool z0 = (variant & 0x20000) == 0;           // short path for tiles without a boundary (A/B: crc_stream_z0 0)
   const bool lm = (variant2 & 0x1) == 0;              // chunk boundaries through LDS bytes (A/B: crc_stream_lm 0)
+  const bool fsp = (variant2 & 0x2) != 0;             // A/B: finish multiplies spread over 8 lanes (crc_stream_fsp)
   const void* fn = batch ? (w12 ? (const void*)crc32_stream_kernel<0, 768, 2, true>
                                 : (const void*)crc32_stream_kernel<0, 1024, 2, true>)
                  : (tstore && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, false>
                  : (win == 1 && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 1>
                  : (win == 0 && !w12 && ablate == 0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 0>
                  : (dq && !w12 && ablate == 0 && sel2) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, 2>
+                 : (dq && !w12 && ablate == 0 && sel && z0 && lm && fsp) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, 1, true, true, true>
                  : (dq && !w12 && ablate == 0 && sel && z0 && lm) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, 1, true, true>
                  : (dq && !w12 && ablate == 0 && sel && z0) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, 1, true>
                  : (dq && !w12 && ablate == 0 && sel) ? (const void*)crc32_stream_kernel<0, 1024, 2, false, true, 2, true, 1>

@@ -85,8 +85,8 @@ def test_packed_vs_oracle(ctx, stream_ab, sel, dist, shift):
     assert np.array_equal(b, want)
 
 
-@pytest.fixture(params=[(0, 0, 0), (1, 0, 0), (2, 0, 0), (1, 1, 0), (1, 1, 1)],
-                ids=["branch_steps", "select_steps", "branch_free", "dpp_map", "default"])
+@pytest.fixture(params=[(0, 0, 0, 0), (1, 0, 0, 0), (2, 0, 0, 0), (1, 1, 0, 0), (1, 1, 1, 0), (1, 1, 1, 1)],
+                ids=["branch_steps", "select_steps", "branch_free", "dpp_map", "default", "spread_finish"])
 def sel(ctx, request):
     """The stream kernel's boundary words: steps inside the branch (0), the
     branch selecting the step inputs (1, the default), or no branch (2); with
@@ -94,10 +94,12 @@ def sel(ctx, request):
     ctx.set_option("crc_stream_sel", request.param[0])
     ctx.set_option("crc_stream_z0", request.param[1])
     ctx.set_option("crc_stream_lm", request.param[2])
+    ctx.set_option("crc_stream_fsp", request.param[3])
     yield request.param
     ctx.set_option("crc_stream_sel", 1)
     ctx.set_option("crc_stream_z0", 1)
     ctx.set_option("crc_stream_lm", 1)
+    ctx.set_option("crc_stream_fsp", 0)
 
 
 @pytest.mark.parametrize("lens,lead", [([64], 0), ([64], 77), ([1 << 20], 5), ([128] * 700, 0), ([128] * 700, 64),
