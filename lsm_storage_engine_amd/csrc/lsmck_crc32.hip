@@ -1771,7 +1771,10 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     }
     if constexpr (Z0 && ABLATE == 0 && !BATCH) {
       if (cnt == 0u) {  // (uniform) no boundary in the tile
-        uint32_t z0 = U[0], z1 = U[16];
+        // the carry (the record's raw CRC up to this tile, aligned to its start)
+        // enters as lane 0's initial register: the Horner shift of lane 0 then
+        // carries it to the tile end with the chunk (no separate multiply)
+        uint32_t z0 = U[0] ^ (lane == 0u ? carry : 0u), z1 = U[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
           z0 = crc_step_x(smem, z0, k + 1 < 16 ? U[k + 1] : 0u, lo, hi);
@@ -1780,7 +1783,7 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
         uint32_t dz = 63u - lane;
         asm volatile("" : "+v"(dz));  // not hoisted: eight loop-invariant column addresses spilled
         const uint32_t XZ = wave_prefix_xor(walk_mulcol(shift_bytes32<2>(smem, z0) ^ z1, dz));
-        carry = (uint32_t)__builtin_amdgcn_readlane((int)XZ, 63) ^ walk_mulcol_uniform<Z0>(carry, 64u, lane);
+        carry = (uint32_t)__builtin_amdgcn_readlane((int)XZ, 63);
         return;
       }
     }
