@@ -1869,7 +1869,12 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     // boundary; the 0xFFFFFFFF init folded in), so the boundary lane only
     // swaps the input of its ordinary word step -- no extra lookups -- and
     // keeps c ^ u and u of that word for its capture.
-    uint32_t c0 = U[0], c1 = U[16], x0 = 0u, x1 = 0u, ub0 = 0u, ub1 = 0u;
+    // Z0 (carry in): the carry enters as lane 0's initial register here too.
+    // Up to the tile's first boundary it then rides in lane 0's chain: into
+    // the capture (a boundary in chain 0 of chunk 0), R0 (one in chain 1), or
+    // the Horner value of chunk 0; a reset drops it after the boundary, so no
+    // record but the carried one sees it
+    uint32_t c0 = U[0] ^ ((Z0 && lane == 0u) ? carry : 0u), c1 = U[16], x0 = 0u, x1 = 0u, ub0 = 0u, ub1 = 0u;
     const uint32_t Km = Km0 | Km1;
     uint32_t kb0 = 32u, kb1 = 32u, s0 = 0u, s1 = 0u;
     if constexpr (SEL == 2) {
@@ -1959,7 +1964,7 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
     // --- records: window lane i finishes the record that ends at boundary bt0 + i
     const uint32_t ca = ra >> 7, cb = rb >> 7;
     const uint32_t c00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ca);
-    const uint32_t cterm = na ? walk_mulcol_uniform<Z0>(carry, c00, lane) : 0u;
+    const uint32_t cterm = (Z0 || !na) ? 0u : walk_mulcol_uniform<Z0>(carry, c00, lane);
     // Y = X[c-1] of the window lane's end chunk c; the record began at the
     // previous window lane's chunk, whose Y is one DPP shift away (lane 0:
     // `first`, the carry term or the other half's last Y)
@@ -2073,7 +2078,7 @@ __global__ __launch_bounds__(BLOCK) void crc32_stream_kernel(CrcParams P) {
                              : (uint32_t)__builtin_amdgcn_readlane((int)ca, (int)(na - 1u));
       carry = X63 ^ (cl ? (uint32_t)__builtin_amdgcn_readlane((int)X, (int)(cl - 1u)) : 0u);
     } else {
-      carry = X63 ^ walk_mulcol_uniform<Z0>(carry, 64u, lane);
+      carry = X63 ^ (Z0 ? 0u : walk_mulcol_uniform<Z0>(carry, 64u, lane));
     }
   };
 
