@@ -4,8 +4,11 @@
 
 One step = one pass of the hot path (lsmck_crc32_batch*) over one batch of
 synthetic records already resident in HBM.  Default workload (N = 1) is
-BASELINE config 2: 2^24 fixed 4 KiB SSTable blocks = 64 GiB per GPU.  With
---gpus N > 1 the workload is BASELINE config 4: one process per GPU, and rank
+BASELINE config 3, the north_star's "synthetic variable-length KV records
+(64 B-64 KiB)": 2^26 Zipf-length records packed back to back (~97 GiB, the
+largest single-GPU config).  --config 2 runs the fixed 4 KiB blocks (64 GiB),
+--config 1 the 256 B WAL payloads.  With --gpus N > 1 the workload is BASELINE
+config 4: one process per GPU, and rank
 r checksums shard r = blocks [r*2^26, (r+1)*2^26) of the same global block
 stream, 2^26 x 4 KiB = 256 GiB per GPU (weak scaling, record-sharded, no
 data-path collective); the control plane (barrier, max of per-rank times, the
@@ -16,7 +19,7 @@ per-rank summary digests) goes over torch.distributed (gloo).
 (before anything touches the GPU) and exits with its status; under a launcher
 WORLD_SIZE must equal --gpus.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|1]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3|2|1]
                   [--blocks-per-gpu B] [--no-cpu-baseline]
 
 Prints ONE JSON line on rank 0 (see DESIGN.md section 5 for every field).
@@ -55,7 +58,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3])
+    ap.add_argument("--config", type=int, default=0, choices=[0, 1, 2, 3],
+                    help="0 (default): config 3 at N = 1, config 4 (config 2's blocks, 2^26 per GPU) at N > 1")
     ap.add_argument("--blocks-per-gpu", type=int, default=0, help="override the per-GPU record count")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-records", type=int, default=0)
@@ -78,6 +82,12 @@ def parse():
     ap.add_argument("--pack-align", type=int, default=1,
                     help="diagnostic: config 3 record offsets rounded up to this many bytes")
     return ap.parse_args()
+
+
+def resolve_config(config, world):
+    """--config 0 (default): BASELINE config 3 (north_star's variable-length
+    records) at N = 1; config 4's fixed 4 KiB shard per rank at N > 1."""
+    return config or (2 if world > 1 else 3)
 
 
 def traffic_from_profiles(workload_key):
@@ -154,7 +164,7 @@ def main():
     if a.stream != 1:
         ctx.set_option("crc_stream", a.stream)
 
-    cfg = a.config
+    cfg = resolve_config(a.config, world)
     seed = SEED[cfg]
     if cfg == 2:
         # N > 1: BASELINE config 4, 2^26 blocks per GPU (256 GiB; 2^26/N per rank
@@ -334,10 +344,25 @@ def main():
     total_payload = payload * world
     value = total_payload / GIB / (wall_max / a.steps)
     achieved_gbs = algo_bytes / (ev_ms * 1e-3) / 1e9
-    # diagnostics have no committed traffic
-    # (the committed traffic is per launch of the default record count only)
-    wkey = None if (a.desc or a.pack_align > 1 or a.blocks_per_gpu or world > 1) else f"{'sha256_' if sha else ''}config{cfg}"
-    traffic = traffic_from_profiles(wkey)
+    # PMC traffic per launch from the committed profiles.  Config 4 (a shard of
+    # fixed 4 KiB blocks per rank): measured on the 2^26-block shard; a reduced
+    # shard (the shared-GPU rehearsal) scales it by its block count, since the
+    # kernel's bytes are per block.  Other diagnostics have no committed traffic.
+    c4 = cfg == 2 and not sha and not a.desc and (world > 1 or nrec == (1 << 26))
+    if c4:
+        t4 = traffic_from_profiles("config4")
+        traffic = None if t4 is None else round(t4 * nrec / float(1 << 26), 1)
+    else:
+        wkey = None if (a.desc or a.pack_align > 1 or a.blocks_per_gpu) else f"{'sha256_' if sha else ''}config{cfg}"
+        traffic = traffic_from_profiles(wkey)
+    # every rank's own launch time (HIP events on its stream) and wall time
+    mine_t = {"rank": rank, "launch_ms_hip_events": round(ev_ms, 4), "wall_ms_per_step": round(wall * 1e3 / a.steps, 4),
+              "frac": round(algo_bytes / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine_t)
+    else:
+        per_rank = [mine_t]
 
     res = {
         "metric": METRIC,
@@ -375,7 +400,12 @@ def main():
                        else "crc32_wring_kernel"),
             "algorithmic_bytes_per_launch": algo_bytes,
             "launch_ms_hip_events": round(ev_ms, 4),
+            # achieved and launch_ms are rank 0's; every rank's are under per_rank
+            "launch_ms_min_max_over_ranks": [min(r["launch_ms_hip_events"] for r in per_rank),
+                                             max(r["launch_ms_hip_events"] for r in per_rank)],
+            "frac_min_over_ranks": min(r["frac"] for r in per_rank),
         },
+        "per_rank": per_rank,
         "cpu_baseline": None,
         "hip_runtime": _lib._foreign_hip_runtime_loaded(),
     }
@@ -452,6 +482,8 @@ def main():
         allsum = [mine]
     if rank == 0:
         res["summary_crc32"] = allsum[0]
+        for pr, sm in zip(res["per_rank"], allsum):
+            pr["summary_crc32"] = sm
         gold = golden_summaries()
         if world > 1 or (cfg == 2 and nrec == (1 << 26)):
             res["rank_summaries_crc32"] = allsum

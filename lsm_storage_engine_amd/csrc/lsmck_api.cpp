@@ -43,6 +43,7 @@ constexpr int kVariantNoStream = 0x200000;  // descriptor batches: no stream ker
 constexpr int kVariantStreamOnly = 0x400000;  // diagnostic: the stream kernel alone (ineligible batches get no CRCs)
 constexpr size_t kChunkBytes = 64ull << 20;                // host staging chunk (payload)
 constexpr size_t kChunkRecs = 1u << 20;                    // host staging chunk (records)
+constexpr int kWalHostWalk = 0x7FFF0001;  // internal: the GPU header walk declined the log; walk it on the host
 
 struct HipFail {
   hipError_t e;
@@ -241,6 +242,9 @@ struct lsmck_ctx {
   std::mutex wal_mu;  // guards wal_host for the duration of one device-image replay
   size_t wal_chunk = 32u << 20;
   int wal_gpu_walk = 1;  // lsmck_wal_replay_verify of a device image: header walk on the GPU (0 = copy back, host walk)
+  // the GPU walk's scratch budget: this many bytes per log byte + 256 MiB (and
+  // at most half the free device memory); over it the log takes the host walk
+  size_t wal_walk_budget_per_byte = 8;
   // host images of at least this many bytes are uploaded whole and walked on
   // the GPU (0 = always the host walk)
   size_t wal_upload_min = 1u << 20;
@@ -1079,6 +1083,8 @@ static int wal_bitmap_ensure(lsmck_ctx* ctx, size_t n) {
 static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck_wal_rec* recs, size_t cap,
                              size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected,
                              bool marked = false) {
+  // the candidate count is a u32 on the device: from 2^32 log bytes on it could wrap
+  if (n >= (1ull << 32)) return kWalHostWalk;
   std::lock_guard<std::mutex> lk(ctx->mu);
   DevGuard g(ctx->dev);
   auto& W = ctx->wd;
@@ -1095,14 +1101,30 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
   if (rc) return launch_rc(rc, "wal mark/scan kernels");
   HIPCHK(hipMemcpyAsync(W.h_info + 3, d_total, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  const uint32_t nc = (uint32_t)(W.h_info[3] & 0xFFFFFFFFull);
+  const uint64_t nc64 = W.h_info[3] & 0xFFFFFFFFull;
+  // The jump tables grow with the CANDIDATE count -- every 0x01/0x02 byte
+  // that could start a header -- not with the record count: a valid log whose
+  // payloads are dense in those bytes needs up to ~120x its size (levels x nc
+  // x 4 B of J alone), and past 2^31 candidates the u32 ranks would reach the
+  // END/BAD sentinels.  Over a budget, or when an allocation fails, the replay
+  // takes the serial host walk instead (kWalHostWalk), as the reference would
+  // replay the same log.
+  if (nc64 >= (1ull << 31)) return kWalHostWalk;
+  const uint32_t nc = (uint32_t)nc64;
   int levels = 0;
-  while (levels < 32 && (1ull << levels) <= nc) ++levels;  // 2^levels > nc
-  if ((rc = ensure_dev(&W.pos, &W.cap_pos, std::max<size_t>(nc, 1))) ||
-      (rc = ensure_dev(&W.J, &W.cap_J, std::max<size_t>((size_t)levels * nc, 1))) ||
-      (rc = ensure_dev(&W.badpos, &W.cap_badpos, std::max<size_t>(nc, 1))) ||
-      (rc = ensure_dev(&W.chain, &W.cap_chain, (size_t)1 << levels)))
-    return rc;
+  while ((1ull << levels) <= nc) ++levels;  // 2^levels > nc, levels <= 31
+  const size_t need = (size_t)nc * (8 + 8 + 4 * (size_t)levels) + ((size_t)4 << levels);
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+  const size_t budget = std::min(free_b / 2, ctx->wal_walk_budget_per_byte * n + ((size_t)256 << 20));
+  if (need > budget) return kWalHostWalk;
+  if (ensure_dev(&W.pos, &W.cap_pos, std::max<size_t>(nc, 1)) ||
+      ensure_dev(&W.J, &W.cap_J, std::max<size_t>((size_t)levels * nc, 1)) ||
+      ensure_dev(&W.badpos, &W.cap_badpos, std::max<size_t>(nc, 1)) ||
+      ensure_dev(&W.chain, &W.cap_chain, (size_t)1 << levels)) {
+    (void)hipGetLastError();  // the failed hipMalloc's sticky error
+    return kWalHostWalk;
+  }
   rc = lsmk_wal_chain(img, n, W.bits, W.pre, nc, levels, W.pos, W.J, W.badpos, W.chain, W.info, st);
   if (rc) return launch_rc(rc, "wal chain kernels");
   HIPCHK(hipMemcpyAsync(W.h_info, W.info, 24, hipMemcpyDeviceToHost, st));
@@ -1196,15 +1218,17 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
   if (rc) return rc;
   if ((flags & LSMCK_DEVICE) && ctx->wal_gpu_walk) {
     std::lock_guard<std::mutex> wl(ctx->wal_mu);  // the walk's bitmap (ctx->wd) is shared with the upload path
-    return wal_replay_device(ctx, wal, n, recs, cap, nrec, bad_index, bad_crc, bad_expected);
-  }
-  if (!(flags & LSMCK_DEVICE) && ctx->wal_upload_min && n >= ctx->wal_upload_min) {
+    rc = wal_replay_device(ctx, wal, n, recs, cap, nrec, bad_index, bad_crc, bad_expected);
+    if (rc != kWalHostWalk) return rc;
+    // (the GPU walk declined: the image is copied back and walked on the host below)
+  } else if (!(flags & LSMCK_DEVICE) && ctx->wal_upload_min && n >= ctx->wal_upload_min) {
     // Host image: one upload (~36 GiB/s through the staging slots) and the GPU
     // header walk, instead of the serial host walk (~12 GiB/s) -- the records
     // and offsets are the same, they index the caller's image
     std::lock_guard<std::mutex> wl(ctx->wal_mu);
     if ((rc = wal_upload(ctx, wal, n, (flags & LSMCK_HOST_PINNED) != 0))) return rc;
-    return wal_replay_device(ctx, ctx->d_wimg, n, recs, cap, nrec, bad_index, bad_crc, bad_expected, true);
+    rc = wal_replay_device(ctx, ctx->d_wimg, n, recs, cap, nrec, bad_index, bad_crc, bad_expected, true);
+    if (rc != kWalHostWalk) return rc;
   }
   const uint8_t* h = wal;
   // Device image: the walk reads a host copy, made by DMA into a pinned

@@ -555,6 +555,12 @@ struct Db {
     for (size_t i = 0; i < nrec; ++i) {
       size_t kl, got;
       const char* p = payload(i, &kl, &got);
+      if (recs[i].type == 1 && got < recs[i].klen) {
+        // an Insert cut at EOF inside its key whose CRC matches the short
+        // bytes: data.split_off(key_len) panics (wal.rs:142)
+        snprintf(msg, sizeof msg, "`at` split index (is %u) should be <= len (is %zu)", recs[i].klen, got);
+        panic_exit(msg);
+      }
       kr[i] = {std::string_view(p, kl), (uint32_t)i};
     }
     std::stable_sort(kr.begin(), kr.end(), [](const KeyRec& a, const KeyRec& b) { return a.k < b.k; });
@@ -788,14 +794,61 @@ std::string utf8_lossy(const std::string& in) {
   return o;
 }
 
-// split_whitespace (command.rs:17)
+// read_line into a String (server.rs:18-20): a line that is not valid UTF-8
+// is an Err, and the reference shuts the connection down (server.rs:70-81)
+bool valid_utf8_line(const std::string& in) {
+  const unsigned char* s = (const unsigned char*)in.data();
+  const size_t n = in.size();
+  for (size_t i = 0; i < n;) {
+    const unsigned c = s[i];
+    if (c < 0x80) {
+      ++i;
+      continue;
+    }
+    size_t need;
+    unsigned lo = 0x80, hi = 0xBF;
+    if (c >= 0xC2 && c <= 0xDF) need = 1;
+    else if (c == 0xE0) need = 2, lo = 0xA0;
+    else if ((c >= 0xE1 && c <= 0xEC) || c == 0xEE || c == 0xEF) need = 2;
+    else if (c == 0xED) need = 2, hi = 0x9F;
+    else if (c == 0xF0) need = 3, lo = 0x90;
+    else if (c >= 0xF1 && c <= 0xF3) need = 3;
+    else if (c == 0xF4) need = 3, hi = 0x8F;
+    else return false;
+    for (size_t k = 1; k <= need; ++k) {
+      if (i + k >= n) return false;
+      const unsigned b = s[i + k];
+      if (k == 1 ? (b < lo || b > hi) : (b < 0x80 || b > 0xBF)) return false;
+    }
+    i += need + 1;
+  }
+  return true;
+}
+
+// Rust's char::is_whitespace (Unicode White_Space) at s[i] of a valid UTF-8
+// string: returns the encoded length of the whitespace character, 0 if none
+size_t ws_len(const std::string& s, size_t i) {
+  const unsigned char c = (unsigned char)s[i];
+  if (c == ' ' || (c >= 0x09 && c <= 0x0D)) return 1;
+  if (c < 0xC2) return 0;
+  const unsigned char c1 = i + 1 < s.size() ? (unsigned char)s[i + 1] : 0;
+  if (c == 0xC2) return (c1 == 0x85 || c1 == 0xA0) ? 2 : 0;  // U+0085, U+00A0
+  const unsigned char c2 = i + 2 < s.size() ? (unsigned char)s[i + 2] : 0;
+  if (c == 0xE1) return (c1 == 0x9A && c2 == 0x80) ? 3 : 0;  // U+1680
+  if (c == 0xE2 && c1 == 0x80) return ((c2 >= 0x80 && c2 <= 0x8A) || c2 == 0xA8 || c2 == 0xA9 || c2 == 0xAF) ? 3 : 0;
+  if (c == 0xE2 && c1 == 0x81) return c2 == 0x9F ? 3 : 0;    // U+205F
+  if (c == 0xE3) return (c1 == 0x80 && c2 == 0x80) ? 3 : 0;  // U+3000
+  return 0;
+}
+
+// split_whitespace (command.rs:17) on a valid UTF-8 line
 std::vector<std::string> split_ws(const std::string& s) {
   std::vector<std::string> out;
   size_t i = 0;
   while (i < s.size()) {
-    while (i < s.size() && (isspace((unsigned char)s[i]) || s[i] == '\v')) ++i;
+    for (size_t w; i < s.size() && (w = ws_len(s, i)) != 0;) i += w;
     size_t j = i;
-    while (j < s.size() && !(isspace((unsigned char)s[j]) || s[j] == '\v')) ++j;
+    while (j < s.size() && ws_len(s, j) == 0) ++j;
     if (j > i) out.push_back(s.substr(i, j - i));
     i = j;
   }
@@ -804,6 +857,7 @@ std::vector<std::string> split_ws(const std::string& s) {
 
 // handle_client (server.rs:16-84); false ends the connection
 bool handle_line(Db& db, const std::string& line, std::string* resp) {
+  if (!valid_utf8_line(line)) return false;  // read_line's Err: the connection is shut down
   const std::vector<std::string> a = split_ws(line);
   if (a.empty()) {
     *resp = "Supported commands: get, insert, update, delete\n";

@@ -6,6 +6,7 @@ GPU tree verify and WAL replay) and exposes the JSON it reports; ``Client``
 speaks the newline-terminated protocol: ``insert k v`` / ``update k v`` ->
 "ok", ``delete k`` -> "ok", ``get k`` -> the value or "<k> not found".
 """
+import collections
 import json
 import os
 import queue
@@ -34,6 +35,13 @@ class Server:
         if exit_after_load:
             cmd.append("--exit-after-load")
         self.proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        # stderr is drained on its own thread into a bounded tail: an undrained
+        # pipe fills at 64 KiB (LSMCK_TREE_TRACE prints a line per round) and
+        # the server would block in write(2) in the middle of a load
+        self._err = collections.deque(maxlen=256)
+        self._err_thread = threading.Thread(target=lambda: [self._err.append(x) for x in iter(self.proc.stderr.readline, "")],
+                                            daemon=True)
+        self._err_thread.start()
         self.loaded = None
         self.port = None
         # the event lines come through a reader thread (select() on a buffered
@@ -50,7 +58,7 @@ class Server:
                 raise TimeoutError("lsmck_server did not start")
             if not line:
                 rc = self.proc.wait()
-                raise ServerExited(rc, self.proc.stderr.read())
+                raise ServerExited(rc, self.stderr_tail())
             ev = json.loads(line)
             if ev["event"] == "loaded":
                 self.loaded = ev
@@ -58,6 +66,12 @@ class Server:
                 self.port = ev["port"]
         if exit_after_load:
             self.proc.wait(timeout=60)
+
+    def stderr_tail(self):
+        """The last lines the server wrote to stderr (all of them once it has exited)."""
+        if self.proc.poll() is not None:
+            self._err_thread.join(timeout=5)
+        return "".join(self._err)
 
     def kill(self):
         """SIGKILL: no flush, no clean shutdown (a crash)."""

@@ -148,6 +148,8 @@ class CommandLog:
                 raise CorruptedData(crc, saved)
             raise WalPanic(f"data corruption encountered ({crc:08x}) != {saved:08x}")
         if t == INSERT:
+            if len(data) < klen:  # cut at EOF inside the key: data.split_off(key_len) panics (wal.rs:142)
+                raise WalPanic(_split_off_msg(klen, len(data)))
             return Insert(data[:klen], data[klen:])
         return Remove(data)
 
@@ -180,12 +182,19 @@ class CommandLog:
             # (read_to_end on take(), :132) -- the same bytes the CRC covered
             data = img[k0:k0 + ((kl + vl) & 0xFFFFFFFF)]
             if t == INSERT:
+                if len(data) < kl:  # cut at EOF inside the key: split_off panics (wal.rs:142)
+                    raise WalPanic(_split_off_msg(kl, len(data)))
                 out.append(Insert(data[:kl], data[kl:]))  # data.split_off(key_len), wal.rs:142
             else:
                 out.append(Remove(data))
             consumed = k0 + len(data)
         self.file.seek(pos + consumed)
         return out
+
+
+def _split_off_msg(at, length):
+    """Vec::split_off's panic message (the reference's wal.rs:142 on a key cut at EOF)."""
+    return f"`at` split index (is {at}) should be <= len (is {length})"
 
 
 class MemTable:

@@ -177,6 +177,13 @@ def test_wal_iterator_errors(golden):
     with pytest.raises(wal.InvalidCommandType):
         list(wal.CommandLog.new_in_memory(bytes(b)))
     assert len(list(wal.CommandLog.new_in_memory(img[:recs[50]["off"] + 3]))) == 50
+    # the last Insert cut at EOF inside its key, CRC matching the short bytes:
+    # data.split_off(key_len) panics (wal.rs:142)
+    short = bytes(img[recs[0]["off"] + 13:recs[0]["off"] + 14])
+    tail = bytes([1]) + O.crc32(short).to_bytes(4, "little") + (10).to_bytes(4, "little") + \
+        (5).to_bytes(4, "little") + short
+    with pytest.raises(wal.WalPanic, match="split index"):
+        list(wal.CommandLog.new_in_memory(img + tail))
 
 
 def test_command_log_file_roundtrip(tmp_path):

@@ -46,8 +46,26 @@ def test_bench_gpus2_launches_two_ranks():
     assert r["scaling"] == "weak"
     want = [_oracle_shard_summary(k, nrec) for k in range(2)]
     assert r["rank_summaries_crc32"] == want
+    # the N > 1 line is evaluable: PMC traffic (config 4's, scaled to the
+    # reduced shard) and every rank's own launch time
+    assert r["roofline"]["traffic"] is not None and r["roofline"]["traffic"] > 0
+    assert [p["rank"] for p in r["per_rank"]] == [0, 1]
+    lo, hi = r["roofline"]["launch_ms_min_max_over_ranks"]
+    assert 0 < lo <= hi
+    assert all(0 < p["frac"] < 1 for p in r["per_rank"])
+    assert [p["summary_crc32"] for p in r["per_rank"]] == want
     # value = both ranks' payload over the slowest rank's time
     assert abs(r["value"] - 2 * nrec * 4096 / 2**30 / (r["ms_per_step"] * 1e-3)) / r["value"] < 0.01
+
+
+def test_bench_default_workload_is_config3():
+    """N = 1 defaults to BASELINE config 3 (north_star's 64 B-64 KiB records);
+    N > 1 to config 4's fixed-block shard."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.resolve_config(0, 1) == 3
+    assert bench.resolve_config(0, 8) == 2
+    assert bench.resolve_config(2, 1) == 2
 
 
 def test_bench_world_size_mismatch_fails():

@@ -150,6 +150,39 @@ def test_truncated_payload_with_matching_crc(ctx):
     assert gpu_log.file.tell() == len(img)
 
 
+def test_key_cut_at_eof_with_matching_crc_panics(ctx):
+    """A last Insert cut at EOF inside its KEY whose CRC matches the short
+    bytes: the CRC check passes, then data.split_off(key_len) panics
+    (wal.rs:142).  The iterator and the batch replay both raise WalPanic."""
+    good = O.wal_insert(b"alpha", b"one")
+    short = b"kkk"  # klen 10 + vlen 5 announced, 3 bytes present
+    tail = bytes([1]) + O.crc32(short).to_bytes(4, "little") + (10).to_bytes(4, "little") + \
+        (5).to_bytes(4, "little") + short
+    img = good + tail
+    with pytest.raises(wal.WalPanic, match="split index"):
+        list(wal.CommandLog.new_in_memory(img))
+    with pytest.raises(wal.WalPanic, match="split index"):
+        wal.CommandLog.new_in_memory(img).replay_verify(ctx)
+
+
+def test_walk_candidate_flood_falls_back_to_the_host_walk(ctx):
+    """A valid multi-MiB log whose keys and values are all 0x01 bytes: every
+    byte is a header candidate for the GPU walk, whose jump tables would need
+    ~100x the log in device memory.  The replay falls back to the serial host
+    walk (host image and device image) and reports the same records."""
+    img = b"".join(O.wal_insert(b"\x01" * 40, b"\x01" * 200) for _ in range(16000))  # 4 MiB
+    same(ctx, img)
+    d = ctx.alloc(len(img))
+    try:
+        d.upload(np.frombuffer(img, np.uint8))
+        recs, st, _ = ctx.wal_replay_verify(len(img), device_ptr=d.ptr)
+        ost, orecs, _ = O.wal_replay(img)
+        assert st == ost == 0
+        assert [int(r["rec_off"]) for r in recs] == [r.rec_off for r in orecs]
+    finally:
+        d.free()
+
+
 def test_gpu_header_walk_big_binary_log(ctx):
     """A log whose payloads are random bytes (so many bytes inside payloads look
     like command types: bogus candidate starts for the GPU walk), device-resident:

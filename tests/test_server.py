@@ -122,19 +122,45 @@ def test_start_refuses_corrupt_tree_and_wal(tmp_path):
     assert ei.value.rc == 101 and "CorruptedData" in ei.value.stderr
 
 
+def test_start_panics_on_key_cut_at_eof(tmp_path):
+    """The log's last Insert is cut at EOF inside its key and its CRC matches
+    the bytes that are there: the replay's data.split_off(key_len) panics
+    (wal.rs:142), so Db::load does too."""
+    base = str(tmp_path / "db")
+    tree.synthesize_tree(base, 1 << 20, wal_records=200)
+    wal = os.path.join(base, "wal", "wal.log")
+    short = b"kkk"
+    tail = bytes([1]) + O.crc32(short).to_bytes(4, "little") + (10).to_bytes(4, "little") + \
+        (5).to_bytes(4, "little") + short
+    with open(wal, "ab") as f:
+        f.write(tail)
+    with pytest.raises(ServerExited) as ei:
+        Server(base)
+    assert ei.value.rc == 101 and "split index" in ei.value.stderr
+
+
 def test_client_protocol_edges(tmp_path):
     base = str(tmp_path / "db")
     srv = Server(base)
     try:
         c = srv.client()
-        assert c.call(b"insert", b"a", b"\xc3\xa9t\xe9") == b"ok"  # value bytes from the wire
-        assert c.call(b"get", b"a") == "ét�".encode()  # String::from_utf8_lossy
+        assert c.call(b"insert", b"a", "ét".encode()) == b"ok"  # value bytes from the wire
+        assert c.call(b"get", b"a") == "ét".encode()
         assert c.call(b"insert  b\t c  extra") == b"ok"  # split_whitespace; extra args ignored
         assert c.call(b"get", b"b") == b"c"
         assert c.call(b"delete", b"b") == b"ok"
         assert c.call(b"get", b"b") == b"b not found"
+        # split_whitespace splits on Unicode White_Space (U+00A0, U+3000), not only ASCII
+        assert c.call("insert\u00a0x\u3000y".encode()) == b"ok"
+        assert c.call(b"get", b"x") == b"y"
         c.close()
-        assert Client(srv.port).call(b"get", b"a") == "ét�".encode()
+        assert Client(srv.port).call(b"get", b"a") == "ét".encode()
+        # a line that is not UTF-8: read_line into a String fails and the
+        # reference shuts the connection down (server.rs:70-81)
+        c3 = srv.client()
+        with pytest.raises(ConnectionError):
+            c3.call(b"insert", b"a", b"\xc3\xa9t\xe9")
+        assert Client(srv.port).call(b"get", b"a") == "ét".encode()  # nothing was applied
     finally:
         srv.kill()
 
