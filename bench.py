@@ -63,7 +63,11 @@ def parse():
     ap.add_argument("--blocks-per-gpu", type=int, default=0, help="override the per-GPU record count")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-records", type=int, default=0)
-    ap.add_argument("--variants", default="", help="comma list of crc_chains values to A/B in interleaved rounds")
+    ap.add_argument("--variants", default="",
+                    help="comma list of A/B variants timed in interleaved rounds, each a '+' list of "
+                         "s<n> (crc_stream: 0 walking kernel only, 1 default), a<n> (crc_ablate: 3 payload "
+                         "loads only, 2 stream kernel without loads), p<n> (sha_pair), b<n> (sha_bucket_shift), "
+                         "f<n> (sha_bucket_from); '-' is the default")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--no-stream-ceiling", action="store_true",
                     help="skip the loads-only ceiling run of the same kernel (roofline.loads_only_ceiling)")
@@ -75,10 +79,9 @@ def parse():
                     help="crc32 = the WAL record checksum (headline); sha256 = the SSTable digest "
                          "(checksums.rs) over the same records, reported against its int32 VALU roof")
     ap.add_argument("--stream", type=int, default=1, choices=[0, 1],
-                    help="packed batches of >= 64-byte records (config 3): 1 = stream kernel (default), "
-                         "0 = walking kernel (A/B)")
-    ap.add_argument("--walk", type=int, default=1, choices=[0, 1],
-                    help="descriptor batches: 1 = walking kernel (default), 0 = r01 tile-map kernel (A/B)")
+                    help="descriptor batches: 1 = stream kernel (default), 0 = walking kernel (A/B)")
+    ap.add_argument("--wal-framed", action="store_true",
+                    help="config 3's records framed as wal.rs Insert records (13-byte headers between the payloads)")
     ap.add_argument("--pack-align", type=int, default=1,
                     help="diagnostic: config 3 record offsets rounded up to this many bytes")
     return ap.parse_args()
@@ -159,8 +162,6 @@ def main():
     stream = torch.cuda.Stream(device=local)  # a real stream: the null stream's handle (0) means
     sptr = stream.cuda_stream                 # "the context's own stream" to liblsmck
     ctx = Context(local)
-    if a.walk != 1:
-        ctx.set_option("crc_walk", a.walk)
     if a.stream != 1:
         ctx.set_option("crc_stream", a.stream)
 
@@ -192,12 +193,22 @@ def main():
         lens = gen_zipf_lengths(seed + rank, nrec)
         offs = np.zeros(nrec, dtype=np.uint64)
         A = max(1, a.pack_align)
-        slot = ((lens.astype(np.uint64) + (A - 1)) // A) * A  # A = 1: packed back to back
-        np.cumsum(slot[:-1], out=offs[1:])
+        if a.wal_framed:  # wal.rs:178-182: [u8 1][u32 crc][u32 klen][u32 vlen] in front of every payload
+            offs[:] = 13
+            offs[1:] += lens[:-1].astype(np.uint64) + np.uint64(13)
+            offs = np.cumsum(offs, dtype=np.uint64)
+        else:
+            slot = ((lens.astype(np.uint64) + (A - 1)) // A) * A  # A = 1: packed back to back
+            np.cumsum(slot[:-1], out=offs[1:])
         nbytes = int(offs[-1]) + int(lens[-1])
         byte_off = 0
-        workload = (f"config3: {nrec} mixed-length records per GPU (64 B-64 KiB, Zipf s=1.5, packed, unaligned; "
-                    f"{nbytes / GIB:.1f} GiB), device-resident")
+        if a.wal_framed:
+            workload = (f"config3w: {nrec} mixed-length records per GPU (64 B-64 KiB, Zipf s=1.5) framed as wal.rs "
+                        f"Insert records: a 13-byte header before every payload, unaligned ({nbytes / GIB:.1f} GiB "
+                        "image), device-resident")
+        else:
+            workload = (f"config3: {nrec} mixed-length records per GPU (64 B-64 KiB, Zipf s=1.5, packed, unaligned; "
+                        f"{nbytes / GIB:.1f} GiB), device-resident")
         if A > 1:
             workload += f" [diagnostic: offsets aligned to {A} B]"
 
@@ -246,49 +257,18 @@ def main():
         vs = a.variants.split(",")
         ab = {v: [] for v in vs}
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        defaults = {"crc_stream": 1, "crc_ablate": 0, "sha_pair": 1, "sha_bucket_shift": 2, "sha_bucket_from": 128}
+        keys = {"s": "crc_stream", "a": "crc_ablate", "p": "sha_pair", "b": "sha_bucket_shift", "f": "sha_bucket_from"}
         for _ in range(a.rounds):
             for v in vs:
-                # "c<k>" = crc_chains k;  "g<k>" = crc_chains k with the generic multiply;
-                # "a<k>" = diagnostic ablation k (timing only); optional suffix
-                # "w<n>" = crc_wg_waves n (descriptor kernel); "l<n>" = crc_loads n
-                # (1 global, 2 raw buffer); "r<n>" = crc_ring n (1 = two-slot kernel)
-                # "b<n>" = sha_bucket_shift n (SHA order: 2^n-block buckets for 128..1023 blocks)
-                # "f<n>" = sha_bucket_from n (first block count of the coarse buckets)
-                # "o<n>" = crc_order n (fixed ring kernel tile order; 3 = default)
-                # "p<n>" = sha_pair n (SHA-256: two blocks per load window)
-                # "s<n>" = crc_stream n (descriptor batches: 1 stream kernel where eligible, 0 walking kernel)
-                # "q<n>" = crc_stream_batch n (stream kernel: records finished in batches of 64)
-                # "t<n>" = crc_stream_qstore n (stream kernel: 2 queued 256-B output blocks pushed at the next
-                #          tile (default), 1 pushed at once, 0 per-tile stores)
-                # "y<n>" = crc_stream_fsp n (stream kernel: finish multiplies spread over 8 lanes)
-                # "m<n>" = crc_stream_lm n (stream kernel: 1 chunk boundaries through LDS bytes, default)
-                # "k<n>" = crc_walk_opq n (walking kernel: carry multiply offsets recomputed)
-                # "z<n>" = crc_stream_z0 n (stream kernel: 1 short path for tiles without a boundary, default)
-                # "e<n>" = crc_stream_sel n (stream kernel: 1 boundary branches only select the step inputs, default)
-                # "v<n>" = crc_stream_window n (stream kernel: 2 sliding, 1 second half on demand, 0 reloaded)
-                m = re.fullmatch(r"([cga])(\d+)(?:w(\d+))?(?:l(\d))?(?:r(\d))?(?:b(\d))?(?:f(\d+))?(?:o(\d))?(?:p(\d))?(?:s(\d))?(?:q(\d))?(?:t(\d))?(?:v(\d))?(?:e(\d))?(?:z(\d))?(?:k(\d))?(?:m(\d))?(?:y(\d))?", v)
-                if not m:
-                    raise SystemExit(f"bad variant {v!r}")
-                kind, num, waves = m.group(1), int(m.group(2)), int(m.group(3) or 0)
-                ctx.set_option("crc_chains", num if kind in "cg" else 0)
-                ctx.set_option("crc_generic_mul", 1 if kind == "g" else 0)
-                ctx.set_option("crc_ablate", num if kind == "a" else 0)
-                ctx.set_option("crc_wg_waves", waves)
-                ctx.set_option("crc_loads", int(m.group(4) or 0))
-                ctx.set_option("crc_ring", int(m.group(5) or 0))
-                ctx.set_option("sha_bucket_shift", int(m.group(6)) if m.group(6) is not None else 2)
-                ctx.set_option("sha_bucket_from", int(m.group(7) or 128))
-                ctx.set_option("crc_order", int(m.group(8)) if m.group(8) is not None else 3)
-                ctx.set_option("sha_pair", int(m.group(9)) if m.group(9) is not None else 1)
-                ctx.set_option("crc_stream", int(m.group(10)) if m.group(10) is not None else 1)
-                ctx.set_option("crc_stream_batch", int(m.group(11) or 0))
-                ctx.set_option("crc_stream_qstore", int(m.group(12)) if m.group(12) is not None else 2)
-                ctx.set_option("crc_stream_window", int(m.group(13)) if m.group(13) is not None else 2)
-                ctx.set_option("crc_stream_sel", int(m.group(14)) if m.group(14) is not None else 1)
-                ctx.set_option("crc_stream_z0", int(m.group(15)) if m.group(15) is not None else 1)
-                ctx.set_option("crc_walk_opq", int(m.group(16) or 0))
-                ctx.set_option("crc_stream_lm", int(m.group(17)) if m.group(17) is not None else 1)
-                ctx.set_option("crc_stream_fsp", int(m.group(18) or 0))
+                opts = dict(defaults)
+                for part in ([] if v == "-" else v.split("+")):
+                    m = re.fullmatch(r"([sapbf])(\d+)", part)
+                    if not m:
+                        raise SystemExit(f"bad variant {v!r}")
+                    opts[keys[m.group(1)]] = int(m.group(2))
+                for k, val in opts.items():
+                    ctx.set_option(k, val)
                 step()
                 e0.record(stream)
                 for _ in range(a.steps):
@@ -296,25 +276,8 @@ def main():
                 e1.record(stream)
                 ctx.sync(sptr)
                 ab[v].append(e0.elapsed_time(e1) / a.steps)
-        ctx.set_option("crc_chains", 0)
-        ctx.set_option("crc_generic_mul", 0)
-        ctx.set_option("crc_ablate", 0)
-        ctx.set_option("crc_wg_waves", 0)
-        ctx.set_option("crc_loads", 0)
-        ctx.set_option("crc_ring", 0)
-        ctx.set_option("sha_bucket_shift", 2)
-        ctx.set_option("sha_bucket_from", 128)
-        ctx.set_option("sha_pair", 1)
-        ctx.set_option("crc_stream", 1)
-        ctx.set_option("crc_stream_batch", 0)
-        ctx.set_option("crc_stream_qstore", 2)
-        ctx.set_option("crc_stream_window", 2)
-        ctx.set_option("crc_stream_sel", 1)
-        ctx.set_option("crc_stream_z0", 1)
-        ctx.set_option("crc_walk_opq", 0)
-        ctx.set_option("crc_stream_lm", 1)
-        ctx.set_option("crc_stream_fsp", 0)
-        ctx.set_option("crc_order", 3)
+        for k, val in defaults.items():
+            ctx.set_option(k, val)
         ab = {str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                        "GiBps_median": payload / GIB / (float(np.median(t)) * 1e-3)} for v, t in ab.items()}
 
@@ -353,7 +316,8 @@ def main():
         t4 = traffic_from_profiles("config4")
         traffic = None if t4 is None else round(t4 * nrec / float(1 << 26), 1)
     else:
-        wkey = None if (a.desc or a.pack_align > 1 or a.blocks_per_gpu) else f"{'sha256_' if sha else ''}config{cfg}"
+        cname = f"config{cfg}" + ("w" if a.wal_framed else "")
+        wkey = None if (a.desc or a.pack_align > 1 or a.blocks_per_gpu) else f"{'sha256_' if sha else ''}{cname}"
         traffic = traffic_from_profiles(wkey)
     # every rank's own launch time (HIP events on its stream) and wall time
     mine_t = {"rank": rank, "launch_ms_hip_events": round(ev_ms, 4), "wall_ms_per_step": round(wall * 1e3 / a.steps, 4),
@@ -395,8 +359,7 @@ def main():
             # fixed records whose segment count divides 64 (configs 1, 2) run the
             # whole-tile ring kernel by default (lsmck_crc32.hip, LSMCK_DEFAULT_RING)
             # config 3 is packed with records >= 64 B: the stream kernel takes it
-            "kernel": (("crc32_stream_kernel" if (cfg == 3 and a.walk and a.stream) else
-                        "crc32_walk_kernel" if a.walk else "crc32_desc_kernel") if (cfg == 3 or a.desc)
+            "kernel": (("crc32_stream_kernel" if a.stream else "crc32_walk_kernel") if (cfg == 3 or a.desc)
                        else "crc32_wring_kernel"),
             "algorithmic_bytes_per_launch": algo_bytes,
             "launch_ms_hip_events": round(ev_ms, 4),
@@ -493,7 +456,8 @@ def main():
                 res["summary_matches_oracle"] = allsum == g4[:world]
         elif not a.blocks_per_gpu and a.pack_align <= 1:
             # against the oracle's full-size value (default layouts only)
-            g = gold.get(f"config{cfg}", {}).get("summary_sha256" if sha else "summary_crc32")
+            g = gold.get(f"config{cfg}" + ("w" if a.wal_framed and cfg == 3 else ""), {}).get(
+                "summary_sha256" if sha else "summary_crc32")
             if g:
                 res["summary_matches_oracle"] = res["summary_crc32"] == g
 

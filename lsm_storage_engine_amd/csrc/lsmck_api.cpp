@@ -38,7 +38,6 @@ using lsmck::ShaParams;
 namespace {
 
 constexpr uint64_t kMaxSegsPerLaunch = (1ull << 32) - 64;  // 32-bit segment indices in the kernels
-constexpr int kVariantTileMap = 0x100000;  // descriptor batches: the r01 tile-map kernel instead of the walking one
 constexpr int kVariantNoStream = 0x200000;  // descriptor batches: no stream kernel for packed >= 64-byte records (A/B)
 constexpr int kVariantStreamOnly = 0x400000;  // diagnostic: the stream kernel alone (ineligible batches get no CRCs)
 constexpr size_t kChunkBytes = 64ull << 20;                // host staging chunk (payload)
@@ -95,8 +94,6 @@ int ensure_pinned(T** p, size_t* cap, size_t need) {
 struct DescScratch {
   uint64_t* block_sum = nullptr;  // per 1024-record block
   size_t cap_bs = 0;
-  uint32_t* tile_info = nullptr;  // 4 u32 per tile
-  size_t cap_tf = 0;
   uint64_t* total = nullptr;  // device, 1 u64
   // SHA-256 dispatch order (lsmck_order.hip)
   uint16_t* sha_keys = nullptr;
@@ -113,7 +110,6 @@ struct DescScratch {
     if (sflag) (void)hipFree(sflag);
     if (scuts) (void)hipFree(scuts);
     if (block_sum) (void)hipFree(block_sum);
-    if (tile_info) (void)hipFree(tile_info);
     if (total) (void)hipFree(total);
     if (sha_keys) (void)hipFree(sha_keys);
     if (sha_order) (void)hipFree(sha_order);
@@ -185,9 +181,7 @@ struct lsmck_ctx {
   std::mutex mu;
   DescScratch scratch;           // device-mode descriptor scratch
   hipEvent_t scratch_ev = nullptr;
-  uint64_t* h_total = nullptr;   // pinned
   unsigned long long* d_verify = nullptr;  // [n_bad, first_bad]
-  uint32_t* d_work = nullptr;              // work counters of the claimed-block kernels, one per stage + 1
   unsigned long long* h_verify = nullptr;  // pinned
   // device verify / device WAL replay (grow-only; part of the scratch, ordered by scratch_ev)
   uint32_t* d_vcrc = nullptr;  // computed CRCs
@@ -226,8 +220,7 @@ struct lsmck_ctx {
   uint32_t* h_wexp = nullptr;
   size_t cap_hwexp = 0;
   Stage stage[2];
-  int variant = 0;  // kernel variant for A/B timing (LSMCK_CRC_CHAINS=1|2|4); 0 = default
-  int variant2 = 0;  // more A/B bits (0x1: crc_stream_lm 0); 0 = default
+  int variant = 0;  // A/B and diagnostic bits (crc_ablate, crc_stream, sha_order); 0 = default
   uint32_t tree_active = 0;  // whole-tree verify: files in flight (0 = kTreeActive)
   uint32_t tree_slice = 0;   // whole-tree verify: bytes of a file per round (0 = kTreeSlice)
   long tree_open = -1;       // whole-tree verify: files kept open between slices (-1 = RLIMIT_NOFILE budget)
@@ -296,7 +289,6 @@ int ensure_scratch(DescScratch& sc, size_t nblocks) {
 }
 
 void fill_tables(lsmck_ctx* ctx, CrcParams* P) {
-  P->work = ctx->d_work;
   P->kseg = ctx->d_kseg;
   P->khi = ctx->d_khi;
   P->tinit = ctx->d_tinit;
@@ -335,41 +327,17 @@ int crc_fixed_device(lsmck_ctx* ctx, const uint8_t* base, size_t stride, uint32_
 
 // Descriptor CRC on device pointers with known (host) total segment count
 // (host staging path) or unknown (device path: read back after the scan).
+// trusted: the library's own batch (host-staged chunks, WAL payloads): sorted,
+// not overlapping, the bytes between records inside the same buffer -- the
+// stream kernel takes it without the device check or the walking kernel.
 int crc_desc_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const uint64_t* off, const uint32_t* len,
-                    size_t n, uint32_t* out, hipStream_t st, int64_t known_total, uint64_t* h_total) {
+                    size_t n, uint32_t* out, hipStream_t st, bool trusted = false) {
   if (n == 0) return 0;
   if (n >= (1ull << 32)) return lsmck_host::set_error(LSMCK_EINVAL, "more than 2^32-1 records in one batch");
-  if (!(ctx->variant & kVariantTileMap)) {
-    // walking kernel (default): scratch sized by the record count, nothing
-    // read back, every CRC stored once -- asynchronous on st
-    int rc = ensure_scratch(sc, (size_t)lsmk_walk_sb_count(n));
-    if (rc) return rc;
-    CrcParams P{};
-    P.base = base;
-    P.off = off;
-    P.len = len;
-    P.nrec = n;
-    P.total_segs = sc.total;
-    P.out = out;
-    fill_tables(ctx, &P);
-    if (!(ctx->variant & kVariantNoStream)) {
-      // packed batches of >= 64-byte records: the stream kernel (decided on
-      // the device; the walking kernel below then exits at once)
-      if (!sc.sflag) HIPCHK(hipMalloc((void**)&sc.sflag, 16));
-      if ((rc = ensure_dev(&sc.scuts, &sc.cap_cuts, (size_t)lsmk_stream_waves(ctx->ncu) + 1))) return rc;
-      P.sflag = sc.sflag;
-      P.scuts = sc.scuts;
-      rc = lsmk_launch_crc32_stream(&P, ctx->ncu, ctx->variant, ctx->variant2, st);
-      if (rc) return launch_rc(rc, "crc32_stream kernel");
-      if (ctx->variant & kVariantStreamOnly) return 0;
-    }
-    rc = lsmk_launch_crc32_walk(&P, sc.block_sum, ctx->ncu, ctx->variant, st);
-    return rc ? launch_rc(rc, "crc32_walk kernel") : 0;
-  }
-  size_t nb = (size_t)lsmk_scan_block_count(n);
-  int rc = ensure_scratch(sc, nb);
+  // walking kernel: scratch sized by the record count, nothing read back,
+  // every CRC stored once -- asynchronous on st
+  int rc = ensure_scratch(sc, (size_t)lsmk_walk_sb_count(n));
   if (rc) return rc;
-  HIPCHK(hipMemsetAsync(out, 0, n * 4, st));
   CrcParams P{};
   P.base = base;
   P.off = off;
@@ -378,26 +346,20 @@ int crc_desc_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const 
   P.total_segs = sc.total;
   P.out = out;
   fill_tables(ctx, &P);
-  rc = lsmk_launch_crc32_scan(&P, sc.block_sum, st);
-  if (rc) return launch_rc(rc, "crc32 scan");
-  uint64_t total;
-  if (known_total >= 0) {
-    total = (uint64_t)known_total;
-  } else {
-    HIPCHK(hipMemcpyAsync(h_total, sc.total, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    total = *h_total;
+  if (!(ctx->variant & kVariantNoStream)) {
+    // sorted batches, packed or with small gaps: the stream kernel (a
+    // caller's batch is checked on the device; when it is not eligible the
+    // walking kernel below takes it, else that kernel exits at once)
+    if (!sc.sflag) HIPCHK(hipMalloc((void**)&sc.sflag, 16));
+    if ((rc = ensure_dev(&sc.scuts, &sc.cap_cuts, (size_t)lsmk_stream_waves(ctx->ncu) + 1))) return rc;
+    P.sflag = sc.sflag;
+    P.scuts = sc.scuts;
+    rc = lsmk_launch_crc32_stream(&P, ctx->ncu, ctx->variant, trusted ? 1 : 0, st);
+    if (rc) return launch_rc(rc, "crc32_stream kernel");
+    if (trusted || (ctx->variant & kVariantStreamOnly)) return 0;
   }
-  if (total >= kMaxSegsPerLaunch)
-    return lsmck_host::set_error(LSMCK_EINVAL, "batch exceeds 2^32 128-byte segments; split it");
-  if (total == 0) return 0;
-  size_t ntiles = (size_t)((total + 63) / 64);
-  if ((rc = ensure_dev(&sc.tile_info, &sc.cap_tf, 4 * ntiles))) return rc;
-  HIPCHK(hipMemsetAsync(sc.tile_info, 0, 16 * ntiles, st));
-  P.tile_info = sc.tile_info;
-  rc = lsmk_launch_crc32_desc(&P, sc.block_sum, ctx->ncu, ctx->variant, st);
-  if (rc) return launch_rc(rc, "crc32_desc kernel");
-  return 0;
+  rc = lsmk_launch_crc32_walk(&P, sc.block_sum, ctx->ncu, ctx->variant, st);
+  return rc ? launch_rc(rc, "crc32_walk kernel") : 0;
 }
 
 // Variable-length batches of at least this many messages run in decreasing
@@ -598,9 +560,9 @@ int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
     }
     if (J.kind == CRC) {
       if (J.off) {
-        int64_t total = 0;
-        for (size_t i = 0; i < cnt; ++i) total += S.h_len[i] ? (S.h_len[i] + 127u) / 128u : 1u;
-        rc = crc_desc_device(ctx, S.scratch, S.d_pay, S.d_off, S.d_len, cnt, (uint32_t*)S.d_out, S.s, total, nullptr);
+        // the staged chunk is sorted by construction: its whole span (sorted,
+        // not overlapping: `mono`), or the records packed in order
+        rc = crc_desc_device(ctx, S.scratch, S.d_pay, S.d_off, S.d_len, cnt, (uint32_t*)S.d_out, S.s, true);
       } else {
         // fixed records: the span starts at record r (gathered: packed at stride flen)
         rc = crc_fixed_device(ctx, S.d_pay, use_span ? J.stride : J.flen, J.flen, cnt, (uint32_t*)S.d_out, S.s);
@@ -636,10 +598,11 @@ int check_ctx(lsmck_ctx* ctx) {
 // context's pooled buffers; synchronous (the counts come back to the host).
 // Caller holds ctx->mu and orders st on the scratch.
 int device_verify(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len,
-                  const uint32_t* expected, size_t n, hipStream_t st, uint64_t* n_bad, uint64_t* first_bad) {
+                  const uint32_t* expected, size_t n, hipStream_t st, uint64_t* n_bad, uint64_t* first_bad,
+                  bool trusted = false) {
   int rc = ensure_dev(&ctx->d_vcrc, &ctx->cap_vcrc, std::max<size_t>(n, 1));
   if (rc) return rc;
-  rc = crc_desc_device(ctx, ctx->scratch, base, off, len, n, ctx->d_vcrc, st, -1, ctx->h_total);
+  rc = crc_desc_device(ctx, ctx->scratch, base, off, len, n, ctx->d_vcrc, st, trusted);
   if (rc) return rc;
   HIPCHK(hipMemsetAsync(ctx->d_verify, 0, 8, st));         // n_bad
   HIPCHK(hipMemsetAsync(ctx->d_verify + 1, 0xFF, 8, st));  // first_bad = ~0
@@ -686,7 +649,6 @@ lsmck_ctx* lsmck_ctx_create(int device) {
   }
   lsmck_ctx* ctx = new lsmck_ctx();
   ctx->dev = device;
-  if (const char* v = getenv("LSMCK_CRC_CHAINS")) ctx->variant = atoi(v);
   ctx->ncu = pr.multiProcessorCount;
   // combination tables
   std::vector<uint32_t> master(4096), kseg(65536), khi(65536), tinit(130, 0u);
@@ -716,10 +678,8 @@ lsmck_ctx* lsmck_ctx_create(int device) {
             hipMemcpy(ctx->d_khi, khi.data(), 65536 * 4, hipMemcpyHostToDevice) == hipSuccess &&
             hipMemcpy(ctx->d_tinit, tinit.data(), 130 * 4, hipMemcpyHostToDevice) == hipSuccess &&
             hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming) == hipSuccess &&
-            hipHostMalloc((void**)&ctx->h_total, 64, hipHostMallocDefault) == hipSuccess &&
             hipHostMalloc((void**)&ctx->h_verify, 64, hipHostMallocDefault) == hipSuccess &&
-            hipMalloc((void**)&ctx->d_verify, 64) == hipSuccess &&
-            hipMalloc((void**)&ctx->d_work, 256) == hipSuccess;
+            hipMalloc((void**)&ctx->d_verify, 64) == hipSuccess;
   if (!ok) {
     lsmck_host::set_error(LSMCK_ENOMEM, "context allocation failed");
     lsmck_ctx_destroy(ctx);
@@ -732,36 +692,11 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if (!key) return lsmck_host::set_error(LSMCK_EINVAL, "null key");
-  if (!strcmp(key, "crc_chains")) {
-    if (value != 0 && value != 1 && value != 2 && value != 4)
-      return lsmck_host::set_error(LSMCK_EINVAL, "crc_chains must be 0, 1, 2 or 4");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~0xF) | (int)value;
-    return 0;
-  }
-  if (!strcmp(key, "crc_generic_mul")) {  // A/B: 1 = per-lane LDS columns off for fixed records
-    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_generic_mul must be 0 or 1");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~0x10) | (value ? 0x10 : 0);
-    return 0;
-  }
-  if (!strcmp(key, "crc_ablate")) {  // diagnostic only: timing ablations, results are garbage
-    if (value < 0 || value > 15) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0..15");
+  if (!strcmp(key, "crc_ablate")) {  // diagnostic only (results are garbage): 3 = payload loads only (the
+                                     // bench's loads-only ceiling), 2 = stream kernel without payload loads
+    if (value != 0 && value != 2 && value != 3) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0, 2 or 3");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->variant = (ctx->variant & ~0xF00) | ((int)value << 8);
-    return 0;
-  }
-  if (!strcmp(key, "crc_wg_waves")) {  // A/B: waves per workgroup of the descriptor kernel
-    if (value != 0 && value != 12 && value != 16)
-      return lsmck_host::set_error(LSMCK_EINVAL, "crc_wg_waves must be 0, 12 or 16");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~0x20) | (value == 12 ? 0x20 : 0);
-    return 0;
-  }
-  if (!strcmp(key, "crc_ring")) {  // A/B: fixed-record ring kernel (0 default, 1 two-slot kernel, 2/3 ring slots)
-    if (value < 0 || value > 3) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ring must be 0..3");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~0xF000) | ((int)value << 12);
     return 0;
   }
   if (!strcmp(key, "tree_active_files")) {  // whole-tree verify: files in flight (0 = 8192); tests use few
@@ -849,86 +784,13 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->variant = (ctx->variant & ~0x10000) | (value ? 0 : 0x10000);
     return 0;
   }
-  if (!strcmp(key, "crc_order")) {  // A/B: fixed ring kernel tile order, 0 strided, 1 contiguous, 2 claimed blocks,
-                                    // 3 contiguous with the CRCs stored as queued 256-B blocks (default), 4
-                                    // strided with the CRCs of 16 tiles gathered in LDS (<= 4 records per tile),
-                                    // 5 strided with each tile's store after the next tile's loads
-    if (value < 0 || value > 5) return lsmck_host::set_error(LSMCK_EINVAL, "crc_order must be 0..5");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    // stored as order + 1 (0 = the default)
-    ctx->variant = (ctx->variant & ~0x7000000) | ((value == LSMCK_DEFAULT_ORDER ? 0 : (int)value + 1) << 24);
-    return 0;
-  }
-  if (!strcmp(key, "crc_stream_batch")) {  // A/B: stream kernel, records finished in batches of 64 (1) or per tile (0)
-    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_batch must be 0 or 1");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~0x800000) | (value ? 0x800000 : 0);
-    return 0;
-  }
-  if (!strcmp(key, "crc_stream_window")) {  // A/B: stream kernel boundary window, 2 = sliding (default),
-                                            // 1 = reloaded, second half on demand, 0 = both halves reloaded
-    if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_window must be 0, 1 or 2");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~0x18000000) | ((int)(2 - value) << 27);
-    return 0;
-  }
-  if (!strcmp(key, "crc_stream_fsp")) {  // A/B: stream kernel finish multiplies spread over 8 lanes per record (1)
-    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_fsp must be 0 or 1");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant2 = (ctx->variant2 & ~0x2) | (value ? 0x2 : 0);
-    return 0;
-  }
-  if (!strcmp(key, "crc_stream_lm")) {  // A/B: stream kernel chunk boundaries through LDS bytes (1, default)
-    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_lm must be 0 or 1");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant2 = (ctx->variant2 & ~0x1) | (value ? 0 : 0x1);
-    return 0;
-  }
-  if (!strcmp(key, "crc_walk_opq")) {  // A/B: walking kernel, the carry multiply's lane offsets recomputed (1)
-    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_walk_opq must be 0 or 1");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (int)(((unsigned)ctx->variant & ~0x80000000u) | (value ? 0x80000000u : 0u));
-    return 0;
-  }
-  if (!strcmp(key, "crc_stream_z0")) {  // A/B: stream kernel short path for tiles where no record ends (1, default)
-    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_z0 must be 0 or 1");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~0x20000) | (value ? 0 : 0x20000);
-    return 0;
-  }
-  if (!strcmp(key, "crc_stream_sel")) {  // A/B: stream kernel word steps after the boundary branch (1, default),
-                                         // in it (0), or no branch: inputs selected per step (2)
-    if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_sel must be 0, 1 or 2");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~0xC0000) | (value == 0 ? 0x40000 : value == 2 ? 0x80000 : 0);
-    return 0;
-  }
-  if (!strcmp(key, "crc_stream_qstore")) {  // A/B: stream kernel CRCs stored as queued 256-B blocks, pushed
-                                            // at the next tile (2, default) or at once (1); or per tile (0)
-    // or the queue's push deferred to the next tile (2)
-    if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream_qstore must be 0, 1 or 2");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~0x60000000) | (value == 0 ? 0x20000000 : value == 1 ? 0x40000000 : 0);
-    return 0;
-  }
-  if (!strcmp(key, "crc_stream")) {  // A/B: descriptor batches, 1 = stream kernel for packed >= 64-byte records
-                                     // (default), 0 = walking kernel only, 2 = stream kernel only (diagnostic)
+  if (!strcmp(key, "crc_stream")) {  // A/B: descriptor batches, 1 = stream kernel for sorted batches (default),
+                                     // 0 = walking kernel only, 2 = stream kernel only (diagnostic: a declined
+                                     // caller batch gets no CRCs)
     if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_stream must be 0, 1 or 2");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->variant = (ctx->variant & ~(kVariantNoStream | kVariantStreamOnly)) |
                    (value == 0 ? kVariantNoStream : value == 2 ? kVariantStreamOnly : 0);
-    return 0;
-  }
-  if (!strcmp(key, "crc_walk")) {  // A/B: descriptor batches, 1 = walking kernel (default), 0 = r01 tile-map kernel
-    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "crc_walk must be 0 or 1");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~kVariantTileMap) | (value ? 0 : kVariantTileMap);
-    return 0;
-  }
-  if (!strcmp(key, "crc_loads")) {  // A/B: payload load instruction, 0 default, 1 global, 2 raw buffer
-    if (value < 0 || value > 2) return lsmck_host::set_error(LSMCK_EINVAL, "crc_loads must be 0, 1 or 2");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->variant = (ctx->variant & ~0xC0) | (value == 1 ? 0x40 : 0) | (value == 2 ? 0x80 : 0);
     return 0;
   }
   return lsmck_host::set_error(LSMCK_EINVAL, "unknown option");
@@ -949,7 +811,6 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   if (ctx->d_tinit) (void)hipFree(ctx->d_tinit);
   if (ctx->d_zero) (void)hipFree(ctx->d_zero);
   if (ctx->d_verify) (void)hipFree(ctx->d_verify);
-  if (ctx->d_work) (void)hipFree(ctx->d_work);
   for (void* p : {(void*)ctx->wd.bits, (void*)ctx->wd.pre, (void*)ctx->wd.bsum, (void*)ctx->wd.pos, (void*)ctx->wd.J,
                   (void*)ctx->wd.badpos, (void*)ctx->wd.chain, (void*)ctx->wd.recs, (void*)ctx->wd.info})
     if (p) (void)hipFree(p);
@@ -958,7 +819,6 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
     if (p) (void)hipFree(p);
   for (void* p : {(void*)ctx->h_woff, (void*)ctx->h_wlen, (void*)ctx->h_wexp})
     if (p) (void)hipHostFree(p);
-  if (ctx->h_total) (void)hipHostFree(ctx->h_total);
   if (ctx->h_verify) (void)hipHostFree(ctx->h_verify);
   if (ctx->wal_host) (void)hipHostFree(ctx->wal_host);
   if (ctx->d_wimg) (void)hipFree(ctx->d_wimg);
@@ -977,7 +837,7 @@ int lsmck_crc32_batch(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, 
   if (flags & LSMCK_DEVICE) {
     ScratchOrder so(ctx, pick_stream(ctx, stream));
     if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
-    return crc_desc_device(ctx, ctx->scratch, base, off, len, n, out, so.st, -1, ctx->h_total);
+    return crc_desc_device(ctx, ctx->scratch, base, off, len, n, out, so.st);
   }
   HostJob J{CRC, base, off, len, 0, 0, n, (uint8_t*)out, (flags & LSMCK_HOST_PINNED) != 0};
   return run_host_job(ctx, J);
@@ -1140,7 +1000,8 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
       return rc;
     rc = lsmk_wal_emit(img, n, W.chain, W.pos, W.info, (uint32_t)m, W.recs, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st);
     if (rc) return launch_rc(rc, "wal emit kernel");
-    rc = device_verify(ctx, img, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, m, st, &nbad, &first);
+    // the payloads of one image in log order: the stream kernel, no eligibility check
+    rc = device_verify(ctx, img, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, m, st, &nbad, &first, true);
     if (rc < 0) return rc;
   }
   const size_t accepted = nbad ? (size_t)first : m;
@@ -1343,7 +1204,7 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
       HIPCHK(hipMemcpyAsync(ctx->d_woff, ctx->h_woff, m * 8, hipMemcpyHostToDevice, so.st));
       HIPCHK(hipMemcpyAsync(ctx->d_wlen, ctx->h_wlen, m * 4, hipMemcpyHostToDevice, so.st));
       HIPCHK(hipMemcpyAsync(ctx->d_wexp, ctx->h_wexp, m * 4, hipMemcpyHostToDevice, so.st));
-      rc = device_verify(ctx, wal, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, m, so.st, &nb, &first);
+      rc = device_verify(ctx, wal, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, m, so.st, &nb, &first, true);
       if (rc < 0) return rc;
     } else if (overlap) {
       int prc = 0;

@@ -7,10 +7,6 @@
 
 #include "lsmck.h"
 
-// fixed-record ring kernel tile order (crc_order): 3 = one contiguous tile
-// range per wave, CRCs stored as queued 256-byte blocks (A/B: profiles/r02/q)
-#define LSMCK_DEFAULT_ORDER 3
-
 namespace lsmck {
 
 // CRC-32 batch job.  Records are either fixed ([r*stride, r*stride+flen)) or
@@ -22,18 +18,16 @@ struct CrcParams {
   uint64_t stride;            // fixed mode
   uint32_t flen;              // fixed mode
   uint64_t nrec;
-  uint32_t* tile_info;        // descriptor mode scratch: per 64-segment tile {r0, q0, start mask lo, hi}
-  uint64_t* total_segs;       // descriptor mode scratch: total segments (device)
-  uint32_t* out;              // nrec CRCs (zeroed before the launch)
+  uint64_t* total_segs;       // walking kernel scratch: total segments (device)
+  uint32_t* out;              // nrec CRCs
   const uint32_t* kseg;       // x^(8*128*k) mod P, k < 2^16
   const uint32_t* khi;        // x^(8*128*65536*k) mod P, k < 2^16
   const uint32_t* tinit;      // 0xFFFFFFFF (x) x^(8*m) mod P, m = 0..128; [129] = 0
   const uint32_t* master;     // slicing-by-4 tables T0..T3 (4 x 256), then shift tables ST_1..ST_3 (3 x 4 x 256)
   const uint32_t* zero;       // 256 zero bytes (16-aligned): the load window of empty segments
   const uint64_t* sb_prefix;  // walking descriptor kernel: exclusive segment prefix per WALK_SB-record superblock
-  uint32_t* work;             // fixed ring kernel, claimed-block order: work counter (zeroed by the launcher)
-  uint32_t* sflag;            // stream kernel: nonzero = packed batch of >= 64-byte records (the walking kernel then exits)
-  uint64_t* scuts;            // stream kernel: first boundary of each wave's range (waves + 1 entries)
+  uint32_t* sflag;            // stream kernel: nonzero = it takes the batch (the walking kernel then exits)
+  uint64_t* scuts;            // stream kernel: first record of each wave's range (waves + 1 entries)
 };
 
 // SHA-256 batch job (lane per message).
@@ -72,17 +66,15 @@ struct ShaSliceParams {
 
 extern "C" {
 int lsmk_launch_crc32_fixed(const lsmck::CrcParams* P, int ncu, int variant, hipStream_t st);
-uint64_t lsmk_scan_block_count(uint64_t n);
-int lsmk_launch_crc32_scan(const lsmck::CrcParams* P, uint64_t* block_sum, hipStream_t st);
-int lsmk_launch_crc32_desc(const lsmck::CrcParams* P, const uint64_t* block_sum, int ncu, int variant, hipStream_t st);
 int lsmk_launch_sha256(const lsmck::ShaParams* P, hipStream_t st);
 int lsmk_launch_sha256_slices(const lsmck::ShaSliceParams* P, hipStream_t st);
 uint64_t lsmk_walk_sb_count(uint64_t n);
 int lsmk_launch_crc32_walk(const lsmck::CrcParams* P, uint64_t* sb_prefix, int ncu, int variant, hipStream_t st);
-// stream kernel for packed batches of records >= 64 B (eligibility decided on
-// the device: P->sflag, P->scuts hold lsmk_stream_waves(ncu) + 1 entries)
+// stream kernel for sorted, non-overlapping batches (packed or with small gaps;
+// a caller's batch is checked on the device unless `trusted`: P->sflag;
+// P->scuts holds lsmk_stream_waves(ncu) + 1 entries)
 uint32_t lsmk_stream_waves(int ncu);
-int lsmk_launch_crc32_stream(const lsmck::CrcParams* P, int ncu, int variant, int variant2, hipStream_t st);
+int lsmk_launch_crc32_stream(const lsmck::CrcParams* P, int ncu, int variant, int trusted, hipStream_t st);
 uint64_t lsmk_wal_words(uint64_t n);
 uint64_t lsmk_wal_scan_blocks(uint64_t n);
 int lsmk_wal_mark_range(const uint8_t* img, uint64_t n, uint64_t b0, uint64_t b1, uint64_t* bits, uint32_t* pre,

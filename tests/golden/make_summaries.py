@@ -15,11 +15,15 @@ with these values; bench.py prints the GPU's as "summary_crc32".
   config 2: 2^24 x 4096 B, seed 0x5EED0002
   config 3: 2^26 Zipf(1.5) records of 64 B - 64 KiB packed back to back,
             lengths from the seed, bytes from the same seed
+  config 3w: config 3's records framed as wal.rs Insert records: record i's
+            payload starts 13 bytes (its header) after record i-1 ends
+            (off_i = 13 (i+1) + sum of the earlier lengths); bytes from the
+            same seed over the whole image, CRC-32 only (bench.py --wal-framed)
   config 4: 8 per-GPU shards of 2^26 x 4096 B (256 GiB each) of config 2's
             block stream (seed 0x5EED0002): shard r = blocks [r*2^26, (r+1)*2^26),
             CRC-32 only (bench.py --gpus N: rank r checksums shard r)
 
-Run:  python3 tests/golden/make_summaries.py [crc|sha|all|config4]   (updates summaries.json here)
+Run:  python3 tests/golden/make_summaries.py [crc|sha|all|config4|config3w]   (updates summaries.json here)
 """
 import concurrent.futures as cf
 import json
@@ -68,6 +72,13 @@ def summary(seed, offs, lens, sha, byte_off=0):
     return "%08x" % crc
 
 
+def layout_wal(lens, header=13):
+    """payload descriptors of records framed with a `header`-byte header each"""
+    offs = np.full(len(lens), header, dtype=np.uint64)
+    offs[1:] += lens[:-1].astype(np.uint64) + np.uint64(header)
+    return np.cumsum(offs, dtype=np.uint64), lens
+
+
 def layout(cfg):
     if cfg == 1:
         n, L = 1 << 20, 256
@@ -87,6 +98,17 @@ def main():
     res["method"] = ("oracle digest per record (1 GiB chunks), zlib.crc32 of the output array "
                      "(LE u32 CRCs / 32-B SHA-256 digests)")
     t0 = time.time()
+    if what == "config3w":
+        offs, lens = layout_wal(O.gen_zipf_lengths(0x5EED0003, 1 << 26))
+        e = res.setdefault("config3w", {})
+        e.update({"records": len(offs), "payload_bytes": int(lens.astype(np.uint64).sum()),
+                  "image_bytes": int(offs[-1]) + int(lens[-1]), "seed": hex(0x5EED0003), "header_bytes": 13,
+                  "summary_crc32": summary(0x5EED0003, offs, lens, False)})
+        print("config3w", e, round(time.time() - t0, 1), flush=True)
+        with open(OUT, "w") as f:
+            json.dump(res, f, indent=1)
+            f.write("\n")
+        return
     if what == "config4":
         n, L = 1 << 26, 4096
         offs, lens = np.arange(n, dtype=np.uint64) * np.uint64(L), np.full(n, L, dtype=np.uint32)

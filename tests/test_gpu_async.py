@@ -174,16 +174,16 @@ def test_device_descriptor_batch_is_asynchronous(ctx):
         hip.destroy(s)
 
 
-@pytest.mark.parametrize("walk", [0, 1])
-def test_walk_and_tile_map_kernels_agree(ctx, walk):
-    """The walking kernel (default) and the r01 tile-map kernel (crc_walk 0)
-    give the oracle's CRCs on records from empty to several MiB (records
-    spanning many tiles carry their value across tiles), packed, scattered
-    and overlapping."""
+@pytest.mark.parametrize("stream", [0, 1])
+def test_walk_and_stream_kernels_agree(ctx, stream):
+    """The walking kernel alone (crc_stream 0) and the default dispatch (the
+    stream kernel for the sorted staged chunks) give the oracle's CRCs on
+    records from empty to several MiB (records spanning many tiles carry their
+    value across tiles), packed, scattered and overlapping."""
     rng = np.random.default_rng(21)
     total = 64 << 20
     data = O.gen_stream(0x31, 0, total)
-    ctx.set_option("crc_walk", walk)
+    ctx.set_option("crc_stream", stream)
     try:
         for trial in range(4):
             n = int(rng.integers(1, 30000))
@@ -207,31 +207,25 @@ def test_walk_and_tile_map_kernels_agree(ctx, walk):
                 ln = np.minimum(ln, 40000).astype(np.uint32)
                 off = rng.integers(0, total - 40000, n).astype(np.uint64)
             got = ctx.crc32(data, off, ln)
-            assert np.array_equal(got, O.crc32_batch(data, off, ln, threads=8)), (walk, kind)
+            assert np.array_equal(got, O.crc32_batch(data, off, ln, threads=8)), (stream, kind)
     finally:
-        ctx.set_option("crc_walk", 1)
+        ctx.set_option("crc_stream", 1)
 
 
-@pytest.mark.parametrize("order", [0, 1, 2, 3, 4, 5])
-def test_fixed_ring_tile_orders(ctx, order):
-    """The fixed-record ring kernel walks its tiles strided (0), as one
-    contiguous range per wave (1, and 3 with the CRCs stored as queued 256-B
-    blocks) or as claimed 16-tile blocks (2): the same CRCs either way,
-    including a last partial tile and fewer tiles than waves."""
-    ctx.set_option("crc_order", order)
-    try:
-        for length, nb in ((4096, 1 << 16), (4096, 77), (256, 100003), (1024, 5000), (128, 777777), (8192, 9999),
-                           (2048, 1 << 20)):
-            d = ctx.alloc(nb * length)
-            out = ctx.alloc(4 * nb)
-            try:
-                ctx.gen_stream(d.ptr, 0x44 + length, 0, nb * length)
-                ctx.crc32_fixed_device(d.ptr, length, length, nb, out.ptr)
-                ctx.sync()
-                host = O.gen_stream(0x44 + length, 0, nb * length)
-                assert np.array_equal(out.download(np.uint32), O.crc32_fixed(host, length, length, nb, threads=8))
-            finally:
-                d.free()
-                out.free()
-    finally:
-        ctx.set_option("crc_order", 3)
+def test_fixed_ring_contiguous_ranges(ctx):
+    """The fixed-record ring kernel walks one contiguous range of tiles per
+    wave and stores the CRCs as queued 256-B blocks: a last partial tile,
+    fewer tiles than waves, block edges inside a wave's range."""
+    for length, nb in ((4096, 1 << 16), (4096, 77), (256, 100003), (1024, 5000), (128, 777777), (8192, 9999),
+                       (2048, 1 << 20)):
+        d = ctx.alloc(nb * length)
+        out = ctx.alloc(4 * nb)
+        try:
+            ctx.gen_stream(d.ptr, 0x44 + length, 0, nb * length)
+            ctx.crc32_fixed_device(d.ptr, length, length, nb, out.ptr)
+            ctx.sync()
+            host = O.gen_stream(0x44 + length, 0, nb * length)
+            assert np.array_equal(out.download(np.uint32), O.crc32_fixed(host, length, length, nb, threads=8))
+        finally:
+            d.free()
+            out.free()

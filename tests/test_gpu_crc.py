@@ -131,25 +131,17 @@ def test_device_generated_fixed_4k(ctx):
     assert np.array_equal(out.download(np.uint32), O.crc32_fixed(host, 4096, 4096, n, threads=8))
 
 
-@pytest.mark.parametrize("ring,waves", [(0, 0), (1, 0), (2, 0), (3, 0), (2, 12), (3, 12)])
 @pytest.mark.parametrize("length,n", [(4096, (1 << 15) + 37), (256, (1 << 18) + 5), (128, 5000), (8192, 3)])
-def test_fixed_ring_depths(ctx, ring, waves, length, n):
+def test_fixed_ring_tiles(ctx, length, n):
     """Fixed records whose segment count divides 64 run the whole-tile ring
-    kernel ("crc_ring" 2 or 3 slots; 1 = the two-slot kernel): several tiles per
-    wave with a remainder that is not a multiple of the ring's unroll, and
-    batches where most waves have no tile."""
+    kernel: several tiles per wave with a remainder, and batches where most
+    waves have no tile."""
     nbytes = n * length
     d = ctx.alloc(nbytes)
     ctx.gen_stream(d.ptr, 0x5EED0020 + length, 0, nbytes)
     out = ctx.alloc(4 * n)
-    ctx.set_option("crc_ring", ring)
-    ctx.set_option("crc_wg_waves", waves)
-    try:
-        ctx.crc32_fixed_device(d.ptr, length, length, n, out.ptr)
-        ctx.sync()
-    finally:
-        ctx.set_option("crc_ring", 0)
-        ctx.set_option("crc_wg_waves", 0)
+    ctx.crc32_fixed_device(d.ptr, length, length, n, out.ptr)
+    ctx.sync()
     host = O.gen_stream(0x5EED0020 + length, 0, nbytes)
     assert np.array_equal(out.download(np.uint32), O.crc32_fixed(host, length, length, n, threads=8))
     d.free()
@@ -165,8 +157,9 @@ def _summaries():
 
 def test_config2_full_size_properties(ctx):
     """BASELINE config 2 at full size (2^24 x 4 KiB = 64 GiB, device-resident):
-    (1) the fixed-record kernel and the descriptor kernel (different code
-        paths: implicit offsets vs scan + tile map) agree on every record;
+    (1) the fixed-record kernel and the descriptor path (different code
+        paths: implicit offsets vs the stream kernel over off/len) agree on
+        every record;
     (2) a sample of 4096 records spread over the whole buffer matches the oracle."""
     n = 1 << 24
     nbytes = n * 4096
@@ -194,39 +187,41 @@ def test_config2_full_size_properties(ctx):
         buf.free()
 
 
-@pytest.mark.parametrize("chains,generic,loads,ring", [(1, 0, 0, 1), (2, 0, 0, 1), (4, 0, 0, 1), (2, 1, 0, 1),
-                                                       (2, 0, 1, 1), (2, 0, 2, 1), (1, 0, 2, 1), (4, 1, 2, 1),
-                                                       (2, 0, 2, 2), (2, 0, 2, 3), (2, 0, 0, 0)])
-def test_kernel_variants_agree(ctx, chains, generic, loads, ring):
-    """Every kernel variant (lsmck_ctx_set_option "crc_chains", "crc_generic_mul",
-    "crc_loads", "crc_ring") is bit-exact."""
-    rng = np.random.default_rng(100 + chains)
+def test_fixed_kernel_paths_agree(ctx):
+    """Every fixed-record path is bit-exact: the ring kernel (dword-aligned,
+    segment count dividing 64), the two-slot kernel with per-lane columns
+    (a stride too wide for one buffer window), whole segments whose count does
+    not divide 64 (records straddle tiles), and unaligned records."""
+    rng = np.random.default_rng(100)
     n = 6000
     ln = rng.integers(0, 9000, n).astype(np.uint32)
     ln[:5] = [0, 1, 3, 128, 129]
     off, total = _packed(ln, gap_rng=rng, align_shift=2)
-    data = O.gen_stream(40 + chains, 0, total + 8)
-    ctx.set_option("crc_chains", chains)
-    ctx.set_option("crc_generic_mul", generic)
-    ctx.set_option("crc_loads", loads)
-    ctx.set_option("crc_ring", ring)
-    try:
-        got = ctx.crc32(data, off, ln)
-        fixed = ctx.crc32_fixed(data, 4096, 4096, total // 4096)
-        small = ctx.crc32_fixed(data, 256, 256, total // 256)
-        odd = ctx.crc32_fixed(data[1:], 300, 297, (total - 8) // 300)
-        # dword-aligned, whole segments, 3 per record: records straddle tiles
-        three = ctx.crc32_fixed(data[4:], 388, 384, (total - 8) // 388)
-    finally:
-        ctx.set_option("crc_chains", 0)
-        ctx.set_option("crc_generic_mul", 0)
-        ctx.set_option("crc_loads", 0)
-        ctx.set_option("crc_ring", 0)
+    data = O.gen_stream(42, 0, total + 8)
+    got = ctx.crc32(data, off, ln)
+    fixed = ctx.crc32_fixed(data, 4096, 4096, total // 4096)
+    small = ctx.crc32_fixed(data, 256, 256, total // 256)
+    odd = ctx.crc32_fixed(data[1:], 300, 297, (total - 8) // 300)
+    three = ctx.crc32_fixed(data[4:], 388, 384, (total - 8) // 388)
     assert np.array_equal(three, O.crc32_fixed(data[4:], 388, 384, (total - 8) // 388, threads=8))
     assert np.array_equal(small, O.crc32_fixed(data, 256, 256, total // 256, threads=8))
     assert np.array_equal(got, O.crc32_batch(data, off, ln, threads=8))
     assert np.array_equal(fixed, O.crc32_fixed(data, 4096, 4096, total // 4096, threads=8))
     assert np.array_equal(odd, O.crc32_fixed(data[1:], 300, 297, (total - 8) // 300, threads=8))
+    # device records a stride beyond one buffer window apart (2^31 / 65): the
+    # two-slot kernel with per-lane columns (host batches would be gathered)
+    stride, nb = 40 << 20, 4
+    d = ctx.alloc(stride * (nb - 1) + 4096)
+    out = ctx.alloc(4 * nb)
+    try:
+        ctx.gen_stream(d.ptr, 43, 0, stride * (nb - 1) + 4096)
+        ctx.crc32_fixed_device(d.ptr, stride, 4096, nb, out.ptr)
+        ctx.sync()
+        host = O.gen_stream(43, 0, stride * (nb - 1) + 4096)
+        assert np.array_equal(out.download(np.uint32), O.crc32_fixed(host, stride, 4096, nb))
+    finally:
+        d.free()
+        out.free()
 
 
 def _device_crc(ctx, data, off, ln):
@@ -314,6 +309,40 @@ def test_config3_full_size_summary(ctx):
     assert "%08x" % zlib.crc32(got.astype("<u4").tobytes()) == _summaries()["config3"]["summary_crc32"]
     for buf in (d, d_o, d_l, out):
         buf.free()
+
+
+def test_config3w_full_size_summary(ctx):
+    """Config 3's 2^26 records framed as wal.rs Insert records (a 13-byte header
+    before every payload, ~98 GiB image, device-resident) through the caller
+    entry point: the stream kernel takes the gapped batch, and the CRC-32 of
+    the whole output array equals the oracle's (make_summaries.py config3w)."""
+    import zlib
+    from lsm_storage_engine_amd.device import gen_zipf_lengths
+    g = _summaries()["config3w"]
+    n = 1 << 26
+    ln = gen_zipf_lengths(0x5EED0003, n)
+    off = np.full(n, 13, dtype=np.uint64)
+    off[1:] += ln[:-1].astype(np.uint64) + np.uint64(13)
+    off = np.cumsum(off, dtype=np.uint64)
+    total = int(off[-1]) + int(ln[-1])
+    assert total == g["image_bytes"]
+    d = ctx.alloc(total + 64)
+    d_o, d_l, out = ctx.alloc(off.nbytes), ctx.alloc(ln.nbytes), ctx.alloc(4 * n)
+    try:
+        ctx.gen_stream(d.ptr, 0x5EED0003, 0, total)
+        d_o.upload(off)
+        d_l.upload(ln)
+        ctx.set_option("crc_stream", 2)  # the stream kernel alone: a declined batch would leave outputs unwritten
+        try:
+            ctx.crc32_device(d.ptr, d_o.ptr, d_l.ptr, n, out.ptr)
+            ctx.sync()
+        finally:
+            ctx.set_option("crc_stream", 1)
+        got = out.download(np.uint32)
+        assert "%08x" % zlib.crc32(got.astype("<u4").tobytes()) == g["summary_crc32"]
+    finally:
+        for buf in (d, d_o, d_l, out):
+            buf.free()
 
 
 def test_multicontext_host_batches():

@@ -1,9 +1,12 @@
-"""The stream kernel (crc32_stream_kernel, lsmck_crc32.hip): packed batches of
-records of at least 64 bytes checksummed from aligned 128-byte chunks of the
-byte stream, record boundaries as CRC register resets.  Every case is checked
-against the oracle (crc 1.x's algorithm, oracle/lsmck_oracle.c) and against the
-walking kernel on the same records (crc_stream 0).  tools/stream_sim.py is the
-CPU model of the same algebra."""
+"""The stream kernel (crc32_stream_kernel, lsmck_crc32.hip): sorted batches of
+records -- packed back to back, or with gaps between them like the payloads of
+a WAL image (wal.rs:165-196: a 13- or 9-byte header before each payload) --
+checksummed from aligned 128-byte chunks of the byte stream, record starts as
+CRC register resets and record ends as captures; records under 64 bytes by
+their window lane.  Every case is checked against the oracle (crc 1.x's
+algorithm, oracle/lsmck_oracle.c) and against the walking kernel on the same
+records (crc_stream 0).  tools/stream_sim.py is the CPU model of the same
+algebra."""
 import zlib
 
 import numpy as np
@@ -20,6 +23,13 @@ def _packed(lens, lead):
     if len(lens) > 1:
         np.cumsum(lens[:-1].astype(np.uint64), out=off[1:])
     return off + np.uint64(lead), lens
+
+
+def _gapped(lens, gaps, lead):
+    """record i starts gaps[i] bytes after record i-1 ends (record 0: lead + gaps[0])"""
+    lens = np.asarray(lens, dtype=np.uint32)
+    step = np.asarray(gaps, dtype=np.uint64) + np.concatenate([[0], lens[:-1]]).astype(np.uint64)
+    return np.cumsum(step) + np.uint64(lead), lens
 
 
 def _device(ctx, data, off, ln, shift=0, exact=False):
@@ -62,7 +72,7 @@ def stream_ab(ctx):
 
 @pytest.mark.parametrize("dist,shift", [("min", 0), ("min", 3), ("short", 1), ("mixed", 0), ("mixed", 2),
                                         ("long", 0), ("zipf", 3)])
-def test_packed_vs_oracle(ctx, stream_ab, sel, dist, shift):
+def test_packed_vs_oracle(ctx, stream_ab, dist, shift):
     rng = np.random.default_rng(zlib.crc32(f"{dist}{shift}".encode()))
     n = 40000 if dist != "long" else 1500
     if dist == "min":  # 64-byte records: two boundaries in half the chunks
@@ -85,26 +95,9 @@ def test_packed_vs_oracle(ctx, stream_ab, sel, dist, shift):
     assert np.array_equal(b, want)
 
 
-@pytest.fixture(params=[(0, 0, 0, 0), (1, 0, 0, 0), (2, 0, 0, 0), (1, 1, 0, 0), (1, 1, 1, 0), (1, 1, 1, 1)],
-                ids=["branch_steps", "select_steps", "branch_free", "dpp_map", "default", "spread_finish"])
-def sel(ctx, request):
-    """The stream kernel's boundary words: steps inside the branch (0), the
-    branch selecting the step inputs (1, the default), or no branch (2); with
-    and without the short path for tiles without a boundary (default: with)."""
-    ctx.set_option("crc_stream_sel", request.param[0])
-    ctx.set_option("crc_stream_z0", request.param[1])
-    ctx.set_option("crc_stream_lm", request.param[2])
-    ctx.set_option("crc_stream_fsp", request.param[3])
-    yield request.param
-    ctx.set_option("crc_stream_sel", 1)
-    ctx.set_option("crc_stream_z0", 1)
-    ctx.set_option("crc_stream_lm", 1)
-    ctx.set_option("crc_stream_fsp", 0)
-
-
 @pytest.mark.parametrize("lens,lead", [([64], 0), ([64], 77), ([1 << 20], 5), ([128] * 700, 0), ([128] * 700, 64),
                                        ([192, 64] * 500, 0), ([64] * 129 + [8192] * 3, 0), ([100] * 3, 127)])
-def test_boundary_positions(ctx, stream_ab, sel, lens, lead):
+def test_boundary_positions(ctx, stream_ab, lens, lead):
     """One record; records on the 128-byte grid (every boundary at chunk byte
     0, or at byte 64: a chain start); 64-byte records over a whole tile."""
     off, ln = _packed(lens, lead)
@@ -125,22 +118,90 @@ def test_allocation_ends_with_last_record(ctx):
         assert np.array_equal(got, O.crc32_batch(data, off, ln)), end_pad
 
 
-@pytest.mark.parametrize("case", ["short_record", "gap", "overlap", "unsorted"])
+@pytest.mark.parametrize("kind", ["wal", "gaps", "short_mixed", "empties", "tiny"])
+def test_gapped_batches_vs_oracle(ctx, stream_ab, kind):
+    """Records with gaps between them: WAL payloads (13- or 9-byte headers in
+    between), gaps of 0..64 bytes, records under 64 bytes among long ones
+    (checksummed by their window lane), empty records at their predecessor's
+    end, and tiles of hundreds of tiny records (several windows per tile).
+    The stream kernel alone takes every one of these batches."""
+    rng = np.random.default_rng(zlib.crc32(kind.encode()))
+    n = 30000
+    if kind == "wal":
+        lens = rng.choice([5, 17, 40, 63, 64, 65, 100, 128, 300, 1000, 5000, 9000], n)
+        gaps = rng.choice([13, 9], n)
+    elif kind == "gaps":
+        lens = rng.choice([64, 65, 67, 100, 127, 128, 129, 191, 192, 255, 1000, 4096, 9000], n)
+        gaps = rng.integers(0, 65, n)
+    elif kind == "short_mixed":
+        lens = np.where(rng.random(n) < 0.5, rng.integers(1, 64, n), rng.integers(64, 3000, n))
+        gaps = rng.integers(0, 20, n)
+    elif kind == "empties":
+        lens = rng.choice([0, 0, 1, 3, 63, 64, 200, 4000], n)
+        gaps = np.where(lens == 0, 0, rng.integers(0, 14, n))
+        lens[0] = 77
+    else:  # tiny: ~250 records per 8 KiB tile
+        lens = rng.integers(1, 40, n * 4)
+        gaps = rng.choice([13, 9, 0], n * 4)
+    off, ln = _gapped(lens, gaps, int(rng.integers(0, 300)))
+    data = O.gen_stream(0x57AE0600 + len(kind), 0, int(off[-1]) + int(ln[-1]) + 16)
+    want = O.crc32_batch(data, off, ln, threads=8)
+    a, b = stream_ab(data, off, ln, shift=int(rng.integers(0, 4)))
+    assert np.array_equal(a, want)
+    assert np.array_equal(b, want)
+
+
+def test_short_records_at_page_and_allocation_edges(ctx, stream_ab):
+    """Records of 1..63 bytes starting 0..15 bytes after 4 KiB boundaries of a
+    page-aligned device buffer (long records with small gaps in between), and
+    batches whose last record is short and ends the allocation: the window lane
+    loads only the dwords that hold record bytes."""
+    off, ln = [], []
+    end = 0
+    for page in range(1, 60):
+        s = page * 4096 + page % 16          # the short record's start
+        off.append(end + 5)                  # a long record up to 3 bytes before it
+        ln.append(s - 3 - (end + 5))
+        off.append(s)
+        ln.append(1 + page % 63)
+        end = s + ln[-1]
+    off, ln = np.asarray(off, dtype=np.uint64), np.asarray(ln, dtype=np.uint32)
+    data = O.gen_stream(0x57AE0700, 0, int(off[-1]) + int(ln[-1]) + 16)
+    want = O.crc32_batch(data, off, ln)
+    a, b = stream_ab(data, off, ln)
+    assert np.array_equal(a, want) and np.array_equal(b, want)
+    for end_pad in range(0, 8):
+        off2, ln2 = _gapped([200, 63 - end_pad, 5 + end_pad], [0, 13, 9], 3)
+        data2 = O.gen_stream(0x57AE0800 + end_pad, 0, int(off2[-1]) + int(ln2[-1]))
+        ctx.set_option("crc_stream", 2)
+        try:
+            got = _device(ctx, data2, off2, ln2, exact=True)
+        finally:
+            ctx.set_option("crc_stream", 1)
+        assert np.array_equal(got, O.crc32_batch(data2, off2, ln2)), end_pad
+
+
+@pytest.mark.parametrize("case", ["overlap", "unsorted", "gap65", "empty_with_gap", "empty_first"])
 def test_ineligible_batches_take_the_walking_kernel(ctx, case):
-    """Not a packed batch of >= 64-byte records: the stream kernel declines
-    (decided on the device) and the walking kernel's results are exact."""
+    """A caller's batch the stream kernel cannot read safely or in order --
+    overlapping or unsorted records, a gap over 64 bytes, an empty record away
+    from its predecessor's end, an empty first record: it declines (decided on
+    the device) and the walking kernel's results are exact."""
     rng = np.random.default_rng(5)
     lens = rng.integers(64, 3000, 5000)
     off, ln = _packed(lens, 0)
-    if case == "short_record":
-        ln[2500] = 63
-    elif case == "gap":
-        off[2500:] += np.uint64(1)
-    elif case == "overlap":
+    if case == "overlap":
         off[2500] -= np.uint64(1)
-    else:
+    elif case == "unsorted":
         off[[10, 20]] = off[[20, 10]]
         ln[[10, 20]] = ln[[20, 10]]
+    elif case == "gap65":
+        off[2500:] += np.uint64(65)
+    elif case == "empty_with_gap":
+        off[2500:] += np.uint64(3)
+        ln[2500] = 0
+    else:
+        ln[0] = 0
     data = O.gen_stream(0x57AE0300, 0, int(off.max()) + 4000)
     got = _device(ctx, data, off, ln)
     assert np.array_equal(got, O.crc32_batch(data, off, ln, threads=8))
@@ -158,34 +219,3 @@ def test_host_batches_use_it_too(ctx):
     off, ln = _packed(rng.integers(64, 5000, 60000), 11)
     data = O.gen_stream(0x57AE0400, 0, int(off[-1]) + int(ln[-1]) + 8)
     assert np.array_equal(ctx.crc32(data, off, ln), O.crc32_batch(data, off, ln, threads=8))
-
-
-@pytest.mark.parametrize("waves,ring,batch,qstore,window", [(12, 0, 0, 1, 2), (12, 3, 0, 1, 2), (0, 0, 1, 1, 2),
-                                                           (12, 0, 1, 1, 2), (0, 0, 0, 0, 2), (0, 0, 0, 1, 1),
-                                                           (0, 0, 0, 1, 0), (0, 0, 0, 2, 2), (0, 0, 0, 1, 2)])
-def test_workgroup_and_slot_variants(ctx, waves, ring, batch, qstore, window):
-    """The 12-wave workgroup form (168 VGPRs) with two and three payload slots
-    in flight, the records finished in batches of 64, per-tile stores instead
-    of queued 256-B blocks, and the reloaded boundary windows: same CRCs as the
-    oracle."""
-    rng = np.random.default_rng(8)
-    lens = rng.choice([64, 65, 100, 127, 128, 129, 300, 1000, 4096, 20000], 50000)
-    off, ln = _packed(lens, 13)
-    data = O.gen_stream(0x57AE0500, 0, int(off[-1]) + int(ln[-1]) + 8)
-    want = O.crc32_batch(data, off, ln, threads=8)
-    ctx.set_option("crc_wg_waves", waves)
-    ctx.set_option("crc_ring", ring)
-    ctx.set_option("crc_stream_batch", batch)
-    ctx.set_option("crc_stream_qstore", qstore)
-    ctx.set_option("crc_stream_window", window)
-    ctx.set_option("crc_stream", 2)
-    try:
-        got = _device(ctx, data, off, ln)
-    finally:
-        ctx.set_option("crc_wg_waves", 0)
-        ctx.set_option("crc_ring", 0)
-        ctx.set_option("crc_stream_batch", 0)
-        ctx.set_option("crc_stream_qstore", 2)
-        ctx.set_option("crc_stream_window", 2)
-        ctx.set_option("crc_stream", 1)
-    assert np.array_equal(got, want)

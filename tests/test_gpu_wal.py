@@ -183,6 +183,31 @@ def test_walk_candidate_flood_falls_back_to_the_host_walk(ctx):
         d.free()
 
 
+@pytest.mark.parametrize("device", [False, True])
+def test_framed_small_records_log(ctx, device):
+    """A log of many small records -- keys and values of 0..40 bytes, empty
+    Inserts and Removes among them, ~300 records per 8 KiB tile: the payload
+    CRCs run on the stream kernel (several windows per tile, the short records
+    checksummed by their window lane, the headers between payloads dropped),
+    host image (uploaded) and device image alike."""
+    rng = np.random.default_rng(33)
+    parts = []
+    for i in range(120000):
+        r = int(rng.integers(0, 10))
+        if r == 0:
+            parts.append(O.wal_remove(b"k%d" % i if i % 3 else b""))
+        else:
+            parts.append(O.wal_insert(b"k%d" % i if r > 1 else b"", rng.bytes(int(rng.integers(0, 41)))))
+    img = b"".join(parts)
+    same(ctx, img, device=device)
+    # a corrupted payload in the middle is found (first bad record in log order)
+    st, recs, _ = O.wal_replay(img)
+    r = next(r for r in recs[60000:] if r.type == 1 and r.klen + r.vlen > 0)
+    b = bytearray(img)
+    b[r.payload_off] ^= 0x40
+    same(ctx, bytes(b), device=device)
+
+
 def test_gpu_header_walk_big_binary_log(ctx):
     """A log whose payloads are random bytes (so many bytes inside payloads look
     like command types: bogus candidate starts for the GPU walk), device-resident:

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 evidence in one GPU call.  Steps are picked by STEPS (space list):
-#   c4pmc smoke pytest bench c2 kt c3pmc sha (run in this order)
+#   c4pmc smoke quick pytest bench c3w c2 kt c3pmc sha (run in this order)
 # Every GPU step has its own time limit; any failure ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -20,6 +20,10 @@ fi
 if has smoke; then
   timeout -k 10 240 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$R.log 2>&1; step smoke $?
 fi
+if has quick; then  # the stream kernel's own tests first (a fast signal)
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_stream.py tests/test_gpu_wal.py -m gpu -q -rf -x --timeout 300 --timeout-method thread > gpurun_out/pytest_quick_$R.log 2>&1; rc=$?
+  tail -15 gpurun_out/pytest_quick_$R.log; step quick $rc
+fi
 if has pytest; then
   timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -rf -x --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu_$R.log 2>&1; rc=$?
   tail -3 gpurun_out/pytest_gpu_$R.log; step pytest $rc
@@ -27,6 +31,10 @@ fi
 if has bench; then  # the driver's default line: config 3
   timeout -k 10 400 python3 bench.py > gpurun_out/bench_${R}_c3.log 2>&1; step bench_c3 $?
   tail -1 gpurun_out/bench_${R}_c3.log
+fi
+if has c3w; then  # config 3 framed as a WAL image (13-byte headers between the payloads)
+  timeout -k 10 400 python3 bench.py --wal-framed > gpurun_out/bench_${R}_c3w.log 2>&1; step bench_c3w $?
+  tail -1 gpurun_out/bench_${R}_c3w.log
 fi
 if has c2; then
   timeout -k 10 400 python3 bench.py --config 2 > gpurun_out/bench_${R}_c2.log 2>&1; step bench_c2 $?
