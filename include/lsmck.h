@@ -149,34 +149,14 @@ const char* lsmck_last_error(void);
 int lsmck_device_count(void);
 
 /* Tuning knobs of a context (no effect on results, only on speed):
- *   "crc_chains"  independent CRC register chains per lane in the CRC kernels:
- *                 1, 2 or 4 (0 = built-in default).  Used by bench.py --variants
- *                 to A/B kernel variants in one process.
- *   "crc_generic_mul"  1 = fixed records use the generic GF(2) multiply instead of
- *                 per-lane precomputed columns (A/B switch); 0 = default.
- *   "crc_ablate"  DIAGNOSTIC ONLY, results are invalid while set: 1 = the fixed
- *                 kernel loads but does not checksum, 2 = checksums without
- *                 loading, 3 = payload loads only (no table gathers, no
- *                 reduction or store); 4..6 (descriptor kernel, valid only
- *                 for 4 KiB records at 4 KiB stride): 3 with tile_info
- *                 synthesized, + off/len synthesized, + aligned loads;
- *                 7 = 3 without the D_32 load; descriptor kernel, no payload
- *                 loads and 2 chains: 11 = all compute, 8 = without the
- *                 segment-factor multiply, 9 = without the first-segment
- *                 masks, 10 = without the alignbyte funnel; 12 = loads only
- *                 with the real descriptor map but the aligned (FAST) payload
- *                 loads (4 KiB records at 4 KiB stride only); packed
- *                 batches only (record r+1 starts where r ends): 13 = loads
- *                 only in a raw-buffer-load form of the general window,
- *                 14 = the full kernel with that load form;
- *                 0 = off.  Locates the kernels' ceilings.
- *   "crc_wg_waves"  waves per workgroup of the descriptor CRC kernel and of
- *                 the whole-tile ring kernel: 12 or 16 (0 = built-in default).
- *                 A/B switch: 12 waves leave 168 VGPRs per lane for the load
- *                 pipeline, 16 leave 128.
- *   "crc_loads"   payload load instruction of the fixed-record CRC kernel:
- *                 1 = global_load, 2 = raw buffer_load from a per-tile base
- *                 (0 = built-in default).  A/B switch.
+ *   "crc_stream"  descriptor CRC batches: 1 = the stream kernel for sorted
+ *                 batches (default), 0 = the walking kernel only (A/B),
+ *                 2 = the stream kernel only (DIAGNOSTIC: a caller batch it
+ *                 declines gets no CRCs).
+ *   "crc_ablate"  DIAGNOSTIC ONLY, results are invalid while set: 3 = payload
+ *                 loads only (ring, stream and walking kernels: the bench's
+ *                 loads-only ceiling), 2 = the stream kernel without payload
+ *                 loads; 0 = off.
  *   "sha_order"   variable-length SHA-256 batches of >= 2048 messages run in
  *                 decreasing length order (1, default) or batch order (0).
  *                 A/B switch; digests are identical either way.
@@ -205,27 +185,6 @@ int lsmck_device_count(void);
  *   "tree_open_files"  files kept open from their first slice to their last
  *                 (-1 = default: as many as RLIMIT_NOFILE leaves after a
  *                 1024-descriptor reserve; the rest reopen per slice).
- *   "crc_ring"    fixed records whose segment count divides 64 (4 KiB, 256 B ...):
- *                 1 = two-slot kernel, 2 or 3 = whole-tile ring kernel with that
- *                 many load slots (0 = built-in default).  A/B switch.
- *   "crc_order"   ring kernel tile order: 3 = one contiguous tile range per
- *                 wave, CRCs stored as 256-byte blocks (default); 0 strided,
- *                 1 contiguous, 2 claimed blocks, 4 strided with the CRCs
- *                 gathered in LDS, 5 strided with deferred stores.  A/B switch.
- *   "crc_stream_window"  stream kernel boundary window: 2 sliding (default),
- *                 1 reloaded with the second half on demand, 0 reloaded.
- *   "crc_stream_qstore"  stream kernel CRC stores: 2 queued 256-byte blocks
- *                 pushed at the next tile (default), 1 pushed at once, 0 per tile.
- *   "crc_stream_sel"  stream kernel boundary words: 1 = the branch selects the
- *                 step inputs (default), 0 = steps inside the branch, 2 = no
- *                 branch.
- *   "crc_stream_z0"  stream kernel short path for tiles in which no record
- *                 ends: 1 (default) or 0.
- *   "crc_stream_lm"  stream kernel chunk boundaries through LDS bytes (1,
- *                 default) or DPP reductions (0).
- *   "crc_stream_fsp"  stream kernel finish multiplies spread over 8 lanes per
- *                 record (1) or one per record lane (0, default).  A/B
- *                 switches; results are identical in every form.
  * Returns 0, or LSMCK_EINVAL for an unknown key / value. */
 int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
 
@@ -235,7 +194,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
 
 /* CRC-32 of n records: record i = base[off[i] .. off[i]+len[i]).  The batch
  * form of checksum_ieee for WAL replay / bulk append (src/wal.rs:135,153,177).
- * stream: hipStream_t (NULL = the context's default stream). */
+ * Any offsets, lengths and order.  A device batch whose records are sorted,
+ * do not overlap, lie at most 64 bytes apart (a WAL's 13- / 9-byte headers)
+ * and whose empty records sit at their predecessor's end runs on the stream
+ * kernel (decided on the device, nothing read back); any other batch on the
+ * walking kernel.  Host batches are staged in order and always take the
+ * stream kernel.  stream: hipStream_t (NULL = the context's default stream). */
 int lsmck_crc32_batch(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len, size_t n,
                       uint32_t* out, unsigned flags, void* stream);
 

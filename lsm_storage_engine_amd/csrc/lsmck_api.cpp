@@ -938,6 +938,19 @@ static int wal_bitmap_ensure(lsmck_ctx* ctx, size_t n) {
   return 0;
 }
 
+// LSMCK_WAL_TRACE=1: the replay's phases on stderr (seconds since the call began)
+struct WalTrace {
+  bool on = getenv("LSMCK_WAL_TRACE") != nullptr;
+  timespec t0{};
+  WalTrace() { clock_gettime(CLOCK_MONOTONIC, &t0); }
+  void mark(const char* what) const {
+    if (!on) return;
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    fprintf(stderr, "wal_trace %-24s %.6f\n", what, (double)(t.tv_sec - t0.tv_sec) + 1e-9 * (double)(t.tv_nsec - t0.tv_nsec));
+  }
+};
+
 // marked: the candidate bitmap of img is already in ctx->wd (wal_upload marks
 // each chunk behind its copy)
 static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck_wal_rec* recs, size_t cap,
@@ -947,6 +960,7 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
   if (n >= (1ull << 32)) return kWalHostWalk;
   std::lock_guard<std::mutex> lk(ctx->mu);
   DevGuard g(ctx->dev);
+  const WalTrace tr;
   auto& W = ctx->wd;
   int rc;
   if ((rc = wal_bitmap_ensure(ctx, n))) return rc;
@@ -961,6 +975,7 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
   if (rc) return launch_rc(rc, "wal mark/scan kernels");
   HIPCHK(hipMemcpyAsync(W.h_info + 3, d_total, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  tr.mark("mark+scan (sync)");
   const uint64_t nc64 = W.h_info[3] & 0xFFFFFFFFull;
   // The jump tables grow with the CANDIDATE count -- every 0x01/0x02 byte
   // that could start a header -- not with the record count: a valid log whose
@@ -989,6 +1004,7 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
   if (rc) return launch_rc(rc, "wal chain kernels");
   HIPCHK(hipMemcpyAsync(W.h_info, W.info, 24, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  tr.mark("chain (sync)");
   const size_t m = (size_t)W.h_info[0];
   const uint32_t term = (uint32_t)W.h_info[1];
   const uint64_t badq = W.h_info[2];
@@ -1004,9 +1020,11 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
     rc = device_verify(ctx, img, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, m, st, &nbad, &first, true);
     if (rc < 0) return rc;
   }
+  tr.mark("emit+crc+compare (sync)");
   const size_t accepted = nbad ? (size_t)first : m;
   if (recs && accepted) HIPCHK(hipMemcpy(recs, W.recs, std::min(accepted, cap) * sizeof(lsmck_wal_rec),
                                          hipMemcpyDeviceToHost));
+  tr.mark("records to host");
   if (nrec) *nrec = accepted;
   if (nbad) {
     lsmck_wal_rec r;
@@ -1034,6 +1052,7 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
 static int wal_upload(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned) {
   std::lock_guard<std::mutex> lk(ctx->mu);
   DevGuard g(ctx->dev);
+  const WalTrace tr;
   int rc;
   if ((rc = ensure_dev(&ctx->d_wimg, &ctx->cap_wimg, n + 16)) || (rc = wal_bitmap_ensure(ctx, n))) return rc;
   // the candidate bitmap of each chunk is marked right behind its copy (the
@@ -1067,6 +1086,7 @@ static int wal_upload(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned)
     if (rc) return launch_rc(rc, "wal mark kernel");
   }
   for (auto& S : ctx->stage) HIPCHK(hipStreamSynchronize(S.s));
+  tr.mark("upload (pageable)");
   guard.ok = true;
   return 0;
 }

@@ -728,21 +728,24 @@ __global__ __launch_bounds__(1024) void scan_phase2(uint64_t* __restrict__ block
 #define WALK_SB 256u
 #define LDS_WCOLS_OFF LDS_COLS_OFF  // [8 groups][65 d][4 u32] columns of x^(8*128*d), d = 0..64 (8320 B)
 
+// a wave per superblock, grid-strided over a grid of a few waves per CU (a
+// batch the stream kernel took costs one small launch that exits at once)
 __global__ __launch_bounds__(1024) void walk_phase1(const uint32_t* __restrict__ len, uint64_t n,
                                                      uint64_t* __restrict__ sb_sum, const uint32_t* skip) {
   if (skip && *skip) return;  // the stream kernel took the batch
   const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t sb = (uint64_t)blockIdx.x * 16u + (threadIdx.x >> 6);
-  if (sb * WALK_SB >= n) return;  // wave-uniform
-  const uint64_t r0 = sb * WALK_SB + lane * 4u;
-  uint32_t l[4];
-  load_len4(len, n, r0, l);
-  uint64_t x = 0;
+  const uint64_t nsb = (n + WALK_SB - 1u) / WALK_SB;
+  for (uint64_t sb = (uint64_t)blockIdx.x * 16u + (threadIdx.x >> 6); sb < nsb; sb += (uint64_t)gridDim.x * 16u) {
+    const uint64_t r0 = sb * WALK_SB + lane * 4u;
+    uint32_t l[4];
+    load_len4(len, n, r0, l);
+    uint64_t x = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) x += (r0 + j < n) ? rec_nseg(l[j]) : 0u;
+    for (int j = 0; j < 4; ++j) x += (r0 + j < n) ? rec_nseg(l[j]) : 0u;
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-  if (lane == 0) sb_sum[sb] = x;
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+    if (lane == 0) sb_sum[sb] = x;
+  }
 }
 
 // columns K*x^i (i = 0..31) of K = x^(8*128*d), d = 0..64, for the Horner shifts
@@ -1005,7 +1008,7 @@ __global__ __launch_bounds__(1024) void crc32_walk_kernel(CrcParams P) {
 // starts at its first record's start (the bytes in front are dropped).
 // Eligibility: every batch the library builds itself (host-staged chunks, WAL
 // replay) is sorted by construction and its gaps lie inside one buffer; a
-// caller's device batch is checked on the device first (stream_check) and
+// caller's device batch is checked on the device first (stream_prep) and
 // the walking kernel, launched after this one, takes it when it is not.
 #define STREAM_LONG 64u      // records of at least this many bytes go through the chains
 #define STREAM_MAX_GAP 64u   // caller batches: at most this many bytes between two records
@@ -1056,21 +1059,49 @@ __device__ __forceinline__ uint32_t stream_xinv(uint32_t t) {  // x^(-8(4-t))
 // empty and every later empty record sits at its predecessor's end.  Then every
 // 4 KiB page a 128-byte chunk of [off[0], end) lies on holds a byte of some
 // record, so the chunk loads touch only the caller's pages.
-__global__ __launch_bounds__(1024) void stream_check(const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
-                                                     uint64_t n, uint32_t* __restrict__ flag) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// A caller's batch: the eligibility check and the wave cuts in ONE pass over
+// the descriptors (4 records per thread).  Cut w (0 < w < W) = the first
+// record starting at or after target(w) = off[0] + span*w/W: the record i with
+// off[i-1] < target(w) <= off[i] writes it.  Cuts of a batch that fails the
+// check are never used (the kernel exits on the flag).
+__global__ __launch_bounds__(256) void stream_prep(CrcParams P, uint32_t W) {
+  const uint64_t n = P.nrec;
+  const uint64_t i0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
+  const uint64_t o0 = P.off[0], span = P.off[n - 1] + P.len[n - 1] - o0;
+  if (i0 == 0) {
+    P.scuts[0] = 0;
+    P.scuts[W] = n;
+    for (uint64_t w = 1; w < W && span * w / W == 0u; ++w) P.scuts[w] = 0;  // targets at off[0]
+  }
   bool bad = false;
-  if (i < n) {
-    const uint64_t o = off[i];
-    const uint32_t l = len[i];
-    bad = i == 0 && l == 0u;
-    if (i + 1 < n) {
-      const uint64_t o1 = off[i + 1], e = o + l;
-      const uint32_t l1 = len[i + 1];
-      bad = bad || o1 < e || o1 - e > STREAM_MAX_GAP || (l1 == 0u && o1 != e);
+  if (i0 < n) {
+    uint64_t o[5];
+    uint32_t l[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const uint64_t i = i0 + j < n ? i0 + j : n - 1;
+      o[j] = P.off[i];
+      l[j] = P.len[i];
+    }
+    bad = i0 == 0 && l[0] == 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (i0 + j + 1 >= n) {  // the last record: the targets past its start cut at n
+        if (i0 + j + 1 == n)
+          for (uint64_t w = span ? ((o[j] - o0 + 1u) * W + span - 1u) / span : W; w < W; ++w) P.scuts[w] = n;
+        break;
+      }
+      const uint64_t e = o[j] + l[j];
+      const bool b = o[j + 1] < e || o[j + 1] - e > STREAM_MAX_GAP || (l[j + 1] == 0u && o[j + 1] != e);
+      bad = bad || b;
+      if (b || o[j + 1] == o[j]) continue;
+      // the targets in (o[j], o[j+1]]: from the first w with target(w) > o[j]
+      const uint64_t d = o[j] - o0;
+      for (uint64_t w = span ? ((d + 1u) * W + span - 1u) / span : W; w < W && o0 + span * w / W <= o[j + 1]; ++w)
+        P.scuts[w] = i0 + j + 1;
     }
   }
-  if (__any(bad) && (threadIdx.x & 63u) == 0u) *flag = 0u;  // plain stores of one value: no atomic needed
+  if (__any(bad) && (threadIdx.x & 63u) == 0u) *P.sflag = 0u;  // plain stores of one value: no atomic needed
 }
 
 // cut w, w = 0..W: the first record starting at or after off[0] + span*w/W
@@ -1183,9 +1214,10 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
   }
   const uint32_t lane = threadIdx.x & 63u;
   // this wave's event map: 64 chunks x {end in chain 0, start in chain 0, end
-  // in chain 1, start in chain 1}, each the chain byte + 1 (0 = none)
+  // in chain 1, start in chain 1}, each the chain byte j = 4 word + t (0..63),
+  // 0xFF = none (bit 7: absent; an absent byte's word, 63, matches no word)
   const uint32_t smap = LDS_SMAP_OFF + (threadIdx.x >> 6) * 256u;
-  *(__attribute__((address_space(3))) uint32_t*)(size_t)(smap + 4u * lane) = 0u;
+  *(__attribute__((address_space(3))) uint32_t*)(size_t)(smap + 4u * lane) = 0xFFFFFFFFu;
   __syncthreads();
   const uint32_t lo = (lane & 31u) * 4u, hi = lo | 0x10000u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -1250,6 +1282,43 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
 
   auto process = [&](const uint32_t (&U)[32], uint64_t t, auto&& issue_next) {
     const int64_t tb = tbase(t);
+    // --- a tile with no event at all (43% of config 3's: records of 8 KiB
+    // and more) is told by the window's first record alone, a scalar test:
+    // ends are sorted, so when record bt does not end here no later one does,
+    // and none starts before bt ends.  Such a tile skips the map.
+    {
+      const uint64_t fo = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(Wo >> 32)) << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)Wo);
+      const uint32_t fl = (uint32_t)__builtin_amdgcn_readfirstlane((int)Wl);
+      const int64_t fe = (int64_t)(fo + fl) - tb, fs = (int64_t)fo - tb;
+      if (bt >= r_hi || (fe >= 8192 && !(fl >= STREAM_LONG && fs >= 0 && fs < 8192))) {
+        issue_next();
+        __builtin_amdgcn_sched_barrier(0);
+        if (dqcnt) qpush(dqv, dqcnt);
+        dqcnt = 0;
+        if constexpr (ABLATE == 3) {  // diagnostic: payload loads only
+          uint32_t x = 0;
+#pragma unroll
+          for (int k = 0; k < 32; ++k) x ^= U[k];
+          if (x == 0x9E3779B1u) P.out[0] = x;
+          return;
+        }
+        // the carry (the open record's raw CRC up to this tile, aligned to
+        // its start) enters as lane 0's initial register: the Horner shift of
+        // lane 0 then carries it to the tile end with the chunk
+        uint32_t z0 = U[0] ^ (lane == 0u ? carry : 0u), z1 = U[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          z0 = crc_step_x(smem, z0, k + 1 < 16 ? U[k + 1] : 0u, lo, hi);
+          z1 = crc_step_x(smem, z1, k + 1 < 16 ? U[17 + k] : 0u, lo, hi);
+        }
+        uint32_t dz = 63u - lane;
+        asm volatile("" : "+v"(dz));  // not hoisted: eight loop-invariant column addresses spilled
+        const uint32_t XZ = wave_prefix_xor(walk_mulcol(shift_bytes32<2>(smem, z0) ^ z1, dz));
+        carry = (uint32_t)__builtin_amdgcn_readlane((int)XZ, 63);
+        return;
+      }
+    }
     // --- map: the window's records that end in this tile write their events
     // (long records) into the wave's LDS map; a tile in which all 64 window
     // records end walks the next window too (rare: records of ~128 B or less)
@@ -1271,8 +1340,8 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
       rs = (int32_t)(s64 < -128 ? -128 : (s64 > 8191 ? 8191 : s64));
       const bool ev_e = ends && lng, ev_s = sin && lng;
       typedef __attribute__((address_space(3))) unsigned char lds_u8w_t;
-      if (ev_e) *(lds_u8w_t*)(size_t)(smap + 4u * ((uint32_t)re >> 7) + (((uint32_t)re >> 5) & 2u)) = (unsigned char)((re & 63) + 1);
-      if (ev_s) *(lds_u8w_t*)(size_t)(smap + 4u * ((uint32_t)rs >> 7) + (((uint32_t)rs >> 5) & 2u) + 1u) = (unsigned char)((rs & 63) + 1);
+      if (ev_e) *(lds_u8w_t*)(size_t)(smap + 4u * ((uint32_t)re >> 7) + (((uint32_t)re >> 5) & 2u)) = (unsigned char)(re & 63);
+      if (ev_s) *(lds_u8w_t*)(size_t)(smap + 4u * ((uint32_t)rs >> 7) + (((uint32_t)rs >> 5) & 2u) + 1u) = (unsigned char)(rs & 63);
       Kw |= wave_or_u32((ev_e ? 1u << (((uint32_t)re & 127u) >> 2) : 0u) | (ev_s ? 1u << (((uint32_t)rs & 127u) >> 2) : 0u));
       shorts = shorts || __any(ends && !lng);
       if (cntw < 64u) break;
@@ -1282,8 +1351,6 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     }
     const uint64_t bt0 = bt;
     bt = wb + cntw;
-    // no event at all: no record ends here, and the open record started before
-    const bool z = nwin == 0u && cntw == 0u && !__builtin_amdgcn_readfirstlane((int)(sin && lng));
     // the next tile's window: this one shifted by cntw (lands while this tile is checksummed)
     {
       const uint32_t src = lane + cntw;
@@ -1306,31 +1373,13 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     __builtin_amdgcn_sched_barrier(0);
     if (dqcnt) qpush(dqv, dqcnt);
     dqcnt = 0;
-    if constexpr (ABLATE == 0) {
-      if (z) {  // (uniform) no event in the tile
-        // the carry (the open record's raw CRC up to this tile, aligned to
-        // its start) enters as lane 0's initial register: the Horner shift of
-        // lane 0 then carries it to the tile end with the chunk
-        uint32_t z0 = U[0] ^ (lane == 0u ? carry : 0u), z1 = U[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          z0 = crc_step_x(smem, z0, k + 1 < 16 ? U[k + 1] : 0u, lo, hi);
-          z1 = crc_step_x(smem, z1, k + 1 < 16 ? U[17 + k] : 0u, lo, hi);
-        }
-        uint32_t dz = 63u - lane;
-        asm volatile("" : "+v"(dz));  // not hoisted: eight loop-invariant column addresses spilled
-        const uint32_t XZ = wave_prefix_xor(walk_mulcol(shift_bytes32<2>(smem, z0) ^ z1, dz));
-        carry = (uint32_t)__builtin_amdgcn_readlane((int)XZ, 63);
-        return;
-      }
-    }
     // --- chunk-lane view: this chunk's events (byte + 1 in its chain, 0 = none)
     typedef __attribute__((address_space(3))) uint32_t lds_u32w_t;
-    uint32_t ev = *(lds_u32w_t*)(size_t)(smap + 4u * lane);
-    if (ev) *(lds_u32w_t*)(size_t)(smap + 4u * lane) = 0u;
-    const uint64_t M1 = __ballot((ev & 0x00FF00FFu) != 0u);  // chunks holding an end
-    const uint64_t Ms = __ballot((ev & 0xFF00FF00u) != 0u);  // chunks holding a start
-    const bool ke0 = __any((ev & 0xFFu) != 0u), ke1 = __any((ev & 0xFF0000u) != 0u);
+    const uint32_t ev = *(lds_u32w_t*)(size_t)(smap + 4u * lane);
+    if (ev != 0xFFFFFFFFu) *(lds_u32w_t*)(size_t)(smap + 4u * lane) = 0xFFFFFFFFu;
+    const uint64_t M1 = __ballot((~ev & 0x00800080u) != 0u);  // chunks holding an end
+    const uint64_t Ms = __ballot((~ev & 0x80008000u) != 0u);  // chunks holding a start
+    const bool ke0 = __any((~ev & 0x80u) != 0u), ke1 = __any((~ev & 0x800000u) != 0u);
     if (ABLATE == 3) {  // diagnostic: payload loads only
       uint32_t x = 0;
 #pragma unroll
@@ -1345,35 +1394,46 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     // the tile's first start it rides in lane 0's chain, into that record's
     // capture, R0 or the Horner value of chunk 0; a reset drops it.
     uint32_t c0 = U[0] ^ (lane == 0u ? carry : 0u), c1 = U[16], x0 = 0u, x1 = 0u, ub0 = 0u, ub1 = 0u;
-    const uint32_t Km = (Kw & 0xFFFFu) | (Kw >> 16);
+    // a chain's events at word k: end byte (ev >> 8*(2h)) and start byte
+    // (ev >> 8*(2h+1)), each 4 word + t; a word matches k only when present
+    auto at = [&](uint32_t e, int sh, int k) -> bool { return ((e >> (sh + 2)) & 63u) == (uint32_t)k; };
+    auto mlo_of = [&](uint32_t e, int sh) -> uint32_t {  // the mask of the start word's t bytes before it
+      return __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0u, ((e >> sh) & 3u) << 3);
+    };
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const uint32_t w0 = k + 1 < 16 ? U[k + 1] : 0u, w1 = k + 1 < 16 ? U[17 + k] : 0u;
       uint32_t i0 = c0, i1 = c1, n0 = w0, n1 = w1;
-      if (Km & (1u << k)) {
+      // (uniform) some lane's chain 0 / chain 1 has an event in word k: the
+      // branches only select the steps' inputs; both steps follow them, so
+      // their eight lookups issue together
+      if (Kw & (1u << k)) {
         uint32_t e = ev;
         asm volatile("" : "+v"(e));  // recomputed here, not hoisted: fewer VGPRs through the loop
-        const uint32_t be0 = e & 0xFFu, bs0 = (e >> 8) & 0xFFu, be1 = (e >> 16) & 0xFFu, bs1 = e >> 24;
-        // chain byte j + 1 at word k: (j >> 2) == k  <=>  ((b - 1) >> 2) == k, b != 0
-        const bool me0 = be0 && ((be0 - 1u) >> 2) == (uint32_t)k, ms0 = bs0 && ((bs0 - 1u) >> 2) == (uint32_t)k;
-        const bool me1 = be1 && ((be1 - 1u) >> 2) == (uint32_t)k, ms1 = bs1 && ((bs1 - 1u) >> 2) == (uint32_t)k;
-        const uint32_t mlo0 = (1u << (((bs0 - 1u) & 3u) << 3)) - 1u, mlo1 = (1u << (((bs1 - 1u) & 3u) << 3)) - 1u;
-        x0 = me0 ? c0 : x0;
-        ub0 = me0 ? U[k] : ub0;
-        x1 = me1 ? c1 : x1;
-        ub1 = me1 ? U[16 + k] : ub1;
-        i0 = ms0 ? ~(U[k] | mlo0) : c0;
-        n0 = ms0 ? (w0 ^ mlo0) : w0;
-        i1 = ms1 ? ~(U[16 + k] | mlo1) : c1;
-        n1 = ms1 ? (w1 ^ mlo1) : w1;
+        const bool me = at(e, 0, k), ms = at(e, 8, k);
+        const uint32_t mlo = mlo_of(e, 8);
+        x0 = me ? c0 : x0;
+        ub0 = me ? U[k] : ub0;
+        i0 = ms ? ~(U[k] | mlo) : c0;
+        n0 = ms ? (w0 ^ mlo) : w0;
+      }
+      if (Kw & (0x10000u << k)) {
+        uint32_t e = ev;
+        asm volatile("" : "+v"(e));
+        const bool me = at(e, 16, k), ms = at(e, 24, k);
+        const uint32_t mlo = mlo_of(e, 24);
+        x1 = me ? c1 : x1;
+        ub1 = me ? U[16 + k] : ub1;
+        i1 = ms ? ~(U[16 + k] | mlo) : c1;
+        n1 = ms ? (w1 ^ mlo) : w1;
       }
       c0 = crc_step_x(smem, i0, n0, lo, hi);
       c1 = crc_step_x(smem, i1, n1, lo, hi);
     }
-    const uint32_t cap0 = ke0 ? stream_capture(smem, x0, ub0, ((ev & 0xFFu) - 1u) & 3u, lo) : 0u;
-    const uint32_t cap1 = ke1 ? stream_capture(smem, x1, ub1, (((ev >> 16) & 0xFFu) - 1u) & 3u, lo) : 0u;
+    const uint32_t cap0 = ke0 ? stream_capture(smem, x0, ub0, ev & 3u, lo) : 0u;
+    const uint32_t cap1 = ke1 ? stream_capture(smem, x1, ub1, (ev >> 16) & 3u, lo) : 0u;
     const uint32_t R0 = c0;
-    const uint32_t T = (ev >> 24) ? c1 : (shift_bytes32<2>(smem, c0) ^ c1);
+    const uint32_t T = (ev >> 31) ? (shift_bytes32<2>(smem, c0) ^ c1) : c1;
     // --- Horner inside the tile: T to the chunk before the next END's chunk
     const uint64_t above = lane == 63u ? 0ull : (M1 >> (lane + 1u)) << (lane + 1u);
     const uint32_t cn = above ? (uint32_t)__builtin_ctzll(above) : 64u;
@@ -1505,10 +1565,11 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   if (n == 0) return 0;
   hipError_t e = hipMemsetAsync(P->sflag, 1, 4, st);
   if (e != hipSuccess) return -(int)e;
-  if (!trusted)
-    hipLaunchKernelGGL(stream_check, dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0, st, P->off, P->len, n, P->sflag);
   const uint32_t W = lsmk_stream_waves(ncu);
-  hipLaunchKernelGGL(stream_cuts, dim3((W + 1u + 255u) / 256u), dim3(256), 0, st, *P, W);
+  if (trusted)  // the library's own sorted batch: the cuts by binary search
+    hipLaunchKernelGGL(stream_cuts, dim3((W + 1u + 255u) / 256u), dim3(256), 0, st, *P, W);
+  else  // a caller's batch: check + cuts in one pass over its descriptors
+    hipLaunchKernelGGL(stream_prep, dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, st, *P, W);
   const int ablate = (variant >> 8) & 0xF;
   const void* fn = ablate == 3 ? (const void*)crc32_stream_kernel<3>
                  : ablate == 2 ? (const void*)crc32_stream_kernel<2> : (const void*)crc32_stream_kernel<0>;
@@ -1532,7 +1593,8 @@ extern "C" int lsmk_launch_crc32_walk(const CrcParams* P, uint64_t* sb_prefix, i
   const uint64_t n = P->nrec;
   if (n == 0) return 0;
   const uint64_t nsb = lsmk_walk_sb_count(n);
-  hipLaunchKernelGGL(walk_phase1, dim3((unsigned)((nsb + 15) / 16)), dim3(1024), 0, st, P->len, n, sb_prefix,
+  const uint64_t nblk = std::min<uint64_t>((nsb + 15) / 16, (uint64_t)ncu * 2u);
+  hipLaunchKernelGGL(walk_phase1, dim3((unsigned)nblk), dim3(1024), 0, st, P->len, n, sb_prefix,
                      (const uint32_t*)P->sflag);
   hipLaunchKernelGGL(scan_phase2, dim3(1), dim3(1024), 0, st, sb_prefix, (uint32_t)nsb, P->total_segs,
                      (const uint32_t*)P->sflag);
