@@ -80,6 +80,9 @@ def parse():
                          "(checksums.rs) over the same records, reported against its int32 VALU roof")
     ap.add_argument("--stream", type=int, default=1, choices=[0, 1],
                     help="descriptor batches: 1 = stream kernel (default), 0 = walking kernel (A/B)")
+    ap.add_argument("--sorted", action="store_true",
+                    help="descriptor batches with LSMCK_SORTED: the caller asserts its records are sorted inside "
+                         "one readable span, so the device-side check of the descriptors is skipped")
     ap.add_argument("--wal-framed", action="store_true",
                     help="config 3's records framed as wal.rs Insert records (13-byte headers between the payloads)")
     ap.add_argument("--pack-align", type=int, default=1,
@@ -211,6 +214,8 @@ def main():
                         f"{nbytes / GIB:.1f} GiB), device-resident")
         if A > 1:
             workload += f" [diagnostic: offsets aligned to {A} B]"
+        if a.sorted:
+            workload += " [LSMCK_SORTED: caller-asserted order, no device-side descriptor check]"
 
     sha = a.digest == "sha256"
     data = ctx.alloc(nbytes + 64)
@@ -232,7 +237,7 @@ def main():
             sha_blocks = int(((lens.astype(np.uint64) + 9 + 63) // 64).sum())
         else:
             def step():
-                ctx.crc32_device(data.ptr, d_off.ptr, d_len.ptr, nrec, out.ptr, sptr)
+                ctx.crc32_device(data.ptr, d_off.ptr, d_len.ptr, nrec, out.ptr, sptr, sorted_span=a.sorted)
         algo_bytes = payload + 12 * nrec + (32 if sha else 4) * nrec
     else:
         payload = nbytes

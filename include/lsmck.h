@@ -50,6 +50,13 @@ extern "C" {
 #define LSMCK_DEVICE 0x1u      /* base/off/len/out are device pointers; async on `stream` */
 #define LSMCK_HOST 0x0u        /* host (pageable) pointers; staged through pinned memory; synchronous */
 #define LSMCK_HOST_PINNED 0x2u /* host pointers already pinned (hipHostMalloc); DMA without a copy */
+/* with LSMCK_DEVICE, descriptor CRC batches only: the caller asserts that its
+ * records are sorted by offset, do not overlap, and that every byte between
+ * the first record's start and the last record's end lies in memory it may
+ * read (one buffer, e.g. a WAL image or a data file).  The stream kernel then
+ * takes the batch without the device-side check of its descriptors (one pass
+ * over them; lsmck_wal_replay_verify does the same for its own payloads). */
+#define LSMCK_SORTED 0x4u
 
 /* ======================================================================== */
 /* 1. Scalar CPU entry points                                                */

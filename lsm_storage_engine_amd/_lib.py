@@ -37,6 +37,7 @@ SSTABLE_MAX_LEVEL = 5
 DEVICE = 0x1
 HOST = 0x0
 HOST_PINNED = 0x2
+SORTED = 0x4  # LSMCK_SORTED: device descriptors sorted inside one readable span (include/lsmck.h)
 
 u8p = C.POINTER(C.c_uint8)
 u32p = C.POINTER(C.c_uint32)

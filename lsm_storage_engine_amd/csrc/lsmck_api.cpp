@@ -837,7 +837,7 @@ int lsmck_crc32_batch(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, 
   if (flags & LSMCK_DEVICE) {
     ScratchOrder so(ctx, pick_stream(ctx, stream));
     if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
-    return crc_desc_device(ctx, ctx->scratch, base, off, len, n, out, so.st);
+    return crc_desc_device(ctx, ctx->scratch, base, off, len, n, out, so.st, (flags & LSMCK_SORTED) != 0);
   }
   HostJob J{CRC, base, off, len, 0, 0, n, (uint8_t*)out, (flags & LSMCK_HOST_PINNED) != 0};
   return run_host_job(ctx, J);
@@ -867,7 +867,7 @@ int lsmck_crc32_verify_batch(lsmck_ctx* ctx, const uint8_t* base, const uint64_t
     DevGuard g(ctx->dev);
     ScratchOrder so(ctx, pick_stream(ctx, stream));
     if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
-    rc = device_verify(ctx, base, off, len, expected, n, so.st, n_bad, first_bad);
+    rc = device_verify(ctx, base, off, len, expected, n, so.st, n_bad, first_bad, (flags & LSMCK_SORTED) != 0);
     return rc;
   }
   std::vector<uint32_t> crc(n);

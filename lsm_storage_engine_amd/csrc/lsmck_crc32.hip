@@ -1012,28 +1012,14 @@ __global__ __launch_bounds__(1024) void crc32_walk_kernel(CrcParams P) {
 // the walking kernel, launched after this one, takes it when it is not.
 #define STREAM_LONG 64u      // records of at least this many bytes go through the chains
 #define STREAM_MAX_GAP 64u   // caller batches: at most this many bytes between two records
-// LDS columns K (x) x^i, i = 0..31 (128 B per factor K) of the finish factors,
-// in areas this kernel does not otherwise use: x^(8m) for m = 0..31 over the
-// shift-by-32-bytes table, m = 32..63 over the shift-by-96-bytes table (only
-// shift-by-64 is used here), x^(-8(4-t)) for t = 0..3 in the klo area
-#define LDS_XMC_OFF(m) ((m) < 32u ? LDS_SHIFT_OFF + (m) * 128u : LDS_SHIFT_OFF + 8192u + ((m) - 32u) * 128u)
-#define LDS_XIC_OFF(t) (LDS_KLO_OFF + (t) * 128u)
-
-// v (x) K from K's 32 LDS columns at `base` (8 ds_read_b128 + 32 v_bitop3).
-// (The generic gf2_mulmod here had its factor folded into 32 hoisted shifted
-// copies: ~70 spilled VGPRs.)
-__device__ __forceinline__ uint32_t stream_mulcol(uint32_t v, uint32_t base) {
-  uint32_t p = 0;
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    const u32x4 c = lds_ld128(base + g * 16u);
-    p = __builtin_amdgcn_bitop3_b32(p, c.x, (uint32_t)((int32_t)(v << (4 * g + 0)) >> 31), 0x78);
-    p = __builtin_amdgcn_bitop3_b32(p, c.y, (uint32_t)((int32_t)(v << (4 * g + 1)) >> 31), 0x78);
-    p = __builtin_amdgcn_bitop3_b32(p, c.z, (uint32_t)((int32_t)(v << (4 * g + 2)) >> 31), 0x78);
-    p = __builtin_amdgcn_bitop3_b32(p, c.w, (uint32_t)((int32_t)(v << (4 * g + 3)) >> 31), 0x78);
-  }
-  return p;
-}
+// The finish multiply v (x) x^(8m), m = 4q + r (0..63): v (x) x^(32q) from
+// nibble tables -- NT_q[n][e] = (e << 4n) (x) x^(32q), 16 factors x 8 nibbles
+// x 16 entries = 8 KiB, in areas this kernel does not otherwise use (q < 8
+// over the shift-by-32-bytes table, q >= 8 over the shift-by-96-bytes table;
+// only shift-by-64 is used here) -- then r zero-byte steps of the register by
+// slicing-by-r.  8 + 3 LDS reads and ~30 VALU, against the ~64 VALU of a
+// 32-column multiply (8 ds_read_b128 + 32 bfe + 32 bitop3).
+#define LDS_NT_OFF(q) ((q) < 8u ? LDS_SHIFT_OFF + (q) * 512u : LDS_SHIFT_OFF + 8192u + ((q) - 8u) * 512u)
 
 // The exact capture at an end at byte t of word u: the register s before the
 // word advanced over the word's t bytes before the end (the ending record's
@@ -1050,8 +1036,15 @@ __device__ __forceinline__ uint32_t stream_capture(const unsigned char* smem, ui
   return ((cx ^ u) >> (t << 3)) ^ (t >= 1u ? l0 : 0u) ^ (t >= 2u ? l1 : 0u) ^ (t >= 3u ? l2 : 0u);
 }
 
-__device__ __forceinline__ uint32_t stream_xinv(uint32_t t) {  // x^(-8(4-t))
-  return t == 0u ? 0x5b358fd3u : (t == 1u ? 0x1f81b6e1u : (t == 2u ? 0xd7125358u : 0x6567cb95u));
+// v (x) x^(8m), m = 0..63 (see LDS_NT_OFF)
+__device__ __forceinline__ uint32_t stream_mulx8(const unsigned char* smem, uint32_t v, uint32_t m, uint32_t lo) {
+  const uint32_t base = LDS_NT_OFF(m >> 2);
+  uint32_t l[8];
+#pragma unroll
+  for (int n = 0; n < 8; ++n) l[n] = lds_ld(smem, base + 64u * n + (__builtin_amdgcn_ubfe(v, 4u * n, 4u) << 2));
+  const uint32_t p = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(l[0], l[1], l[2], 0x96),
+                                                 __builtin_amdgcn_bitop3_b32(l[3], l[4], l[5], 0x96), l[6] ^ l[7], 0x96);
+  return stream_capture(smem, p, 0u, m & 3u, lo);  // r zero bytes: (p >> 8r) ^ slicing-by-r
 }
 
 // A caller's device batch takes the stream kernel when its records are sorted
@@ -1194,23 +1187,13 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
   if (!*P.sflag) return;  // a caller's batch that is not sorted / packed enough: the walking kernel takes it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   build_lds_tables(smem, P);
-  __syncthreads();  // the walk columns reuse the khi area, x^(8m) the klo area
+  __syncthreads();  // the walk columns reuse the khi area, the nibble tables the shift areas
   build_walk_cols(P);
-  if (threadIdx.x >= 128u && threadIdx.x < 196u) {  // the finish factors' columns
-    const uint32_t f = threadIdx.x - 128u;
-    uint32_t K, base;
-    if (f < 64u) {  // x^(8m): m zero-byte steps of the register from x^0
-      K = 0x80000000u;
-      for (uint32_t i = 0; i < f; ++i) K = (K >> 8) ^ P.master[K & 0xFFu];
-      base = LDS_XMC_OFF(f);
-    } else {
-      K = stream_xinv(f - 64u);
-      base = LDS_XIC_OFF(f - 64u);
-    }
-    for (uint32_t i = 0; i < 32u; ++i) {
-      *(__attribute__((address_space(3))) uint32_t*)(size_t)(base + 4u * i) = K;
-      K = (K >> 1) ^ (0xEDB88320u & (0u - (K & 1u)));
-    }
+  for (uint32_t i = threadIdx.x; i < 2048u; i += blockDim.x) {  // the finish multiply's nibble tables
+    const uint32_t q = i >> 7, nib = (i >> 4) & 7u, e = i & 15u;
+    uint32_t K = 0x80000000u;  // x^(32q): 4q zero-byte steps of the register from x^0
+    for (uint32_t b = 0; b < 4u * q; ++b) K = (K >> 8) ^ P.master[K & 0xFFu];
+    *(__attribute__((address_space(3))) uint32_t*)(size_t)(LDS_NT_OFF(q) + 64u * nib + 4u * e) = gf2_mulmod(e << (4u * nib), K);
   }
   const uint32_t lane = threadIdx.x & 63u;
   // this wave's event map: 64 chunks x {end in chain 0, start in chain 0, end
@@ -1235,14 +1218,15 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
   const uint64_t ntile = t_last >= t_first ? t_last - t_first + 1u : 0u;
   auto tbase = [&](uint64_t t) -> int64_t { return a0 + (int64_t)(t << 13); };
 
-  // the window: off / len of records bt + lane (clamped to n - 1; masked at use)
-  uint64_t Wo;
-  uint32_t Wl;
+  // the window: start and end of records bt + lane (clamped to n - 1; masked
+  // at use), both absolute: the tile tests are one 64-bit compare each, the
+  // tile-relative bytes the low words' difference
+  uint64_t Wo, We;
   auto win_load = [&](uint64_t b) {
     const uint64_t i = b + lane;
     const uint64_t ic = i < n ? i : n - 1u;
     Wo = P.off[ic];
-    Wl = P.len[ic];
+    We = Wo + P.len[ic];
   };
   uint64_t bt = r_lo;  // the first record that has not ended yet
   uint32_t carry = 0;  // the record open at the tile's end, its raw value aligned to the tile's end
@@ -1289,9 +1273,10 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     {
       const uint64_t fo = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(Wo >> 32)) << 32) |
                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)Wo);
-      const uint32_t fl = (uint32_t)__builtin_amdgcn_readfirstlane((int)Wl);
-      const int64_t fe = (int64_t)(fo + fl) - tb, fs = (int64_t)fo - tb;
-      if (bt >= r_hi || (fe >= 8192 && !(fl >= STREAM_LONG && fs >= 0 && fs < 8192))) {
+      const uint64_t fe_ = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(We >> 32)) << 32) |
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)We);
+      const int64_t fe = (int64_t)fe_ - tb, fs = (int64_t)fo - tb;
+      if (bt >= r_hi || (fe >= 8192 && !(fe_ - fo >= STREAM_LONG && fs >= 0 && fs < 8192))) {
         issue_next();
         __builtin_amdgcn_sched_barrier(0);
         if (dqcnt) qpush(dqv, dqcnt);
@@ -1327,17 +1312,20 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     uint64_t wb = bt;      // base of the window being mapped
     uint32_t nwin = 0;     // full windows (64 records ending here) before the last one
     uint32_t cntw;         // records of the last window ending here
-    int32_t re, rs;        // the last window's tile-relative end and start (start clamped to >= -128)
+    int32_t re, rs;        // the last window's tile-relative end and start
     bool lng, sin;         // long record; its start lies in this tile
+    const int64_t te = tb + 8192;
     for (;;) {
-      const int64_t e64 = (int64_t)(Wo + Wl) - tb, s64 = (int64_t)Wo - tb;
-      const bool inr = wb + lane < r_hi;
-      const bool ends = inr && e64 < 8192;
+      const uint64_t lim = r_hi - wb;  // > 0: bt < r_hi here
+      const bool inr = lane < (lim < 64u ? (uint32_t)lim : 64u);
+      const bool ends = inr && (int64_t)We < te;
       cntw = (uint32_t)__builtin_popcountll(__ballot(ends));
-      lng = Wl >= STREAM_LONG;
-      sin = inr && s64 >= 0 && s64 < 8192;
-      re = (int32_t)(ends ? e64 : 8191);
-      rs = (int32_t)(s64 < -128 ? -128 : (s64 > 8191 ? 8191 : s64));
+      lng = (uint32_t)We - (uint32_t)Wo >= STREAM_LONG;  // the length (< 2^32) from the low words
+      sin = inr && (int64_t)Wo >= tb && (int64_t)Wo < te;
+      // tile-relative bytes from the low words: exact whenever they are used
+      // (an end in the tile; a start in the tile, or a short record's)
+      re = ends ? (int32_t)((uint32_t)We - (uint32_t)tb) : 8191;
+      rs = (int32_t)((uint32_t)Wo - (uint32_t)tb);
       const bool ev_e = ends && lng, ev_s = sin && lng;
       typedef __attribute__((address_space(3))) unsigned char lds_u8w_t;
       if (ev_e) *(lds_u8w_t*)(size_t)(smap + 4u * ((uint32_t)re >> 7) + (((uint32_t)re >> 5) & 2u)) = (unsigned char)(re & 63);
@@ -1355,16 +1343,17 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     {
       const uint32_t src = lane + cntw;
       const int sp = (int)((src & 63u) << 2);
-      const uint32_t wlo = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)(uint32_t)Wo);
-      const uint32_t whi = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)(uint32_t)(Wo >> 32));
-      const uint32_t wl = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)Wl);
-      Wo = ((uint64_t)whi << 32) | wlo;
-      Wl = wl;
+      const uint32_t olo = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)(uint32_t)Wo);
+      const uint32_t ohi = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)(uint32_t)(Wo >> 32));
+      const uint32_t elo = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)(uint32_t)We);
+      const uint32_t ehi = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)(uint32_t)(We >> 32));
+      Wo = ((uint64_t)ohi << 32) | olo;
+      We = ((uint64_t)ehi << 32) | elo;
       if (src >= 64u) {  // the new entries only
         const uint64_t i2 = bt + lane;
         const uint64_t ic = i2 < n ? i2 : n - 1u;
         Wo = P.off[ic];
-        Wl = P.len[ic];
+        We = Wo + P.len[ic];
       }
     }
     // then the payload one tile ahead: after the window, so that waiting for
@@ -1456,7 +1445,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
       if (in && lng_) {
         const bool h = j >= 64u;
         const uint32_t Pv = h ? (shift_bytes32<2>(smem, H) ^ R0c) : H;
-        fv = ~(stream_mulcol(Pv, LDS_XMC_OFF(j & 63u)) ^ (h ? A1c : A0c));
+        fv = ~(stream_mulx8(smem, Pv, j & 63u, lo) ^ (h ? A1c : A0c));
       }
       return fv;
     };

@@ -161,8 +161,10 @@ class Context:
         return rc, nb.value, fb.value
 
     # --- CRC-32, device pointers (async on stream) ----------------------------
-    def crc32_device(self, base, off, length, n, out, stream=None):
-        _lib.check(self.lib.lsmck_crc32_batch(self.handle, base, off, length, n, out, _lib.DEVICE, stream),
+    def crc32_device(self, base, off, length, n, out, stream=None, sorted_span=False):
+        """sorted_span: LSMCK_SORTED, the caller asserts its records are sorted inside one readable span"""
+        flags = _lib.DEVICE | (_lib.SORTED if sorted_span else 0)
+        _lib.check(self.lib.lsmck_crc32_batch(self.handle, base, off, length, n, out, flags, stream),
                    "crc32_batch(device)")
 
     def crc32_fixed_device(self, base, stride, length, n, out, stream=None):

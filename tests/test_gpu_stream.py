@@ -32,9 +32,10 @@ def _gapped(lens, gaps, lead):
     return np.cumsum(step) + np.uint64(lead), lens
 
 
-def _device(ctx, data, off, ln, shift=0, exact=False):
+def _device(ctx, data, off, ln, shift=0, exact=False, sorted_span=False):
     """CRCs of device-resident records; the data at `shift` bytes into its
-    allocation; `exact`: the allocation ends with the last record's byte."""
+    allocation; `exact`: the allocation ends with the last record's byte;
+    `sorted_span`: LSMCK_SORTED (no device-side check of the descriptors)."""
     n = len(off)
     size = int(off[-1]) + int(ln[-1]) if exact else len(data)
     d = ctx.alloc(size + shift)
@@ -43,7 +44,7 @@ def _device(ctx, data, off, ln, shift=0, exact=False):
     out.upload(np.full(n, 0xA5A5A5A5, dtype=np.uint32))  # unwritten outputs show
     d_o.upload(off)
     d_l.upload(ln)
-    ctx.crc32_device(d.ptr + shift, d_o.ptr, d_l.ptr, n, out.ptr)
+    ctx.crc32_device(d.ptr + shift, d_o.ptr, d_l.ptr, n, out.ptr, sorted_span=sorted_span)
     ctx.sync()
     got = out.download(np.uint32)
     for b in (d, d_o, d_l, out):
@@ -210,6 +211,27 @@ def test_ineligible_batches_take_the_walking_kernel(ctx, case):
         assert (_device(ctx, data, off, ln) == 0xA5A5A5A5).all()
     finally:
         ctx.set_option("crc_stream", 1)
+
+
+@pytest.mark.parametrize("kind", ["packed", "wal_big_gaps"])
+def test_caller_asserted_sorted_batches(ctx, kind):
+    """LSMCK_SORTED: the caller asserts the order and the readable span, the
+    stream kernel takes the batch without the device check -- also with gaps
+    the check would refuse (a batch inside one allocation)."""
+    rng = np.random.default_rng(17)
+    n = 20000
+    lens = rng.integers(0, 5000, n)
+    lens[0] = 100
+    gaps = np.zeros(n, dtype=np.int64) if kind == "packed" else rng.integers(0, 3000, n)
+    off, ln = _gapped(lens, gaps, 11)
+    data = O.gen_stream(0x57AE0900, 0, int(off[-1]) + int(ln[-1]) + 16)
+    want = O.crc32_batch(data, off, ln, threads=8)
+    ctx.set_option("crc_stream", 2)
+    try:
+        got = _device(ctx, data, off, ln, sorted_span=True)
+    finally:
+        ctx.set_option("crc_stream", 1)
+    assert np.array_equal(got, want)
 
 
 def test_host_batches_use_it_too(ctx):
