@@ -186,6 +186,9 @@ int lsmck_device_count(void);
  *                 on the GPU (default), 0 = read back and walk on the host.
  *   "wal_upload_min"  host images of at least this many bytes are uploaded and
  *                 walked on the GPU (default 1 MiB; 0 = always the host walk).
+ *   "wal_register"  1 = an uploaded host WAL image is DMA'd from the caller's
+ *                 own pages, pinned in place for the call (hipHostRegister),
+ *                 instead of through the pinned staging copy (default 0).  A/B.
  *   "wal_chunk_bytes"  lsmck_wal_replay_verify of a host image: CRC batches
  *                 of this many payload bytes run on a helper thread while the
  *                 walk goes on (default 32 MiB; 0 = one batch after the walk).

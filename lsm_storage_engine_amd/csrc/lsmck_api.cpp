@@ -213,6 +213,8 @@ struct lsmck_ctx {
     unsigned long long* info = nullptr;  // [records, terminal, bad position, candidates (u32 at info+3)]
     unsigned long long* h_info = nullptr;  // pinned
   } wd;
+  lsmck_wal_rec* h_wrecs = nullptr;  // device WAL replay: the records' pinned landing buffer (grow-only)
+  size_t cap_hwrecs = 0;
   uint64_t* h_woff = nullptr;  // pinned staging of the same
   size_t cap_hwoff = 0;
   uint32_t* h_wlen = nullptr;
@@ -238,6 +240,7 @@ struct lsmck_ctx {
   // the GPU walk's scratch budget: this many bytes per log byte + 256 MiB (and
   // at most half the free device memory); over it the log takes the host walk
   size_t wal_walk_budget_per_byte = 8;
+  int wal_register = 0;  // host WAL images: hipHostRegister the caller's pages instead of the staging copy (A/B)
   // host images of at least this many bytes are uploaded whole and walked on
   // the GPU (0 = always the host walk)
   size_t wal_upload_min = 1u << 20;
@@ -748,6 +751,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->wal_gpu_walk = (int)value;
     return 0;
   }
+  if (!strcmp(key, "wal_register")) {  // A/B: host WAL image uploaded by DMA from its own pages, pinned in place
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "wal_register must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_register = (int)value;
+    return 0;
+  }
   if (!strcmp(key, "wal_upload_min")) {  // A/B: host WAL images from this size go to the GPU walk (0 = never)
     if (value < 0) return lsmck_host::set_error(LSMCK_EINVAL, "wal_upload_min: >= 0");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -820,6 +829,7 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   for (void* p : {(void*)ctx->h_woff, (void*)ctx->h_wlen, (void*)ctx->h_wexp})
     if (p) (void)hipHostFree(p);
   if (ctx->h_verify) (void)hipHostFree(ctx->h_verify);
+  if (ctx->h_wrecs) (void)hipHostFree(ctx->h_wrecs);
   if (ctx->wal_host) (void)hipHostFree(ctx->wal_host);
   if (ctx->d_wimg) (void)hipFree(ctx->d_wimg);
   if (ctx->scratch_ev) (void)hipEventDestroy(ctx->scratch_ev);
@@ -1016,20 +1026,40 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
       return rc;
     rc = lsmk_wal_emit(img, n, W.chain, W.pos, W.info, (uint32_t)m, W.recs, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st);
     if (rc) return launch_rc(rc, "wal emit kernel");
+    // the records go to a pinned buffer while the CRC pass runs (DMA at the
+    // link rate, no sync of its own; a copy into the caller's pageable array
+    // ran at a few GiB/s, page faults included)
+    if (recs && cap) {
+      if ((rc = ensure_pinned(&ctx->h_wrecs, &ctx->cap_hwrecs, m))) return rc;
+      HIPCHK(hipMemcpyAsync(ctx->h_wrecs, W.recs, m * sizeof(lsmck_wal_rec), hipMemcpyDeviceToHost, st));
+    }
     // the payloads of one image in log order: the stream kernel, no eligibility check
     rc = device_verify(ctx, img, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, m, st, &nbad, &first, true);
     if (rc < 0) return rc;
   }
   tr.mark("emit+crc+compare (sync)");
   const size_t accepted = nbad ? (size_t)first : m;
-  if (recs && accepted) HIPCHK(hipMemcpy(recs, W.recs, std::min(accepted, cap) * sizeof(lsmck_wal_rec),
-                                         hipMemcpyDeviceToHost));
+  if (recs && cap && accepted) {  // pinned -> the caller's array, on several threads (first touch of its pages)
+    const size_t cnt = std::min(accepted, cap), bytes = cnt * sizeof(lsmck_wal_rec);
+    const unsigned T = bytes >= (4u << 20) ? std::max(1u, std::min(ctx->stage_threads, 8u)) : 1u;
+    std::vector<std::thread> pool;
+    auto part = [&](unsigned t) {
+      const size_t a = cnt * t / T, b = cnt * (t + 1) / T;
+      memcpy(recs + a, ctx->h_wrecs + a, (b - a) * sizeof(lsmck_wal_rec));
+    };
+    for (unsigned t = 1; t < T; ++t) pool.emplace_back(part, t);
+    part(0);
+    for (auto& th : pool) th.join();
+  }
   tr.mark("records to host");
   if (nrec) *nrec = accepted;
   if (nbad) {
     lsmck_wal_rec r;
     uint32_t got = 0;
-    HIPCHK(hipMemcpy(&r, W.recs + first, sizeof r, hipMemcpyDeviceToHost));
+    if (recs && cap)
+      r = ctx->h_wrecs[first];
+    else
+      HIPCHK(hipMemcpy(&r, W.recs + first, sizeof r, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(&got, ctx->d_vcrc + first, 4, hipMemcpyDeviceToHost));
     if (bad_index) *bad_index = first;
     if (bad_expected) *bad_expected = r.crc;
@@ -1058,11 +1088,28 @@ static int wal_upload(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned)
   // the candidate bitmap of each chunk is marked right behind its copy (the
   // marking then overlaps the rest of the upload)
   auto& W = ctx->wd;
-  if (pinned) {
-    HIPCHK(hipMemcpyAsync(ctx->d_wimg, img, n, hipMemcpyHostToDevice, ctx->stream0));
-    rc = lsmk_wal_mark_range(ctx->d_wimg, n, 0, n, W.bits, W.pre, ctx->stream0);
-    if (rc) return launch_rc(rc, "wal mark kernel");
+  // "wal_register": pin the caller's pageable pages in place (hipHostRegister)
+  // and DMA straight from them, instead of the staging copy (A/B)
+  bool registered = false;
+  uint8_t* reg_base = nullptr;
+  if (!pinned && ctx->wal_register && n >= (1u << 20)) {
+    const uintptr_t pa = (uintptr_t)img & ~(uintptr_t)4095, pe = ((uintptr_t)img + n + 4095) & ~(uintptr_t)4095;
+    reg_base = (uint8_t*)pa;
+    registered = hipHostRegister(reg_base, pe - pa, hipHostRegisterDefault) == hipSuccess;
+    if (!registered) (void)hipGetLastError();
+    tr.mark("hipHostRegister");
+  }
+  if (pinned || registered) {
+    // chunked, so that each chunk's candidate marking runs behind its DMA
+    for (size_t o = 0; o < n; o += kChunkBytes) {
+      const size_t c = std::min(kChunkBytes, n - o);
+      HIPCHK(hipMemcpyAsync(ctx->d_wimg + o, img + o, c, hipMemcpyHostToDevice, ctx->stream0));
+      rc = lsmk_wal_mark_range(ctx->d_wimg, n, o, o + c, W.bits, W.pre, ctx->stream0);
+      if (rc) return launch_rc(rc, "wal mark kernel");
+    }
     HIPCHK(hipStreamSynchronize(ctx->stream0));
+    if (registered) (void)hipHostUnregister(reg_base);
+    tr.mark(registered ? "upload (registered)" : "upload (pinned)");
     return 0;
   }
   StageGuard guard{ctx};

@@ -104,6 +104,37 @@ def test_big_generated_log(ctx):
     assert same(ctx, img) == 0
 
 
+@pytest.mark.parametrize("register", [0, 1])
+def test_registered_upload(ctx, register):
+    """``wal_register`` 1: an uploaded host image is DMA'd from its own pages
+    (pinned in place for the call, unaligned start and end) -- same records
+    and the same first bad record as the staged upload and the oracle."""
+    rng = np.random.default_rng(21)
+    blob = O.gen_stream(6, 0, 1 << 20)
+    parts = []
+    for i in range(6000):
+        kl, vl = int(rng.integers(0, 40)), int(rng.integers(0, 3000))
+        k = blob[i % 500:i % 500 + kl].tobytes()
+        parts.append(O.wal_remove(k) if i % 13 == 0 else O.wal_insert(k, blob[(5 * i) % 900000:(5 * i) % 900000 + vl].tobytes()))
+    img = b"".join(parts)
+    assert len(img) > (4 << 20)
+    ctx.set_option("wal_register", register)
+    try:
+        assert same(ctx, img) == 0
+        raw = bytearray(len(img) + 8)
+        raw[3:3 + len(img)] = img  # a view at an odd address inside a larger buffer
+        view = memoryview(raw)[3:3 + len(img)]
+        recs, st, _ = ctx.wal_replay_verify(view)
+        ost, orecs, _ = O.wal_replay(img)
+        assert st == ost == 0
+        assert [(r.rec_off, r.crc) for r in recs] == [(r.rec_off, r.crc) for r in orecs]
+        b = bytearray(img)
+        b[len(img) // 2] ^= 0x10
+        assert same(ctx, bytes(b)) in (1, 2, 3)
+    finally:
+        ctx.set_option("wal_register", 0)
+
+
 @pytest.mark.parametrize("chunk", [1, 4096, 65536, 0])
 def test_overlapped_chunks(ctx, golden, chunk):
     """The host-image replay runs its CRC batches while the walk goes on

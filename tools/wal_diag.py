@@ -66,6 +66,9 @@ def main():
     recs, st, _ = ctx.wal_replay_verify(img)
     assert st == 0 and len(recs) == n
     res["replay_total_s"] = best(lambda: ctx.wal_replay_verify(img))  # default: uploaded, GPU header walk
+    ctx.set_option("wal_register", 1)  # A/B: the caller's pages pinned in place, DMA without the staging copy
+    res["replay_registered_s"] = best(lambda: ctx.wal_replay_verify(img))
+    ctx.set_option("wal_register", 0)
     ctx.set_option("wal_upload_min", 0)  # the host walk for the A/Bs below
     res["replay_hostwalk_s"] = best(lambda: ctx.wal_replay_verify(img))
     for pf in (0, 1024, 4096, 16384, 65536):
