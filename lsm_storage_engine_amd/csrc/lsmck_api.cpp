@@ -782,7 +782,9 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     return 0;
   }
   if (!strcmp(key, "sha_pair")) {  // A/B: SHA-256 batch kernel loads two blocks (a 128-B line) per window
-    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "sha_pair must be 0 or 1");
+    // 2: diagnostic, the pair kernel's main loop without payload loads (digests invalid);
+    // 3: line-aligned loads realigned through LDS rows
+    if (value < 0 || value > 3) return lsmck_host::set_error(LSMCK_EINVAL, "sha_pair must be 0..3");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->sha_pair = (int)value;
     return 0;

@@ -160,8 +160,12 @@ __device__ __forceinline__ void compress_win(uint32_t (&h)[8], const ShaWin& W, 
 struct ShaWin2 {
   uint32_t d[33];
 };
+template <int ABL = 0>
 __device__ __forceinline__ void issue_win2(const unsigned char* base, uint64_t off, uint64_t p0, ShaWin2& W) {
-  const unsigned char* s = base + off + p0;
+  // ABL 1 (option sha_pair 2, diagnostic): every window reloads the message's
+  // first one (in bounds, cache resident after the first), so almost no HBM
+  // traffic -- digests invalid
+  const unsigned char* s = base + off + (ABL == 1 ? 0u : p0);
   const unsigned char* p = s - ((uintptr_t)s & 3);
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
@@ -185,12 +189,44 @@ __device__ __forceinline__ void compress_win2(uint32_t (&h)[8], const ShaWin2& W
   sha256_compress(h, w);
 }
 
+// Line-aligned windows (MODE 2, option sha_pair 3; A/B): a 132-byte window at
+// a message's own offset straddles two 128-B lines, and a lane's next window
+// starts in the second of them -- when that line has left L2 in between it is
+// fetched twice (config 3: 1.37x the payload).  Here every load
+// is one whole aligned line L_k = (A & ~127) + 128k, each line is loaded once,
+// and pair p (message bytes [128p, 128p+128) + the funnel dword) is realigned
+// through the lane's own 272-byte LDS row: L_p and L_{p+1} are written to it
+// and the 33 dwords from byte (A & 127) & ~3 read back.  Lines stay in
+// registers for two pairs (X = L_p, Y = L_{p+1}, Z = L_{p+2} in flight), so the
+// loop is unrolled by three to rotate them without copies.
+struct ShaLine {
+  u32x4 v[8];
+};
+__device__ __forceinline__ void issue_line(const unsigned char* L0, uint64_t k, ShaLine& X) {
+  const unsigned char* q = L0 + (k << 7);
+#pragma unroll
+  for (int g = 0; g < 8; ++g) X.v[g] = ld128(q + 16 * g);
+  asm volatile("" ::"v"(q));
+}
+__device__ __forceinline__ void compress_lines(uint32_t (&h)[8], const ShaLine& X, const ShaLine& Y, uint32_t* row,
+                                               uint32_t cd, uint32_t sh) {
+#pragma unroll
+  for (int g = 0; g < 8; ++g) *(u32x4*)(row + 4 * g) = X.v[g];
+#pragma unroll
+  for (int g = 0; g < 8; ++g) *(u32x4*)(row + 32 + 4 * g) = Y.v[g];
+  ShaWin2 W;
+  const uint32_t* r = row + cd;
+#pragma unroll
+  for (int j = 0; j < 33; ++j) W.d[j] = r[j];
+  compress_win2(h, W, sh);
+}
+
 // Runs the compression over `len` bytes at base + off into h.  last: these are
 // the message's final bytes -- pad and append the bit length `bits` of the
 // whole message (the slice starts on a 64-byte boundary of the message).  Not
 // last: len is a multiple of 64 and no padding is added (a slice of a message
 // streamed through sha256_slices_kernel).
-template <bool PAIR = false>
+template <bool PAIR = false, int ABL = 0>
 __device__ __forceinline__ void sha256_run(uint32_t (&h)[8], const unsigned char* base, uint64_t off, uint64_t len,
                                            bool last, uint64_t bits) {
   const uintptr_t A = (uintptr_t)(base + off);
@@ -214,18 +250,48 @@ __device__ __forceinline__ void sha256_run(uint32_t (&h)[8], const unsigned char
     nmain = 0;
   }
   uint64_t b = 0;
-  if (PAIR && nmain >= 2) {
+  if (PAIR && ABL == 2 && nmain >= 2) {
+    const uint64_t npair = nmain >> 1;
+    const unsigned char* L0 = (const unsigned char*)(A & ~(uintptr_t)127);
+    const uint32_t c = (uint32_t)(A & 127u), cd = c >> 2;
+    // the last line any pair needs (pair p uses L_p, and L_{p+1} unless the
+    // message is line aligned); loads past it reload it (in bounds, unused)
+    const uint64_t kmax = npair - 1 + (c != 0u);
+    extern __shared__ __attribute__((aligned(16))) uint32_t sha_rows[];
+    uint32_t* row = sha_rows + threadIdx.x * 68u;  // 272-B rows: lanes 4 banks apart
+    ShaLine X, Y, Z;
+    issue_line(L0, 0, X);
+    issue_line(L0, kmax < 1 ? kmax : 1, Y);
+    uint64_t p = 0;
+    for (; p + 3 <= npair; p += 3) {
+      issue_line(L0, kmax < p + 2 ? kmax : p + 2, Z);
+      __builtin_amdgcn_sched_barrier(0);
+      compress_lines(h, X, Y, row, cd, sh);
+      issue_line(L0, kmax < p + 3 ? kmax : p + 3, X);
+      __builtin_amdgcn_sched_barrier(0);
+      compress_lines(h, Y, Z, row, cd, sh);
+      issue_line(L0, kmax < p + 4 ? kmax : p + 4, Y);
+      __builtin_amdgcn_sched_barrier(0);
+      compress_lines(h, Z, X, row, cd, sh);
+    }
+    if (p < npair) {
+      issue_line(L0, kmax < p + 2 ? kmax : p + 2, Z);
+      compress_lines(h, X, Y, row, cd, sh);
+      if (p + 1 < npair) compress_lines(h, Y, Z, row, cd, sh);
+    }
+    b = npair << 1;
+  } else if (PAIR && nmain >= 2) {
     // pairs (2p, 2p+1), p < nmain/2: their 132-byte windows stay inside the
     // message's dwords; an odd last main block goes through the loader below
     const uint64_t npair = nmain >> 1;
     ShaWin2 WA, WB;
-    issue_win2(base, off, 0, WA);
+    issue_win2<ABL>(base, off, 0, WA);
     uint64_t p = 0;
     for (; p + 1 < npair; p += 2) {
-      issue_win2(base, off, (p + 1) << 7, WB);
+      issue_win2<ABL>(base, off, (p + 1) << 7, WB);
       __builtin_amdgcn_sched_barrier(0);
       compress_win2(h, WA, sh);
-      issue_win2(base, off, (p + 2 < npair ? p + 2 : p + 1) << 7, WA);
+      issue_win2<ABL>(base, off, (p + 2 < npair ? p + 2 : p + 1) << 7, WA);
       __builtin_amdgcn_sched_barrier(0);
       compress_win2(h, WB, sh);
     }
@@ -284,7 +350,7 @@ __device__ __forceinline__ void store_digest(unsigned char* out, const uint32_t 
   o[1] = o1;
 }
 
-template <bool PAIR>
+template <bool PAIR, int ABL = 0>
 __global__ __launch_bounds__(256) void sha256_kernel(ShaParams P) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P.nmsg) return;
@@ -293,7 +359,7 @@ __global__ __launch_bounds__(256) void sha256_kernel(ShaParams P) {
   uint64_t len = P.len ? P.len[m] : P.flen;
   uint32_t h[8];
   sha256_iv(h);
-  sha256_run<PAIR>(h, P.base, off, len, true, len << 3);
+  sha256_run<PAIR, ABL>(h, P.base, off, len, true, len << 3);
   store_digest(P.out + 32 * m, h);
 }
 
@@ -366,7 +432,11 @@ using namespace lsmck;
 extern "C" int lsmk_launch_sha256(const ShaParams* P, hipStream_t st) {
   if (P->nmsg == 0) return 0;
   uint64_t blocks = (P->nmsg + 255) / 256;
-  if (P->pair)
+  if (P->pair == 2)  // diagnostic: the pair kernel without its payload loads
+    hipLaunchKernelGGL((sha256_kernel<true, 1>), dim3((unsigned)blocks), dim3(256), 0, st, *P);
+  else if (P->pair == 3)  // line-aligned windows realigned through LDS rows (A/B)
+    hipLaunchKernelGGL((sha256_kernel<true, 2>), dim3((unsigned)blocks), dim3(256), 256 * 272, st, *P);
+  else if (P->pair)
     hipLaunchKernelGGL(sha256_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, *P);
   else
     hipLaunchKernelGGL(sha256_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, *P);

@@ -31,9 +31,10 @@ def test_fips_and_golden_slices(ctx, golden, blob):
         assert got[i].tobytes().hex() == e["sha256"], e
 
 
-@pytest.fixture(params=[0, 1], ids=["win1", "win2"])
+@pytest.fixture(params=[0, 1, 3], ids=["win1", "win2", "lines"])
 def sha_pair(request, ctx):
-    """Both SHA-256 load windows: one block (68 B) or two blocks (132 B) per load."""
+    """The SHA-256 load windows: one block (68 B) or two blocks (132 B) per
+    load, or whole aligned 128-B lines realigned through LDS rows."""
     ctx.set_option("sha_pair", request.param)
     yield request.param
     ctx.set_option("sha_pair", 1)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 evidence in one GPU call.  Steps are picked by STEPS (space list):
-#   c4pmc smoke quick pytest bench c3w c2 kt c3pmc sha (run in this order)
+#   c4pmc smoke quick pytest bench c3w c2 kt c3pmc sha shaab shakt shapmc wal (run in this order)
 # Every GPU step has its own time limit; any failure ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -54,5 +54,24 @@ fi
 if has sha; then
   timeout -k 10 400 python3 bench.py --digest sha256 --config 3 --steps 5 --warmup 1 > gpurun_out/bench_${R}_sha_c3.log 2>&1; step bench_sha_c3 $?
   tail -1 gpurun_out/bench_${R}_sha_c3.log
+fi
+if has shaab; then  # SHA-256 config 3: the pair kernel against its compute-only ablation (sha_pair 2) and single blocks
+  timeout -k 10 600 python3 bench.py --digest sha256 --config 3 --steps 3 --warmup 1 --variants -,p2,p3,p0 --rounds 3 --no-cpu-baseline --no-host-roundtrip --no-stream-ceiling > gpurun_out/ab_${R}_sha_c3.log 2>&1; step ab_sha_c3 $?
+  tail -1 gpurun_out/ab_${R}_sha_c3.log
+fi
+if has shakt; then  # kernel-trace stats of SHA-256 config 3 (the order sort and the hash kernel)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt_${R}_sha_c3 -o kt -- python3 bench.py --digest sha256 --config 3 --steps 5 --warmup 1 --no-cpu-baseline --no-host-roundtrip --no-stream-ceiling > gpurun_out/kt_${R}_sha_c3.log 2>&1; step kt_sha_c3 $?
+  python3 tools/kt_stats.py gpurun_out/kt_${R}_sha_c3 > gpurun_out/kt_stats_${R}_sha_c3.txt
+  cat gpurun_out/kt_stats_${R}_sha_c3.txt
+fi
+if has shapmc; then  # SHA-256 config 3 HBM traffic (FETCH_SIZE / WRITE_SIZE passes)
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d gpurun_out/pmc_${R}_sha_c3_$C -o pmc -- python3 bench.py --digest sha256 --config 3 --steps 3 --warmup 1 --no-cpu-baseline --no-host-roundtrip --no-stream-ceiling > gpurun_out/pmc_${R}_sha_c3_$C.log 2>&1; step pmc_sha_c3_$C $?
+  done
+  python3 tools/pmc_summary.py gpurun_out/pmc_${R}_sha_c3_FETCH_SIZE gpurun_out/pmc_${R}_sha_c3_WRITE_SIZE sha256_config3 > gpurun_out/pmc_summary_${R}_sha_c3.json
+fi
+if has wal; then  # host WAL replay phases (LSMCK_WAL_TRACE) and the registered-upload A/B
+  LSMCK_WAL_TRACE=1 timeout -k 10 300 python3 tools/wal_diag.py > gpurun_out/wal_diag_${R}.log 2>&1; step wal_diag $?
+  tail -30 gpurun_out/wal_diag_${R}.log
 fi
 echo "== done"
