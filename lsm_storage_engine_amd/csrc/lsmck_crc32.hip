@@ -1008,18 +1008,32 @@ __global__ __launch_bounds__(1024) void crc32_walk_kernel(CrcParams P) {
 // starts at its first record's start (the bytes in front are dropped).
 // Eligibility: every batch the library builds itself (host-staged chunks, WAL
 // replay) is sorted by construction and its gaps lie inside one buffer; a
-// caller's device batch is checked on the device first (stream_prep) and
+// caller's device batch is checked on the device first (stream_check) and
 // the walking kernel, launched after this one, takes it when it is not.
 #define STREAM_LONG 64u      // records of at least this many bytes go through the chains
 #define STREAM_MAX_GAP 64u   // caller batches: at most this many bytes between two records
-// The finish multiply v (x) x^(8m), m = 4q + r (0..63): v (x) x^(32q) from
-// nibble tables -- NT_q[n][e] = (e << 4n) (x) x^(32q), 16 factors x 8 nibbles
-// x 16 entries = 8 KiB, in areas this kernel does not otherwise use (q < 8
-// over the shift-by-32-bytes table, q >= 8 over the shift-by-96-bytes table;
-// only shift-by-64 is used here) -- then r zero-byte steps of the register by
-// slicing-by-r.  8 + 3 LDS reads and ~30 VALU, against the ~64 VALU of a
-// 32-column multiply (8 ds_read_b128 + 32 bfe + 32 bitop3).
-#define LDS_NT_OFF(q) ((q) < 8u ? LDS_SHIFT_OFF + (q) * 512u : LDS_SHIFT_OFF + 8192u + ((q) - 8u) * 512u)
+// LDS columns K (x) x^i, i = 0..31 (128 B per factor K) of the finish factors,
+// in areas this kernel does not otherwise use: x^(8m) for m = 0..31 over the
+// shift-by-32-bytes table, m = 32..63 over the shift-by-96-bytes table (only
+// shift-by-64 is used here), x^(-8(4-t)) for t = 0..3 in the klo area
+#define LDS_XMC_OFF(m) ((m) < 32u ? LDS_SHIFT_OFF + (m) * 128u : LDS_SHIFT_OFF + 8192u + ((m) - 32u) * 128u)
+#define LDS_XIC_OFF(t) (LDS_KLO_OFF + (t) * 128u)
+
+// v (x) K from K's 32 LDS columns at `base` (8 ds_read_b128 + 32 v_bitop3).
+// (The generic gf2_mulmod here had its factor folded into 32 hoisted shifted
+// copies: ~70 spilled VGPRs.)
+__device__ __forceinline__ uint32_t stream_mulcol(uint32_t v, uint32_t base) {
+  uint32_t p = 0;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    const u32x4 c = lds_ld128(base + g * 16u);
+    p = __builtin_amdgcn_bitop3_b32(p, c.x, (uint32_t)((int32_t)(v << (4 * g + 0)) >> 31), 0x78);
+    p = __builtin_amdgcn_bitop3_b32(p, c.y, (uint32_t)((int32_t)(v << (4 * g + 1)) >> 31), 0x78);
+    p = __builtin_amdgcn_bitop3_b32(p, c.z, (uint32_t)((int32_t)(v << (4 * g + 2)) >> 31), 0x78);
+    p = __builtin_amdgcn_bitop3_b32(p, c.w, (uint32_t)((int32_t)(v << (4 * g + 3)) >> 31), 0x78);
+  }
+  return p;
+}
 
 // The exact capture at an end at byte t of word u: the register s before the
 // word advanced over the word's t bytes before the end (the ending record's
@@ -1036,15 +1050,8 @@ __device__ __forceinline__ uint32_t stream_capture(const unsigned char* smem, ui
   return ((cx ^ u) >> (t << 3)) ^ (t >= 1u ? l0 : 0u) ^ (t >= 2u ? l1 : 0u) ^ (t >= 3u ? l2 : 0u);
 }
 
-// v (x) x^(8m), m = 0..63 (see LDS_NT_OFF)
-__device__ __forceinline__ uint32_t stream_mulx8(const unsigned char* smem, uint32_t v, uint32_t m, uint32_t lo) {
-  const uint32_t base = LDS_NT_OFF(m >> 2);
-  uint32_t l[8];
-#pragma unroll
-  for (int n = 0; n < 8; ++n) l[n] = lds_ld(smem, base + 64u * n + (__builtin_amdgcn_ubfe(v, 4u * n, 4u) << 2));
-  const uint32_t p = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(l[0], l[1], l[2], 0x96),
-                                                 __builtin_amdgcn_bitop3_b32(l[3], l[4], l[5], 0x96), l[6] ^ l[7], 0x96);
-  return stream_capture(smem, p, 0u, m & 3u, lo);  // r zero bytes: (p >> 8r) ^ slicing-by-r
+__device__ __forceinline__ uint32_t stream_xinv(uint32_t t) {  // x^(-8(4-t))
+  return t == 0u ? 0x5b358fd3u : (t == 1u ? 0x1f81b6e1u : (t == 2u ? 0xd7125358u : 0x6567cb95u));
 }
 
 // A caller's device batch takes the stream kernel when its records are sorted
@@ -1129,7 +1136,7 @@ __device__ __forceinline__ void stream_issue(const CrcParams& P, int64_t tb, uin
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<unsigned char*>(P.base + tb), (short)0, (int)(span < 0x7FFFFFFFull ? span : 0x7FFFFFFFull), 0x00020000);
   const uint32_t vo = lane * 128u;
-  if (ABLATE == 2) {  // diagnostic: compute only (no payload loads; results invalid)
+  if (ABLATE == 2 || ABLATE == 4) {  // diagnostic: compute only (no payload loads; results invalid)
 #pragma unroll
     for (int j = 0; j < 32; ++j) u[j] = (uint32_t)tb * 0x9E3779B1u + lane + j;
     return;
@@ -1187,20 +1194,29 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
   if (!*P.sflag) return;  // a caller's batch that is not sorted / packed enough: the walking kernel takes it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   build_lds_tables(smem, P);
-  __syncthreads();  // the walk columns reuse the khi area, the nibble tables the shift areas
+  __syncthreads();  // the walk columns reuse the khi area, x^(8m) the klo area
   build_walk_cols(P);
-  for (uint32_t i = threadIdx.x; i < 2048u; i += blockDim.x) {  // the finish multiply's nibble tables
-    const uint32_t q = i >> 7, nib = (i >> 4) & 7u, e = i & 15u;
-    uint32_t K = 0x80000000u;  // x^(32q): 4q zero-byte steps of the register from x^0
-    for (uint32_t b = 0; b < 4u * q; ++b) K = (K >> 8) ^ P.master[K & 0xFFu];
-    *(__attribute__((address_space(3))) uint32_t*)(size_t)(LDS_NT_OFF(q) + 64u * nib + 4u * e) = gf2_mulmod(e << (4u * nib), K);
+  if (threadIdx.x >= 128u && threadIdx.x < 196u) {  // the finish factors' columns
+    const uint32_t f = threadIdx.x - 128u;
+    uint32_t K, base;
+    if (f < 64u) {  // x^(8m): m zero-byte steps of the register from x^0
+      K = 0x80000000u;
+      for (uint32_t i = 0; i < f; ++i) K = (K >> 8) ^ P.master[K & 0xFFu];
+      base = LDS_XMC_OFF(f);
+    } else {
+      K = stream_xinv(f - 64u);
+      base = LDS_XIC_OFF(f - 64u);
+    }
+    for (uint32_t i = 0; i < 32u; ++i) {
+      *(__attribute__((address_space(3))) uint32_t*)(size_t)(base + 4u * i) = K;
+      K = (K >> 1) ^ (0xEDB88320u & (0u - (K & 1u)));
+    }
   }
   const uint32_t lane = threadIdx.x & 63u;
   // this wave's event map: 64 chunks x {end in chain 0, start in chain 0, end
-  // in chain 1, start in chain 1}, each the chain byte j = 4 word + t (0..63),
-  // 0xFF = none (bit 7: absent; an absent byte's word, 63, matches no word)
+  // in chain 1, start in chain 1}, each the chain byte + 1 (0 = none)
   const uint32_t smap = LDS_SMAP_OFF + (threadIdx.x >> 6) * 256u;
-  *(__attribute__((address_space(3))) uint32_t*)(size_t)(smap + 4u * lane) = 0xFFFFFFFFu;
+  *(__attribute__((address_space(3))) uint32_t*)(size_t)(smap + 4u * lane) = 0u;
   __syncthreads();
   const uint32_t lo = (lane & 31u) * 4u, hi = lo | 0x10000u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -1218,15 +1234,14 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
   const uint64_t ntile = t_last >= t_first ? t_last - t_first + 1u : 0u;
   auto tbase = [&](uint64_t t) -> int64_t { return a0 + (int64_t)(t << 13); };
 
-  // the window: start and end of records bt + lane (clamped to n - 1; masked
-  // at use), both absolute: the tile tests are one 64-bit compare each, the
-  // tile-relative bytes the low words' difference
-  uint64_t Wo, We;
+  // the window: off / len of records bt + lane (clamped to n - 1; masked at use)
+  uint64_t Wo;
+  uint32_t Wl;
   auto win_load = [&](uint64_t b) {
     const uint64_t i = b + lane;
     const uint64_t ic = i < n ? i : n - 1u;
     Wo = P.off[ic];
-    We = Wo + P.len[ic];
+    Wl = P.len[ic];
   };
   uint64_t bt = r_lo;  // the first record that has not ended yet
   uint32_t carry = 0;  // the record open at the tile's end, its raw value aligned to the tile's end
@@ -1266,28 +1281,66 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
 
   auto process = [&](const uint32_t (&U)[32], uint64_t t, auto&& issue_next) {
     const int64_t tb = tbase(t);
-    // --- a tile with no event at all (43% of config 3's: records of 8 KiB
-    // and more) is told by the window's first record alone, a scalar test:
-    // ends are sorted, so when record bt does not end here no later one does,
-    // and none starts before bt ends.  Such a tile skips the map.
+    // --- map: the window's records that end in this tile write their events
+    // (long records) into the wave's LDS map; a tile in which all 64 window
+    // records end walks the next window too (rare: records of ~128 B or less)
+    uint32_t Kw = 0;       // (uniform) words holding an event: chain 0 bits 0-15, chain 1 bits 16-31
+    bool shorts = false;   // (uniform) a short record ends in this tile
+    uint64_t wb = bt;      // base of the window being mapped
+    uint32_t nwin = 0;     // full windows (64 records ending here) before the last one
+    uint32_t cntw;         // records of the last window ending here
+    int32_t re, rs;        // the last window's tile-relative end and start (start clamped to >= -128)
+    bool lng, sin;         // long record; its start lies in this tile
+    for (;;) {
+      const int64_t e64 = (int64_t)(Wo + Wl) - tb, s64 = (int64_t)Wo - tb;
+      const bool inr = wb + lane < r_hi;
+      const bool ends = inr && e64 < 8192;
+      cntw = (uint32_t)__builtin_popcountll(__ballot(ends));
+      lng = Wl >= STREAM_LONG;
+      sin = inr && s64 >= 0 && s64 < 8192;
+      re = (int32_t)(ends ? e64 : 8191);
+      rs = (int32_t)(s64 < -128 ? -128 : (s64 > 8191 ? 8191 : s64));
+      const bool ev_e = ends && lng, ev_s = sin && lng;
+      typedef __attribute__((address_space(3))) unsigned char lds_u8w_t;
+      if (ev_e) *(lds_u8w_t*)(size_t)(smap + 4u * ((uint32_t)re >> 7) + (((uint32_t)re >> 5) & 2u)) = (unsigned char)((re & 63) + 1);
+      if (ev_s) *(lds_u8w_t*)(size_t)(smap + 4u * ((uint32_t)rs >> 7) + (((uint32_t)rs >> 5) & 2u) + 1u) = (unsigned char)((rs & 63) + 1);
+      Kw |= wave_or_u32((ev_e ? 1u << (((uint32_t)re & 127u) >> 2) : 0u) | (ev_s ? 1u << (((uint32_t)rs & 127u) >> 2) : 0u));
+      shorts = shorts || __any(ends && !lng);
+      if (cntw < 64u) break;
+      wb += 64u;
+      ++nwin;
+      win_load(wb);  // (a dependent load: tiles of many small records only)
+    }
+    const uint64_t bt0 = bt;
+    bt = wb + cntw;
+    // no event at all: no record ends here, and the open record started before
+    const bool z = nwin == 0u && cntw == 0u && !__builtin_amdgcn_readfirstlane((int)(sin && lng));
+    // the next tile's window: this one shifted by cntw (lands while this tile is checksummed)
     {
-      const uint64_t fo = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(Wo >> 32)) << 32) |
-                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)Wo);
-      const uint64_t fe_ = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(We >> 32)) << 32) |
-                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)We);
-      const int64_t fe = (int64_t)fe_ - tb, fs = (int64_t)fo - tb;
-      if (bt >= r_hi || (fe >= 8192 && !(fe_ - fo >= STREAM_LONG && fs >= 0 && fs < 8192))) {
-        issue_next();
-        __builtin_amdgcn_sched_barrier(0);
-        if (dqcnt) qpush(dqv, dqcnt);
-        dqcnt = 0;
-        if constexpr (ABLATE == 3) {  // diagnostic: payload loads only
-          uint32_t x = 0;
-#pragma unroll
-          for (int k = 0; k < 32; ++k) x ^= U[k];
-          if (x == 0x9E3779B1u) P.out[0] = x;
-          return;
-        }
+      const uint32_t src = lane + cntw;
+      const int sp = (int)((src & 63u) << 2);
+      const uint32_t wlo = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)(uint32_t)Wo);
+      const uint32_t whi = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)(uint32_t)(Wo >> 32));
+      const uint32_t wl = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)Wl);
+      Wo = ((uint64_t)whi << 32) | wlo;
+      Wl = wl;
+      if (src >= 64u) {  // the new entries only
+        const uint64_t i2 = bt + lane;
+        const uint64_t ic = i2 < n ? i2 : n - 1u;
+        Wo = P.off[ic];
+        Wl = P.len[ic];
+      }
+    }
+    // then the payload one tile ahead: after the window, so that waiting for
+    // the window at the next tile never waits for that payload
+    issue_next();
+    __builtin_amdgcn_sched_barrier(0);
+    if (dqcnt) qpush(dqv, dqcnt);
+    dqcnt = 0;
+    if constexpr (ABLATE == 0 || ABLATE >= 4) {
+      // (ABLATE 4 / 5, diagnostic: every tile takes this path -- the bulk
+      // chains + Horner cost without / with the payload loads)
+      if (z || ABLATE >= 4) {  // (uniform) no event in the tile
         // the carry (the open record's raw CRC up to this tile, aligned to
         // its start) enters as lane 0's initial register: the Horner shift of
         // lane 0 then carries it to the tile end with the chunk
@@ -1304,71 +1357,13 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
         return;
       }
     }
-    // --- map: the window's records that end in this tile write their events
-    // (long records) into the wave's LDS map; a tile in which all 64 window
-    // records end walks the next window too (rare: records of ~128 B or less)
-    uint32_t Kw = 0;       // (uniform) words holding an event: chain 0 bits 0-15, chain 1 bits 16-31
-    bool shorts = false;   // (uniform) a short record ends in this tile
-    uint64_t wb = bt;      // base of the window being mapped
-    uint32_t nwin = 0;     // full windows (64 records ending here) before the last one
-    uint32_t cntw;         // records of the last window ending here
-    int32_t re, rs;        // the last window's tile-relative end and start
-    bool lng, sin;         // long record; its start lies in this tile
-    const int64_t te = tb + 8192;
-    for (;;) {
-      const uint64_t lim = r_hi - wb;  // > 0: bt < r_hi here
-      const bool inr = lane < (lim < 64u ? (uint32_t)lim : 64u);
-      const bool ends = inr && (int64_t)We < te;
-      cntw = (uint32_t)__builtin_popcountll(__ballot(ends));
-      lng = (uint32_t)We - (uint32_t)Wo >= STREAM_LONG;  // the length (< 2^32) from the low words
-      sin = inr && (int64_t)Wo >= tb && (int64_t)Wo < te;
-      // tile-relative bytes from the low words: exact whenever they are used
-      // (an end in the tile; a start in the tile, or a short record's)
-      re = ends ? (int32_t)((uint32_t)We - (uint32_t)tb) : 8191;
-      rs = (int32_t)((uint32_t)Wo - (uint32_t)tb);
-      const bool ev_e = ends && lng, ev_s = sin && lng;
-      typedef __attribute__((address_space(3))) unsigned char lds_u8w_t;
-      if (ev_e) *(lds_u8w_t*)(size_t)(smap + 4u * ((uint32_t)re >> 7) + (((uint32_t)re >> 5) & 2u)) = (unsigned char)(re & 63);
-      if (ev_s) *(lds_u8w_t*)(size_t)(smap + 4u * ((uint32_t)rs >> 7) + (((uint32_t)rs >> 5) & 2u) + 1u) = (unsigned char)(rs & 63);
-      Kw |= wave_or_u32((ev_e ? 1u << (((uint32_t)re & 127u) >> 2) : 0u) | (ev_s ? 1u << (((uint32_t)rs & 127u) >> 2) : 0u));
-      shorts = shorts || __any(ends && !lng);
-      if (cntw < 64u) break;
-      wb += 64u;
-      ++nwin;
-      win_load(wb);  // (a dependent load: tiles of many small records only)
-    }
-    const uint64_t bt0 = bt;
-    bt = wb + cntw;
-    // the next tile's window: this one shifted by cntw (lands while this tile is checksummed)
-    {
-      const uint32_t src = lane + cntw;
-      const int sp = (int)((src & 63u) << 2);
-      const uint32_t olo = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)(uint32_t)Wo);
-      const uint32_t ohi = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)(uint32_t)(Wo >> 32));
-      const uint32_t elo = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)(uint32_t)We);
-      const uint32_t ehi = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)(uint32_t)(We >> 32));
-      Wo = ((uint64_t)ohi << 32) | olo;
-      We = ((uint64_t)ehi << 32) | elo;
-      if (src >= 64u) {  // the new entries only
-        const uint64_t i2 = bt + lane;
-        const uint64_t ic = i2 < n ? i2 : n - 1u;
-        Wo = P.off[ic];
-        We = Wo + P.len[ic];
-      }
-    }
-    // then the payload one tile ahead: after the window, so that waiting for
-    // the window at the next tile never waits for that payload
-    issue_next();
-    __builtin_amdgcn_sched_barrier(0);
-    if (dqcnt) qpush(dqv, dqcnt);
-    dqcnt = 0;
     // --- chunk-lane view: this chunk's events (byte + 1 in its chain, 0 = none)
     typedef __attribute__((address_space(3))) uint32_t lds_u32w_t;
-    const uint32_t ev = *(lds_u32w_t*)(size_t)(smap + 4u * lane);
-    if (ev != 0xFFFFFFFFu) *(lds_u32w_t*)(size_t)(smap + 4u * lane) = 0xFFFFFFFFu;
-    const uint64_t M1 = __ballot((~ev & 0x00800080u) != 0u);  // chunks holding an end
-    const uint64_t Ms = __ballot((~ev & 0x80008000u) != 0u);  // chunks holding a start
-    const bool ke0 = __any((~ev & 0x80u) != 0u), ke1 = __any((~ev & 0x800000u) != 0u);
+    uint32_t ev = *(lds_u32w_t*)(size_t)(smap + 4u * lane);
+    if (ev) *(lds_u32w_t*)(size_t)(smap + 4u * lane) = 0u;
+    const uint64_t M1 = __ballot((ev & 0x00FF00FFu) != 0u);  // chunks holding an end
+    const uint64_t Ms = __ballot((ev & 0xFF00FF00u) != 0u);  // chunks holding a start
+    const bool ke0 = __any((ev & 0xFFu) != 0u), ke1 = __any((ev & 0xFF0000u) != 0u);
     if (ABLATE == 3) {  // diagnostic: payload loads only
       uint32_t x = 0;
 #pragma unroll
@@ -1383,46 +1378,35 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     // the tile's first start it rides in lane 0's chain, into that record's
     // capture, R0 or the Horner value of chunk 0; a reset drops it.
     uint32_t c0 = U[0] ^ (lane == 0u ? carry : 0u), c1 = U[16], x0 = 0u, x1 = 0u, ub0 = 0u, ub1 = 0u;
-    // a chain's events at word k: end byte (ev >> 8*(2h)) and start byte
-    // (ev >> 8*(2h+1)), each 4 word + t; a word matches k only when present
-    auto at = [&](uint32_t e, int sh, int k) -> bool { return ((e >> (sh + 2)) & 63u) == (uint32_t)k; };
-    auto mlo_of = [&](uint32_t e, int sh) -> uint32_t {  // the mask of the start word's t bytes before it
-      return __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0u, ((e >> sh) & 3u) << 3);
-    };
+    const uint32_t Km = (Kw & 0xFFFFu) | (Kw >> 16);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const uint32_t w0 = k + 1 < 16 ? U[k + 1] : 0u, w1 = k + 1 < 16 ? U[17 + k] : 0u;
       uint32_t i0 = c0, i1 = c1, n0 = w0, n1 = w1;
-      // (uniform) some lane's chain 0 / chain 1 has an event in word k: the
-      // branches only select the steps' inputs; both steps follow them, so
-      // their eight lookups issue together
-      if (Kw & (1u << k)) {
+      if (Km & (1u << k)) {
         uint32_t e = ev;
         asm volatile("" : "+v"(e));  // recomputed here, not hoisted: fewer VGPRs through the loop
-        const bool me = at(e, 0, k), ms = at(e, 8, k);
-        const uint32_t mlo = mlo_of(e, 8);
-        x0 = me ? c0 : x0;
-        ub0 = me ? U[k] : ub0;
-        i0 = ms ? ~(U[k] | mlo) : c0;
-        n0 = ms ? (w0 ^ mlo) : w0;
-      }
-      if (Kw & (0x10000u << k)) {
-        uint32_t e = ev;
-        asm volatile("" : "+v"(e));
-        const bool me = at(e, 16, k), ms = at(e, 24, k);
-        const uint32_t mlo = mlo_of(e, 24);
-        x1 = me ? c1 : x1;
-        ub1 = me ? U[16 + k] : ub1;
-        i1 = ms ? ~(U[16 + k] | mlo) : c1;
-        n1 = ms ? (w1 ^ mlo) : w1;
+        const uint32_t be0 = e & 0xFFu, bs0 = (e >> 8) & 0xFFu, be1 = (e >> 16) & 0xFFu, bs1 = e >> 24;
+        // chain byte j + 1 at word k: (j >> 2) == k  <=>  ((b - 1) >> 2) == k, b != 0
+        const bool me0 = be0 && ((be0 - 1u) >> 2) == (uint32_t)k, ms0 = bs0 && ((bs0 - 1u) >> 2) == (uint32_t)k;
+        const bool me1 = be1 && ((be1 - 1u) >> 2) == (uint32_t)k, ms1 = bs1 && ((bs1 - 1u) >> 2) == (uint32_t)k;
+        const uint32_t mlo0 = (1u << (((bs0 - 1u) & 3u) << 3)) - 1u, mlo1 = (1u << (((bs1 - 1u) & 3u) << 3)) - 1u;
+        x0 = me0 ? c0 : x0;
+        ub0 = me0 ? U[k] : ub0;
+        x1 = me1 ? c1 : x1;
+        ub1 = me1 ? U[16 + k] : ub1;
+        i0 = ms0 ? ~(U[k] | mlo0) : c0;
+        n0 = ms0 ? (w0 ^ mlo0) : w0;
+        i1 = ms1 ? ~(U[16 + k] | mlo1) : c1;
+        n1 = ms1 ? (w1 ^ mlo1) : w1;
       }
       c0 = crc_step_x(smem, i0, n0, lo, hi);
       c1 = crc_step_x(smem, i1, n1, lo, hi);
     }
-    const uint32_t cap0 = ke0 ? stream_capture(smem, x0, ub0, ev & 3u, lo) : 0u;
-    const uint32_t cap1 = ke1 ? stream_capture(smem, x1, ub1, (ev >> 16) & 3u, lo) : 0u;
+    const uint32_t cap0 = ke0 ? stream_capture(smem, x0, ub0, ((ev & 0xFFu) - 1u) & 3u, lo) : 0u;
+    const uint32_t cap1 = ke1 ? stream_capture(smem, x1, ub1, (((ev >> 16) & 0xFFu) - 1u) & 3u, lo) : 0u;
     const uint32_t R0 = c0;
-    const uint32_t T = (ev >> 31) ? (shift_bytes32<2>(smem, c0) ^ c1) : c1;
+    const uint32_t T = (ev >> 24) ? c1 : (shift_bytes32<2>(smem, c0) ^ c1);
     // --- Horner inside the tile: T to the chunk before the next END's chunk
     const uint64_t above = lane == 63u ? 0ull : (M1 >> (lane + 1u)) << (lane + 1u);
     const uint32_t cn = above ? (uint32_t)__builtin_ctzll(above) : 64u;
@@ -1445,7 +1429,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
       if (in && lng_) {
         const bool h = j >= 64u;
         const uint32_t Pv = h ? (shift_bytes32<2>(smem, H) ^ R0c) : H;
-        fv = ~(stream_mulx8(smem, Pv, j & 63u, lo) ^ (h ? A1c : A0c));
+        fv = ~(stream_mulcol(Pv, LDS_XMC_OFF(j & 63u)) ^ (h ? A1c : A0c));
       }
       return fv;
     };
@@ -1494,6 +1478,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     process(U1, t_first + i + 1, [&] { stream_issue<ABLATE>(P, tcl(i + 2), end4, lane, U0); });
   }
   if (i < ntile) process(U0, t_first + i, none);
+  if (ABLATE >= 4 && carry == 0x9E3779B1u) P.out[0] = carry;  // keeps the ablated chains (and loads) alive
   if (ABLATE == 3) return;
   if (dqcnt) qpush(dqv, dqcnt);
   qstore(qv, lane >= qs && lane < qf);
@@ -1560,7 +1545,9 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   else  // a caller's batch: check + cuts in one pass over its descriptors
     hipLaunchKernelGGL(stream_prep, dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, st, *P, W);
   const int ablate = (variant >> 8) & 0xF;
-  const void* fn = ablate == 3 ? (const void*)crc32_stream_kernel<3>
+  const void* fn = ablate == 4 ? (const void*)crc32_stream_kernel<4>
+                 : ablate == 5 ? (const void*)crc32_stream_kernel<5>
+                 : ablate == 3 ? (const void*)crc32_stream_kernel<3>
                  : ablate == 2 ? (const void*)crc32_stream_kernel<2> : (const void*)crc32_stream_kernel<0>;
   const size_t lds = LDS_SCRATCH_OFF + LDS_SMAP_BYTES;
   e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

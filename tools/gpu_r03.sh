@@ -56,7 +56,7 @@ if has sha; then
   tail -1 gpurun_out/bench_${R}_sha_c3.log
 fi
 if has shaab; then  # SHA-256 config 3: the pair kernel against its compute-only ablation (sha_pair 2) and single blocks
-  timeout -k 10 600 python3 bench.py --digest sha256 --config 3 --steps 3 --warmup 1 --variants -,p2,p3,p0 --rounds 3 --no-cpu-baseline --no-host-roundtrip --no-stream-ceiling > gpurun_out/ab_${R}_sha_c3.log 2>&1; step ab_sha_c3 $?
+  timeout -k 10 600 python3 bench.py --digest sha256 --config 3 --steps 3 --warmup 1 --variants=-,p2,p3,p0 --rounds 3 --no-cpu-baseline --no-host-roundtrip --no-stream-ceiling > gpurun_out/ab_${R}_sha_c3.log 2>&1; step ab_sha_c3 $?
   tail -1 gpurun_out/ab_${R}_sha_c3.log
 fi
 if has shakt; then  # kernel-trace stats of SHA-256 config 3 (the order sort and the hash kernel)
