@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <future>
 #include <mutex>
 #include <numeric>
@@ -215,6 +216,7 @@ struct lsmck_ctx {
   } wd;
   lsmck_wal_rec* h_wrecs = nullptr;  // device WAL replay: the records' pinned landing buffer (grow-only)
   size_t cap_hwrecs = 0;
+  hipEvent_t wal_emit_ev = nullptr, wal_recs_ev = nullptr;  // records read back beside the CRC pass
   uint64_t* h_woff = nullptr;  // pinned staging of the same
   size_t cap_hwoff = 0;
   uint32_t* h_wlen = nullptr;
@@ -600,9 +602,11 @@ int check_ctx(lsmck_ctx* ctx) {
 // CRC batch + GPU compare with expected[] (all device pointers) on st, into the
 // context's pooled buffers; synchronous (the counts come back to the host).
 // Caller holds ctx->mu and orders st on the scratch.
+// while_running: host work done after the launches, before the wait (the
+// WAL replay copies its records out meanwhile)
 int device_verify(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint32_t* len,
                   const uint32_t* expected, size_t n, hipStream_t st, uint64_t* n_bad, uint64_t* first_bad,
-                  bool trusted = false) {
+                  bool trusted = false, const std::function<int()>& while_running = {}) {
   int rc = ensure_dev(&ctx->d_vcrc, &ctx->cap_vcrc, std::max<size_t>(n, 1));
   if (rc) return rc;
   rc = crc_desc_device(ctx, ctx->scratch, base, off, len, n, ctx->d_vcrc, st, trusted);
@@ -612,7 +616,9 @@ int device_verify(lsmck_ctx* ctx, const uint8_t* base, const uint64_t* off, cons
   rc = lsmk_launch_crc32_compare(ctx->d_vcrc, expected, n, ctx->d_verify, ctx->d_verify + 1, st);
   if (rc) return launch_rc(rc, "compare kernel");
   HIPCHK(hipMemcpyAsync(ctx->h_verify, ctx->d_verify, 16, hipMemcpyDeviceToHost, st));
+  const int hrc = while_running ? while_running() : 0;
   HIPCHK(hipStreamSynchronize(st));
+  if (hrc) return hrc;
   if (n_bad) *n_bad = ctx->h_verify[0];
   if (first_bad) *first_bad = ctx->h_verify[0] ? ctx->h_verify[1] : n;
   return ctx->h_verify[0] ? 1 : 0;
@@ -832,6 +838,8 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
     if (p) (void)hipHostFree(p);
   if (ctx->h_verify) (void)hipHostFree(ctx->h_verify);
   if (ctx->h_wrecs) (void)hipHostFree(ctx->h_wrecs);
+  if (ctx->wal_emit_ev) (void)hipEventDestroy(ctx->wal_emit_ev);
+  if (ctx->wal_recs_ev) (void)hipEventDestroy(ctx->wal_recs_ev);
   if (ctx->wal_host) (void)hipHostFree(ctx->wal_host);
   if (ctx->d_wimg) (void)hipFree(ctx->d_wimg);
   if (ctx->scratch_ev) (void)hipEventDestroy(ctx->scratch_ev);
@@ -1028,32 +1036,44 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
       return rc;
     rc = lsmk_wal_emit(img, n, W.chain, W.pos, W.info, (uint32_t)m, W.recs, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st);
     if (rc) return launch_rc(rc, "wal emit kernel");
-    // the records go to a pinned buffer while the CRC pass runs (DMA at the
-    // link rate, no sync of its own; a copy into the caller's pageable array
-    // ran at a few GiB/s, page faults included)
+    // The records are read back on a second stream while the CRC pass runs,
+    // into a pinned buffer (DMA at the link rate; a copy into the caller's
+    // pageable array ran at a few GiB/s, page faults included), and copied
+    // into the caller's array on host threads before the CRC pass is waited
+    // for.  All m records go out (the accepted ones are a prefix; the rest of
+    // the caller's array is unspecified).
+    std::function<int()> copy_out;
     if (recs && cap) {
-      if ((rc = ensure_pinned(&ctx->h_wrecs, &ctx->cap_hwrecs, m))) return rc;
-      HIPCHK(hipMemcpyAsync(ctx->h_wrecs, W.recs, m * sizeof(lsmck_wal_rec), hipMemcpyDeviceToHost, st));
+      if ((rc = ensure_pinned(&ctx->h_wrecs, &ctx->cap_hwrecs, m)) || (rc = stage_init(ctx->stage[0]))) return rc;
+      if (!ctx->wal_emit_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_emit_ev, hipEventDisableTiming));
+      if (!ctx->wal_recs_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_recs_ev, hipEventDisableTiming));
+      hipStream_t s2 = ctx->stage[0].s;
+      HIPCHK(hipEventRecord(ctx->wal_emit_ev, st));
+      HIPCHK(hipStreamWaitEvent(s2, ctx->wal_emit_ev, 0));
+      HIPCHK(hipMemcpyAsync(ctx->h_wrecs, W.recs, m * sizeof(lsmck_wal_rec), hipMemcpyDeviceToHost, s2));
+      HIPCHK(hipEventRecord(ctx->wal_recs_ev, s2));
+      copy_out = [&]() -> int {  // pinned -> the caller's array, on several threads (first touch of its pages)
+        HIPCHK(hipEventSynchronize(ctx->wal_recs_ev));
+        const size_t cnt = std::min(m, cap), bytes = cnt * sizeof(lsmck_wal_rec);
+        const unsigned T = bytes >= (4u << 20) ? std::max(1u, std::min(ctx->stage_threads, 8u)) : 1u;
+        std::vector<std::thread> pool;
+        auto part = [&](unsigned t) {
+          const size_t a = cnt * t / T, b = cnt * (t + 1) / T;
+          memcpy(recs + a, ctx->h_wrecs + a, (b - a) * sizeof(lsmck_wal_rec));
+        };
+        for (unsigned t = 1; t < T; ++t) pool.emplace_back(part, t);
+        part(0);
+        for (auto& th : pool) th.join();
+        return 0;
+      };
     }
     // the payloads of one image in log order: the stream kernel, no eligibility check
-    rc = device_verify(ctx, img, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, m, st, &nbad, &first, true);
+    rc = device_verify(ctx, img, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, m, st, &nbad, &first, true, copy_out);
+    if (copy_out) (void)hipEventSynchronize(ctx->wal_recs_ev);  // (an early error return above: the DMA has drained)
     if (rc < 0) return rc;
   }
-  tr.mark("emit+crc+compare (sync)");
+  tr.mark("emit+crc+compare+records (sync)");
   const size_t accepted = nbad ? (size_t)first : m;
-  if (recs && cap && accepted) {  // pinned -> the caller's array, on several threads (first touch of its pages)
-    const size_t cnt = std::min(accepted, cap), bytes = cnt * sizeof(lsmck_wal_rec);
-    const unsigned T = bytes >= (4u << 20) ? std::max(1u, std::min(ctx->stage_threads, 8u)) : 1u;
-    std::vector<std::thread> pool;
-    auto part = [&](unsigned t) {
-      const size_t a = cnt * t / T, b = cnt * (t + 1) / T;
-      memcpy(recs + a, ctx->h_wrecs + a, (b - a) * sizeof(lsmck_wal_rec));
-    };
-    for (unsigned t = 1; t < T; ++t) pool.emplace_back(part, t);
-    part(0);
-    for (auto& th : pool) th.join();
-  }
-  tr.mark("records to host");
   if (nrec) *nrec = accepted;
   if (nbad) {
     lsmck_wal_rec r;

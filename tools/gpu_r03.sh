@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 evidence in one GPU call.  Steps are picked by STEPS (space list):
-#   c4pmc smoke quick pytest bench c3w c2 kt c3pmc sha shaab shakt shapmc wal (run in this order)
+#   c4pmc smoke quick pytest bench c3w c2 kt kt3w c3wpmc c3pmc sha shaab shakt shapmc wal (run in this order)
 # Every GPU step has its own time limit; any failure ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -44,6 +44,17 @@ if has kt; then  # kernel-trace stats of the default bench command
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt_${R}_c3 -o kt -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-roundtrip > gpurun_out/kt_${R}_c3.log 2>&1; step kt_c3 $?
   python3 tools/kt_stats.py gpurun_out/kt_${R}_c3 > gpurun_out/kt_stats_${R}_c3.txt
   cat gpurun_out/kt_stats_${R}_c3.txt
+fi
+if has kt3w; then  # kernel-trace stats of config 3 framed as a WAL image
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt_${R}_c3w -o kt -- python3 bench.py --wal-framed --steps 10 --warmup 2 --no-cpu-baseline --no-host-roundtrip > gpurun_out/kt_${R}_c3w.log 2>&1; step kt_c3w $?
+  python3 tools/kt_stats.py gpurun_out/kt_${R}_c3w > gpurun_out/kt_stats_${R}_c3w.txt
+  cat gpurun_out/kt_stats_${R}_c3w.txt
+fi
+if has c3wpmc; then
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d gpurun_out/pmc_${R}_c3w_$C -o pmc -- python3 bench.py --wal-framed --steps 3 --warmup 1 --no-cpu-baseline --no-host-roundtrip --no-stream-ceiling > gpurun_out/pmc_${R}_c3w_$C.log 2>&1; step pmc_c3w_$C $?
+  done
+  python3 tools/pmc_summary.py gpurun_out/pmc_${R}_c3w_FETCH_SIZE gpurun_out/pmc_${R}_c3w_WRITE_SIZE config3w > gpurun_out/pmc_summary_${R}_c3w.json
 fi
 if has c3pmc; then
   for C in FETCH_SIZE WRITE_SIZE; do
