@@ -21,8 +21,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <functional>
 #include <future>
+#include <memory>
 #include <mutex>
 #include <numeric>
 #include <string>
@@ -32,6 +34,7 @@
 #include "lsmck.h"
 #include "lsmck_device.h"
 #include "lsmck_internal.h"
+#include "lsmck_pool.h"
 
 using lsmck::CrcParams;
 using lsmck::ShaParams;
@@ -217,6 +220,7 @@ struct lsmck_ctx {
   lsmck_wal_rec* h_wrecs = nullptr;  // device WAL replay: the records' pinned landing buffer (grow-only)
   size_t cap_hwrecs = 0;
   hipEvent_t wal_emit_ev = nullptr, wal_recs_ev = nullptr;  // records read back beside the CRC pass
+  std::unique_ptr<lsmck_host::HostPool> pool;  // staging copy threads (created on first use)
   uint64_t* h_woff = nullptr;  // pinned staging of the same
   size_t cap_hwoff = 0;
   uint32_t* h_wlen = nullptr;
@@ -427,19 +431,21 @@ int stage_init(Stage& S) {
 // Pageable payload into a pinned slot.  One thread copies at ~20 GiB/s, below
 // the PCIe link the slot then feeds; large chunks are split over `threads`
 // (contiguous byte ranges, 4 KiB-aligned cuts).
-void stage_copy(uint8_t* dst, const uint8_t* src, size_t n, unsigned threads) {
+lsmck_host::HostPool& host_pool(lsmck_ctx* ctx) {
+  if (!ctx->pool) ctx->pool.reset(new lsmck_host::HostPool());
+  return *ctx->pool;
+}
+
+void stage_copy(lsmck_ctx* ctx, uint8_t* dst, const uint8_t* src, size_t n, unsigned threads) {
   if (threads <= 1 || n < (8u << 20)) {
     memcpy(dst, src, n);
     return;
   }
-  std::vector<std::thread> pool;
   const size_t part = ((n / threads) + 4095) & ~(size_t)4095;
-  for (unsigned t = 1; t < threads; ++t) {
+  host_pool(ctx).run(threads, [=](unsigned t) {
     const size_t a = std::min(n, t * part), b = std::min(n, (t + 1) * part);
-    if (a < b) pool.emplace_back([=] { memcpy(dst + a, src + a, b - a); });
-  }
-  memcpy(dst, src, std::min(n, part));
-  for (auto& th : pool) th.join();
+    if (a < b) memcpy(dst + a, src + a, b - a);
+  });
 }
 
 // Wait for a slot's previous chunk and hand its results to the caller.
@@ -533,17 +539,14 @@ int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
     } else {
       if ((rc = ensure_pinned(&S.h_pay, &S.cap_h_pay, pay_bytes + 16))) return rc;
       if (use_span) {
-        stage_copy(S.h_pay, J.base + span_lo, pay_bytes, ctx->stage_threads);
+        stage_copy(ctx, S.h_pay, J.base + span_lo, pay_bytes, ctx->stage_threads);
       } else if (!J.off) {
         // sparse fixed records: record r+i lands at i*flen
         const unsigned T = pay_bytes >= (8u << 20) ? std::max(1u, ctx->stage_threads) : 1u;
         auto gather = [&](size_t i0, size_t i1) {
           for (size_t i = i0; i < i1; ++i) memcpy(S.h_pay + i * J.flen, J.base + (r + i) * J.stride, J.flen);
         };
-        std::vector<std::thread> pool;
-        for (unsigned t = 1; t < T; ++t) pool.emplace_back(gather, cnt * t / T, cnt * (t + 1) / T);
-        gather(0, cnt / T);
-        for (auto& th : pool) th.join();
+        host_pool(ctx).run(T, [&](unsigned t) { gather(cnt * t / T, cnt * (t + 1) / T); });
       } else {
         // gather: record i lands at its packed position S.h_off[i]; large
         // chunks split the records over stage_threads threads
@@ -551,10 +554,7 @@ int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
         auto gather = [&](size_t i0, size_t i1) {
           for (size_t i = i0; i < i1; ++i) memcpy(S.h_pay + S.h_off[i], J.base + J.off[r + i], J.len[r + i]);
         };
-        std::vector<std::thread> pool;
-        for (unsigned t = 1; t < T; ++t) pool.emplace_back(gather, cnt * t / T, cnt * (t + 1) / T);
-        gather(0, cnt / T);
-        for (auto& th : pool) th.join();
+        host_pool(ctx).run(T, [&](unsigned t) { gather(cnt * t / T, cnt * (t + 1) / T); });
       }
       h_src = S.h_pay;
     }
@@ -1056,14 +1056,10 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
         HIPCHK(hipEventSynchronize(ctx->wal_recs_ev));
         const size_t cnt = std::min(m, cap), bytes = cnt * sizeof(lsmck_wal_rec);
         const unsigned T = bytes >= (4u << 20) ? std::max(1u, std::min(ctx->stage_threads, 8u)) : 1u;
-        std::vector<std::thread> pool;
-        auto part = [&](unsigned t) {
+        host_pool(ctx).run(T, [&](unsigned t) {
           const size_t a = cnt * t / T, b = cnt * (t + 1) / T;
           memcpy(recs + a, ctx->h_wrecs + a, (b - a) * sizeof(lsmck_wal_rec));
-        };
-        for (unsigned t = 1; t < T; ++t) pool.emplace_back(part, t);
-        part(0);
-        for (auto& th : pool) th.join();
+        });
         return 0;
       };
     }
@@ -1148,7 +1144,7 @@ static int wal_upload(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned)
     Stage& S = ctx->stage[slot];
     const size_t c = std::min(kChunkBytes, n - o);
     HIPCHK(hipEventSynchronize(S.done));  // the slot's previous DMA has drained
-    stage_copy(S.h_pay, img + o, c, ctx->stage_threads);
+    stage_copy(ctx, S.h_pay, img + o, c, ctx->stage_threads);
     HIPCHK(hipMemcpyAsync(ctx->d_wimg + o, S.h_pay, c, hipMemcpyHostToDevice, S.s));
     HIPCHK(hipEventRecord(S.done, S.s));
     rc = lsmk_wal_mark_range(ctx->d_wimg, n, o, o + c, W.bits, W.pre, S.s);  // kChunkBytes: a multiple of 64

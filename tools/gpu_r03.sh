@@ -85,4 +85,10 @@ if has wal; then  # host WAL replay phases (LSMCK_WAL_TRACE) and the registered-
   LSMCK_WAL_TRACE=1 timeout -k 10 300 python3 tools/wal_diag.py > gpurun_out/wal_diag_${R}.log 2>&1; step wal_diag $?
   tail -30 gpurun_out/wal_diag_${R}.log
 fi
+if has walkt; then  # kernel trace of the WAL replay (host image and device image)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt_${R}_wal -o kt -- python3 tools/wal_kt.py > gpurun_out/kt_${R}_wal.log 2>&1; step kt_wal $?
+  tail -1 gpurun_out/kt_${R}_wal.log
+  python3 tools/kt_stats.py gpurun_out/kt_${R}_wal > gpurun_out/kt_stats_${R}_wal.txt
+  cat gpurun_out/kt_stats_${R}_wal.txt
+fi
 echo "== done"

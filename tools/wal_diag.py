@@ -37,8 +37,8 @@ def best(fn, reps=5):
     return min(ts)
 
 
-def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 500_000
+def build_image(n, with_descriptors=False):
+    """tree.synthesize_tree's WAL shape: keys 1-39 B, values 0-999 B, 10% removes."""
     rng = np.random.default_rng(5)
     pool = rng.bytes(1 << 20)
     kl = rng.integers(1, 40, size=n)
@@ -58,9 +58,14 @@ def main():
         exp.append(zlib.crc32(d))
         wal += d
     img = np.frombuffer(bytes(wal), dtype=np.uint8)
-    off = np.array(off, dtype=np.uint64)
-    ln = np.array(ln, dtype=np.uint32)
-    exp = np.array(exp, dtype=np.uint32)
+    if not with_descriptors:
+        return img
+    return img, np.array(off, dtype=np.uint64), np.array(ln, dtype=np.uint32), np.array(exp, dtype=np.uint32)
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 500_000
+    img, off, ln, exp = build_image(n, True)
     ctx = Context(0)
     res = {"wal_bytes": len(img), "records": n}
     recs, st, _ = ctx.wal_replay_verify(img)

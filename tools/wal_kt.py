@@ -1,0 +1,46 @@
+"""The default WAL replay (host image: upload + GPU header walk + CRC pass)
+and the device-image replay, ten times each, for a kernel trace:
+  rocprofv3 --kernel-trace --stats -d gpurun_out/kt_wal -o kt -- python3 tools/wal_kt.py
+Same image as tools/wal_diag.py (500k records, 0.24 GB)."""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from lsm_storage_engine_amd.device import Context  # noqa: E402
+import wal_diag  # noqa: E402
+
+
+def main():
+    img = wal_diag.build_image(500_000)
+    ctx = Context(0)
+    out = {}
+    for name, fn in (("host_image", lambda: ctx.wal_replay_verify(img)),):
+        fn()
+        ts = []
+        for _ in range(10):
+            t = time.perf_counter()
+            recs, st, _ = fn()
+            ts.append(time.perf_counter() - t)
+            assert st == 0 and len(recs) == 500_000
+        out[name + "_ms_best"] = round(min(ts) * 1e3, 3)
+    d = ctx.alloc(len(img))
+    d.upload(img)
+    ctx.sync()
+    ts = []
+    for _ in range(10):
+        t = time.perf_counter()
+        recs, st, _ = ctx.wal_replay_verify(len(img), device_ptr=d.ptr)
+        ts.append(time.perf_counter() - t)
+    out["device_image_ms_best"] = round(min(ts) * 1e3, 3)
+    print(out)
+    d.free()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
