@@ -1059,47 +1059,29 @@ __device__ __forceinline__ uint32_t stream_xinv(uint32_t t) {  // x^(-8(4-t))
 // empty and every later empty record sits at its predecessor's end.  Then every
 // 4 KiB page a 128-byte chunk of [off[0], end) lies on holds a byte of some
 // record, so the chunk loads touch only the caller's pages.
-// A caller's batch: the eligibility check and the wave cuts in ONE pass over
-// the descriptors (4 records per thread).  Cut w (0 < w < W) = the first
-// record starting at or after target(w) = off[0] + span*w/W: the record i with
-// off[i-1] < target(w) <= off[i] writes it.  Cuts of a batch that fails the
-// check are never used (the kernel exits on the flag).
-__global__ __launch_bounds__(256) void stream_prep(CrcParams P, uint32_t W) {
+// A caller's batch: the eligibility check, one record per thread with
+// coalesced loads; record i+1's offset and length come from the next lane
+// (lane 63 loads them).  The per-wave cuts follow by binary search
+// (stream_cuts, sorted by then).  A fused check + cuts pass with four records
+// per thread ran 0.31 ms on config 3 against 0.19 + 0.016 for the two.
+__global__ __launch_bounds__(256) void stream_check(CrcParams P) {
   const uint64_t n = P.nrec;
-  const uint64_t i0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
-  const uint64_t o0 = P.off[0], span = P.off[n - 1] + P.len[n - 1] - o0;
-  if (i0 == 0) {
-    P.scuts[0] = 0;
-    P.scuts[W] = n;
-    for (uint64_t w = 1; w < W && span * w / W == 0u; ++w) P.scuts[w] = 0;  // targets at off[0]
+  const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  const uint64_t ic = i < n ? i : n - 1u;
+  const uint64_t o = P.off[ic];
+  const uint32_t l = P.len[ic];
+  uint64_t o1 = ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(o >> 32), 1) << 32) |
+                (uint32_t)__shfl_down((int)(uint32_t)o, 1);
+  uint32_t l1 = (uint32_t)__shfl_down((int)l, 1);
+  if ((threadIdx.x & 63u) == 63u && i + 1u < n) {
+    o1 = P.off[i + 1u];
+    l1 = P.len[i + 1u];
   }
   bool bad = false;
-  if (i0 < n) {
-    uint64_t o[5];
-    uint32_t l[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const uint64_t i = i0 + j < n ? i0 + j : n - 1;
-      o[j] = P.off[i];
-      l[j] = P.len[i];
-    }
-    bad = i0 == 0 && l[0] == 0u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (i0 + j + 1 >= n) {  // the last record: the targets past its start cut at n
-        if (i0 + j + 1 == n)
-          for (uint64_t w = span ? ((o[j] - o0 + 1u) * W + span - 1u) / span : W; w < W; ++w) P.scuts[w] = n;
-        break;
-      }
-      const uint64_t e = o[j] + l[j];
-      const bool b = o[j + 1] < e || o[j + 1] - e > STREAM_MAX_GAP || (l[j + 1] == 0u && o[j + 1] != e);
-      bad = bad || b;
-      if (b || o[j + 1] == o[j]) continue;
-      // the targets in (o[j], o[j+1]]: from the first w with target(w) > o[j]
-      const uint64_t d = o[j] - o0;
-      for (uint64_t w = span ? ((d + 1u) * W + span - 1u) / span : W; w < W && o0 + span * w / W <= o[j + 1]; ++w)
-        P.scuts[w] = i0 + j + 1;
-    }
+  if (i < n) {
+    const uint64_t e = o + l;
+    bad = (i == 0 && l == 0u) ||
+          (i + 1u < n && (o1 < e || o1 - e > STREAM_MAX_GAP || (l1 == 0u && o1 != e)));
   }
   if (__any(bad) && (threadIdx.x & 63u) == 0u) *P.sflag = 0u;  // plain stores of one value: no atomic needed
 }
@@ -1540,10 +1522,9 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   hipError_t e = hipMemsetAsync(P->sflag, 1, 4, st);
   if (e != hipSuccess) return -(int)e;
   const uint32_t W = lsmk_stream_waves(ncu);
-  if (trusted)  // the library's own sorted batch: the cuts by binary search
-    hipLaunchKernelGGL(stream_cuts, dim3((W + 1u + 255u) / 256u), dim3(256), 0, st, *P, W);
-  else  // a caller's batch: check + cuts in one pass over its descriptors
-    hipLaunchKernelGGL(stream_prep, dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, st, *P, W);
+  if (!trusted)  // a caller's batch: checked first (the cuts below then skip on the flag)
+    hipLaunchKernelGGL(stream_check, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, *P);
+  hipLaunchKernelGGL(stream_cuts, dim3((W + 1u + 255u) / 256u), dim3(256), 0, st, *P, W);
   const int ablate = (variant >> 8) & 0xF;
   const void* fn = ablate == 4 ? (const void*)crc32_stream_kernel<4>
                  : ablate == 5 ? (const void*)crc32_stream_kernel<5>
