@@ -247,6 +247,7 @@ struct lsmck_ctx {
   // at most half the free device memory); over it the log takes the host walk
   size_t wal_walk_budget_per_byte = 8;
   int wal_register = 0;  // host WAL images: hipHostRegister the caller's pages instead of the staging copy (A/B)
+  size_t wal_stage_bytes = kChunkBytes;  // host WAL image upload: bytes per staged / DMA'd chunk (A/B)
   // host images of at least this many bytes are uploaded whole and walked on
   // the GPU (0 = always the host walk)
   size_t wal_upload_min = 1u << 20;
@@ -757,6 +758,13 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->wal_gpu_walk = (int)value;
     return 0;
   }
+  if (!strcmp(key, "wal_stage_bytes")) {  // A/B: host WAL image upload chunk (a multiple of 64 KiB, 1..64 MiB)
+    if (value < (1 << 20) || value > (long)kChunkBytes || (value & 0xFFFF))
+      return lsmck_host::set_error(LSMCK_EINVAL, "wal_stage_bytes: a multiple of 64 KiB in [1 MiB, 64 MiB]");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_stage_bytes = (size_t)value;
+    return 0;
+  }
   if (!strcmp(key, "wal_register")) {  // A/B: host WAL image uploaded by DMA from its own pages, pinned in place
     if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "wal_register must be 0 or 1");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1117,10 +1125,13 @@ static int wal_upload(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned)
     if (!registered) (void)hipGetLastError();
     tr.mark("hipHostRegister");
   }
+  // upload chunks ("wal_stage_bytes"): the first chunk's staging copy and the
+  // last one's DMA and marking are not overlapped with anything
+  const size_t ch = ctx->wal_stage_bytes;
   if (pinned || registered) {
     // chunked, so that each chunk's candidate marking runs behind its DMA
-    for (size_t o = 0; o < n; o += kChunkBytes) {
-      const size_t c = std::min(kChunkBytes, n - o);
+    for (size_t o = 0; o < n; o += ch) {
+      const size_t c = std::min(ch, n - o);
       HIPCHK(hipMemcpyAsync(ctx->d_wimg + o, img + o, c, hipMemcpyHostToDevice, ctx->stream0));
       rc = lsmk_wal_mark_range(ctx->d_wimg, n, o, o + c, W.bits, W.pre, ctx->stream0);
       if (rc) return launch_rc(rc, "wal mark kernel");
@@ -1137,17 +1148,17 @@ static int wal_upload(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned)
       HIPCHK(hipStreamSynchronize(S.s));
       S.busy = false;
     }
-    if ((rc = ensure_pinned(&S.h_pay, &S.cap_h_pay, std::min(n, kChunkBytes)))) return rc;
+    if ((rc = ensure_pinned(&S.h_pay, &S.cap_h_pay, std::min(n, ch)))) return rc;
   }
   int slot = 0;
-  for (size_t o = 0; o < n; o += kChunkBytes, slot ^= 1) {
+  for (size_t o = 0; o < n; o += ch, slot ^= 1) {
     Stage& S = ctx->stage[slot];
-    const size_t c = std::min(kChunkBytes, n - o);
+    const size_t c = std::min(ch, n - o);
     HIPCHK(hipEventSynchronize(S.done));  // the slot's previous DMA has drained
     stage_copy(ctx, S.h_pay, img + o, c, ctx->stage_threads);
     HIPCHK(hipMemcpyAsync(ctx->d_wimg + o, S.h_pay, c, hipMemcpyHostToDevice, S.s));
     HIPCHK(hipEventRecord(S.done, S.s));
-    rc = lsmk_wal_mark_range(ctx->d_wimg, n, o, o + c, W.bits, W.pre, S.s);  // kChunkBytes: a multiple of 64
+    rc = lsmk_wal_mark_range(ctx->d_wimg, n, o, o + c, W.bits, W.pre, S.s);  // ch: a multiple of 64
     if (rc) return launch_rc(rc, "wal mark kernel");
   }
   for (auto& S : ctx->stage) HIPCHK(hipStreamSynchronize(S.s));

@@ -104,11 +104,12 @@ def test_big_generated_log(ctx):
     assert same(ctx, img) == 0
 
 
-@pytest.mark.parametrize("register", [0, 1])
-def test_registered_upload(ctx, register):
+@pytest.mark.parametrize("register,stage_mib", [(0, 64), (1, 64), (0, 1), (1, 1)])
+def test_registered_upload(ctx, register, stage_mib):
     """``wal_register`` 1: an uploaded host image is DMA'd from its own pages
     (pinned in place for the call, unaligned start and end) -- same records
-    and the same first bad record as the staged upload and the oracle."""
+    and the same first bad record as the staged upload and the oracle; and
+    in 1 MiB upload chunks (``wal_stage_bytes``), records across chunk ends."""
     rng = np.random.default_rng(21)
     blob = O.gen_stream(6, 0, 1 << 20)
     parts = []
@@ -119,6 +120,7 @@ def test_registered_upload(ctx, register):
     img = b"".join(parts)
     assert len(img) > (4 << 20)
     ctx.set_option("wal_register", register)
+    ctx.set_option("wal_stage_bytes", stage_mib << 20)
     try:
         assert same(ctx, img) == 0
         raw = bytearray(len(img) + 8)
@@ -133,6 +135,7 @@ def test_registered_upload(ctx, register):
         assert same(ctx, bytes(b)) in (1, 2, 3)
     finally:
         ctx.set_option("wal_register", 0)
+        ctx.set_option("wal_stage_bytes", 64 << 20)
 
 
 @pytest.mark.parametrize("chunk", [1, 4096, 65536, 0])
