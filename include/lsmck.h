@@ -189,7 +189,7 @@ int lsmck_device_count(void);
  *   "wal_stage_bytes"  an uploaded host WAL image moves in chunks of this many
  *                 bytes (pageable: copied into a pinned slot, then DMA'd; each
  *                 chunk's candidate marking runs behind its DMA); a multiple
- *                 of 64 KiB in [1 MiB, 64 MiB], default 64 MiB.  A/B.
+ *                 of 64 KiB in [1 MiB, 64 MiB], default 16 MiB.
  *   "wal_register"  1 = an uploaded host WAL image is DMA'd from the caller's
  *                 own pages, pinned in place for the call (hipHostRegister),
  *                 instead of through the pinned staging copy (default 0).  A/B.

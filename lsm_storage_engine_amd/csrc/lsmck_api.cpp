@@ -247,7 +247,11 @@ struct lsmck_ctx {
   // at most half the free device memory); over it the log takes the host walk
   size_t wal_walk_budget_per_byte = 8;
   int wal_register = 0;  // host WAL images: hipHostRegister the caller's pages instead of the staging copy (A/B)
-  size_t wal_stage_bytes = kChunkBytes;  // host WAL image upload: bytes per staged / DMA'd chunk (A/B)
+  // host WAL image upload: bytes per staged / DMA'd chunk.  16 MiB: 6.3 ms
+  // for the 0.24 GB wal_diag image against 6.5 at 64 MiB (the first copy and
+  // the last DMA are not overlapped), 10.7 at 4 MiB (per-chunk costs);
+  // profiles/r03/h/wal_diag_r03h.json
+  size_t wal_stage_bytes = 16u << 20;
   // host images of at least this many bytes are uploaded whole and walked on
   // the GPU (0 = always the host walk)
   size_t wal_upload_min = 1u << 20;

@@ -135,7 +135,7 @@ def test_registered_upload(ctx, register, stage_mib):
         assert same(ctx, bytes(b)) in (1, 2, 3)
     finally:
         ctx.set_option("wal_register", 0)
-        ctx.set_option("wal_stage_bytes", 64 << 20)
+        ctx.set_option("wal_stage_bytes", 16 << 20)
 
 
 @pytest.mark.parametrize("chunk", [1, 4096, 65536, 0])

@@ -71,10 +71,10 @@ def main():
     recs, st, _ = ctx.wal_replay_verify(img)
     assert st == 0 and len(recs) == n
     res["replay_total_s"] = best(lambda: ctx.wal_replay_verify(img))  # default: uploaded, GPU header walk
-    for sb in (4, 8, 16, 32):  # A/B: upload chunk size (pipeline fill / drain against per-chunk cost)
+    for sb in (4, 8, 32, 64):  # A/B: upload chunk size (pipeline fill / drain against per-chunk cost)
         ctx.set_option("wal_stage_bytes", sb << 20)
         res[f"replay_stage_{sb}MiB_s"] = best(lambda: ctx.wal_replay_verify(img))
-    ctx.set_option("wal_stage_bytes", 64 << 20)
+    ctx.set_option("wal_stage_bytes", 16 << 20)
     ctx.set_option("wal_register", 1)  # A/B: the caller's pages pinned in place, DMA without the staging copy
     res["replay_registered_s"] = best(lambda: ctx.wal_replay_verify(img))
     ctx.set_option("wal_register", 0)
