@@ -94,6 +94,22 @@ int ensure_pinned(T** p, size_t* cap, size_t need) {
   return 0;
 }
 
+// ensure_dev that keeps the first `keep` elements (copied on st)
+template <typename T>
+int ensure_dev_keep(T** p, size_t* cap, size_t need, size_t keep, hipStream_t st) {
+  if (*cap >= need && *p) return 0;
+  if (!keep || !*p) return ensure_dev(p, cap, need);
+  const size_t want = std::max(need, *cap * 3 / 2);
+  T* q = nullptr;
+  HIPCHK(hipMalloc((void**)&q, want * sizeof(T)));
+  HIPCHK(hipMemcpyAsync(q, *p, keep * sizeof(T), hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipStreamSynchronize(st));
+  (void)hipFree(*p);
+  *p = q;
+  *cap = want;
+  return 0;
+}
+
 // Scratch of the descriptor CRC path (one per in-flight launch).
 struct DescScratch {
   uint64_t* block_sum = nullptr;  // per 1024-record block
@@ -247,6 +263,7 @@ struct lsmck_ctx {
   // at most half the free device memory); over it the log takes the host walk
   size_t wal_walk_budget_per_byte = 8;
   int wal_register = 0;  // host WAL images: hipHostRegister the caller's pages instead of the staging copy (A/B)
+  int wal_split = 1;     // host WAL images of two upload chunks or more: walk the first half during the second's upload
   // host WAL image upload: bytes per staged / DMA'd chunk.  16 MiB: 6.3 ms
   // for the 0.24 GB wal_diag image against 6.5 at 64 MiB (the first copy and
   // the last DMA are not overlapped), 10.7 at 4 MiB (per-chunk costs);
@@ -708,7 +725,7 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
   if (!key) return lsmck_host::set_error(LSMCK_EINVAL, "null key");
   if (!strcmp(key, "crc_ablate")) {  // diagnostic only (results are garbage): 3 = payload loads only (the
                                      // bench's loads-only ceiling), 2 = stream kernel without payload loads
-    if (value != 0 && (value < 2 || value > 5)) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0, 2, 3, 4 or 5");
+    if (value != 0 && (value < 2 || value > 6)) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0 or 2..6");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->variant = (ctx->variant & ~0xF00) | ((int)value << 8);
     return 0;
@@ -767,6 +784,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
       return lsmck_host::set_error(LSMCK_EINVAL, "wal_stage_bytes: a multiple of 64 KiB in [1 MiB, 64 MiB]");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->wal_stage_bytes = (size_t)value;
+    return 0;
+  }
+  if (!strcmp(key, "wal_split")) {  // A/B: host WAL image walked in two parts behind its upload (0 = whole)
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "wal_split must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_split = (int)value;
     return 0;
   }
   if (!strcmp(key, "wal_register")) {  // A/B: host WAL image uploaded by DMA from its own pages, pinned in place
@@ -983,27 +1006,24 @@ struct WalTrace {
   }
 };
 
-// marked: the candidate bitmap of img is already in ctx->wd (wal_upload marks
-// each chunk behind its copy)
-static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck_wal_rec* recs, size_t cap,
-                             size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected,
-                             bool marked = false) {
-  // the candidate count is a u32 on the device: from 2^32 log bytes on it could wrap
-  if (n >= (1ull << 32)) return kWalHostWalk;
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  DevGuard g(ctx->dev);
-  const WalTrace tr;
+// One header walk over the candidates of words [w0, w1), from position
+// `start` (a prefix walk when lim < n: lsmck_wal.hip wal_succ), its records
+// emitted at index `at` of the record / descriptor arrays.  Caller holds
+// ctx->mu; st is ordered after the scratch users.
+struct WalPart {
+  size_t m = 0;        // records
+  uint32_t term = 0;   // terminal code (WAL_END / BAD / STOP / STOPSELF, lsmck_wal.hip)
+  uint64_t tpos = 0;   // BAD position, or where a prefix walk resumes
+};
+constexpr uint32_t kWalBad = 0xFFFFFFFEu, kWalStop = 0xFFFFFFFDu, kWalStopSelf = 0xFFFFFFFCu;
+
+static int wal_walk_part(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t w0, uint64_t w1, uint64_t start,
+                         uint64_t lim, bool marked, size_t at, hipStream_t st, WalPart* out, const WalTrace& tr) {
   auto& W = ctx->wd;
   int rc;
-  if ((rc = wal_bitmap_ensure(ctx, n))) return rc;
-  if (!W.info) HIPCHK(hipMalloc((void**)&W.info, 64));
-  if (!W.h_info) HIPCHK(hipHostMalloc((void**)&W.h_info, 64, hipHostMallocDefault));
-  ScratchOrder so(ctx, ctx->stream0);
-  if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
-  hipStream_t st = so.st;
   uint32_t* d_total = (uint32_t*)(W.info + 3);
   HIPCHK(hipMemsetAsync(d_total, 0, 4, st));
-  rc = lsmk_wal_mark(img, n, W.bits, W.pre, W.bsum, d_total, marked ? 1 : 0, st);
+  rc = lsmk_wal_mark(img, n, W.bits, W.pre, W.bsum, d_total, marked ? 1 : 0, w0, w1, st);
   if (rc) return launch_rc(rc, "wal mark/scan kernels");
   HIPCHK(hipMemcpyAsync(W.h_info + 3, d_total, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
@@ -1013,7 +1033,7 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
   // that could start a header -- not with the record count: a valid log whose
   // payloads are dense in those bytes needs up to ~120x its size (levels x nc
   // x 4 B of J alone), and past 2^31 candidates the u32 ranks would reach the
-  // END/BAD sentinels.  Over a budget, or when an allocation fails, the replay
+  // terminal codes.  Over a budget, or when an allocation fails, the replay
   // takes the serial host walk instead (kWalHostWalk), as the reference would
   // replay the same log.
   if (nc64 >= (1ull << 31)) return kWalHostWalk;
@@ -1032,28 +1052,48 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
     (void)hipGetLastError();  // the failed hipMalloc's sticky error
     return kWalHostWalk;
   }
-  rc = lsmk_wal_chain(img, n, W.bits, W.pre, nc, levels, W.pos, W.J, W.badpos, W.chain, W.info, st);
+  rc = lsmk_wal_chain(img, n, W.bits, W.pre, nc, levels, W.pos, W.J, W.badpos, W.chain, W.info, w0, w1, start, lim,
+                      st);
   if (rc) return launch_rc(rc, "wal chain kernels");
   HIPCHK(hipMemcpyAsync(W.h_info, W.info, 24, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   tr.mark("chain (sync)");
-  const size_t m = (size_t)W.h_info[0];
-  const uint32_t term = (uint32_t)W.h_info[1];
-  const uint64_t badq = W.h_info[2];
-  // records -> lsmck_wal_rec, payload descriptors, stored CRCs; one CRC batch + compare
+  out->m = (size_t)W.h_info[0];
+  out->term = (uint32_t)W.h_info[1];
+  out->tpos = W.h_info[2];
+  if (out->m) {  // records -> lsmck_wal_rec, payload descriptors, stored CRCs (after the first `at`)
+    const size_t tot = at + out->m;
+    if ((rc = ensure_dev_keep(&W.recs, &W.cap_recs, tot, at, st)) ||
+        (rc = ensure_dev_keep(&ctx->d_woff, &ctx->cap_woff, tot, at, st)) ||
+        (rc = ensure_dev_keep(&ctx->d_wlen, &ctx->cap_wlen, tot, at, st)) ||
+        (rc = ensure_dev_keep(&ctx->d_wexp, &ctx->cap_wexp, tot, at, st)) ||
+        (rc = ensure_dev_keep(&ctx->d_vcrc, &ctx->cap_vcrc, tot, at, st)))
+      return rc;
+    rc = lsmk_wal_emit(img, n, W.chain, W.pos, W.info, (uint32_t)out->m, W.recs + at, ctx->d_woff + at,
+                       ctx->d_wlen + at, ctx->d_wexp + at, st);
+    if (rc) return launch_rc(rc, "wal emit kernel");
+  }
+  return 0;
+}
+
+// The CRC pass over records [at, at + m): their payloads in log order (the
+// stream kernel, no eligibility check), CRCs into d_vcrc + at.  Asynchronous.
+static int wal_crc_part(lsmck_ctx* ctx, const uint8_t* img, size_t at, size_t m, hipStream_t st) {
+  if (!m) return 0;
+  return crc_desc_device(ctx, ctx->scratch, img, ctx->d_woff + at, ctx->d_wlen + at, m, ctx->d_vcrc + at, st, true);
+}
+
+// After the CRC pass of all m records: the compare, the records to the caller
+// (read back on a second stream and copied out on host threads while the
+// compare drains), and the replay's outcome (the first bad record in log
+// order, or a bad type byte after the last record at badq).
+static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t term, uint64_t badq, lsmck_wal_rec* recs,
+                      size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected,
+                      hipStream_t st, const WalTrace& tr) {
+  auto& W = ctx->wd;
+  int rc;
   uint64_t nbad = 0, first = m;
   if (m) {
-    if ((rc = ensure_dev(&W.recs, &W.cap_recs, m)) || (rc = ensure_dev(&ctx->d_woff, &ctx->cap_woff, m)) ||
-        (rc = ensure_dev(&ctx->d_wlen, &ctx->cap_wlen, m)) || (rc = ensure_dev(&ctx->d_wexp, &ctx->cap_wexp, m)))
-      return rc;
-    rc = lsmk_wal_emit(img, n, W.chain, W.pos, W.info, (uint32_t)m, W.recs, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st);
-    if (rc) return launch_rc(rc, "wal emit kernel");
-    // The records are read back on a second stream while the CRC pass runs,
-    // into a pinned buffer (DMA at the link rate; a copy into the caller's
-    // pageable array ran at a few GiB/s, page faults included), and copied
-    // into the caller's array on host threads before the CRC pass is waited
-    // for.  All m records go out (the accepted ones are a prefix; the rest of
-    // the caller's array is unspecified).
     std::function<int()> copy_out;
     if (recs && cap) {
       if ((rc = ensure_pinned(&ctx->h_wrecs, &ctx->cap_hwrecs, m)) || (rc = stage_init(ctx->stage[0]))) return rc;
@@ -1075,12 +1115,22 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
         return 0;
       };
     }
-    // the payloads of one image in log order: the stream kernel, no eligibility check
-    rc = device_verify(ctx, img, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, m, st, &nbad, &first, true, copy_out);
-    if (copy_out) (void)hipEventSynchronize(ctx->wal_recs_ev);  // (an early error return above: the DMA has drained)
-    if (rc < 0) return rc;
+    HIPCHK(hipMemsetAsync(ctx->d_verify, 0, 8, st));         // n_bad
+    HIPCHK(hipMemsetAsync(ctx->d_verify + 1, 0xFF, 8, st));  // first_bad = ~0
+    rc = lsmk_launch_crc32_compare(ctx->d_vcrc, ctx->d_wexp, m, ctx->d_verify, ctx->d_verify + 1, st);
+    if (rc) {
+      if (copy_out) (void)hipEventSynchronize(ctx->wal_recs_ev);
+      return launch_rc(rc, "compare kernel");
+    }
+    HIPCHK(hipMemcpyAsync(ctx->h_verify, ctx->d_verify, 16, hipMemcpyDeviceToHost, st));
+    const int hrc = copy_out ? copy_out() : 0;
+    if (copy_out) (void)hipEventSynchronize(ctx->wal_recs_ev);
+    HIPCHK(hipStreamSynchronize(st));
+    if (hrc) return hrc;
+    nbad = ctx->h_verify[0];
+    first = nbad ? ctx->h_verify[1] : m;
   }
-  tr.mark("emit+crc+compare+records (sync)");
+  tr.mark("crc+compare+records (sync)");
   const size_t accepted = nbad ? (size_t)first : m;
   if (nrec) *nrec = accepted;
   if (nbad) {
@@ -1096,7 +1146,7 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
     if (bad_crc) *bad_crc = got;
     return r.type == 1 ? LSMCK_WAL_CORRUPTED : LSMCK_WAL_REMOVE_PANIC;
   }
-  if (term == 0xFFFFFFFEu) {  // InvalidCommandType at the record after the last one
+  if (term == kWalBad) {  // InvalidCommandType at the record after the last one
     uint8_t t = 0;
     HIPCHK(hipMemcpy(&t, img + badq, 1, hipMemcpyDeviceToHost));
     if (bad_index) *bad_index = m;
@@ -1106,69 +1156,198 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
   return 0;
 }
 
-// A host image uploaded whole into ctx->d_wimg (caller holds wal_mu): pinned
-// images by one DMA; pageable ones through the two staging slots, each 64 MiB
-// chunk copied on stage_threads threads while the other slot's DMA runs.
-static int wal_upload(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned) {
+static int wal_walk_setup(lsmck_ctx* ctx, size_t n) {
+  auto& W = ctx->wd;
+  int rc;
+  if ((rc = wal_bitmap_ensure(ctx, n))) return rc;
+  if (!W.info) HIPCHK(hipMalloc((void**)&W.info, 64));
+  if (!W.h_info) HIPCHK(hipHostMalloc((void**)&W.h_info, 64, hipHostMallocDefault));
+  return 0;
+}
+
+// A device-resident image (or an uploaded one: `marked`, its candidate bitmap
+// is already in ctx->wd -- wal_upload marks each chunk behind its copy): one
+// walk, one CRC pass.
+static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck_wal_rec* recs, size_t cap,
+                             size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected,
+                             bool marked = false) {
+  // the candidate count is a u32 on the device: from 2^32 log bytes on it could wrap
+  if (n >= (1ull << 32)) return kWalHostWalk;
   std::lock_guard<std::mutex> lk(ctx->mu);
   DevGuard g(ctx->dev);
   const WalTrace tr;
   int rc;
-  if ((rc = ensure_dev(&ctx->d_wimg, &ctx->cap_wimg, n + 16)) || (rc = wal_bitmap_ensure(ctx, n))) return rc;
-  // the candidate bitmap of each chunk is marked right behind its copy (the
-  // marking then overlaps the rest of the upload)
+  if ((rc = wal_walk_setup(ctx, n))) return rc;
+  ScratchOrder so(ctx, ctx->stream0);
+  if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
+  hipStream_t st = so.st;
+  WalPart P;
+  if ((rc = wal_walk_part(ctx, img, n, 0, lsmk_wal_words(n), 0, n, marked, 0, st, &P, tr))) return rc;
+  if ((rc = wal_crc_part(ctx, img, 0, P.m, st))) return rc;
+  return wal_finish(ctx, img, P.m, P.term, P.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr);
+}
+
+// Host WAL image upload into ctx->d_wimg, in chunks of "wal_stage_bytes"
+// alternating over the two staging slots, each chunk's candidate marking
+// queued behind its copy (the marking then overlaps the rest of the upload).
+// Pageable images go through the slot's pinned buffer (copied on
+// stage_threads threads while the other slot's DMA runs); pinned (or
+// registered) ones are DMA'd straight from the caller's pages.  Bytes
+// [lo, hi), lo a multiple of the chunk size.  Caller holds ctx->mu and a
+// StageGuard; the slots' streams carry the work (wait on them).
+struct WalUpload {
+  const uint8_t* img;
+  size_t n;
+  bool direct;  // pinned or registered: no staging copy
+  int slot = 0;
+};
+static int wal_upload_range(lsmck_ctx* ctx, WalUpload& U, size_t lo, size_t hi) {
   auto& W = ctx->wd;
-  // "wal_register": pin the caller's pageable pages in place (hipHostRegister)
-  // and DMA straight from them, instead of the staging copy (A/B)
-  bool registered = false;
-  uint8_t* reg_base = nullptr;
-  if (!pinned && ctx->wal_register && n >= (1u << 20)) {
-    const uintptr_t pa = (uintptr_t)img & ~(uintptr_t)4095, pe = ((uintptr_t)img + n + 4095) & ~(uintptr_t)4095;
-    reg_base = (uint8_t*)pa;
-    registered = hipHostRegister(reg_base, pe - pa, hipHostRegisterDefault) == hipSuccess;
-    if (!registered) (void)hipGetLastError();
-    tr.mark("hipHostRegister");
-  }
-  // upload chunks ("wal_stage_bytes"): the first chunk's staging copy and the
-  // last one's DMA and marking are not overlapped with anything
+  int rc;
   const size_t ch = ctx->wal_stage_bytes;
-  if (pinned || registered) {
-    // chunked, so that each chunk's candidate marking runs behind its DMA
-    for (size_t o = 0; o < n; o += ch) {
-      const size_t c = std::min(ch, n - o);
-      HIPCHK(hipMemcpyAsync(ctx->d_wimg + o, img + o, c, hipMemcpyHostToDevice, ctx->stream0));
-      rc = lsmk_wal_mark_range(ctx->d_wimg, n, o, o + c, W.bits, W.pre, ctx->stream0);
-      if (rc) return launch_rc(rc, "wal mark kernel");
+  for (size_t o = lo; o < hi; o += ch, U.slot ^= 1) {
+    Stage& S = ctx->stage[U.slot];
+    const size_t c = std::min(ch, hi - o);
+    HIPCHK(hipEventSynchronize(S.done));  // the slot's previous DMA has drained
+    if (U.direct) {
+      HIPCHK(hipMemcpyAsync(ctx->d_wimg + o, U.img + o, c, hipMemcpyHostToDevice, S.s));
+    } else {
+      stage_copy(ctx, S.h_pay, U.img + o, c, ctx->stage_threads);
+      HIPCHK(hipMemcpyAsync(ctx->d_wimg + o, S.h_pay, c, hipMemcpyHostToDevice, S.s));
     }
-    HIPCHK(hipStreamSynchronize(ctx->stream0));
-    if (registered) (void)hipHostUnregister(reg_base);
-    tr.mark(registered ? "upload (registered)" : "upload (pinned)");
-    return 0;
+    HIPCHK(hipEventRecord(S.done, S.s));
+    rc = lsmk_wal_mark_range(ctx->d_wimg, U.n, o, o + c, W.bits, W.pre, S.s);  // ch: a multiple of 64
+    if (rc) return launch_rc(rc, "wal mark kernel");
   }
-  StageGuard guard{ctx};
+  return 0;
+}
+
+// the slots' work so far, ordered before stream st
+static int wal_upload_fence(lsmck_ctx* ctx, hipStream_t st) {
+  for (auto& S : ctx->stage) {
+    HIPCHK(hipEventRecord(S.done, S.s));
+    HIPCHK(hipStreamWaitEvent(st, S.done, 0));
+  }
+  return 0;
+}
+
+// "wal_register": pin the caller's pageable pages in place for the call
+// (hipHostRegister) and DMA straight from them, instead of the staging copy.
+struct HostRegistration {
+  uint8_t* base = nullptr;
+  bool on = false;
+  HostRegistration(const uint8_t* img, size_t n) {
+    const uintptr_t pa = (uintptr_t)img & ~(uintptr_t)4095, pe = ((uintptr_t)img + n + 4095) & ~(uintptr_t)4095;
+    base = (uint8_t*)pa;
+    on = hipHostRegister(base, pe - pa, hipHostRegisterDefault) == hipSuccess;
+    if (!on) (void)hipGetLastError();
+  }
+  ~HostRegistration() {
+    if (on) (void)hipHostUnregister(base);
+  }
+};
+
+static int wal_upload_prepare(lsmck_ctx* ctx, size_t n, bool direct) {
+  int rc;
+  if ((rc = ensure_dev(&ctx->d_wimg, &ctx->cap_wimg, n + 16)) || (rc = wal_walk_setup(ctx, n))) return rc;
   for (auto& S : ctx->stage) {
     if ((rc = stage_init(S))) return rc;
     if (S.busy) {  // a failed host batch's slot: nothing to retire here
       HIPCHK(hipStreamSynchronize(S.s));
       S.busy = false;
     }
-    if ((rc = ensure_pinned(&S.h_pay, &S.cap_h_pay, std::min(n, ch)))) return rc;
+    if (!direct && (rc = ensure_pinned(&S.h_pay, &S.cap_h_pay, std::min(n, ctx->wal_stage_bytes)))) return rc;
   }
-  int slot = 0;
-  for (size_t o = 0; o < n; o += ch, slot ^= 1) {
-    Stage& S = ctx->stage[slot];
-    const size_t c = std::min(ch, n - o);
-    HIPCHK(hipEventSynchronize(S.done));  // the slot's previous DMA has drained
-    stage_copy(ctx, S.h_pay, img + o, c, ctx->stage_threads);
-    HIPCHK(hipMemcpyAsync(ctx->d_wimg + o, S.h_pay, c, hipMemcpyHostToDevice, S.s));
-    HIPCHK(hipEventRecord(S.done, S.s));
-    rc = lsmk_wal_mark_range(ctx->d_wimg, n, o, o + c, W.bits, W.pre, S.s);  // ch: a multiple of 64
-    if (rc) return launch_rc(rc, "wal mark kernel");
-  }
+  return 0;
+}
+
+// The whole host image uploaded (and marked) before the walk (caller holds wal_mu).
+static int wal_upload(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned) {
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DevGuard g(ctx->dev);
+  const WalTrace tr;
+  std::unique_ptr<HostRegistration> reg;
+  if (!pinned && ctx->wal_register && n >= (1u << 20)) reg.reset(new HostRegistration(img, n));
+  WalUpload U{img, n, pinned || (reg && reg->on)};
+  int rc;
+  if ((rc = wal_upload_prepare(ctx, n, U.direct))) return rc;
+  StageGuard guard{ctx};
+  if ((rc = wal_upload_range(ctx, U, 0, n))) return rc;
   for (auto& S : ctx->stage) HIPCHK(hipStreamSynchronize(S.s));
-  tr.mark("upload (pageable)");
+  tr.mark("upload");
   guard.ok = true;
   return 0;
+}
+
+constexpr int kWalNoSplit = 0x7FFF0002;  // internal: the image is too small to upload in two parts
+
+// A host image uploaded in two parts ("wal_split", default on from 64 MiB):
+// the prefix [0, a) is walked (lsmck_wal.hip's prefix walk: records that end
+// by a) and its CRC pass launched on stream0, on a helper thread, while this
+// thread uploads the rest; the walk then resumes where the prefix stopped
+// (the next header, or the first record that did not end by a).  The walk's
+// own time then hides behind the upload except for the second part's.
+// Caller holds wal_mu.
+static int wal_replay_split(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned, lsmck_wal_rec* recs,
+                            size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected) {
+  const size_t ch = ctx->wal_stage_bytes;
+  const size_t a = (n / 2) / ch * ch;
+  if (n >= (1ull << 32) || a < ch || n - a < ch) return kWalNoSplit;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DevGuard g(ctx->dev);
+  const WalTrace tr;
+  std::unique_ptr<HostRegistration> reg;
+  if (!pinned && ctx->wal_register) reg.reset(new HostRegistration(img, n));
+  // on every return: no DMA from the caller's pages still running (and none
+  // from registered pages once they are unregistered, right after this)
+  struct SyncStages {
+    lsmck_ctx* c;
+    ~SyncStages() {
+      for (auto& S : c->stage)
+        if (S.s) (void)hipStreamSynchronize(S.s);
+    }
+  } sync_stages{ctx};
+  WalUpload U{img, n, pinned || (reg && reg->on)};
+  int rc;
+  if ((rc = wal_upload_prepare(ctx, n, U.direct))) return rc;
+  ScratchOrder so(ctx, ctx->stream0);
+  if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
+  hipStream_t st = so.st;
+  const uint8_t* d = ctx->d_wimg;
+  WalPart P1, P2;
+  {
+    StageGuard guard{ctx};
+    if ((rc = wal_upload_range(ctx, U, 0, a)) || (rc = wal_upload_fence(ctx, st))) return rc;
+    tr.mark("upload part 1 issued");
+    auto prefix = std::async(std::launch::async, [&]() -> std::pair<int, std::string> {
+      DevGuard gd(ctx->dev);  // (a new thread's current device is device 0)
+      int r = wal_walk_part(ctx, d, n, 0, a >> 6, 0, a, true, 0, st, &P1, tr);
+      if (!r) r = wal_crc_part(ctx, d, 0, P1.m, st);
+      return {r, r ? std::string(lsmck_last_error()) : std::string()};
+    });
+    rc = wal_upload_range(ctx, U, a, n);
+    const auto pr = prefix.get();
+    if (rc) return rc;
+    if (pr.first) {
+      if (pr.first != kWalHostWalk) lsmck_host::set_error(pr.first, pr.second.c_str());
+      for (auto& S : ctx->stage) HIPCHK(hipStreamSynchronize(S.s));
+      guard.ok = true;
+      return pr.first;  // (kWalHostWalk: the image is whole on the device; the caller walks it on the host)
+    }
+    if ((rc = wal_upload_fence(ctx, st))) return rc;
+    tr.mark("upload part 2 issued");
+    guard.ok = true;
+  }
+  if (P1.term != kWalStop && P1.term != kWalStopSelf)  // the log ended inside the prefix
+    return wal_finish(ctx, d, P1.m, P1.term, P1.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr);
+  // resume at r: the words from r's to the prefix end lost their counts to
+  // the prefix scan; mark them again, then walk words [r/64, end) from r
+  const uint64_t r = P1.tpos;
+  if (r < a && (rc = lsmk_wal_mark_range(d, n, r & ~(uint64_t)63, a, ctx->wd.bits, ctx->wd.pre, st)))
+    return launch_rc(rc, "wal mark kernel");
+  if ((rc = wal_walk_part(ctx, d, n, r >> 6, lsmk_wal_words(n), r, n, true, P1.m, st, &P2, tr))) return rc;
+  if ((rc = wal_crc_part(ctx, d, P1.m, P2.m, st))) return rc;
+  return wal_finish(ctx, d, P1.m + P2.m, P2.term, P2.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr);
 }
 
 extern "C" {
@@ -1187,8 +1366,13 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
     // header walk, instead of the serial host walk (~12 GiB/s) -- the records
     // and offsets are the same, they index the caller's image
     std::lock_guard<std::mutex> wl(ctx->wal_mu);
-    if ((rc = wal_upload(ctx, wal, n, (flags & LSMCK_HOST_PINNED) != 0))) return rc;
-    rc = wal_replay_device(ctx, ctx->d_wimg, n, recs, cap, nrec, bad_index, bad_crc, bad_expected, true);
+    const bool pinned = (flags & LSMCK_HOST_PINNED) != 0;
+    rc = ctx->wal_split ? wal_replay_split(ctx, wal, n, pinned, recs, cap, nrec, bad_index, bad_crc, bad_expected)
+                        : kWalNoSplit;
+    if (rc == kWalNoSplit) {
+      if ((rc = wal_upload(ctx, wal, n, pinned))) return rc;
+      rc = wal_replay_device(ctx, ctx->d_wimg, n, recs, cap, nrec, bad_index, bad_crc, bad_expected, true);
+    }
     if (rc != kWalHostWalk) return rc;
   }
   const uint8_t* h = wal;

@@ -80,10 +80,10 @@ uint64_t lsmk_wal_scan_blocks(uint64_t n);
 int lsmk_wal_mark_range(const uint8_t* img, uint64_t n, uint64_t b0, uint64_t b1, uint64_t* bits, uint32_t* pre,
                         hipStream_t st);
 int lsmk_wal_mark(const uint8_t* img, uint64_t n, uint64_t* bits, uint32_t* pre, uint32_t* bsum, uint32_t* total,
-                  int marked, hipStream_t st);
+                  int marked, uint64_t w0, uint64_t w1, hipStream_t st);
 int lsmk_wal_chain(const uint8_t* img, uint64_t n, const uint64_t* bits, const uint32_t* pre, uint32_t nc, int levels,
-                   uint64_t* pos, uint32_t* J, uint64_t* badpos, uint32_t* chain, unsigned long long* info,
-                   hipStream_t st);
+                   uint64_t* pos, uint32_t* J, uint64_t* badpos, uint32_t* chain, unsigned long long* info, uint64_t w0,
+                   uint64_t w1, uint64_t start, uint64_t lim, hipStream_t st);
 int lsmk_wal_emit(const uint8_t* img, uint64_t n, const uint32_t* chain, const uint64_t* pos,
                   const unsigned long long* info, uint32_t m, lsmck_wal_rec* recs, uint64_t* poff, uint32_t* plen,
                   uint32_t* pcrc, hipStream_t st);

@@ -30,6 +30,10 @@ namespace lsmck {
 
 #define WAL_END 0xFFFFFFFFu  // chain ends cleanly (EOF at or inside the next header)
 #define WAL_BAD 0xFFFFFFFEu  // the next byte is not a command type
+// prefix walks (lim < n: only the bytes before lim are on the device yet)
+#define WAL_STOP 0xFFFFFFFDu      // the next record starts at badpos[c]: resume the walk there
+#define WAL_STOPSELF 0xFFFFFFFCu  // this record does not end by lim: resume the walk at its own position
+#define WAL_TERM_MIN 0xFFFFFFFCu  // entries >= this are terminals (absorbing)
 
 __device__ __forceinline__ uint32_t rd32(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
@@ -161,20 +165,28 @@ __device__ __forceinline__ uint32_t cand_rank(const uint64_t* __restrict__ bits,
   return pre[w] + (uint32_t)__popcll(bits[w] & ((1ull << b) - 1ull));
 }
 
-// 3. positions and successors of the candidates: thread per 64-byte word
+// 3. positions and successors of the candidates of words [w0, w1) (their
+// ranks: pre, scanned over the same words): thread per 64-byte word.  A prefix
+// walk (lim < n) takes a record only when its header and payload end by lim,
+// and stops at a next header that does not start 13 bytes before lim.
 __global__ __launch_bounds__(256) void wal_succ(const uint8_t* __restrict__ img, uint64_t n,
                                                  const uint64_t* __restrict__ bits, const uint32_t* __restrict__ pre,
                                                  uint64_t* __restrict__ pos, uint32_t* __restrict__ J0,
-                                                 uint64_t* __restrict__ badpos) {
-  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t nw = (n + 63) >> 6;
-  if (w >= nw) return;
+                                                 uint64_t* __restrict__ badpos, uint64_t w0, uint64_t w1, uint64_t lim) {
+  const uint64_t w = w0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= w1) return;
   uint64_t m = bits[w];
   uint32_t c = pre[w];
   while (m) {
     const uint32_t b = (uint32_t)__builtin_ctzll(m);
     m &= m - 1;
     const uint64_t p = (w << 6) + b;
+    pos[c] = p;
+    if (lim < n && p + 13u > lim) {  // (a header not yet readable in full)
+      J0[c] = WAL_STOPSELF;
+      ++c;
+      continue;
+    }
     const uint8_t t = img[p];
     const uint32_t h = hdr_len(t);
     const uint32_t klen = rd32(img + p + 5);
@@ -183,7 +195,12 @@ __global__ __launch_bounds__(256) void wal_succ(const uint8_t* __restrict__ img,
     const uint64_t avail = n - (p + h);
     const uint64_t q = p + h + (dlen <= avail ? (uint64_t)dlen : avail);
     uint32_t s;
-    if (q >= n) {
+    if (lim < n && p + h + (uint64_t)dlen > lim) {
+      s = WAL_STOPSELF;
+    } else if (lim < n && q + 13u > lim) {
+      s = WAL_STOP;
+      badpos[c] = q;
+    } else if (q >= n) {
       s = WAL_END;  // wal.rs:76-77: EOF on the next header's type byte
     } else {
       const uint8_t t2 = img[q];
@@ -196,22 +213,22 @@ __global__ __launch_bounds__(256) void wal_succ(const uint8_t* __restrict__ img,
         s = cand_rank(bits, pre, q);
       }
     }
-    pos[c] = p;
     J0[c] = s;
     ++c;
   }
 }
 
-// the chain's first entry: candidate 0 when position 0 is one; otherwise the
-// log ends before its first record: empty (END) or a bad type byte at 0
+// the chain's first entry: the candidate at position `start` when it is one;
+// otherwise the log ends there: empty (END) or a bad type byte at start
 __global__ void wal_chain_init(const uint8_t* __restrict__ img, uint64_t n, const uint64_t* __restrict__ bits,
-                               uint32_t* __restrict__ chain, unsigned long long* __restrict__ info) {
-  const bool cand = n && (bits[0] & 1ull);
-  const bool bad = n && img[0] != 1 && img[0] != 2;
-  chain[0] = cand ? 0u : (bad ? WAL_BAD : WAL_END);
+                               const uint32_t* __restrict__ pre, uint64_t start, uint32_t* __restrict__ chain,
+                               unsigned long long* __restrict__ info) {
+  const bool cand = start < n && ((bits[start >> 6] >> (start & 63u)) & 1ull);
+  const bool bad = start < n && img[start] != 1 && img[start] != 2;
+  chain[0] = cand ? cand_rank(bits, pre, start) : (bad ? WAL_BAD : WAL_END);
   info[0] = 0;
   info[1] = bad ? WAL_BAD : WAL_END;
-  info[2] = 0;  // bad position
+  info[2] = start;  // bad position
 }
 
 // 4. one doubling level: Jn[c] = J[J[c]] (terminals absorb)
@@ -220,7 +237,7 @@ __global__ __launch_bounds__(256) void wal_double(const uint32_t* __restrict__ J
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= nc) return;
   const uint32_t s = J[c];
-  Jn[c] = s >= WAL_BAD ? s : J[s];
+  Jn[c] = s >= WAL_TERM_MIN ? s : J[s];
 }
 
 // 5. chain unrolling, one level: chain[L + i] = J_k(chain[i]) for i < L = 2^k
@@ -230,23 +247,25 @@ __global__ __launch_bounds__(256) void wal_unroll(const uint32_t* __restrict__ J
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= L) return;
   const uint32_t c = chain[i];
-  chain[L + i] = c >= WAL_BAD ? c : Jk[c];
+  chain[L + i] = c >= WAL_TERM_MIN ? c : Jk[c];
 }
 
 // the chain's length and how it ends: the first terminal entry (entries are
 // ranks up to it, terminals after); out[0] = records, out[1] = terminal code,
-// out[2..3] = the BAD position (u64)
+// out[2] = the BAD position, or where a prefix walk resumes (STOP: the next
+// header; STOPSELF: the record that did not end by the limit, not counted)
 __global__ __launch_bounds__(256) void wal_chain_end(const uint32_t* __restrict__ chain, uint32_t len,
                                                       const uint32_t* __restrict__ J0, const uint64_t* __restrict__ badpos,
-                                                      unsigned long long* __restrict__ out) {
+                                                      const uint64_t* __restrict__ pos, unsigned long long* __restrict__ out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= len) return;
-  const bool here = chain[i] < WAL_BAD && (i + 1 == len || chain[i + 1] >= WAL_BAD);
+  const bool here = chain[i] < WAL_TERM_MIN && (i + 1 == len || chain[i + 1] >= WAL_TERM_MIN);
   if (!here) return;  // exactly one entry: the chain's last record
   const uint32_t c = chain[i];
-  out[0] = i + 1;
-  out[1] = J0[c];
-  out[2] = J0[c] == WAL_BAD ? badpos[c] : 0ull;
+  const uint32_t code = J0[c];
+  out[0] = code == WAL_STOPSELF ? i : i + 1;
+  out[1] = code;
+  out[2] = (code == WAL_BAD || code == WAL_STOP) ? badpos[c] : (code == WAL_STOPSELF ? pos[c] : 0ull);
 }
 
 // 6. records -> lsmck_wal_rec entries, CRC descriptors and stored CRCs
@@ -305,33 +324,36 @@ extern "C" int lsmk_wal_mark_range(const uint8_t* img, uint64_t n, uint64_t b0, 
 }
 
 // phase 1-2: bitmap, counts (unless `marked`: lsmk_wal_mark_range ran over the
-// whole image), their exclusive scan; *total = candidates
+// whole image), their exclusive scan over words [w0, w1) (ranks relative to
+// word w0); *total = candidates there
 extern "C" int lsmk_wal_mark(const uint8_t* img, uint64_t n, uint64_t* bits, uint32_t* pre, uint32_t* bsum,
-                             uint32_t* total, int marked, hipStream_t st) {
-  const uint64_t nw = lsmk_wal_words(n);
-  if (nw == 0) return 0;
+                             uint32_t* total, int marked, uint64_t w0, uint64_t w1, hipStream_t st) {
+  if (w1 <= w0) return 0;
   if (!marked) {
     const int rc = lsmk_wal_mark_range(img, n, 0, n, bits, pre, st);
     if (rc) return rc;
   }
-  const uint64_t nb = lsmk_wal_scan_blocks(n);
-  hipLaunchKernelGGL(wal_scan_a, dim3((unsigned)nb), dim3(WSCAN_BLOCK), 0, st, pre, nw, bsum);
+  const uint64_t nw = w1 - w0;
+  const uint64_t nb = (nw + WSCAN_BLOCK * WSCAN_ITEMS - 1) / (WSCAN_BLOCK * WSCAN_ITEMS);
+  hipLaunchKernelGGL(wal_scan_a, dim3((unsigned)nb), dim3(WSCAN_BLOCK), 0, st, pre + w0, nw, bsum);
   hipLaunchKernelGGL(wal_scan_b, dim3(1), dim3(1024), 0, st, bsum, (uint32_t)nb, total);
-  hipLaunchKernelGGL(wal_scan_c, dim3((unsigned)nb), dim3(WSCAN_BLOCK), 0, st, pre, nw, bsum);
+  hipLaunchKernelGGL(wal_scan_c, dim3((unsigned)nb), dim3(WSCAN_BLOCK), 0, st, pre + w0, nw, bsum);
   return launch_err();
 }
 
-// phase 3-5 for nc candidates (read back by the host): levels = bit length of
-// nc (2^levels > nc >= the chain's length), J holds levels * nc u32, chain
-// 2^levels u32, info 4 u64 (device): records, terminal code, bad position
+// phase 3-5 for the nc candidates of words [w0, w1) (read back by the host),
+// the chain from position `start` (a multiple-of-64 prefix [0, lim) when lim <
+// n): levels = bit length of nc (2^levels > nc >= the chain's length), J holds
+// levels * nc u32, chain 2^levels u32, info 4 u64 (device): records,
+// terminal code, bad / resume position
 extern "C" int lsmk_wal_chain(const uint8_t* img, uint64_t n, const uint64_t* bits, const uint32_t* pre, uint32_t nc,
                               int levels, uint64_t* pos, uint32_t* J, uint64_t* badpos, uint32_t* chain,
-                              unsigned long long* info, hipStream_t st) {
-  const uint64_t nw = lsmk_wal_words(n);
-  hipLaunchKernelGGL(wal_chain_init, dim3(1), dim3(1), 0, st, img, n, bits, chain, info);
+                              unsigned long long* info, uint64_t w0, uint64_t w1, uint64_t start, uint64_t lim,
+                              hipStream_t st) {
+  hipLaunchKernelGGL(wal_chain_init, dim3(1), dim3(1), 0, st, img, n, bits, pre, start, chain, info);
   if (nc == 0) return launch_err();
-  hipLaunchKernelGGL(wal_succ, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, img, n, bits, pre, pos, J,
-                     badpos);
+  hipLaunchKernelGGL(wal_succ, dim3((unsigned)((w1 - w0 + 255) / 256)), dim3(256), 0, st, img, n, bits, pre, pos, J,
+                     badpos, w0, w1, lim);
   for (int k = 0; k + 1 < levels; ++k)
     hipLaunchKernelGGL(wal_double, dim3((nc + 255) / 256), dim3(256), 0, st, J + (uint64_t)k * nc,
                        J + (uint64_t)(k + 1) * nc, nc);
@@ -340,11 +362,12 @@ extern "C" int lsmk_wal_chain(const uint8_t* img, uint64_t n, const uint64_t* bi
     hipLaunchKernelGGL(wal_unroll, dim3((L + 255) / 256), dim3(256), 0, st, J + (uint64_t)k * nc, chain, L);
   }
   const uint32_t len = 1u << levels;
-  hipLaunchKernelGGL(wal_chain_end, dim3((len + 255) / 256), dim3(256), 0, st, chain, len, J, badpos, info);
+  hipLaunchKernelGGL(wal_chain_end, dim3((len + 255) / 256), dim3(256), 0, st, chain, len, J, badpos, pos, info);
   return launch_err();
 }
 
 // records, descriptors and stored CRCs of the first info[0] chain entries
+// (m: their count, read back by the host)
 extern "C" int lsmk_wal_emit(const uint8_t* img, uint64_t n, const uint32_t* chain, const uint64_t* pos,
                              const unsigned long long* info, uint32_t m, lsmck_wal_rec* recs, uint64_t* poff,
                              uint32_t* plen, uint32_t* pcrc, hipStream_t st) {

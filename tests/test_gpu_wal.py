@@ -138,6 +138,65 @@ def test_registered_upload(ctx, register, stage_mib):
         ctx.set_option("wal_stage_bytes", 16 << 20)
 
 
+def _log_of(sizes, seed=31):
+    """A WAL image of Insert records with the given payload sizes (key 1-8 B)."""
+    rng = np.random.default_rng(seed)
+    blob = O.gen_stream(seed, 0, max(sizes) + 64)
+    parts = []
+    for i, sz in enumerate(sizes):
+        kl = int(min(sz, 1 + (i % 8)))
+        parts.append(O.wal_insert(blob[:kl].tobytes(), blob[kl + (i % 7):kl + (i % 7) + sz - kl].tobytes()))
+    return b"".join(parts)
+
+
+@pytest.mark.parametrize("case", ["straddle_record", "straddle_header", "big_first", "huge_middle", "tail_cut",
+                                  "bad_type_prefix", "bad_type_suffix", "corrupt_prefix", "corrupt_suffix"])
+def test_split_replay(ctx, case):
+    """A host image uploaded in two parts (``wal_split``, 1 MiB chunks): the
+    first half's walk stops at the split point (a record or a header across
+    it, a first record longer than the half, a record spanning many chunks)
+    and resumes there; bad type bytes, truncation and corruptions on either
+    side -- the same records and outcome as the whole-image walk and the
+    oracle."""
+    rng = np.random.default_rng(41)
+    sizes = [int(x) for x in rng.integers(1, 3000, 3000)]
+    img = bytearray(_log_of(sizes))  # ~4.5 MiB: the split point a = 2 MiB
+    n = len(img)
+    a = (n // 2) // (1 << 20) * (1 << 20)
+    offs = [r.rec_off for r in O.wal_replay(bytes(img))[1]]
+    k = next(i for i, o in enumerate(offs) if o >= a)  # first record at or past a
+    if case == "straddle_record":  # the record before a ends well past a
+        pass
+    elif case == "straddle_header":  # a header across a: rebuild so that a record starts at a - 5
+        pre = sizes[:k - 1]
+        used = len(_log_of(pre))
+        fill = a - 5 - used - 13
+        img = bytearray(_log_of(pre + [fill] + sizes[k:]))
+    elif case == "big_first":  # the first record is longer than the first half
+        img = bytearray(_log_of([n // 2 + 12345] + sizes[:200]))
+    elif case == "huge_middle":  # a record spanning the split point and several chunks
+        img = bytearray(_log_of(sizes[:k - 3] + [3 << 20] + sizes[k:]))
+    elif case == "tail_cut":  # truncated inside the last record's payload
+        img = img[:-7]
+    elif case == "bad_type_prefix":
+        img[offs[k // 2]] = 7
+    elif case == "bad_type_suffix":
+        img[offs[k + 50]] = 0
+    elif case == "corrupt_prefix":
+        img[offs[k - 2] + 20] ^= 0x40
+    elif case == "corrupt_suffix":
+        img[offs[k + 3] + 16] ^= 0x01
+    img = bytes(img)
+    ctx.set_option("wal_stage_bytes", 1 << 20)
+    try:
+        for split in (1, 0):
+            ctx.set_option("wal_split", split)
+            same(ctx, img)
+    finally:
+        ctx.set_option("wal_split", 1)
+        ctx.set_option("wal_stage_bytes", 16 << 20)
+
+
 @pytest.mark.parametrize("chunk", [1, 4096, 65536, 0])
 def test_overlapped_chunks(ctx, golden, chunk):
     """The host-image replay runs its CRC batches while the walk goes on
