@@ -236,6 +236,10 @@ struct lsmck_ctx {
   lsmck_wal_rec* h_wrecs = nullptr;  // device WAL replay: the records' pinned landing buffer (grow-only)
   size_t cap_hwrecs = 0;
   hipEvent_t wal_emit_ev = nullptr, wal_recs_ev = nullptr;  // records read back beside the CRC pass
+  lsmck_wal_rec* h_wrecs1 = nullptr;  // split host-image replay: the first part's records (pinned, grow-only)
+  size_t cap_hwrecs1 = 0;
+  hipStream_t wal_rs = nullptr;       // ... read back on their own stream while the second part uploads
+  hipEvent_t wal_emit1_ev = nullptr;
   std::unique_ptr<lsmck_host::HostPool> pool;  // staging copy threads (created on first use)
   uint64_t* h_woff = nullptr;  // pinned staging of the same
   size_t cap_hwoff = 0;
@@ -875,6 +879,9 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   if (ctx->h_wrecs) (void)hipHostFree(ctx->h_wrecs);
   if (ctx->wal_emit_ev) (void)hipEventDestroy(ctx->wal_emit_ev);
   if (ctx->wal_recs_ev) (void)hipEventDestroy(ctx->wal_recs_ev);
+  if (ctx->h_wrecs1) (void)hipHostFree(ctx->h_wrecs1);
+  if (ctx->wal_emit1_ev) (void)hipEventDestroy(ctx->wal_emit1_ev);
+  if (ctx->wal_rs) (void)hipStreamDestroy(ctx->wal_rs);
   if (ctx->wal_host) (void)hipHostFree(ctx->wal_host);
   if (ctx->d_wimg) (void)hipFree(ctx->d_wimg);
   if (ctx->scratch_ev) (void)hipEventDestroy(ctx->scratch_ev);
@@ -1087,30 +1094,33 @@ static int wal_crc_part(lsmck_ctx* ctx, const uint8_t* img, size_t at, size_t m,
 // (read back on a second stream and copied out on host threads while the
 // compare drains), and the replay's outcome (the first bad record in log
 // order, or a bad type byte after the last record at badq).
+// done: records [0, done) are already in the caller's array (the split
+// replay's first part, from ctx->h_wrecs1); the rest land in ctx->h_wrecs.
 static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t term, uint64_t badq, lsmck_wal_rec* recs,
                       size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected,
-                      hipStream_t st, const WalTrace& tr) {
+                      hipStream_t st, const WalTrace& tr, size_t done = 0) {
   auto& W = ctx->wd;
   int rc;
   uint64_t nbad = 0, first = m;
   if (m) {
     std::function<int()> copy_out;
-    if (recs && cap) {
-      if ((rc = ensure_pinned(&ctx->h_wrecs, &ctx->cap_hwrecs, m)) || (rc = stage_init(ctx->stage[0]))) return rc;
+    const size_t todo = m - done;
+    if (recs && cap && todo) {
+      if ((rc = ensure_pinned(&ctx->h_wrecs, &ctx->cap_hwrecs, todo)) || (rc = stage_init(ctx->stage[0]))) return rc;
       if (!ctx->wal_emit_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_emit_ev, hipEventDisableTiming));
       if (!ctx->wal_recs_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_recs_ev, hipEventDisableTiming));
       hipStream_t s2 = ctx->stage[0].s;
       HIPCHK(hipEventRecord(ctx->wal_emit_ev, st));
       HIPCHK(hipStreamWaitEvent(s2, ctx->wal_emit_ev, 0));
-      HIPCHK(hipMemcpyAsync(ctx->h_wrecs, W.recs, m * sizeof(lsmck_wal_rec), hipMemcpyDeviceToHost, s2));
+      HIPCHK(hipMemcpyAsync(ctx->h_wrecs, W.recs + done, todo * sizeof(lsmck_wal_rec), hipMemcpyDeviceToHost, s2));
       HIPCHK(hipEventRecord(ctx->wal_recs_ev, s2));
       copy_out = [&]() -> int {  // pinned -> the caller's array, on several threads (first touch of its pages)
         HIPCHK(hipEventSynchronize(ctx->wal_recs_ev));
-        const size_t cnt = std::min(m, cap), bytes = cnt * sizeof(lsmck_wal_rec);
+        const size_t cnt = std::min(m, cap) > done ? std::min(m, cap) - done : 0, bytes = cnt * sizeof(lsmck_wal_rec);
         const unsigned T = bytes >= (4u << 20) ? std::max(1u, std::min(ctx->stage_threads, 8u)) : 1u;
         host_pool(ctx).run(T, [&](unsigned t) {
           const size_t a = cnt * t / T, b = cnt * (t + 1) / T;
-          memcpy(recs + a, ctx->h_wrecs + a, (b - a) * sizeof(lsmck_wal_rec));
+          memcpy(recs + done + a, ctx->h_wrecs + a, (b - a) * sizeof(lsmck_wal_rec));
         });
         return 0;
       };
@@ -1136,8 +1146,10 @@ static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t ter
   if (nbad) {
     lsmck_wal_rec r;
     uint32_t got = 0;
-    if (recs && cap)
-      r = ctx->h_wrecs[first];
+    if (recs && cap && first < done)
+      r = ctx->h_wrecs1[first];
+    else if (recs && cap && m > done)
+      r = ctx->h_wrecs[first - done];
     else
       HIPCHK(hipMemcpy(&r, W.recs + first, sizeof r, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(&got, ctx->d_vcrc + first, 4, hipMemcpyDeviceToHost));
@@ -1279,6 +1291,23 @@ static int wal_upload(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned)
   return 0;
 }
 
+// The split replay's first m records (emitted on st) into the caller's array
+// on this (helper) thread, through ctx->h_wrecs1 and the records' own stream.
+static int wal_records_early(lsmck_ctx* ctx, size_t m, lsmck_wal_rec* recs, size_t cap, hipStream_t st, size_t* done) {
+  int rc;
+  if ((rc = ensure_pinned(&ctx->h_wrecs1, &ctx->cap_hwrecs1, m))) return rc;
+  if (!ctx->wal_rs) HIPCHK(hipStreamCreateWithFlags(&ctx->wal_rs, hipStreamNonBlocking));
+  if (!ctx->wal_emit1_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_emit1_ev, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(ctx->wal_emit1_ev, st));
+  HIPCHK(hipStreamWaitEvent(ctx->wal_rs, ctx->wal_emit1_ev, 0));
+  HIPCHK(hipMemcpyAsync(ctx->h_wrecs1, ctx->wd.recs, m * sizeof(lsmck_wal_rec), hipMemcpyDeviceToHost, ctx->wal_rs));
+  HIPCHK(hipStreamSynchronize(ctx->wal_rs));
+  const size_t cnt = std::min(m, cap);
+  memcpy(recs, ctx->h_wrecs1, cnt * sizeof(lsmck_wal_rec));  // (one thread: the pool is staging the upload)
+  *done = m;
+  return 0;
+}
+
 constexpr int kWalNoSplit = 0x7FFF0002;  // internal: the image is too small to upload in two parts
 
 // A host image uploaded in two parts ("wal_split", default on from 64 MiB):
@@ -1315,6 +1344,7 @@ static int wal_replay_split(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool p
   hipStream_t st = so.st;
   const uint8_t* d = ctx->d_wimg;
   WalPart P1, P2;
+  size_t done = 0;  // records already in the caller's array
   {
     StageGuard guard{ctx};
     if ((rc = wal_upload_range(ctx, U, 0, a)) || (rc = wal_upload_fence(ctx, st))) return rc;
@@ -1323,6 +1353,9 @@ static int wal_replay_split(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool p
       DevGuard gd(ctx->dev);  // (a new thread's current device is device 0)
       int r = wal_walk_part(ctx, d, n, 0, a >> 6, 0, a, true, 0, st, &P1, tr);
       if (!r) r = wal_crc_part(ctx, d, 0, P1.m, st);
+      // the first part's records to the caller now, on their own stream, while
+      // the second part uploads
+      if (!r && recs && cap && P1.m) r = wal_records_early(ctx, P1.m, recs, cap, st, &done);
       return {r, r ? std::string(lsmck_last_error()) : std::string()};
     });
     rc = wal_upload_range(ctx, U, a, n);
@@ -1339,7 +1372,7 @@ static int wal_replay_split(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool p
     guard.ok = true;
   }
   if (P1.term != kWalStop && P1.term != kWalStopSelf)  // the log ended inside the prefix
-    return wal_finish(ctx, d, P1.m, P1.term, P1.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr);
+    return wal_finish(ctx, d, P1.m, P1.term, P1.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr, done);
   // resume at r: the words from r's to the prefix end lost their counts to
   // the prefix scan; mark them again, then walk words [r/64, end) from r
   const uint64_t r = P1.tpos;
@@ -1347,7 +1380,8 @@ static int wal_replay_split(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool p
     return launch_rc(rc, "wal mark kernel");
   if ((rc = wal_walk_part(ctx, d, n, r >> 6, lsmk_wal_words(n), r, n, true, P1.m, st, &P2, tr))) return rc;
   if ((rc = wal_crc_part(ctx, d, P1.m, P2.m, st))) return rc;
-  return wal_finish(ctx, d, P1.m + P2.m, P2.term, P2.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr);
+  return wal_finish(ctx, d, P1.m + P2.m, P2.term, P2.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr,
+                    done);
 }
 
 extern "C" {

@@ -71,6 +71,22 @@ def main():
     recs, st, _ = ctx.wal_replay_verify(img)
     assert st == 0 and len(recs) == n
     res["replay_total_s"] = best(lambda: ctx.wal_replay_verify(img))  # default: uploaded, GPU header walk
+    # the same through the C ABI into one records array reused across calls
+    # (the wrapper allocates a worst-case n/9-record array per call)
+    import ctypes as C
+    from lsm_storage_engine_amd import _lib
+    from lsm_storage_engine_amd.device import WAL_REC_DTYPE
+    rbuf = np.empty(len(img) // 9 + 1, dtype=WAL_REC_DTYPE)
+    out = (C.c_size_t(), C.c_uint64(), C.c_uint32(), C.c_uint32())
+
+    def reuse():
+        rc = ctx.lib.lsmck_wal_replay_verify(ctx.handle, img.ctypes.data, len(img), _lib.HOST, rbuf.ctypes.data,
+                                             len(rbuf), *[C.byref(x) for x in out])
+        assert rc == 0 and out[0].value == n
+    res["replay_reuse_recs_s"] = best(reuse)
+    ctx.set_option("wal_split", 0)  # A/B: the whole image uploaded before the walk
+    res["replay_nosplit_s"] = best(lambda: ctx.wal_replay_verify(img))
+    ctx.set_option("wal_split", 1)
     for sb in (4, 8, 32, 64):  # A/B: upload chunk size (pipeline fill / drain against per-chunk cost)
         ctx.set_option("wal_stage_bytes", sb << 20)
         res[f"replay_stage_{sb}MiB_s"] = best(lambda: ctx.wal_replay_verify(img))
