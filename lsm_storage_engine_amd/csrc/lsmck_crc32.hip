@@ -1320,7 +1320,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     __builtin_amdgcn_sched_barrier(0);
     if (dqcnt) qpush(dqv, dqcnt);
     dqcnt = 0;
-    if constexpr (ABLATE == 0 || ABLATE == 4 || ABLATE == 5 || ABLATE == 6) {
+    if constexpr (ABLATE == 0 || ABLATE >= 4) {
       // (ABLATE 4 / 5, diagnostic: every tile takes this path -- the bulk
       // chains + Horner cost without / with the payload loads)
       if (z || ABLATE == 4 || ABLATE == 5) {  // (uniform) no event in the tile
@@ -1361,7 +1361,8 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     // the tile's first start it rides in lane 0's chain, into that record's
     // capture, R0 or the Horner value of chunk 0; a reset drops it.
     uint32_t c0 = U[0] ^ (lane == 0u ? carry : 0u), c1 = U[16], x0 = 0u, x1 = 0u, ub0 = 0u, ub1 = 0u;
-    const uint32_t Km = (Kw & 0xFFFFu) | (Kw >> 16);
+    // (ABLATE 8, diagnostic: no per-word event bodies -- results invalid)
+    const uint32_t Km = ABLATE == 8 ? 0u : (Kw & 0xFFFFu) | (Kw >> 16);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const uint32_t w0 = k + 1 < 16 ? U[k + 1] : 0u, w1 = k + 1 < 16 ? U[17 + k] : 0u;
@@ -1409,7 +1410,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
       uint32_t fv = 0u;
       // only the lanes holding a long record from here on (a few per tile):
       // the LDS reads below cost per active lane
-      if (in && lng_) {
+      if (in && lng_ && ABLATE != 7) {  // (ABLATE 7, diagnostic: no finish multiply -- results invalid)
         const bool h = j >= 64u;
         const uint32_t Pv = h ? (shift_bytes32<2>(smem, H) ^ R0c) : H;
         fv = ~(stream_mulcol(Pv, LDS_XMC_OFF(j & 63u)) ^ (h ? A1c : A0c));
@@ -1461,7 +1462,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     process(U1, t_first + i + 1, [&] { stream_issue<ABLATE>(P, tcl(i + 2), end4, lane, U0); });
   }
   if (i < ntile) process(U0, t_first + i, none);
-  if ((ABLATE == 4 || ABLATE == 5) && carry == 0x9E3779B1u) P.out[0] = carry;  // keeps the ablated chains (and loads) alive
+  if ((ABLATE == 4 || ABLATE == 5 || ABLATE == 7) && carry == 0x9E3779B1u) P.out[0] = carry;  // keeps the ablated chains (and loads) alive
   if (ABLATE == 3) return;
   if (dqcnt) qpush(dqv, dqcnt);
   qstore(qv, lane >= qs && lane < qf);
@@ -1530,6 +1531,8 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   const void* fn = ablate == 4 ? (const void*)crc32_stream_kernel<4>
                  : ablate == 5 ? (const void*)crc32_stream_kernel<5>
                  : ablate == 6 ? (const void*)crc32_stream_kernel<6>
+                 : ablate == 7 ? (const void*)crc32_stream_kernel<7>
+                 : ablate == 8 ? (const void*)crc32_stream_kernel<8>
                  : ablate == 3 ? (const void*)crc32_stream_kernel<3>
                  : ablate == 2 ? (const void*)crc32_stream_kernel<2> : (const void*)crc32_stream_kernel<0>;
   const size_t lds = LDS_SCRATCH_OFF + LDS_SMAP_BYTES;
