@@ -269,6 +269,18 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
                             size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc,
                             uint32_t* bad_expected);
 
+/* Batch framing of Insert records in a device-resident log, in place: payload
+ * i (key || value, len[i] bytes) already lies at img + off[i], and its
+ * 13-byte header (CommandLog::log, src/wal.rs:165-196) is written to
+ * img + off[i] - 13 -- type 1, crc[i], klen = min(len[i], kmax), vlen = the
+ * rest.  The batch form of lsmck_wal_encode_insert for logs built on the
+ * GPU (a log of many GiB is framed in one launch); crc[i] is normally
+ * lsmck_crc32_batch's output for the same payloads.  img, off, len, crc:
+ * device pointers; asynchronous on `stream` (NULL = the context's stream).
+ * Returns 0 or a negative hipError_t. */
+int lsmck_wal_frame_insert_device(lsmck_ctx* ctx, uint8_t* img, const uint64_t* off, const uint32_t* len,
+                                  const uint32_t* crc, size_t n, uint32_t kmax, void* stream);
+
 /* Whole-tree SSTable verify: the batch form of Checksums::verify over many
  * tables (Db::load, src/tokio/db.rs:37-59 -> src/tokio/sstable.rs:34).
  * Streams every data/index file in slices: 8192 files in flight (largest

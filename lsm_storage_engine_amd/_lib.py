@@ -99,6 +99,7 @@ SIGNATURES = [
     ("lsmck_sha256_batch_fixed", C.c_int, [vp, vp, sz, C.c_uint32, sz, vp, C.c_uint, vp]),
     ("lsmck_wal_replay_verify", C.c_int,
      [vp, vp, sz, C.c_uint, vp, sz, C.POINTER(sz), u64p, u32p, u32p]),  # recs: lsmck_wal_rec[cap]
+    ("lsmck_wal_frame_insert_device", C.c_int, [vp, vp, vp, vp, vp, sz, C.c_uint32, vp]),
     ("lsmck_checksums_verify_many", C.c_int,
      [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), sz, C.POINTER(C.c_int)]),
     ("lsmck_tree_verify", C.c_int, [vp, C.c_char_p, C.POINTER(TreeReport)]),

@@ -47,6 +47,7 @@ constexpr int kVariantStreamOnly = 0x400000;  // diagnostic: the stream kernel a
 constexpr size_t kChunkBytes = 64ull << 20;                // host staging chunk (payload)
 constexpr size_t kChunkRecs = 1u << 20;                    // host staging chunk (records)
 constexpr int kWalHostWalk = 0x7FFF0001;  // internal: the GPU header walk declined the log; walk it on the host
+constexpr int kWalTooBig = 0x7FFF0003;    // internal: one walk's jump tables would not fit; walk in smaller parts
 
 struct HipFail {
   hipError_t e;
@@ -267,6 +268,7 @@ struct lsmck_ctx {
   // at most half the free device memory); over it the log takes the host walk
   size_t wal_walk_budget_per_byte = 8;
   int wal_register = 0;  // host WAL images: hipHostRegister the caller's pages instead of the staging copy (A/B)
+  size_t wal_part_bytes = 0;  // GPU WAL walk: bytes per part (0 = the whole log, parts only when it does not fit)
   int wal_split = 1;     // host WAL images of two upload chunks or more: walk the first half during the second's upload
   // host WAL image upload: bytes per staged / DMA'd chunk.  16 MiB: 6.3 ms
   // for the 0.24 GB wal_diag image against 6.5 at 64 MiB (the first copy and
@@ -790,6 +792,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->wal_stage_bytes = (size_t)value;
     return 0;
   }
+  if (!strcmp(key, "wal_part_bytes")) {  // GPU WAL walk in parts of this many bytes (0 = whole; tests / A/B)
+    if (value < 0) return lsmck_host::set_error(LSMCK_EINVAL, "wal_part_bytes: >= 0");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_part_bytes = (size_t)value;
+    return 0;
+  }
   if (!strcmp(key, "wal_split")) {  // A/B: host WAL image walked in two parts behind its upload (0 = whole)
     if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "wal_split must be 0 or 1");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1021,6 +1029,7 @@ struct WalPart {
   size_t m = 0;        // records
   uint32_t term = 0;   // terminal code (WAL_END / BAD / STOP / STOPSELF, lsmck_wal.hip)
   uint64_t tpos = 0;   // BAD position, or where a prefix walk resumes
+  double over = 0;     // kWalTooBig: the scratch it needed over the budget (ratio)
 };
 constexpr uint32_t kWalBad = 0xFFFFFFFEu, kWalStop = 0xFFFFFFFDu, kWalStopSelf = 0xFFFFFFFCu;
 
@@ -1040,10 +1049,12 @@ static int wal_walk_part(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t 
   // that could start a header -- not with the record count: a valid log whose
   // payloads are dense in those bytes needs up to ~120x its size (levels x nc
   // x 4 B of J alone), and past 2^31 candidates the u32 ranks would reach the
-  // terminal codes.  Over a budget, or when an allocation fails, the replay
-  // takes the serial host walk instead (kWalHostWalk), as the reference would
-  // replay the same log.
-  if (nc64 >= (1ull << 31)) return kWalHostWalk;
+  // terminal codes.  Over a budget, or when an allocation fails, this walk
+  // declines (kWalTooBig) and the caller walks the log in smaller parts.
+  if (nc64 >= (1ull << 31)) {
+    out->over = (double)nc64 / (double)(1ull << 30);
+    return kWalTooBig;
+  }
   const uint32_t nc = (uint32_t)nc64;
   int levels = 0;
   while ((1ull << levels) <= nc) ++levels;  // 2^levels > nc, levels <= 31
@@ -1051,13 +1062,17 @@ static int wal_walk_part(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t 
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
   const size_t budget = std::min(free_b / 2, ctx->wal_walk_budget_per_byte * n + ((size_t)256 << 20));
-  if (need > budget) return kWalHostWalk;
+  if (need > budget) {
+    out->over = (double)need / (double)std::max<size_t>(budget, 1);
+    return kWalTooBig;
+  }
   if (ensure_dev(&W.pos, &W.cap_pos, std::max<size_t>(nc, 1)) ||
       ensure_dev(&W.J, &W.cap_J, std::max<size_t>((size_t)levels * nc, 1)) ||
       ensure_dev(&W.badpos, &W.cap_badpos, std::max<size_t>(nc, 1)) ||
       ensure_dev(&W.chain, &W.cap_chain, (size_t)1 << levels)) {
     (void)hipGetLastError();  // the failed hipMalloc's sticky error
-    return kWalHostWalk;
+    out->over = 2.0;
+    return kWalTooBig;
   }
   rc = lsmk_wal_chain(img, n, W.bits, W.pre, nc, levels, W.pos, W.J, W.badpos, W.chain, W.info, w0, w1, start, lim,
                       st);
@@ -1177,14 +1192,64 @@ static int wal_walk_setup(lsmck_ctx* ctx, size_t n) {
   return 0;
 }
 
+// The walk from position r to the end of the image in parts: each part is a
+// prefix walk over [r, a) (a = r + part, or the end) that resumes where the
+// previous one stopped, its records emitted after the `at` already there and
+// their CRC pass launched.  part 0: the whole rest in one walk first.  A part
+// whose jump tables do not fit (kWalTooBig) is cut to fit and walked again; a
+// record longer than the part doubles the part.  So the walk's scratch stays
+// within its budget and the log may exceed the u32 candidate ranks.  Marks
+// each part's words first unless `marked` (the whole image is marked).
+static int wal_walk_from(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t r, size_t at, size_t part,
+                         bool marked, hipStream_t st, const WalTrace& tr, WalPart* out) {
+  auto& W = ctx->wd;
+  int rc;
+  const uint64_t nw = lsmk_wal_words(n);
+  constexpr size_t kMinPart = 1u << 20;
+  if (!part && n - r >= (1ull << 32)) part = (size_t)1 << 31;  // (per-part ranks are u32)
+  for (;;) {
+    const uint64_t a = (part && n - r > part) ? ((r + part) & ~(uint64_t)63) : n;
+    if (!marked && (rc = lsmk_wal_mark_range(img, n, r & ~(uint64_t)63, a, W.bits, W.pre, st)))
+      return launch_rc(rc, "wal mark kernel");
+    WalPart P;
+    rc = wal_walk_part(ctx, img, n, r >> 6, a == n ? nw : a >> 6, r, a, true, at, st, &P, tr);
+    if (rc == kWalTooBig) {
+      const size_t cur = (size_t)(a - r);
+      size_t next = (size_t)((double)cur / (2.0 * std::max(P.over, 1.0)));
+      next &= ~(size_t)(kMinPart - 1);
+      if (next < kMinPart) {
+        if (cur <= kMinPart) return kWalHostWalk;  // even a 1 MiB part is too dense: the host walk
+        next = kMinPart;
+      }
+      part = next;
+      marked = false;  // (the scan of the declined part replaced its words' counts)
+      continue;
+    }
+    if (rc) return rc;
+    if ((rc = wal_crc_part(ctx, img, at, P.m, st))) return rc;
+    at += P.m;
+    if (a == n || (P.term != kWalStop && P.term != kWalStopSelf)) {
+      out->m = at;
+      out->term = P.term;
+      out->tpos = P.tpos;
+      return 0;
+    }
+    if (P.term == kWalStopSelf && P.tpos == r) {  // a record longer than the part: a longer part
+      part = std::min<size_t>((size_t)(n - r), part * 2);
+      marked = false;
+      continue;
+    }
+    r = P.tpos;
+    marked = false;  // the next part re-marks its words: the scan replaced the counts of [r, a)
+  }
+}
+
 // A device-resident image (or an uploaded one: `marked`, its candidate bitmap
-// is already in ctx->wd -- wal_upload marks each chunk behind its copy): one
-// walk, one CRC pass.
+// is already in ctx->wd -- wal_upload marks each chunk behind its copy): the
+// walk (in parts when its scratch would not fit), one CRC pass per part.
 static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck_wal_rec* recs, size_t cap,
                              size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected,
                              bool marked = false) {
-  // the candidate count is a u32 on the device: from 2^32 log bytes on it could wrap
-  if (n >= (1ull << 32)) return kWalHostWalk;
   std::lock_guard<std::mutex> lk(ctx->mu);
   DevGuard g(ctx->dev);
   const WalTrace tr;
@@ -1194,8 +1259,7 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
   if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
   hipStream_t st = so.st;
   WalPart P;
-  if ((rc = wal_walk_part(ctx, img, n, 0, lsmk_wal_words(n), 0, n, marked, 0, st, &P, tr))) return rc;
-  if ((rc = wal_crc_part(ctx, img, 0, P.m, st))) return rc;
+  if ((rc = wal_walk_from(ctx, img, n, 0, 0, ctx->wal_part_bytes, marked, st, tr, &P))) return rc;
   return wal_finish(ctx, img, P.m, P.term, P.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr);
 }
 
@@ -1321,7 +1385,7 @@ static int wal_replay_split(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool p
                             size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected) {
   const size_t ch = ctx->wal_stage_bytes;
   const size_t a = (n / 2) / ch * ch;
-  if (n >= (1ull << 32) || a < ch || n - a < ch) return kWalNoSplit;
+  if (a < ch || n - a < ch || a >= (1ull << 32)) return kWalNoSplit;
   std::lock_guard<std::mutex> lk(ctx->mu);
   DevGuard g(ctx->dev);
   const WalTrace tr;
@@ -1361,6 +1425,13 @@ static int wal_replay_split(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool p
     rc = wal_upload_range(ctx, U, a, n);
     const auto pr = prefix.get();
     if (rc) return rc;
+    if (pr.first == kWalTooBig) {  // the first half alone is too dense to walk in one part: all of it in parts
+      if ((rc = wal_upload_fence(ctx, st))) return rc;
+      guard.ok = true;
+      WalPart PA;
+      if ((rc = wal_walk_from(ctx, d, n, 0, 0, ctx->wal_part_bytes, false, st, tr, &PA))) return rc;
+      return wal_finish(ctx, d, PA.m, PA.term, PA.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr);
+    }
     if (pr.first) {
       if (pr.first != kWalHostWalk) lsmck_host::set_error(pr.first, pr.second.c_str());
       for (auto& S : ctx->stage) HIPCHK(hipStreamSynchronize(S.s));
@@ -1375,16 +1446,24 @@ static int wal_replay_split(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool p
     return wal_finish(ctx, d, P1.m, P1.term, P1.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr, done);
   // resume at r: the words from r's to the prefix end lost their counts to
   // the prefix scan; mark them again, then walk words [r/64, end) from r
+  // (in parts, when the rest's scratch would not fit)
   const uint64_t r = P1.tpos;
   if (r < a && (rc = lsmk_wal_mark_range(d, n, r & ~(uint64_t)63, a, ctx->wd.bits, ctx->wd.pre, st)))
     return launch_rc(rc, "wal mark kernel");
-  if ((rc = wal_walk_part(ctx, d, n, r >> 6, lsmk_wal_words(n), r, n, true, P1.m, st, &P2, tr))) return rc;
-  if ((rc = wal_crc_part(ctx, d, P1.m, P2.m, st))) return rc;
-  return wal_finish(ctx, d, P1.m + P2.m, P2.term, P2.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr,
-                    done);
+  if ((rc = wal_walk_from(ctx, d, n, r, P1.m, ctx->wal_part_bytes, true, st, tr, &P2))) return rc;
+  return wal_finish(ctx, d, P2.m, P2.term, P2.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr, done);
 }
 
 extern "C" {
+
+int lsmck_wal_frame_insert_device(lsmck_ctx* ctx, uint8_t* img, const uint64_t* off, const uint32_t* len,
+                                  const uint32_t* crc, size_t n, uint32_t kmax, void* stream) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  DevGuard g(ctx->dev);
+  rc = lsmk_wal_frame_insert(img, off, len, crc, n, kmax, pick_stream(ctx, stream));
+  return rc ? launch_rc(rc, "wal frame kernel") : 0;
+}
 
 int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsigned flags, lsmck_wal_rec* recs,
                             size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected) {

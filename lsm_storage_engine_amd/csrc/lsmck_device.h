@@ -84,6 +84,8 @@ int lsmk_wal_mark(const uint8_t* img, uint64_t n, uint64_t* bits, uint32_t* pre,
 int lsmk_wal_chain(const uint8_t* img, uint64_t n, const uint64_t* bits, const uint32_t* pre, uint32_t nc, int levels,
                    uint64_t* pos, uint32_t* J, uint64_t* badpos, uint32_t* chain, unsigned long long* info, uint64_t w0,
                    uint64_t w1, uint64_t start, uint64_t lim, hipStream_t st);
+int lsmk_wal_frame_insert(uint8_t* img, const uint64_t* off, const uint32_t* len, const uint32_t* crc, uint64_t n,
+                          uint32_t kmax, hipStream_t st);
 int lsmk_wal_emit(const uint8_t* img, uint64_t n, const uint32_t* chain, const uint64_t* pos,
                   const unsigned long long* info, uint32_t m, lsmck_wal_rec* recs, uint64_t* poff, uint32_t* plen,
                   uint32_t* pcrc, hipStream_t st);

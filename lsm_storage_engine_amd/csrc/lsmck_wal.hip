@@ -295,9 +295,37 @@ __global__ __launch_bounds__(256) void wal_emit(const uint8_t* __restrict__ img,
   pcrc[i] = r.crc;
 }
 
+// Batch framing of Insert records in place (CommandLog::log, wal.rs:165-196):
+// payload i = key || value already lies at img + off[i]; its 13-byte header
+// goes in front of it: type 1, crc[i], klen = min(len[i], kmax), vlen = the rest.
+// Byte stores (headers start at any offset); a thread per record.
+__global__ __launch_bounds__(256) void wal_frame_insert(uint8_t* __restrict__ img, const uint64_t* __restrict__ off,
+                                                         const uint32_t* __restrict__ len,
+                                                         const uint32_t* __restrict__ crc, uint64_t n, uint32_t kmax) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t* h = img + off[i] - 13u;
+  const uint32_t l = len[i], k = l < kmax ? l : kmax, v = l - k, c = crc[i];
+  h[0] = 1;
+  for (int b = 0; b < 4; ++b) {
+    h[1 + b] = (uint8_t)(c >> (8 * b));
+    h[5 + b] = (uint8_t)(k >> (8 * b));
+    h[9 + b] = (uint8_t)(v >> (8 * b));
+  }
+}
+
 }  // namespace lsmck
 
 using namespace lsmck;
+
+extern "C" int lsmk_wal_frame_insert(uint8_t* img, const uint64_t* off, const uint32_t* len, const uint32_t* crc,
+                                     uint64_t n, uint32_t kmax, hipStream_t st) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(wal_frame_insert, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, img, off, len, crc, n,
+                     kmax);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -(int)e;
+}
 
 static int launch_err() {
   hipError_t e = hipGetLastError();

@@ -221,8 +221,17 @@ class Context:
                    "sha256_batch_fixed(device)")
 
     # --- WAL / SSTable batch verify ---------------------------------------------
-    def wal_replay_verify(self, image, device_ptr=None):
-        """Returns (records, status, (bad_index, bad_crc, bad_expected))."""
+    def wal_frame_insert_device(self, img_ptr, off_ptr, len_ptr, crc_ptr, n, kmax=16, stream=None):
+        """lsmck_wal_frame_insert_device: Insert headers in front of n payloads
+        of a device-resident log (all device pointers)."""
+        _lib.check(self.lib.lsmck_wal_frame_insert_device(self.handle, img_ptr, off_ptr, len_ptr, crc_ptr, n, kmax,
+                                                           stream), "wal_frame_insert_device")
+
+    def wal_replay_verify(self, image, device_ptr=None, cap=None):
+        """Returns (records, status, (bad_index, bad_crc, bad_expected)).
+        cap: records to return at most (default: the n/9 + 1 a log of n
+        bytes can hold; a very large log whose record count is known can ask
+        for fewer -- the status and the count cover the whole log)."""
         if device_ptr is None:
             # any buffer (bytes, bytearray, memoryview, a read-only mmap of the
             # log file) is read in place: no copy of the image
@@ -230,7 +239,7 @@ class Context:
             ptr, n, flags = img.ctypes.data, len(img), _lib.HOST
         else:
             ptr, n, flags = device_ptr, image, _lib.DEVICE
-        cap = n // 9 + 1  # a record is at least 9 bytes (Remove of an empty key)
+        cap = n // 9 + 1 if cap is None else cap  # a record is at least 9 bytes (Remove of an empty key)
         recs = self._wal_recs_buffer(cap)
         nrec = C.c_size_t()
         bi, bc, be = C.c_uint64(), C.c_uint32(), C.c_uint32()

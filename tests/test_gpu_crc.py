@@ -315,7 +315,12 @@ def test_config3w_full_size_summary(ctx):
     """Config 3's 2^26 records framed as wal.rs Insert records (a 13-byte header
     before every payload, ~98 GiB image, device-resident) through the caller
     entry point: the stream kernel takes the gapped batch, and the CRC-32 of
-    the whole output array equals the oracle's (make_summaries.py config3w)."""
+    the whole output array equals the oracle's (make_summaries.py config3w).
+    Then the headers are written in front of the payloads (type 1, those CRCs,
+    klen = min(len, 16)) and the 98.6 GiB log is replayed on the GPU: the header
+    walk in parts (its jump tables for the whole log would not fit), every
+    record found at its offset, every stored CRC checked, the records' CRC
+    summary again the oracle's."""
     import zlib
     from lsm_storage_engine_amd.device import gen_zipf_lengths
     g = _summaries()["config3w"]
@@ -340,6 +345,18 @@ def test_config3w_full_size_summary(ctx):
             ctx.set_option("crc_stream", 1)
         got = out.download(np.uint32)
         assert "%08x" % zlib.crc32(got.astype("<u4").tobytes()) == g["summary_crc32"]
+        # the same image as a WAL: headers in front of the payloads, then the replay
+        ctx.wal_frame_insert_device(d.ptr, d_o.ptr, d_l.ptr, out.ptr, n, 16)
+        ctx.sync()
+        d_l.free()
+        out.free()
+        recs, st, bad = ctx.wal_replay_verify(total, device_ptr=d.ptr, cap=n)
+        assert st == 0, bad
+        assert len(recs) == n
+        assert np.array_equal(recs.payload_off, off)
+        assert np.array_equal(recs.rec_off, off - np.uint64(13))
+        assert np.array_equal(recs.klen.astype(np.uint64) + recs.vlen, ln.astype(np.uint64))
+        assert "%08x" % zlib.crc32(np.ascontiguousarray(recs.crc).astype("<u4").tobytes()) == g["summary_crc32"]
     finally:
         for buf in (d, d_o, d_l, out):
             buf.free()

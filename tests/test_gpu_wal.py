@@ -3,6 +3,7 @@ restatement of wal.rs:68-84,122-163: same records, same first error in log
 order (CorruptedData / Remove panic / InvalidCommandType), same clean end at a
 truncated header."""
 import os
+import zlib
 
 import numpy as np
 import pytest
@@ -192,9 +193,55 @@ def test_split_replay(ctx, case):
         for split in (1, 0):
             ctx.set_option("wal_split", split)
             same(ctx, img)
+        # the device image walked in 1 MiB parts (wal_part_bytes), aligned and not
+        ctx.set_option("wal_part_bytes", 1 << 20)
+        same(ctx, img, device=True)
+        same(ctx, img, device=True, shift=5)
     finally:
         ctx.set_option("wal_split", 1)
         ctx.set_option("wal_stage_bytes", 16 << 20)
+        ctx.set_option("wal_part_bytes", 0)
+
+
+def test_frame_insert_device(ctx):
+    """lsmck_wal_frame_insert_device writes the Insert headers in front of
+    payloads already in a device log: byte-identical to the oracle's framing
+    (klen = min(len, kmax); empty payloads; records at odd offsets)."""
+    rng = np.random.default_rng(51)
+    ln = rng.integers(0, 300, 4000).astype(np.uint32)
+    ln[:4] = [0, 1, 16, 17]
+    blob = O.gen_stream(52, 0, int(ln.sum()) + 64)
+    pays = []
+    o = 0
+    for l in ln:
+        pays.append(blob[o:o + int(l)].tobytes())
+        o += int(l)
+    want = b"".join(O.wal_insert(p[:min(len(p), 16)], p[min(len(p), 16):]) for p in pays)
+    off = np.zeros(len(ln), dtype=np.uint64)
+    pos = 0
+    for i, l in enumerate(ln):
+        off[i] = pos + 13
+        pos += 13 + int(l)
+    assert pos == len(want)
+    img = bytearray(b"\xAA" * len(want))  # headers: garbage until framed
+    for i, p in enumerate(pays):
+        img[int(off[i]):int(off[i]) + len(p)] = p
+    crc = np.array([zlib.crc32(p) for p in pays], dtype=np.uint32)
+    d = ctx.alloc(len(img) + 3)
+    bufs = [ctx.alloc(a.nbytes) for a in (off, ln, crc)]
+    try:
+        d.upload(np.frombuffer(bytes(img), np.uint8), offset=3)
+        for b_, a_ in zip(bufs, (off, ln, crc)):
+            b_.upload(a_)
+        ctx.wal_frame_insert_device(d.ptr + 3, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, len(ln), 16)
+        ctx.sync()
+        got = d.download(np.uint8)[3:3 + len(want)].tobytes()
+        assert got == want
+        assert same(ctx, got) == 0
+    finally:
+        d.free()
+        for b_ in bufs:
+            b_.free()
 
 
 @pytest.mark.parametrize("chunk", [1, 4096, 65536, 0])
@@ -258,11 +305,12 @@ def test_key_cut_at_eof_with_matching_crc_panics(ctx):
         wal.CommandLog.new_in_memory(img).replay_verify(ctx)
 
 
-def test_walk_candidate_flood_falls_back_to_the_host_walk(ctx):
+def test_walk_candidate_flood(ctx):
     """A valid multi-MiB log whose keys and values are all 0x01 bytes: every
-    byte is a header candidate for the GPU walk, whose jump tables would need
-    ~100x the log in device memory.  The replay falls back to the serial host
-    walk (host image and device image) and reports the same records."""
+    byte is a header candidate for the GPU walk, whose jump tables for the
+    whole log would need ~100x the log in device memory.  The walk goes in
+    parts small enough for its budget (host image and device image) and
+    reports the same records."""
     img = b"".join(O.wal_insert(b"\x01" * 40, b"\x01" * 200) for _ in range(16000))  # 4 MiB
     same(ctx, img)
     d = ctx.alloc(len(img))
