@@ -197,8 +197,8 @@ def main():
         offs = np.zeros(nrec, dtype=np.uint64)
         A = max(1, a.pack_align)
         if a.wal_framed:  # wal.rs:178-182: [u8 1][u32 crc][u32 klen][u32 vlen] in front of every payload
-            offs[:] = 13
-            offs[1:] += lens[:-1].astype(np.uint64) + np.uint64(13)
+            offs[:] = 13  # payload i+1 starts len[i] + 13 after payload i
+            offs[1:] += lens[:-1].astype(np.uint64)
             offs = np.cumsum(offs, dtype=np.uint64)
         else:
             slot = ((lens.astype(np.uint64) + (A - 1)) // A) * A  # A = 1: packed back to back

@@ -74,8 +74,8 @@ def summary(seed, offs, lens, sha, byte_off=0):
 
 def layout_wal(lens, header=13):
     """payload descriptors of records framed with a `header`-byte header each"""
-    offs = np.full(len(lens), header, dtype=np.uint64)
-    offs[1:] += lens[:-1].astype(np.uint64) + np.uint64(header)
+    offs = np.full(len(lens), header, dtype=np.uint64)  # payload i+1 starts len[i] + header after payload i
+    offs[1:] += lens[:-1].astype(np.uint64)
     return np.cumsum(offs, dtype=np.uint64), lens
 
 

@@ -317,7 +317,7 @@ def test_config3w_full_size_summary(ctx):
     entry point: the stream kernel takes the gapped batch, and the CRC-32 of
     the whole output array equals the oracle's (make_summaries.py config3w).
     Then the headers are written in front of the payloads (type 1, those CRCs,
-    klen = min(len, 16)) and the 98.6 GiB log is replayed on the GPU: the header
+    klen = min(len, 16)) and the 97.8 GiB log is replayed on the GPU: the header
     walk in parts (its jump tables for the whole log would not fit), every
     record found at its offset, every stored CRC checked, the records' CRC
     summary again the oracle's."""
@@ -326,8 +326,8 @@ def test_config3w_full_size_summary(ctx):
     g = _summaries()["config3w"]
     n = 1 << 26
     ln = gen_zipf_lengths(0x5EED0003, n)
-    off = np.full(n, 13, dtype=np.uint64)
-    off[1:] += ln[:-1].astype(np.uint64) + np.uint64(13)
+    off = np.full(n, 13, dtype=np.uint64)  # payload i+1 starts len[i] + 13 after payload i
+    off[1:] += ln[:-1].astype(np.uint64)
     off = np.cumsum(off, dtype=np.uint64)
     total = int(off[-1]) + int(ln[-1])
     assert total == g["image_bytes"]
