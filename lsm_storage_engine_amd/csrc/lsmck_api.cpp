@@ -731,7 +731,7 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
   if (!key) return lsmck_host::set_error(LSMCK_EINVAL, "null key");
   if (!strcmp(key, "crc_ablate")) {  // diagnostic only (results are garbage): 3 = payload loads only (the
                                      // bench's loads-only ceiling), 2 = stream kernel without payload loads
-    if (value != 0 && (value < 2 || value > 8)) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0 or 2..8");
+    if (value != 0 && (value < 2 || value > 10)) return lsmck_host::set_error(LSMCK_EINVAL, "crc_ablate must be 0 or 2..10");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->variant = (ctx->variant & ~0xF00) | ((int)value << 8);
     return 0;

@@ -1010,6 +1010,12 @@ __global__ __launch_bounds__(1024) void crc32_walk_kernel(CrcParams P) {
 // replay) is sorted by construction and its gaps lie inside one buffer; a
 // caller's device batch is checked on the device first (stream_check) and
 // the walking kernel, launched after this one, takes it when it is not.
+#ifndef LSMCK_ZFAST
+#define LSMCK_ZFAST 0  // A/B: tiles without events detected from record bt alone (skip the map)
+#endif
+#ifndef LSMCK_PREDEC
+#define LSMCK_PREDEC 0  // A/B: event words pre-decoded once per tile (1: one body per word, 2: one per chain)
+#endif
 #define STREAM_LONG 64u      // records of at least this many bytes go through the chains
 #define STREAM_MAX_GAP 64u   // caller batches: at most this many bytes between two records
 // LDS columns K (x) x^i, i = 0..31 (128 B per factor K) of the finish factors,
@@ -1118,7 +1124,7 @@ __device__ __forceinline__ void stream_issue(const CrcParams& P, int64_t tb, uin
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<unsigned char*>(P.base + tb), (short)0, (int)(span < 0x7FFFFFFFull ? span : 0x7FFFFFFFull), 0x00020000);
   const uint32_t vo = lane * 128u;
-  if (ABLATE == 2 || ABLATE == 4) {  // diagnostic: compute only (no payload loads; results invalid)
+  if (ABLATE == 2 || ABLATE == 4 || ABLATE == 10) {  // diagnostic: compute only (no payload loads; results invalid)
 #pragma unroll
     for (int j = 0; j < 32; ++j) u[j] = (uint32_t)tb * 0x9E3779B1u + lane + j;
     return;
@@ -1183,7 +1189,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     uint32_t K, base;
     if (f < 64u) {  // x^(8m): m zero-byte steps of the register from x^0
       K = 0x80000000u;
-      for (uint32_t i = 0; i < f; ++i) K = (K >> 8) ^ P.master[K & 0xFFu];
+      for (uint32_t i = 0; i < f; ++i) K = (K >> 8) ^ lds_ld(smem, 256u * (K & 0xFFu));  // T0 (replica 0)
       base = LDS_XMC_OFF(f);
     } else {
       K = stream_xinv(f - 64u);
@@ -1262,8 +1268,45 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
   // loads are issued (nothing between a tile's checksum and the next issue)
   uint32_t dqv = 0, dqcnt = 0;
 
+  // a tile without events: the straight chains, the Horner shift of every
+  // chunk to the tile end and the carry.  The carry (the open record's raw
+  // CRC up to this tile, aligned to its start) enters as lane 0's initial
+  // register: the Horner shift of lane 0 then carries it to the tile end with
+  // the chunk.
+  auto bulk = [&](const uint32_t (&U)[32]) {
+    uint32_t z0 = U[0] ^ (lane == 0u ? carry : 0u), z1 = U[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      z0 = crc_step_x(smem, z0, k + 1 < 16 ? U[k + 1] : 0u, lo, hi);
+      z1 = crc_step_x(smem, z1, k + 1 < 16 ? U[17 + k] : 0u, lo, hi);
+    }
+    uint32_t dz = 63u - lane;
+    asm volatile("" : "+v"(dz));  // not hoisted: eight loop-invariant column addresses spilled
+    const uint32_t XZ = wave_prefix_xor(walk_mulcol(shift_bytes32<2>(smem, z0) ^ z1, dz));
+    carry = (uint32_t)__builtin_amdgcn_readlane((int)XZ, 63);
+  };
+
   auto process = [&](const uint32_t (&U)[32], uint64_t t, auto&& issue_next) {
     const int64_t tb = tbase(t);
+    if constexpr (ABLATE == 9 || ABLATE == 10) {  // diagnostic: the bulk chains + Horner alone, no window / map
+      issue_next();                               // (10: without the payload loads); results invalid
+      __builtin_amdgcn_sched_barrier(0);
+      bulk(U);
+      return;
+    }
+    // No event in the tile, decided from record bt alone (scalar): it ends
+    // past the tile (then so does every later record) and it did not start
+    // here as a long record.  Such a tile skips the map and the window slide.
+    bool zf = false;
+#if LSMCK_ZFAST
+    if constexpr (ABLATE == 0 || ABLATE >= 6) {
+      const uint32_t so_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)Wo);
+      const uint32_t so_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(Wo >> 32));
+      const uint32_t sl = (uint32_t)__builtin_amdgcn_readfirstlane((int)Wl);
+      const int64_t s0 = (int64_t)(((uint64_t)so_hi << 32) | so_lo) - tb;
+      zf = bt >= r_hi || (s0 + (int64_t)sl >= 8192 && (s0 < 0 || sl < STREAM_LONG));
+    }
+#endif
     // --- map: the window's records that end in this tile write their events
     // (long records) into the wave's LDS map; a tile in which all 64 window
     // records end walks the next window too (rare: records of ~128 B or less)
@@ -1271,35 +1314,36 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     bool shorts = false;   // (uniform) a short record ends in this tile
     uint64_t wb = bt;      // base of the window being mapped
     uint32_t nwin = 0;     // full windows (64 records ending here) before the last one
-    uint32_t cntw;         // records of the last window ending here
-    int32_t re, rs;        // the last window's tile-relative end and start (start clamped to >= -128)
-    bool lng, sin;         // long record; its start lies in this tile
-    for (;;) {
-      const int64_t e64 = (int64_t)(Wo + Wl) - tb, s64 = (int64_t)Wo - tb;
-      const bool inr = wb + lane < r_hi;
-      const bool ends = inr && e64 < 8192;
-      cntw = (uint32_t)__builtin_popcountll(__ballot(ends));
-      lng = Wl >= STREAM_LONG;
-      sin = inr && s64 >= 0 && s64 < 8192;
-      re = (int32_t)(ends ? e64 : 8191);
-      rs = (int32_t)(s64 < -128 ? -128 : (s64 > 8191 ? 8191 : s64));
-      const bool ev_e = ends && lng, ev_s = sin && lng;
-      typedef __attribute__((address_space(3))) unsigned char lds_u8w_t;
-      if (ev_e) *(lds_u8w_t*)(size_t)(smap + 4u * ((uint32_t)re >> 7) + (((uint32_t)re >> 5) & 2u)) = (unsigned char)((re & 63) + 1);
-      if (ev_s) *(lds_u8w_t*)(size_t)(smap + 4u * ((uint32_t)rs >> 7) + (((uint32_t)rs >> 5) & 2u) + 1u) = (unsigned char)((rs & 63) + 1);
-      Kw |= wave_or_u32((ev_e ? 1u << (((uint32_t)re & 127u) >> 2) : 0u) | (ev_s ? 1u << (((uint32_t)rs & 127u) >> 2) : 0u));
-      shorts = shorts || __any(ends && !lng);
-      if (cntw < 64u) break;
-      wb += 64u;
-      ++nwin;
-      win_load(wb);  // (a dependent load: tiles of many small records only)
-    }
+    uint32_t cntw = 0;     // records of the last window ending here
+    int32_t re = 8191, rs = 8191;  // the last window's tile-relative end and start (start clamped to >= -128)
+    bool lng = false, sin = false;  // long record; its start lies in this tile
     const uint64_t bt0 = bt;
-    bt = wb + cntw;
-    // no event at all: no record ends here, and the open record started before
-    const bool z = nwin == 0u && cntw == 0u && !__builtin_amdgcn_readfirstlane((int)(sin && lng));
-    // the next tile's window: this one shifted by cntw (lands while this tile is checksummed)
-    {
+    bool z = zf;
+    if (!zf) {
+      for (;;) {
+        const int64_t e64 = (int64_t)(Wo + Wl) - tb, s64 = (int64_t)Wo - tb;
+        const bool inr = wb + lane < r_hi;
+        const bool ends = inr && e64 < 8192;
+        cntw = (uint32_t)__builtin_popcountll(__ballot(ends));
+        lng = Wl >= STREAM_LONG;
+        sin = inr && s64 >= 0 && s64 < 8192;
+        re = (int32_t)(ends ? e64 : 8191);
+        rs = (int32_t)(s64 < -128 ? -128 : (s64 > 8191 ? 8191 : s64));
+        const bool ev_e = ends && lng, ev_s = sin && lng;
+        typedef __attribute__((address_space(3))) unsigned char lds_u8w_t;
+        if (ev_e) *(lds_u8w_t*)(size_t)(smap + 4u * ((uint32_t)re >> 7) + (((uint32_t)re >> 5) & 2u)) = (unsigned char)((re & 63) + 1);
+        if (ev_s) *(lds_u8w_t*)(size_t)(smap + 4u * ((uint32_t)rs >> 7) + (((uint32_t)rs >> 5) & 2u) + 1u) = (unsigned char)((rs & 63) + 1);
+        Kw |= wave_or_u32((ev_e ? 1u << (((uint32_t)re & 127u) >> 2) : 0u) | (ev_s ? 1u << (((uint32_t)rs & 127u) >> 2) : 0u));
+        shorts = shorts || __any(ends && !lng);
+        if (cntw < 64u) break;
+        wb += 64u;
+        ++nwin;
+        win_load(wb);  // (a dependent load: tiles of many small records only)
+      }
+      bt = wb + cntw;
+      // no event at all: no record ends here, and the open record started before
+      z = nwin == 0u && cntw == 0u && !__builtin_amdgcn_readfirstlane((int)(sin && lng));
+      // the next tile's window: this one shifted by cntw (lands while this tile is checksummed)
       const uint32_t src = lane + cntw;
       const int sp = (int)((src & 63u) << 2);
       const uint32_t wlo = (uint32_t)__builtin_amdgcn_ds_bpermute(sp, (int)(uint32_t)Wo);
@@ -1324,19 +1368,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
       // (ABLATE 4 / 5, diagnostic: every tile takes this path -- the bulk
       // chains + Horner cost without / with the payload loads)
       if (z || ABLATE == 4 || ABLATE == 5) {  // (uniform) no event in the tile
-        // the carry (the open record's raw CRC up to this tile, aligned to
-        // its start) enters as lane 0's initial register: the Horner shift of
-        // lane 0 then carries it to the tile end with the chunk
-        uint32_t z0 = U[0] ^ (lane == 0u ? carry : 0u), z1 = U[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          z0 = crc_step_x(smem, z0, k + 1 < 16 ? U[k + 1] : 0u, lo, hi);
-          z1 = crc_step_x(smem, z1, k + 1 < 16 ? U[17 + k] : 0u, lo, hi);
-        }
-        uint32_t dz = 63u - lane;
-        asm volatile("" : "+v"(dz));  // not hoisted: eight loop-invariant column addresses spilled
-        const uint32_t XZ = wave_prefix_xor(walk_mulcol(shift_bytes32<2>(smem, z0) ^ z1, dz));
-        carry = (uint32_t)__builtin_amdgcn_readlane((int)XZ, 63);
+        bulk(U);
         return;
       }
     }
@@ -1361,6 +1393,43 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     // the tile's first start it rides in lane 0's chain, into that record's
     // capture, R0 or the Horner value of chunk 0; a reset drops it.
     uint32_t c0 = U[0] ^ (lane == 0u ? carry : 0u), c1 = U[16], x0 = 0u, x1 = 0u, ub0 = 0u, ub1 = 0u;
+#if LSMCK_PREDEC
+    // events pre-decoded once per tile: per event byte (chain byte j + 1, 0 =
+    // none) the word index + 0x20 (0x1F = none), and the start masks
+    uint32_t kw = (((ev | 0x80808080u) - 0x01010101u) >> 2) & 0x3F3F3F3Fu;
+    uint32_t mlo0 = (1u << (((((ev >> 8) & 0xFFu) - 1u) & 3u) << 3)) - 1u;
+    uint32_t mlo1 = (1u << ((((ev >> 24) - 1u) & 3u) << 3)) - 1u;
+    const uint32_t Km0 = ABLATE == 8 ? 0u : Kw & 0xFFFFu, Km1 = ABLATE == 8 ? 0u : Kw >> 16;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t w0 = k + 1 < 16 ? U[k + 1] : 0u, w1 = k + 1 < 16 ? U[17 + k] : 0u;
+      uint32_t i0 = c0, i1 = c1, n0 = w0, n1 = w1;
+#if LSMCK_PREDEC == 2
+      if (Km0 & (1u << k)) {
+#else
+      if ((Km0 | Km1) & (1u << k)) {
+#endif
+        asm volatile("" : "+v"(kw), "+v"(mlo0));
+        const bool me0 = (kw & 0xFFu) == 0x20u + k, ms0 = ((kw >> 8) & 0xFFu) == 0x20u + k;
+        x0 = me0 ? c0 : x0;
+        ub0 = me0 ? U[k] : ub0;
+        i0 = ms0 ? ~(U[k] | mlo0) : c0;
+        n0 = ms0 ? (w0 ^ mlo0) : w0;
+#if LSMCK_PREDEC == 2
+      }
+      if (Km1 & (1u << k)) {
+#endif
+        asm volatile("" : "+v"(kw), "+v"(mlo1));
+        const bool me1 = ((kw >> 16) & 0xFFu) == 0x20u + k, ms1 = (kw >> 24) == 0x20u + k;
+        x1 = me1 ? c1 : x1;
+        ub1 = me1 ? U[16 + k] : ub1;
+        i1 = ms1 ? ~(U[16 + k] | mlo1) : c1;
+        n1 = ms1 ? (w1 ^ mlo1) : w1;
+      }
+      c0 = crc_step_x(smem, i0, n0, lo, hi);
+      c1 = crc_step_x(smem, i1, n1, lo, hi);
+    }
+#else
     // (ABLATE 8, diagnostic: no per-word event bodies -- results invalid)
     const uint32_t Km = ABLATE == 8 ? 0u : (Kw & 0xFFFFu) | (Kw >> 16);
 #pragma unroll
@@ -1387,12 +1456,15 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
       c0 = crc_step_x(smem, i0, n0, lo, hi);
       c1 = crc_step_x(smem, i1, n1, lo, hi);
     }
+#endif
     const uint32_t cap0 = ke0 ? stream_capture(smem, x0, ub0, ((ev & 0xFFu) - 1u) & 3u, lo) : 0u;
     const uint32_t cap1 = ke1 ? stream_capture(smem, x1, ub1, (((ev >> 16) & 0xFFu) - 1u) & 3u, lo) : 0u;
     const uint32_t R0 = c0;
     const uint32_t T = (ev >> 24) ? c1 : (shift_bytes32<2>(smem, c0) ^ c1);
     // --- Horner inside the tile: T to the chunk before the next END's chunk
-    const uint64_t above = lane == 63u ? 0ull : (M1 >> (lane + 1u)) << (lane + 1u);
+    uint32_t l1 = lane + 1u;
+    asm volatile("" : "+v"(l1));  // not hoisted: the loop-invariant lane mask spilled (a vmcnt(0) reload)
+    const uint64_t above = lane == 63u ? 0ull : (M1 >> l1) << l1;
     const uint32_t cn = above ? (uint32_t)__builtin_ctzll(above) : 64u;
     const uint32_t X = wave_prefix_xor(walk_mulcol(T, cn - 1u - lane));
     // --- records: the window lane of a record finishes it
@@ -1462,7 +1534,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     process(U1, t_first + i + 1, [&] { stream_issue<ABLATE>(P, tcl(i + 2), end4, lane, U0); });
   }
   if (i < ntile) process(U0, t_first + i, none);
-  if ((ABLATE == 4 || ABLATE == 5 || ABLATE == 7) && carry == 0x9E3779B1u) P.out[0] = carry;  // keeps the ablated chains (and loads) alive
+  if ((ABLATE == 4 || ABLATE == 5 || ABLATE == 7 || ABLATE == 9 || ABLATE == 10) && carry == 0x9E3779B1u) P.out[0] = carry;  // keeps the ablated chains (and loads) alive
   if (ABLATE == 3) return;
   if (dqcnt) qpush(dqv, dqcnt);
   qstore(qv, lane >= qs && lane < qf);
@@ -1528,7 +1600,9 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
     hipLaunchKernelGGL(stream_check, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, *P);
   hipLaunchKernelGGL(stream_cuts, dim3((W + 1u + 255u) / 256u), dim3(256), 0, st, *P, W);
   const int ablate = (variant >> 8) & 0xF;
-  const void* fn = ablate == 4 ? (const void*)crc32_stream_kernel<4>
+  const void* fn = ablate == 9 ? (const void*)crc32_stream_kernel<9>
+                 : ablate == 10 ? (const void*)crc32_stream_kernel<10>
+                 : ablate == 4 ? (const void*)crc32_stream_kernel<4>
                  : ablate == 5 ? (const void*)crc32_stream_kernel<5>
                  : ablate == 6 ? (const void*)crc32_stream_kernel<6>
                  : ablate == 7 ? (const void*)crc32_stream_kernel<7>
