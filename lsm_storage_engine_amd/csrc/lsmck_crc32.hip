@@ -1010,12 +1010,6 @@ __global__ __launch_bounds__(1024) void crc32_walk_kernel(CrcParams P) {
 // replay) is sorted by construction and its gaps lie inside one buffer; a
 // caller's device batch is checked on the device first (stream_check) and
 // the walking kernel, launched after this one, takes it when it is not.
-#ifndef LSMCK_ZFAST
-#define LSMCK_ZFAST 0  // A/B: tiles without events detected from record bt alone (skip the map)
-#endif
-#ifndef LSMCK_PREDEC
-#define LSMCK_PREDEC 0  // A/B: event words pre-decoded once per tile (1: one body per word, 2: one per chain)
-#endif
 #define STREAM_LONG 64u      // records of at least this many bytes go through the chains
 #define STREAM_MAX_GAP 64u   // caller batches: at most this many bytes between two records
 // LDS columns K (x) x^i, i = 0..31 (128 B per factor K) of the finish factors,
@@ -1065,31 +1059,48 @@ __device__ __forceinline__ uint32_t stream_xinv(uint32_t t) {  // x^(-8(4-t))
 // empty and every later empty record sits at its predecessor's end.  Then every
 // 4 KiB page a 128-byte chunk of [off[0], end) lies on holds a byte of some
 // record, so the chunk loads touch only the caller's pages.
-// A caller's batch: the eligibility check, one record per thread with
-// coalesced loads; record i+1's offset and length come from the next lane
-// (lane 63 loads them).  The per-wave cuts follow by binary search
-// (stream_cuts, sorted by then).  A fused check + cuts pass with four records
-// per thread ran 0.31 ms on config 3 against 0.19 + 0.016 for the two.
+// A caller's batch: the eligibility check, four records per thread (off[]
+// as two 16-byte loads and len[] as one when both arrays are 16-byte aligned,
+// element loads otherwise); the next thread's first record comes from the
+// next lane (lane 63 loads it).  The per-wave cuts follow by binary search
+// (stream_cuts, sorted by then).  One record per thread ran 0.18 ms on config
+// 3; a fused check + cuts pass 0.31 ms.
+template <bool VEC>
 __global__ __launch_bounds__(256) void stream_check(CrcParams P) {
   const uint64_t n = P.nrec;
-  const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  const uint64_t ic = i < n ? i : n - 1u;
-  const uint64_t o = P.off[ic];
-  const uint32_t l = P.len[ic];
-  uint64_t o1 = ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(o >> 32), 1) << 32) |
-                (uint32_t)__shfl_down((int)(uint32_t)o, 1);
-  uint32_t l1 = (uint32_t)__shfl_down((int)l, 1);
-  if ((threadIdx.x & 63u) == 63u && i + 1u < n) {
-    o1 = P.off[i + 1u];
-    l1 = P.len[i + 1u];
+  const uint64_t i0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
+  uint64_t o[5];
+  uint32_t l[5];
+  if (VEC && i0 + 4u <= n) {
+    const u32x4 a = *(const u32x4*)(P.off + i0), b = *(const u32x4*)(P.off + i0 + 2u);
+    const u32x4 c = *(const u32x4*)(P.len + i0);
+    o[0] = ((uint64_t)a.y << 32) | a.x;
+    o[1] = ((uint64_t)a.w << 32) | a.z;
+    o[2] = ((uint64_t)b.y << 32) | b.x;
+    o[3] = ((uint64_t)b.w << 32) | b.z;
+    l[0] = c.x; l[1] = c.y; l[2] = c.z; l[3] = c.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t i = i0 + j < n ? i0 + j : n - 1u;
+      o[j] = P.off[i];
+      l[j] = P.len[i];
+    }
   }
-  bool bad = false;
-  if (i < n) {
-    const uint64_t e = o + l;
-    bad = (i == 0 && l == 0u) ||
-          (i + 1u < n && (o1 < e || o1 - e > STREAM_MAX_GAP || (l1 == 0u && o1 != e)));
+  // the next thread's first record
+  o[4] = ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(o[0] >> 32), 1) << 32) | (uint32_t)__shfl_down((int)(uint32_t)o[0], 1);
+  l[4] = (uint32_t)__shfl_down((int)l[0], 1);
+  if ((threadIdx.x & 63u) == 63u && i0 + 4u < n) {
+    o[4] = P.off[i0 + 4u];
+    l[4] = P.len[i0 + 4u];
   }
-  if (__any(bad) && (threadIdx.x & 63u) == 0u) *P.sflag = 0u;  // plain stores of one value: no atomic needed
+  bool bad = i0 == 0 && n > 0 && l[0] == 0u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint64_t e = o[j] + l[j];
+    bad = bad || (i0 + j + 1u < n && (o[j + 1] < e || o[j + 1] - e > STREAM_MAX_GAP || (l[j + 1] == 0u && o[j + 1] != e)));
+  }
+  if (bad) *P.sflag = 0u;  // plain stores of one value: no atomic needed
 }
 
 // cut w, w = 0..W: the first record starting at or after off[0] + span*w/W
@@ -1298,7 +1309,6 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     // past the tile (then so does every later record) and it did not start
     // here as a long record.  Such a tile skips the map and the window slide.
     bool zf = false;
-#if LSMCK_ZFAST
     if constexpr (ABLATE == 0 || ABLATE >= 6) {
       const uint32_t so_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)Wo);
       const uint32_t so_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(Wo >> 32));
@@ -1306,7 +1316,6 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
       const int64_t s0 = (int64_t)(((uint64_t)so_hi << 32) | so_lo) - tb;
       zf = bt >= r_hi || (s0 + (int64_t)sl >= 8192 && (s0 < 0 || sl < STREAM_LONG));
     }
-#endif
     // --- map: the window's records that end in this tile write their events
     // (long records) into the wave's LDS map; a tile in which all 64 window
     // records end walks the next window too (rare: records of ~128 B or less)
@@ -1393,43 +1402,6 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     // the tile's first start it rides in lane 0's chain, into that record's
     // capture, R0 or the Horner value of chunk 0; a reset drops it.
     uint32_t c0 = U[0] ^ (lane == 0u ? carry : 0u), c1 = U[16], x0 = 0u, x1 = 0u, ub0 = 0u, ub1 = 0u;
-#if LSMCK_PREDEC
-    // events pre-decoded once per tile: per event byte (chain byte j + 1, 0 =
-    // none) the word index + 0x20 (0x1F = none), and the start masks
-    uint32_t kw = (((ev | 0x80808080u) - 0x01010101u) >> 2) & 0x3F3F3F3Fu;
-    uint32_t mlo0 = (1u << (((((ev >> 8) & 0xFFu) - 1u) & 3u) << 3)) - 1u;
-    uint32_t mlo1 = (1u << ((((ev >> 24) - 1u) & 3u) << 3)) - 1u;
-    const uint32_t Km0 = ABLATE == 8 ? 0u : Kw & 0xFFFFu, Km1 = ABLATE == 8 ? 0u : Kw >> 16;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const uint32_t w0 = k + 1 < 16 ? U[k + 1] : 0u, w1 = k + 1 < 16 ? U[17 + k] : 0u;
-      uint32_t i0 = c0, i1 = c1, n0 = w0, n1 = w1;
-#if LSMCK_PREDEC == 2
-      if (Km0 & (1u << k)) {
-#else
-      if ((Km0 | Km1) & (1u << k)) {
-#endif
-        asm volatile("" : "+v"(kw), "+v"(mlo0));
-        const bool me0 = (kw & 0xFFu) == 0x20u + k, ms0 = ((kw >> 8) & 0xFFu) == 0x20u + k;
-        x0 = me0 ? c0 : x0;
-        ub0 = me0 ? U[k] : ub0;
-        i0 = ms0 ? ~(U[k] | mlo0) : c0;
-        n0 = ms0 ? (w0 ^ mlo0) : w0;
-#if LSMCK_PREDEC == 2
-      }
-      if (Km1 & (1u << k)) {
-#endif
-        asm volatile("" : "+v"(kw), "+v"(mlo1));
-        const bool me1 = ((kw >> 16) & 0xFFu) == 0x20u + k, ms1 = (kw >> 24) == 0x20u + k;
-        x1 = me1 ? c1 : x1;
-        ub1 = me1 ? U[16 + k] : ub1;
-        i1 = ms1 ? ~(U[16 + k] | mlo1) : c1;
-        n1 = ms1 ? (w1 ^ mlo1) : w1;
-      }
-      c0 = crc_step_x(smem, i0, n0, lo, hi);
-      c1 = crc_step_x(smem, i1, n1, lo, hi);
-    }
-#else
     // (ABLATE 8, diagnostic: no per-word event bodies -- results invalid)
     const uint32_t Km = ABLATE == 8 ? 0u : (Kw & 0xFFFFu) | (Kw >> 16);
 #pragma unroll
@@ -1456,7 +1428,6 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
       c0 = crc_step_x(smem, i0, n0, lo, hi);
       c1 = crc_step_x(smem, i1, n1, lo, hi);
     }
-#endif
     const uint32_t cap0 = ke0 ? stream_capture(smem, x0, ub0, ((ev & 0xFFu) - 1u) & 3u, lo) : 0u;
     const uint32_t cap1 = ke1 ? stream_capture(smem, x1, ub1, (((ev >> 16) & 0xFFu) - 1u) & 3u, lo) : 0u;
     const uint32_t R0 = c0;
@@ -1527,8 +1498,8 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
   auto tcl = [&](uint64_t x) -> int64_t { return tbase(x < ntile ? t_first + x : t_last); };
   auto none = [] {};
   uint32_t U0[32], U1[32];
-  stream_issue<ABLATE>(P, tcl(0), end4, lane, U0);
   uint64_t i = 0;
+  stream_issue<ABLATE>(P, tcl(0), end4, lane, U0);
   for (; i + 2 <= ntile; i += 2) {
     process(U0, t_first + i, [&] { stream_issue<ABLATE>(P, tcl(i + 1), end4, lane, U1); });
     process(U1, t_first + i + 1, [&] { stream_issue<ABLATE>(P, tcl(i + 2), end4, lane, U0); });
@@ -1597,7 +1568,12 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   if (e != hipSuccess) return -(int)e;
   const uint32_t W = lsmk_stream_waves(ncu);
   if (!trusted)  // a caller's batch: checked first (the cuts below then skip on the flag)
-    hipLaunchKernelGGL(stream_check, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, *P);
+  {
+    const bool vec = ((uintptr_t)P->off % 16u == 0) && ((uintptr_t)P->len % 16u == 0);
+    const dim3 g((unsigned)((n + 1023) / 1024));
+    if (vec) hipLaunchKernelGGL(stream_check<true>, g, dim3(256), 0, st, *P);
+    else hipLaunchKernelGGL(stream_check<false>, g, dim3(256), 0, st, *P);
+  }
   hipLaunchKernelGGL(stream_cuts, dim3((W + 1u + 255u) / 256u), dim3(256), 0, st, *P, W);
   const int ablate = (variant >> 8) & 0xF;
   const void* fn = ablate == 9 ? (const void*)crc32_stream_kernel<9>
