@@ -163,7 +163,8 @@ int lsmck_device_count(void);
  *   "crc_ablate"  DIAGNOSTIC ONLY, results are invalid while set: 3 = payload
  *                 loads only (ring, stream and walking kernels: the bench's
  *                 loads-only ceiling), 2 = the stream kernel without payload
- *                 loads; 0 = off.
+ *                 loads; 4..10 = stream kernel ablations (DESIGN.md 3.1
+ *                 items 10-11); 0 = off.
  *   "sha_order"   variable-length SHA-256 batches of >= 2048 messages run in
  *                 decreasing length order (1, default) or batch order (0).
  *                 A/B switch; digests are identical either way.
