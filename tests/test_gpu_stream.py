@@ -32,19 +32,22 @@ def _gapped(lens, gaps, lead):
     return np.cumsum(step) + np.uint64(lead), lens
 
 
-def _device(ctx, data, off, ln, shift=0, exact=False, sorted_span=False):
+def _device(ctx, data, off, ln, shift=0, exact=False, sorted_span=False, desc_shift=False):
     """CRCs of device-resident records; the data at `shift` bytes into its
     allocation; `exact`: the allocation ends with the last record's byte;
-    `sorted_span`: LSMCK_SORTED (no device-side check of the descriptors)."""
+    `sorted_span`: LSMCK_SORTED (no device-side check of the descriptors);
+    `desc_shift`: off[] 8 and len[] 4 bytes into their allocations (not
+    16-byte aligned: the check's element-load path)."""
     n = len(off)
     size = int(off[-1]) + int(ln[-1]) if exact else len(data)
     d = ctx.alloc(size + shift)
     d.upload(np.ascontiguousarray(data[:size]), offset=shift)
-    d_o, d_l, out = ctx.alloc(8 * n), ctx.alloc(4 * n), ctx.alloc(4 * n)
+    so, sl = (8, 4) if desc_shift else (0, 0)
+    d_o, d_l, out = ctx.alloc(8 * n + so), ctx.alloc(4 * n + sl), ctx.alloc(4 * n)
     out.upload(np.full(n, 0xA5A5A5A5, dtype=np.uint32))  # unwritten outputs show
-    d_o.upload(off)
-    d_l.upload(ln)
-    ctx.crc32_device(d.ptr + shift, d_o.ptr, d_l.ptr, n, out.ptr, sorted_span=sorted_span)
+    d_o.upload(off, offset=so)
+    d_l.upload(ln, offset=sl)
+    ctx.crc32_device(d.ptr + shift, d_o.ptr + so, d_l.ptr + sl, n, out.ptr, sorted_span=sorted_span)
     ctx.sync()
     got = out.download(np.uint32)
     for b in (d, d_o, d_l, out):
@@ -211,6 +214,41 @@ def test_ineligible_batches_take_the_walking_kernel(ctx, case):
         assert (_device(ctx, data, off, ln) == 0xA5A5A5A5).all()
     finally:
         ctx.set_option("crc_stream", 1)
+
+
+@pytest.mark.parametrize("desc_shift", [False, True])
+def test_check_positions_and_descriptor_alignment(ctx, desc_shift):
+    """The device check reads four records per thread (16-byte loads when the
+    descriptor arrays allow them, element loads otherwise): batches of 1..4099
+    records are taken, and one overlap at any position -- each slot of a
+    thread's four, across threads, waves and workgroups, the last record --
+    is caught."""
+    rng = np.random.default_rng(23)
+    for n in (1, 2, 3, 5, 4099):
+        lens = rng.integers(64, 400, n)
+        off, ln = _packed(lens, 5)
+        data = O.gen_stream(0x57AE0A00 + n, 0, int(off[-1]) + int(ln[-1]) + 16)
+        ctx.set_option("crc_stream", 2)
+        try:
+            got = _device(ctx, data, off, ln, desc_shift=desc_shift)
+        finally:
+            ctx.set_option("crc_stream", 1)
+        assert np.array_equal(got, O.crc32_batch(data, off, ln)), n
+    lens = rng.integers(64, 400, 4099)
+    off0, ln = _packed(lens, 5)
+    data = O.gen_stream(0x57AE0B00, 0, int(off0[-1]) + int(ln[-1]) + 16)
+    want = O.crc32_batch(data, off0, ln, threads=8)
+    for p in (1, 2, 3, 4, 5, 252, 255, 256, 257, 1023, 1024, 1025, 4098):
+        off = off0.copy()
+        off[p] -= np.uint64(1)  # record p overlaps record p - 1 by one byte
+        want_p = want.copy()
+        want_p[p] = O.crc32_batch(data, off[p:p + 1], ln[p:p + 1])[0]
+        assert np.array_equal(_device(ctx, data, off, ln, desc_shift=desc_shift), want_p), p
+        ctx.set_option("crc_stream", 2)  # the stream kernel alone declines: nothing written
+        try:
+            assert (_device(ctx, data, off, ln, desc_shift=desc_shift) == 0xA5A5A5A5).all(), p
+        finally:
+            ctx.set_option("crc_stream", 1)
 
 
 @pytest.mark.parametrize("kind", ["packed", "wal_big_gaps"])
