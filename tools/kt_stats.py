@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Kernel-trace statistics from a rocprofv3 rocpd database (results.db) or
-kernel_trace.csv: per kernel name, calls / total / average / min / max (us)."""
+kernel_trace.csv: per kernel name, calls / total / average / median / min / max (us)."""
 import csv
 import glob
 import os
@@ -28,9 +28,11 @@ def main():
             for n, d in rows(f):
                 agg.setdefault(n.split("(")[0][:90], []).append(d / 1000.0)
         print(f"== {arg}")
-        print(f"{'kernel':92s} {'calls':>5s} {'total_us':>12s} {'avg_us':>10s} {'min_us':>10s} {'max_us':>10s}")
+        print(f"{'kernel':92s} {'calls':>5s} {'total_us':>12s} {'avg_us':>10s} {'median_us':>10s} {'min_us':>10s} "
+              f"{'max_us':>10s}")
         for n, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
-            print(f"{n:92s} {len(v):5d} {sum(v):12.1f} {sum(v) / len(v):10.1f} {min(v):10.1f} {max(v):10.1f}")
+            med = sorted(v)[len(v) // 2] if len(v) % 2 else sum(sorted(v)[len(v) // 2 - 1:len(v) // 2 + 1]) / 2
+            print(f"{n:92s} {len(v):5d} {sum(v):12.1f} {sum(v) / len(v):10.1f} {med:10.1f} {min(v):10.1f} {max(v):10.1f}")
 
 
 if __name__ == "__main__":
