@@ -6,7 +6,10 @@
 //     verified in one GPU batch (lsmck_tree_verify: Checksums::verify of every
 //     table, checksums.rs:40-62), then the WAL replayed with its payload CRCs
 //     checked in one GPU batch (lsmck_wal_replay_verify: CommandLog iterator +
-//     MemTable::from_log, wal.rs:68-163, memtable.rs:28-47);
+//     MemTable::from_log, wal.rs:68-163, memtable.rs:28-47).  The replay runs
+//     on its own thread and context while the tree is verified; its outcome is
+//     acted on after the tree's, so a failing start-up reports what the
+//     reference reports;
 //   * every insert / update / delete is appended to the WAL with its CRC-32
 //     from lsmck_crc32_ieee (through lsmck_wal_encode_*: CommandLog::log,
 //     wal.rs:165-196), one write(2) per record as the reference's flushed
@@ -443,9 +446,158 @@ struct Db {
         *L.secs = now_s() - t_idx0;
       });
     };
+    // The WAL is replayed on its own thread (and its own context on the same
+    // GPU) while the tree is verified: the two read different files and
+    // neither result depends on the other.  Its outcome is acted on only after
+    // the tree's, in Db::load's order (db.rs:37-73: the tables, then
+    // MemTable::from_log), so a start-up that fails reports what the
+    // reference reports.  Nothing on disk changes before the tree is verified:
+    // a rotated log (wal.log.flushing) is replayed from memory in front of
+    // wal.log, and merged on disk afterwards.
+    struct WalLoad {
+      int rc = 0;                // lsmck_wal_replay_verify's result, or -1: see err
+      std::string err;           // a message for exit(1) (rc < 0)
+      std::string panic;         // a panic message (the replayed payloads)
+      bool have_older = false;   // a rotated log was found
+      std::string older, newer;  // its bytes and wal.log's (only when have_older)
+      size_t n = 0, nrec = 0;
+      double t_verify = 0, t_wal = 0;
+    } W;
+    std::thread wal_th([this, &W]() {
+      const double t1 = now_s();
+      const uint8_t* img = nullptr;
+      void* map = nullptr;
+      size_t n = 0;
+      int rfd = -1;
+      if (read_file(flushing_path(), &W.older)) {
+        W.have_older = true;
+        read_file(wal_path(), &W.newer);
+        W.older += W.newer;
+        img = (const uint8_t*)W.older.data();
+        n = W.older.size();
+      } else if ((rfd = open(wal_path().c_str(), O_RDONLY | O_CLOEXEC)) >= 0) {
+        struct stat st;
+        fstat(rfd, &st);
+        n = (size_t)st.st_size;
+        if (n) {
+          map = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, rfd, 0);
+          if (map == MAP_FAILED) {
+            W.rc = -1;
+            W.err = std::string("mmap wal: ") + strerror(errno);
+            close(rfd);
+            return;
+          }
+          img = (const uint8_t*)map;
+        }
+      }
+      W.n = n;
+      lsmck_ctx* wctx = lsmck_ctx_create(cfg.device);
+      if (!wctx) {
+        W.rc = -1;
+        W.err = std::string("lsmck_ctx_create: ") + lsmck_last_error();
+      }
+      const size_t cap = n / 9 + 1;  // a record is at least 9 bytes
+      // uninitialised: only the records found are written (a zeroed vector of
+      // 32 B per 9 log bytes cost more than the replay itself)
+      std::unique_ptr<lsmck_wal_rec[]> recs(new lsmck_wal_rec[cap]);
+      size_t nrec = 0;
+      uint64_t bad_index = 0;
+      uint32_t bad_crc = 0, bad_expected = 0;
+      char msg[256];
+      if (wctx) {
+        W.rc = lsmck_wal_replay_verify(wctx, img, n, LSMCK_HOST, recs.get(), cap, &nrec, &bad_index, &bad_crc,
+                                       &bad_expected);
+        if (W.rc < 0) W.err = std::string("lsmck_wal_replay_verify: ") + lsmck_last_error();
+        lsmck_ctx_destroy(wctx);
+      }
+      W.t_verify = now_s() - t1;
+      W.nrec = nrec;
+      if (W.rc == LSMCK_WAL_CORRUPTED) {  // MemTable::from_log(..).expect(..) on Err (db.rs:61-62)
+        snprintf(msg, sizeof msg, "Can't restore memtable from a log: CorruptedData { checksum: %u, expected: %u }",
+                 bad_crc, bad_expected);
+        W.panic = msg;
+      } else if (W.rc == LSMCK_WAL_REMOVE_PANIC) {  // wal.rs:154-159
+        snprintf(msg, sizeof msg, "data corruption encountered (%08x) != %08x", bad_crc, bad_expected);
+        W.panic = msg;
+      } else if (W.rc == LSMCK_WAL_BAD_TYPE) {
+        snprintf(msg, sizeof msg, "Can't restore memtable from a log: InvalidCommandType(%u)", bad_crc);
+        W.panic = msg;
+      }
+      if (W.rc < 0 || !W.panic.empty()) {
+        if (map) munmap(map, n);
+        if (rfd >= 0) close(rfd);
+        return;
+      }
+      // MemTable::from_log (memtable.rs:28-47), on the payload actually read
+      // (short at EOF).  The records are grouped by key (a stable sort keeps log
+      // order inside a key); each key's final state and its share of the
+      // reference's byte count are replayed per key, and the table is built in
+      // key order with an end hint.  Same table and count as inserting record by
+      // record, which took 0.48 s for 500k records (std::map comparisons and
+      // rebalancing).  The count is from_log's: an Insert adds key + value even
+      // over an existing key, a Remove of a present key subtracts its entry.
+      struct KeyRec {
+        std::string_view k;
+        uint32_t i;
+      };
+      std::vector<KeyRec> kr(nrec);
+      auto payload = [&](size_t i, size_t* klen, size_t* got) {
+        const lsmck_wal_rec& r = recs[i];
+        const uint64_t want = (uint64_t)(uint32_t)(r.klen + r.vlen);
+        *got = (size_t)std::min<uint64_t>(want, n - r.payload_off);
+        *klen = r.type == 1 ? (size_t)std::min<uint64_t>(r.klen, *got) : *got;
+        return (const char*)img + r.payload_off;
+      };
+      for (size_t i = 0; i < nrec; ++i) {
+        size_t kl, got;
+        const char* p = payload(i, &kl, &got);
+        if (recs[i].type == 1 && got < recs[i].klen) {
+          // an Insert cut at EOF inside its key whose CRC matches the short
+          // bytes: data.split_off(key_len) panics (wal.rs:142)
+          snprintf(msg, sizeof msg, "`at` split index (is %u) should be <= len (is %zu)", recs[i].klen, got);
+          W.panic = msg;
+          if (map) munmap(map, n);
+          if (rfd >= 0) close(rfd);
+          return;
+        }
+        kr[i] = {std::string_view(p, kl), (uint32_t)i};
+      }
+      std::stable_sort(kr.begin(), kr.end(), [](const KeyRec& a, const KeyRec& b) { return a.k < b.k; });
+      size_t bytes = 0;
+      for (size_t a = 0; a < nrec;) {
+        size_t b = a + 1;
+        while (b < nrec && kr[b].k == kr[a].k) ++b;
+        bool present = false;
+        size_t vlen = 0, last = 0;
+        for (size_t x = a; x < b; ++x) {
+          size_t kl, got;
+          payload(kr[x].i, &kl, &got);
+          if (recs[kr[x].i].type == 1) {
+            bytes += got;  // key + value
+            present = true;
+            vlen = got - kl;
+            last = kr[x].i;
+          } else if (present) {
+            bytes -= vlen + kr[a].k.size();
+            present = false;
+          }
+        }
+        if (present) {
+          size_t kl, got;
+          const char* p = payload(last, &kl, &got);
+          mem.data.emplace_hint(mem.data.end(), std::string(kr[a].k), std::string(p + kl, got - kl));
+        }
+        a = b;
+      }
+      mem.bytes = bytes;
+      if (map) munmap(map, n);
+      if (rfd >= 0) close(rfd);
+      W.t_wal = now_s() - t1;
+    });
     lsmck_tree_report rep;
     int rc = lsmck_tree_verify_listed(ctx, cfg.base.c_str(), &rep, on_listed, &L);
     if (L.th.joinable()) L.th.join();
+    wal_th.join();
     if (rc < 0) {
       fprintf(stderr, "lsmck_tree_verify: %s\n", lsmck_last_error());
       exit(1);
@@ -470,129 +622,31 @@ struct Db {
     }
     const double t_tree = now_s() - t0;
     if (idx_err == 2) panic_exit("Can't open index file");
-    // WAL replay: every payload CRC in one GPU batch
-    const double t1 = now_s();
-    {
+    // the WAL's outcome, in from_log's place
+    if (W.rc < 0) {
+      fprintf(stderr, "%s\n", W.err.c_str());
+      exit(1);
+    }
+    if (!W.panic.empty()) panic_exit(W.panic);
+    if (W.have_older) {
       // a log rotated at a memtable swap whose flush did not complete: its
-      // records come first; merge it in front of wal.log (see the header)
-      std::string older, newer;
-      if (read_file(flushing_path(), &older)) {
-        read_file(wal_path(), &newer);
-        const std::string tmp = wal_path() + ".merge";
-        int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-        if (fd < 0 || !write_all(fd, older.data(), older.size()) || !write_all(fd, newer.data(), newer.size()) ||
-            fsync(fd) != 0 || close(fd) != 0 || rename(tmp.c_str(), wal_path().c_str()) != 0)
-          panic_exit("Can't merge the rotated WAL");
-        unlink(flushing_path().c_str());
-      }
+      // records came first in the replay; merge it in front of wal.log (see
+      // the header)
+      const std::string tmp = wal_path() + ".merge";
+      int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+      if (fd < 0 || !write_all(fd, W.older.data(), W.older.size()) || fsync(fd) != 0 || close(fd) != 0 ||
+          rename(tmp.c_str(), wal_path().c_str()) != 0)
+        panic_exit("Can't merge the rotated WAL");
+      unlink(flushing_path().c_str());
+      std::string().swap(W.older);
     }
     wal_fd = open_wal();
     if (wal_fd < 0) {
       fprintf(stderr, "Can't create WAL file: %s\n", strerror(errno));
       exit(1);
     }
-    struct stat st;
-    fstat(wal_fd, &st);
-    const size_t n = (size_t)st.st_size;
-    const uint8_t* img = nullptr;
-    void* map = nullptr;
-    if (n) {
-      map = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, wal_fd, 0);
-      if (map == MAP_FAILED) {
-        fprintf(stderr, "mmap wal: %s\n", strerror(errno));
-        exit(1);
-      }
-      img = (const uint8_t*)map;
-    }
-    const size_t cap = n / 9 + 1;  // a record is at least 9 bytes
-    // uninitialised: only the records found are written (a zeroed vector of
-    // 32 B per 9 log bytes cost more than the replay itself)
-    std::unique_ptr<lsmck_wal_rec[]> recs(new lsmck_wal_rec[cap]);
-    size_t nrec = 0;
-    uint64_t bad_index = 0;
-    uint32_t bad_crc = 0, bad_expected = 0;
-    rc = lsmck_wal_replay_verify(ctx, img, n, LSMCK_HOST, recs.get(), cap, &nrec, &bad_index, &bad_crc, &bad_expected);
-    const double t_verify = now_s() - t1;
-    if (rc < 0) {
-      fprintf(stderr, "lsmck_wal_replay_verify: %s\n", lsmck_last_error());
-      exit(1);
-    }
-    char msg[256];
-    if (rc == LSMCK_WAL_CORRUPTED) {  // MemTable::from_log(..).expect(..) on Err (db.rs:61-62)
-      snprintf(msg, sizeof msg,
-               "Can't restore memtable from a log: CorruptedData { checksum: %u, expected: %u }", bad_crc,
-               bad_expected);
-      panic_exit(msg);
-    }
-    if (rc == LSMCK_WAL_REMOVE_PANIC) {  // wal.rs:154-159
-      snprintf(msg, sizeof msg, "data corruption encountered (%08x) != %08x", bad_crc, bad_expected);
-      panic_exit(msg);
-    }
-    if (rc == LSMCK_WAL_BAD_TYPE) {
-      snprintf(msg, sizeof msg, "Can't restore memtable from a log: InvalidCommandType(%u)", bad_crc);
-      panic_exit(msg);
-    }
-    // MemTable::from_log (memtable.rs:28-47), on the payload actually read
-    // (short at EOF).  The records are grouped by key (a stable sort keeps log
-    // order inside a key); each key's final state and its share of the
-    // reference's byte count are replayed per key, and the table is built in
-    // key order with an end hint.  Same table and count as inserting record by
-    // record, which took 0.48 s for 500k records (std::map comparisons and
-    // rebalancing).  The count is from_log's: an Insert adds key + value even
-    // over an existing key, a Remove of a present key subtracts its entry.
-    struct KeyRec {
-      std::string_view k;
-      uint32_t i;
-    };
-    std::vector<KeyRec> kr(nrec);
-    auto payload = [&](size_t i, size_t* klen, size_t* got) {
-      const lsmck_wal_rec& r = recs[i];
-      const uint64_t want = (uint64_t)(uint32_t)(r.klen + r.vlen);
-      *got = (size_t)std::min<uint64_t>(want, n - r.payload_off);
-      *klen = r.type == 1 ? (size_t)std::min<uint64_t>(r.klen, *got) : *got;
-      return (const char*)img + r.payload_off;
-    };
-    for (size_t i = 0; i < nrec; ++i) {
-      size_t kl, got;
-      const char* p = payload(i, &kl, &got);
-      if (recs[i].type == 1 && got < recs[i].klen) {
-        // an Insert cut at EOF inside its key whose CRC matches the short
-        // bytes: data.split_off(key_len) panics (wal.rs:142)
-        snprintf(msg, sizeof msg, "`at` split index (is %u) should be <= len (is %zu)", recs[i].klen, got);
-        panic_exit(msg);
-      }
-      kr[i] = {std::string_view(p, kl), (uint32_t)i};
-    }
-    std::stable_sort(kr.begin(), kr.end(), [](const KeyRec& a, const KeyRec& b) { return a.k < b.k; });
-    size_t bytes = 0;
-    for (size_t a = 0; a < nrec;) {
-      size_t b = a + 1;
-      while (b < nrec && kr[b].k == kr[a].k) ++b;
-      bool present = false;
-      size_t vlen = 0, last = 0;
-      for (size_t x = a; x < b; ++x) {
-        size_t kl, got;
-        payload(kr[x].i, &kl, &got);
-        if (recs[kr[x].i].type == 1) {
-          bytes += got;  // key + value
-          present = true;
-          vlen = got - kl;
-          last = kr[x].i;
-        } else if (present) {
-          bytes -= vlen + kr[a].k.size();
-          present = false;
-        }
-      }
-      if (present) {
-        size_t kl, got;
-        const char* p = payload(last, &kl, &got);
-        mem.data.emplace_hint(mem.data.end(), std::string(kr[a].k), std::string(p + kl, got - kl));
-      }
-      a = b;
-    }
-    mem.bytes = bytes;
-    if (map) munmap(map, n);
-    const double t_wal = now_s() - t1;
+    const size_t n = W.n, nrec = W.nrec;
+    const double t_verify = W.t_verify, t_wal = W.t_wal;
     uint64_t ntab = 0;
     for (auto& l : levels) ntab += l.size();
     printf("{\"event\": \"loaded\", \"tables\": %llu, \"table_bytes\": %llu, \"tree_verify_s\": %.6f, "
