@@ -2180,11 +2180,68 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
   rep->first_index = UINT64_MAX;
   struct timespec t0;
   clock_gettime(CLOCK_MONOTONIC, &t0);
-  std::vector<std::string> mpath;
   struct {
     std::vector<lsmck_table_entry> ents;
     std::vector<std::string> dps, ips, cps;
   } listed;  // lives until the verify returns (lsmck_tree_verify_listed's contract)
+  // The metadata files are parsed while the level directories are still
+  // being read: the scan hands batches of names to the parsing threads as it
+  // goes (a readdir of the 1.1 M names of a 229k-table tree and the 229k
+  // small-file opens cost about the same, and only the opens parallelise).
+  // 8 threads: small-file system calls contend in the kernel (229k metadata
+  // files: 1 thread 1.25 s, 4 1.01 s, 8 0.80 s, 16 0.89 s, 32 1.25 s)
+  struct ListBatch {
+    std::vector<std::string> path;
+    std::vector<lsmck_host::TableMeta> meta;
+    std::vector<int> st;
+  };
+  struct Lister {
+    std::vector<std::unique_ptr<ListBatch>> batches;  // load order
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t next = 0;
+    bool done = false;
+    std::vector<std::thread> th;
+    void finish() {
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        done = true;
+      }
+      cv.notify_all();
+      for (auto& t : th)
+        if (t.joinable()) t.join();
+    }
+    ~Lister() { finish(); }
+  } lister;
+  {
+    const unsigned lthreads = ctx->tree_list_threads ? ctx->tree_list_threads : kListThreads;
+    for (unsigned t = 0; t < lthreads; ++t)
+      lister.th.emplace_back([&lister]() {
+        for (;;) {
+          ListBatch* b;
+          {
+            std::unique_lock<std::mutex> lk(lister.mu);
+            lister.cv.wait(lk, [&] { return lister.next < lister.batches.size() || lister.done; });
+            if (lister.next >= lister.batches.size()) return;
+            b = lister.batches[lister.next++].get();
+          }
+          b->meta.resize(b->path.size());
+          b->st.assign(b->path.size(), 0);
+          for (size_t i = 0; i < b->path.size(); ++i)
+            if (lsmck_host::read_metadata_json(b->path[i].c_str(), &b->meta[i])) b->st[i] = LSMCK_META_PANIC;
+        }
+      });
+  }
+  std::unique_ptr<ListBatch> cur(new ListBatch);
+  auto publish = [&]() {
+    if (cur->path.empty()) return;
+    {
+      std::lock_guard<std::mutex> lk(lister.mu);
+      lister.batches.push_back(std::move(cur));
+    }
+    lister.cv.notify_one();
+    cur.reset(new ListBatch);
+  };
   for (int lv = 0; lv < LSMCK_SSTABLE_MAX_LEVEL; ++lv) {
     const std::string dir = lsmck_host::path_push(base, "level-" + std::to_string(lv));
     if ((rc = mkdir_p(dir))) return lsmck_host::set_errno_error(-rc, "create_dir_all", dir.c_str());
@@ -2202,9 +2259,22 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
         break;
       }
       if (!strcmp(e->d_name, ".") || !strcmp(e->d_name, "..")) continue;
-      if (strstr(e->d_name, "metadata") && valid_utf8(e->d_name)) mpath.push_back(dir + "/" + e->d_name);
+      if (strstr(e->d_name, "metadata") && valid_utf8(e->d_name)) {
+        cur->path.push_back(dir + "/" + e->d_name);
+        if (cur->path.size() == 1024) publish();
+      }
     }
     closedir(d);
+  }
+  publish();
+  lister.finish();
+  std::vector<std::string> mpath;
+  std::vector<lsmck_host::TableMeta> meta;
+  std::vector<int> st;
+  for (auto& b : lister.batches) {
+    for (auto& x : b->path) mpath.push_back(std::move(x));
+    for (auto& x : b->meta) meta.push_back(std::move(x));
+    st.insert(st.end(), b->st.begin(), b->st.end());
   }
   const size_t n = mpath.size();
   // While the metadata files are parsed, each context's staging slots, device
@@ -2256,13 +2326,6 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
       (void)ensure_dev(&c->tree.state, &c->tree.cap_state, 8ull * active);
       (void)ensure_dev(&c->tree.digests, &c->tree.cap_digests, 32 * 2 * n);
     });
-  std::vector<lsmck_host::TableMeta> meta(n);
-  std::vector<int> st(n, 0);
-  // 8 threads: small-file system calls contend in the kernel (229k metadata
-  // files: 1 thread 1.25 s, 4 1.01 s, 8 0.80 s, 16 0.89 s, 32 1.25 s)
-  host_parallel(n, [&](size_t i) {
-    if (lsmck_host::read_metadata_json(mpath[i].c_str(), &meta[i])) st[i] = LSMCK_META_PANIC;
-  }, ctx->tree_list_threads ? ctx->tree_list_threads : kListThreads);
   // table paths: construct_path = base_path / level-<level> / file (sstable_metadata.rs:43-48)
   std::vector<std::string> dp, ip, cp;
   std::vector<size_t> which;
