@@ -69,6 +69,7 @@ def main():
         if s:
             times.append(dt)
         print(f"replay {s}: {dt * 1e3:.1f} ms", file=sys.stderr, flush=True)
+        del recs  # the wrapper reuses its records array once no result refers to it
     d.free()
     best, med = min(times), float(np.median(times))
     print(json.dumps({
