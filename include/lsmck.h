@@ -172,6 +172,10 @@ int lsmck_device_count(void);
  *                 of from..1023 compression blocks share a bucket per
  *                 2^shift blocks (defaults 2 and 128; shift 0 = exact block
  *                 counts).  A/B switch; digests are identical either way.
+ *   "sha_short_blocks"  in that order, messages of at most this many
+ *                 compression blocks run on a lean kernel with more waves per
+ *                 SIMD (default 12; 0 = every message on the window kernel).
+ *                 Digests are identical either way.
  *   "tree_active_files" / "tree_slice_bytes"  lsmck_checksums_verify_many's
  *                 files in flight (0 = 8192) and bytes of a file per round
  *                 (0 = 128 KiB; a multiple of 64).  Tests use small values.

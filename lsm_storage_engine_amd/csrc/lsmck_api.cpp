@@ -123,6 +123,8 @@ struct DescScratch {
   size_t cap_order = 0;
   unsigned char* sort_tmp = nullptr;
   size_t cap_tmp = 0;
+  uint64_t* sha_split = nullptr;  // device, 1 u64: where the order's short tail starts
+  size_t cap_split = 0;
   // stream kernel (lsmck_crc32.hip): eligibility flag, per-wave boundary cuts
   uint32_t* sflag = nullptr;
   uint64_t* scuts = nullptr;
@@ -135,6 +137,7 @@ struct DescScratch {
     if (sha_keys) (void)hipFree(sha_keys);
     if (sha_order) (void)hipFree(sha_order);
     if (sort_tmp) (void)hipFree(sort_tmp);
+    if (sha_split) (void)hipFree(sha_split);
     *this = DescScratch();
   }
 };
@@ -257,6 +260,7 @@ struct lsmck_ctx {
   int sha_bucket_shift = 2;  // SHA order key: 2^shift-block buckets for from..1023 blocks (0 = exact; A/B: DESIGN.md 3.2)
   int sha_bucket_from = 128;
   int sha_pair = 1;  // SHA-256 batches: two blocks per load window (A/B: DESIGN.md 3.2)
+  int sha_short_blocks = 12;  // SHA-256 ordered batches: messages of at most this many blocks on the lean kernel (0 = off)
   unsigned tree_list_threads = 0;  // lsmck_tree_verify: metadata parsing threads (0 = kListThreads)
   size_t wal_prefetch = 4096;  // lsmck_wal_replay_verify: host walk's prefetch distance in bytes (0 = off)
   uint8_t* wal_host = nullptr;  // lsmck_wal_replay_verify of a device image: pinned host copy (grow-only)
@@ -419,6 +423,11 @@ int sha_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const uint6
     rc = lsmk_sha_order(len, n, sc.sha_keys, sc.sha_order, sc.sort_tmp, &tmp, ctx->sha_bucket_shift, ctx->sha_bucket_from, st);
     if (rc) return launch_rc(rc, "sha order (radix sort)");
     order = sc.sha_order;
+    if (ctx->sha_short_blocks > 0) {
+      if ((rc = ensure_dev(&sc.sha_split, &sc.cap_split, 1))) return rc;
+      rc = lsmk_sha_split(sc.sha_keys, n, (uint32_t)ctx->sha_short_blocks, sc.sha_split, st);
+      if (rc) return launch_rc(rc, "sha split");
+    }
   }
   ShaParams P{};
   P.base = base;
@@ -430,6 +439,7 @@ int sha_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const uint6
   P.order = order;
   P.out = out32;
   P.pair = (uint32_t)ctx->sha_pair;
+  P.split = (order && ctx->sha_short_blocks > 0) ? sc.sha_split : nullptr;
   int rc = lsmk_launch_sha256(&P, st);
   return rc ? launch_rc(rc, "sha256 kernel") : 0;
 }
@@ -832,6 +842,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     if (value < 0 || value > 6) return lsmck_host::set_error(LSMCK_EINVAL, "sha_bucket_shift: 0..6");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->sha_bucket_shift = (int)value;
+    return 0;
+  }
+  if (!strcmp(key, "sha_short_blocks")) {  // A/B: the lean kernel takes an ordered batch's messages of <= N blocks
+    if (value < 0 || value > 127) return lsmck_host::set_error(LSMCK_EINVAL, "sha_short_blocks: 0..127");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->sha_short_blocks = (int)value;
     return 0;
   }
   if (!strcmp(key, "sha_pair")) {  // A/B: SHA-256 batch kernel loads two blocks (a 128-B line) per window

@@ -41,6 +41,7 @@ struct ShaParams {
   const uint32_t* order;      // optional permutation (longest first), may be null
   unsigned char* out;         // 32 bytes per message
   uint32_t pair;              // 1: two blocks per load window (A/B, lsmck_sha256.hip ShaWin2)
+  const uint64_t* split;      // device: order index where the short tail starts (lean kernel), null = none
 };
 
 // One slice of a message streamed through sha256_slices_kernel.
@@ -93,6 +94,7 @@ int lsmk_launch_crc32_compare(const uint32_t* crc, const uint32_t* expected, uin
                                unsigned long long* n_bad, unsigned long long* first_bad, hipStream_t st);
 int lsmk_sha_order(const uint32_t* len, size_t n, uint16_t* keys_out, uint32_t* order, void* tmp, size_t* tmp_bytes,
                    int coarse, int from, hipStream_t st);
+int lsmk_sha_split(const uint16_t* keys, size_t n, uint32_t t, uint64_t* split, hipStream_t st);
 int lsmk_launch_gen_stream(unsigned char* dst, uint64_t seed, uint64_t byte_off, uint64_t n, hipStream_t st);
 }
 #endif

@@ -57,3 +57,21 @@ extern "C" int lsmk_sha_order(const uint32_t* len, size_t n, uint16_t* keys_out,
   hipError_t e = rocprim::radix_sort_pairs_desc(tmp, *tmp_bytes, keys, keys_out, idx, order, n, 0, 11, st);
   return e == hipSuccess ? 0 : -(int)e;
 }
+
+// The first position in the order whose key is at most `t` blocks (keys are
+// sorted descending; below sha_bucket_from a key is the exact block count):
+// where the short messages start.  One thread, binary search.
+__global__ void sha_split_kernel(const uint16_t* keys, uint64_t n, uint32_t t, uint64_t* split) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (keys[mid] > t) lo = mid + 1; else hi = mid;
+  }
+  *split = lo;
+}
+
+extern "C" int lsmk_sha_split(const uint16_t* keys, size_t n, uint32_t t, uint64_t* split, hipStream_t st) {
+  hipLaunchKernelGGL(sha_split_kernel, dim3(1), dim3(1), 0, st, keys, (uint64_t)n, t, split);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : -(int)e;
+}

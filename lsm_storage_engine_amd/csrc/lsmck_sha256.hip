@@ -353,13 +353,54 @@ __device__ __forceinline__ void store_digest(unsigned char* out, const uint32_t 
 template <bool PAIR, int ABL = 0>
 __global__ __launch_bounds__(256) void sha256_kernel(ShaParams P) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P.nmsg) return;
+  if (i >= P.nmsg || (P.split && i >= *P.split)) return;  // (the short tail: sha256_short_kernel)
   uint64_t m = P.order ? P.order[i] : i;
   uint64_t off = P.off ? P.off[m] : m * P.stride;
   uint64_t len = P.len ? P.len[m] : P.flen;
   uint32_t h[8];
   sha256_iv(h);
   sha256_run<PAIR, ABL>(h, P.base, off, len, true, len << 3);
+  store_digest(P.out + 32 * m, h);
+}
+
+// The short tail of a length-ordered batch (a few blocks per message): no
+// load windows in flight, so few VGPRs (102: 4 waves per SIMD against the
+// window kernel's 3) to cover each message's dependent round trips (order ->
+// descriptor -> payload).  Config 3 (same box, ms): every message on the
+// window kernel 65.3; messages of <= 3 / 6 / 12 / 16 / 32 blocks here 64.6 /
+// 64.4 / 64.2 / 64.3 / 64.9 (default 12: "sha_short_blocks").  Compiled for 5
+// waves (96 VGPRs, 4 spilled) it ran 64.4 against 64.2.
+__global__ __launch_bounds__(256) void sha256_short_kernel(ShaParams P) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.nmsg || i < *P.split) return;
+  const uint64_t m = P.order[i];
+  const uint64_t off = P.off ? P.off[m] : m * P.stride;
+  const uint64_t len = P.len[m];
+  const uintptr_t A = (uintptr_t)(P.base + off);
+  const uint64_t nb = (len + 9 + 63) >> 6;
+  uint32_t h[8];
+  sha256_iv(h);
+  for (uint64_t b = 0; b < nb; ++b) {
+    const uint64_t p0 = b << 6;
+    uint32_t w[16];
+    load_block(A, len, p0, w);
+    if (p0 + 64 > len) {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        int64_t c = (int64_t)len - (int64_t)(p0 + 4 * t);
+        uint32_t mask = c >= 4 ? 0xFFFFFFFFu : (c <= 0 ? 0u : ((1u << (8 * c)) - 1u));
+        uint32_t pad = (c >= 0 && c < 4) ? (0x80u << (8 * c)) : 0u;
+        w[t] = (w[t] & mask) | pad;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t) w[t] = __builtin_bswap32(w[t]);
+    if (b == nb - 1) {
+      w[14] = (uint32_t)(len >> 29);
+      w[15] = (uint32_t)(len << 3);
+    }
+    sha256_compress(h, w);
+  }
   store_digest(P.out + 32 * m, h);
 }
 
@@ -440,6 +481,8 @@ extern "C" int lsmk_launch_sha256(const ShaParams* P, hipStream_t st) {
     hipLaunchKernelGGL(sha256_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, *P);
   else
     hipLaunchKernelGGL(sha256_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, *P);
+  if (P->split && P->order && P->len)  // the short tail of the order (its start on the device)
+    hipLaunchKernelGGL(sha256_short_kernel, dim3((unsigned)blocks), dim3(256), 0, st, *P);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
 }

@@ -174,6 +174,40 @@ def test_length_sorted_batch(ctx, order, shift, start):
     assert np.array_equal(got, O.sha256_batch(data, off, ln, threads=8))
 
 
+@pytest.mark.parametrize("short", [0, 1, 3, 8, 12, 127])
+def test_short_tail_on_the_lean_kernel(ctx, short):
+    """"sha_short_blocks" N: in a length-ordered batch, the messages of at most
+    N compression blocks (the order's tail, found on the device) run on the
+    lean kernel, the rest on the window kernel; every digest at its message's
+    index, identical to the oracle.  Host and device batches."""
+    rng = np.random.default_rng(78 + short)
+    n = 5000
+    ln = O.gen_zipf_lengths(0x5EED0033, n).astype(np.uint32)
+    ln[:10] = [0, 1, 55, 56, 63, 64, 119, 120, 183, 184]  # 1 / 2 / 3 / 4 blocks at the edges
+    ln = ln[rng.permutation(n)]
+    off = np.zeros(n, dtype=np.uint64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.uint64) + rng.integers(0, 5, n - 1).astype(np.uint64))
+    total = int(off[-1]) + int(ln[-1])
+    data = O.gen_stream(0x5EED0034, 0, total + 8)
+    want = O.sha256_batch(data, off, ln, threads=8)
+    ctx.set_option("sha_short_blocks", short)
+    try:
+        assert np.array_equal(ctx.sha256(data, off, ln), want)
+        d, d_o, d_l, out = ctx.alloc(total + 8), ctx.alloc(8 * n), ctx.alloc(4 * n), ctx.alloc(32 * n)
+        try:
+            d.upload(data)
+            d_o.upload(off)
+            d_l.upload(ln)
+            ctx.sha256_device(d.ptr, d_o.ptr, d_l.ptr, n, out.ptr)
+            ctx.sync()
+            assert np.array_equal(out.download(np.uint8).reshape(n, 32), want)
+        finally:
+            for b in (d, d_o, d_l, out):
+                b.free()
+    finally:
+        ctx.set_option("sha_short_blocks", 12)
+
+
 def _summaries():
     import json
     with open(os.path.join(os.path.dirname(__file__), "golden", "summaries.json")) as f:
