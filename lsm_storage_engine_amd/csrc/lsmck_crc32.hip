@@ -584,14 +584,8 @@ __global__ __launch_bounds__(1024) void crc32_wring_kernel(CrcParams P) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const uint32_t ni = n0 + k + R - 1;
-#ifdef LSMCK_WRING_PRIO
-      __builtin_amdgcn_s_setprio(LSMCK_WRING_PRIO);
-#endif
       issue_whole(P, M, vo, tile_of(ni), lane, nsegr, ni < mine ? total : 0u, S[(k + R - 1) % R]);
       __builtin_amdgcn_sched_barrier(0);
-#ifdef LSMCK_WRING_PRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
       if (dcnt) qpush(dv, dcnt);
       const uint32_t ti = n0 + k;  // this slot's tile, valid if ti < mine
       uint32_t v = seg_finish<true, 2, ABLATE, true>(smem, P, S[k % R], lo, hi);
