@@ -204,8 +204,28 @@ int lsmck_device_count(void);
  *   "tree_open_files"  files kept open from their first slice to their last
  *                 (-1 = default: as many as RLIMIT_NOFILE leaves after a
  *                 1024-descriptor reserve; the rest reopen per slice).
+ *   "wal_part_bytes"  the candidate-doubling GPU walk goes in parts of this
+ *                 many bytes (0 = whole, default; otherwise >= 1 MiB; a
+ *                 nonzero value also skips the segment walk).  Tests / A/B.
+ *   "wal_seg_walk"  the GPU header walk: 1 = the segment walk (default;
+ *                 lsmck_segwalk.h), falling back to candidate doubling when
+ *                 its check keeps failing; 0 = candidate doubling only.
+ *   "wal_seg_bytes"  segment walk: bytes per segment (0 = auto, default:
+ *                 ~2^19 segments; else 64..2^30).  Tests use small segments.
+ *   "wal_seg_rounds"  segment walk: check failures repaired before it
+ *                 declines to candidate doubling (default 16).
  * Returns 0, or LSMCK_EINVAL for an unknown key / value. */
 int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
+
+/* What the context's last call of a kind did (diagnostics for tests and
+ * tools; no effect on results):
+ *   "wal_walk_path"  the last lsmck_wal_replay_verify that walked on the GPU
+ *                    or the host: 1 = segment walk, 2 = candidate doubling,
+ *                    3 = host walk.
+ *   "wal_seg_repairs"  its segment walk's repaired check failures.
+ *   "wal_segments"   its segment walk's segment count.
+ * Returns 0 and *value, or LSMCK_EINVAL for an unknown key. */
+int lsmck_ctx_get_stat(lsmck_ctx* ctx, const char* key, long* value);
 
 /* ======================================================================== */
 /* 3. Batch GPU entry points                                                  */

@@ -92,6 +92,7 @@ SIGNATURES = [
     ("lsmck_last_error", C.c_char_p, []),
     ("lsmck_device_count", C.c_int, []),
     ("lsmck_ctx_set_option", C.c_int, [vp, C.c_char_p, C.c_long]),
+    ("lsmck_ctx_get_stat", C.c_int, [vp, C.c_char_p, C.POINTER(C.c_long)]),
     ("lsmck_crc32_batch", C.c_int, [vp, vp, vp, vp, sz, vp, C.c_uint, vp]),
     ("lsmck_crc32_batch_fixed", C.c_int, [vp, vp, sz, C.c_uint32, sz, vp, C.c_uint, vp]),
     ("lsmck_crc32_verify_batch", C.c_int, [vp, vp, vp, vp, vp, sz, C.c_uint, vp, u64p, u64p]),

@@ -35,6 +35,7 @@
 #include "lsmck_device.h"
 #include "lsmck_internal.h"
 #include "lsmck_pool.h"
+#include "lsmck_segwalk.h"
 
 using lsmck::CrcParams;
 using lsmck::ShaParams;
@@ -236,7 +237,26 @@ struct lsmck_ctx {
     size_t cap_recs = 0;
     unsigned long long* info = nullptr;  // [records, terminal, bad position, candidates (u32 at info+3)]
     unsigned long long* h_info = nullptr;  // pinned
+    // the segment walk (lsmck_segwalk.h): per segment guess, exit, outcome,
+    // records, placement scan; its round outcome (info words, and pinned)
+    uint64_t* sg = nullptr;
+    uint64_t* sx = nullptr;
+    uint64_t* spre = nullptr;
+    uint32_t* scode = nullptr;
+    uint32_t* srecs = nullptr;
+    size_t cap_seg = 0;
+    uint64_t* sbsum = nullptr;
+    size_t cap_sbsum = 0;
+    unsigned long long* sinfo = nullptr;
+    unsigned long long* h_sinfo = nullptr;
   } wd;
+  int wal_seg = 1;           // device WAL walk: 1 = the segment walk first (default), 0 = candidate doubling only
+  uint64_t wal_seg_bytes = 0;  // segment walk: bytes per segment (0 = auto, ~2^19 segments)
+  int wal_seg_rounds = 16;   // segment walk: repairs before it declines to the candidate-doubling walk
+  // what the last device-walked replay did (lsmck_ctx_get_stat "wal_walk_path" / "wal_seg_repairs" / "wal_segments")
+  int last_walk_path = 0;
+  int last_seg_repairs = 0;
+  uint64_t last_segments = 0;
   lsmck_wal_rec* h_wrecs = nullptr;  // device WAL replay: the records' pinned landing buffer (grow-only)
   size_t cap_hwrecs = 0;
   hipEvent_t wal_emit_ev = nullptr, wal_recs_ev = nullptr;  // records read back beside the CRC pass
@@ -803,7 +823,8 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     return 0;
   }
   if (!strcmp(key, "wal_part_bytes")) {  // GPU WAL walk in parts of this many bytes (0 = whole; tests / A/B)
-    if (value < 0) return lsmck_host::set_error(LSMCK_EINVAL, "wal_part_bytes: >= 0");
+    if (value < 0 || (value && value < (1l << 20)))
+      return lsmck_host::set_error(LSMCK_EINVAL, "wal_part_bytes: 0 or >= 1 MiB");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->wal_part_bytes = (size_t)value;
     return 0;
@@ -824,6 +845,25 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     if (value < 0) return lsmck_host::set_error(LSMCK_EINVAL, "wal_upload_min: >= 0");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->wal_upload_min = (size_t)value;
+    return 0;
+  }
+  if (!strcmp(key, "wal_seg_walk")) {  // A/B: device WAL walk, 1 = segment walk first (default), 0 = doubling only
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "wal_seg_walk must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_seg = (int)value;
+    return 0;
+  }
+  if (!strcmp(key, "wal_seg_bytes")) {  // segment walk: bytes per segment (0 = auto; tests force small segments)
+    if (value < 0 || (value && (value < 64 || value > (1l << 30))))
+      return lsmck_host::set_error(LSMCK_EINVAL, "wal_seg_bytes: 0 or 64..2^30");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_seg_bytes = (uint64_t)value;
+    return 0;
+  }
+  if (!strcmp(key, "wal_seg_rounds")) {  // segment walk: repair rounds before declining (0 = decline on any failure)
+    if (value < 0 || value > 1024) return lsmck_host::set_error(LSMCK_EINVAL, "wal_seg_rounds: 0..1024");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_seg_rounds = (int)value;
     return 0;
   }
   if (!strcmp(key, "wal_prefetch")) {  // A/B: bytes the WAL header walk prefetches ahead (0 = off)
@@ -876,6 +916,23 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
   return lsmck_host::set_error(LSMCK_EINVAL, "unknown option");
 }
 
+int lsmck_ctx_get_stat(lsmck_ctx* ctx, const char* key, long* value) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!key || !value) return lsmck_host::set_error(LSMCK_EINVAL, "null key or value");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!strcmp(key, "wal_walk_path")) {
+    *value = ctx->last_walk_path;
+  } else if (!strcmp(key, "wal_seg_repairs")) {
+    *value = ctx->last_seg_repairs;
+  } else if (!strcmp(key, "wal_segments")) {
+    *value = (long)ctx->last_segments;
+  } else {
+    return lsmck_host::set_error(LSMCK_EINVAL, "unknown stat");
+  }
+  return 0;
+}
+
 void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   if (!ctx) return;
   DevGuard g(ctx->dev);
@@ -895,6 +952,10 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
                   (void*)ctx->wd.badpos, (void*)ctx->wd.chain, (void*)ctx->wd.recs, (void*)ctx->wd.info})
     if (p) (void)hipFree(p);
   if (ctx->wd.h_info) (void)hipHostFree(ctx->wd.h_info);
+  for (void* p : {(void*)ctx->wd.sg, (void*)ctx->wd.sx, (void*)ctx->wd.spre, (void*)ctx->wd.scode,
+                  (void*)ctx->wd.srecs, (void*)ctx->wd.sbsum, (void*)ctx->wd.sinfo})
+    if (p) (void)hipFree(p);
+  if (ctx->wd.h_sinfo) (void)hipHostFree(ctx->wd.h_sinfo);
   for (void* p : {(void*)ctx->d_vcrc, (void*)ctx->d_woff, (void*)ctx->d_wlen, (void*)ctx->d_wexp})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)ctx->h_woff, (void*)ctx->h_wlen, (void*)ctx->h_wexp})
@@ -1129,7 +1190,7 @@ static int wal_crc_part(lsmck_ctx* ctx, const uint8_t* img, size_t at, size_t m,
 // replay's first part, from ctx->h_wrecs1); the rest land in ctx->h_wrecs.
 static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t term, uint64_t badq, lsmck_wal_rec* recs,
                       size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected,
-                      hipStream_t st, const WalTrace& tr, size_t done = 0) {
+                      hipStream_t st, const WalTrace& tr, size_t done = 0, bool emit_recorded = false) {
   auto& W = ctx->wd;
   int rc;
   uint64_t nbad = 0, first = m;
@@ -1141,7 +1202,7 @@ static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t ter
       if (!ctx->wal_emit_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_emit_ev, hipEventDisableTiming));
       if (!ctx->wal_recs_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_recs_ev, hipEventDisableTiming));
       hipStream_t s2 = ctx->stage[0].s;
-      HIPCHK(hipEventRecord(ctx->wal_emit_ev, st));
+      if (!emit_recorded) HIPCHK(hipEventRecord(ctx->wal_emit_ev, st));
       HIPCHK(hipStreamWaitEvent(s2, ctx->wal_emit_ev, 0));
       HIPCHK(hipMemcpyAsync(ctx->h_wrecs, W.recs + done, todo * sizeof(lsmck_wal_rec), hipMemcpyDeviceToHost, s2));
       HIPCHK(hipEventRecord(ctx->wal_recs_ev, s2));
@@ -1260,6 +1321,103 @@ static int wal_walk_from(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t 
   }
 }
 
+// The segment walk (lsmck_segwalk.h) of the chain from `start` to the end of
+// the image: every segment's guess and walk, check rounds (one host sync
+// each; a failure is repaired on the device and checked again), then the
+// records emitted after the `at` already there, the emit's completion
+// recorded on ctx->wal_emit_ev (the records' read-back waits for that, not
+// for the CRC pass behind it).  kWalSegDecline: more failures than
+// wal_seg_rounds -- payloads that look like framed records along the chain;
+// the caller walks by candidate doubling instead.
+constexpr int kWalSegDecline = 0x7FFF0004;
+static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t start, size_t at, hipStream_t st,
+                        const WalTrace& tr, WalPart* out) {
+  namespace sg = lsmck::seg;
+  auto& W = ctx->wd;
+  int rc;
+  ctx->last_walk_path = 1;
+  ctx->last_seg_repairs = 0;
+  ctx->last_segments = 0;
+  if (start >= n) {
+    out->m = at;
+    out->term = 0xFFFFFFFFu;  // END
+    out->tpos = 0;
+    return 0;
+  }
+  uint64_t S = lsmk_wal_seg_bytes(n - start, ctx->wal_seg_bytes);
+  sg::SegArgs a{};
+  int resegs = 0;
+  for (int round = 0;; ++round) {
+    if (round == 0) {  // (re)segment and walk every segment
+      const uint64_t K64 = (n - start + S - 1) / S;
+      if (K64 >= (1ull << 31)) return kWalSegDecline;  // (tiny forced segments over a huge log)
+      const uint32_t K = (uint32_t)K64;
+      ctx->last_segments = K;
+      if ((rc = ensure_dev(&W.sbsum, &W.cap_sbsum, (size_t)lsmk_wal_seg_scan_blocks(K) + 1))) return rc;
+      if (W.cap_seg < (size_t)K + 1) {
+        for (void* p : {(void*)W.sg, (void*)W.sx, (void*)W.spre, (void*)W.scode, (void*)W.srecs})
+          if (p) (void)hipFree(p);
+        const size_t c = std::max<size_t>((size_t)K + 1, W.cap_seg * 3 / 2);
+        W.sg = W.sx = W.spre = nullptr;
+        W.scode = W.srecs = nullptr;
+        W.cap_seg = 0;
+        HIPCHK(hipMalloc((void**)&W.sg, c * 8));
+        HIPCHK(hipMalloc((void**)&W.sx, c * 8));
+        HIPCHK(hipMalloc((void**)&W.spre, c * 8));
+        HIPCHK(hipMalloc((void**)&W.scode, c * 4));
+        HIPCHK(hipMalloc((void**)&W.srecs, c * 4));
+        W.cap_seg = c;
+      }
+      if (!W.sinfo) HIPCHK(hipMalloc((void**)&W.sinfo, sg::kInfoWords * 8));
+      if (!W.h_sinfo) HIPCHK(hipHostMalloc((void**)&W.h_sinfo, sg::kInfoWords * 8, hipHostMallocDefault));
+      a = sg::SegArgs{img, n, start, S, K, W.sg, W.sx, W.scode, W.srecs, W.spre, W.sinfo};
+      if ((rc = lsmk_wal_seg_walk(&a, st))) return launch_rc(rc, "wal segment walk kernel");
+    }
+    if ((rc = lsmk_wal_seg_round(&a, W.sbsum, st))) return launch_rc(rc, "wal segment check kernels");
+    HIPCHK(hipMemcpyAsync(W.h_sinfo, W.sinfo, sg::kInfoWords * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    tr.mark("segment walk round (sync)");
+    if ((uint32_t)W.h_sinfo[sg::kInfoFail] == sg::kNoSeg) break;
+    const uint32_t nfail = (uint32_t)W.h_sinfo[sg::kInfoNFail];
+    // Many failures at once: records longer than the segments (a segment
+    // inside one has no true entry, and a bogus start there is taken) --
+    // segments 16x longer, once or twice, unless the caller fixed the size
+    if (round == 0 && !ctx->wal_seg_bytes && resegs < 2 && nfail > std::max<uint32_t>(64, a.K / 512) &&
+        S < (1ull << 30)) {
+      S <<= 4;
+      ++resegs;
+      round = -1;
+      continue;
+    }
+    if (round >= ctx->wal_seg_rounds) {
+      ctx->last_seg_repairs = round;
+      return kWalSegDecline;
+    }
+    // the failing segment's entry is right: rewalk from its exit (and on, for
+    // up to 4096 segments of consecutive failures), then check again
+    if ((rc = lsmk_wal_seg_repair(&a, 4096, st))) return launch_rc(rc, "wal segment repair kernel");
+    ctx->last_seg_repairs = round + 1;
+  }
+  const uint64_t m = W.h_sinfo[sg::kInfoRecs];
+  out->m = at + m;
+  out->term = W.h_sinfo[sg::kInfoCode] == sg::kBad ? kWalBad : 0xFFFFFFFFu;
+  out->tpos = W.h_sinfo[sg::kInfoPos];
+  if (m) {
+    const size_t tot = at + m;
+    if ((rc = ensure_dev_keep(&W.recs, &W.cap_recs, tot, at, st)) ||
+        (rc = ensure_dev_keep(&ctx->d_woff, &ctx->cap_woff, tot, at, st)) ||
+        (rc = ensure_dev_keep(&ctx->d_wlen, &ctx->cap_wlen, tot, at, st)) ||
+        (rc = ensure_dev_keep(&ctx->d_wexp, &ctx->cap_wexp, tot, at, st)) ||
+        (rc = ensure_dev_keep(&ctx->d_vcrc, &ctx->cap_vcrc, tot, at, st)))
+      return rc;
+    if ((rc = lsmk_wal_seg_emit(&a, at, W.recs, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st)))
+      return launch_rc(rc, "wal segment emit kernel");
+  }
+  if (!ctx->wal_emit_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_emit_ev, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(ctx->wal_emit_ev, st));
+  return 0;
+}
+
 // A device-resident image (or an uploaded one: `marked`, its candidate bitmap
 // is already in ctx->wd -- wal_upload marks each chunk behind its copy): the
 // walk (in parts when its scratch would not fit), one CRC pass per part.
@@ -1275,6 +1433,14 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
   if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
   hipStream_t st = so.st;
   WalPart P;
+  rc = ctx->wal_seg && !ctx->wal_part_bytes ? wal_seg_walk(ctx, img, n, 0, 0, st, tr, &P) : kWalSegDecline;
+  if (rc == 0) {  // the CRC pass over every record, then the compare and the records
+    if ((rc = wal_crc_part(ctx, img, 0, P.m, st))) return rc;
+    return wal_finish(ctx, img, P.m, P.term, P.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr, 0,
+                      true);
+  }
+  if (rc != kWalSegDecline) return rc;
+  ctx->last_walk_path = 2;
   if ((rc = wal_walk_from(ctx, img, n, 0, 0, ctx->wal_part_bytes, marked, st, tr, &P))) return rc;
   return wal_finish(ctx, img, P.m, P.term, P.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr);
 }
@@ -1460,10 +1626,21 @@ static int wal_replay_split(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool p
   }
   if (P1.term != kWalStop && P1.term != kWalStopSelf)  // the log ended inside the prefix
     return wal_finish(ctx, d, P1.m, P1.term, P1.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr, done);
-  // resume at r: the words from r's to the prefix end lost their counts to
-  // the prefix scan; mark them again, then walk words [r/64, end) from r
+  // resume at r: the segment walk of the rest (it needs no candidate marks);
+  // when it declines, the words from r's to the prefix end lost their counts
+  // to the prefix scan: mark them again, then walk words [r/64, end) from r
   // (in parts, when the rest's scratch would not fit)
   const uint64_t r = P1.tpos;
+  if (ctx->wal_seg && !ctx->wal_part_bytes) {
+    rc = wal_seg_walk(ctx, d, n, r, P1.m, st, tr, &P2);
+    if (rc == 0) {
+      if ((rc = wal_crc_part(ctx, d, P1.m, P2.m - P1.m, st))) return rc;
+      return wal_finish(ctx, d, P2.m, P2.term, P2.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr,
+                        done, true);
+    }
+    if (rc != kWalSegDecline) return rc;
+  }
+  ctx->last_walk_path = 2;
   if (r < a && (rc = lsmk_wal_mark_range(d, n, r & ~(uint64_t)63, a, ctx->wd.bits, ctx->wd.pre, st)))
     return launch_rc(rc, "wal mark kernel");
   if ((rc = wal_walk_from(ctx, d, n, r, P1.m, ctx->wal_part_bytes, true, st, tr, &P2))) return rc;
@@ -1504,6 +1681,7 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
     }
     if (rc != kWalHostWalk) return rc;
   }
+  ctx->last_walk_path = 3;
   const uint8_t* h = wal;
   // Device image: the walk reads a host copy, made by DMA into a pinned
   // buffer the context keeps (grow-only).  Copying into fresh pageable memory

@@ -90,6 +90,15 @@ int lsmk_wal_frame_insert(uint8_t* img, const uint64_t* off, const uint32_t* len
 int lsmk_wal_emit(const uint8_t* img, uint64_t n, const uint32_t* chain, const uint64_t* pos,
                   const unsigned long long* info, uint32_t m, lsmck_wal_rec* recs, uint64_t* poff, uint32_t* plen,
                   uint32_t* pcrc, hipStream_t st);
+// the segment walk (lsmck_segwalk.h; lsmck_wal.hip wal_seg_*)
+namespace lsmck { namespace seg { struct SegArgs; } }
+uint64_t lsmk_wal_seg_bytes(uint64_t len, uint64_t want);
+uint64_t lsmk_wal_seg_scan_blocks(uint32_t K);
+int lsmk_wal_seg_walk(const lsmck::seg::SegArgs* a, hipStream_t st);
+int lsmk_wal_seg_round(const lsmck::seg::SegArgs* a, uint64_t* bsum, hipStream_t st);
+int lsmk_wal_seg_repair(const lsmck::seg::SegArgs* a, uint32_t budget, hipStream_t st);
+int lsmk_wal_seg_emit(const lsmck::seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff, uint32_t* plen,
+                      uint32_t* pcrc, hipStream_t st);
 int lsmk_launch_crc32_compare(const uint32_t* crc, const uint32_t* expected, uint64_t n,
                                unsigned long long* n_bad, unsigned long long* first_bad, hipStream_t st);
 int lsmk_sha_order(const uint32_t* len, size_t n, uint16_t* keys_out, uint32_t* order, void* tmp, size_t* tmp_bytes,

@@ -1,0 +1,373 @@
+// lsmck_segwalk.h -- the WAL header walk by segments: the per-thread logic of
+// the kernels in lsmck_wal.hip (wal_seg_*), written once for the device and
+// for the host model the CPU tests run (tools/segwalk_sim.cpp).
+//
+// The reference reads the log record by record (src/wal.rs:68-84, 122-163):
+// a header's position is the previous record's end, a serial chain.  Here the
+// log [start, n) is cut into K segments of S bytes and one GPU thread takes
+// each segment:
+//   1. its ENTRY -- the first record of the chain that starts in it -- is
+//      guessed: segment 0's is `start`; any other scans its bytes for command
+//      type bytes (1 Insert, 2 Remove) whose header fits, and takes the first
+//      whose own walk is plausible (kAccept complete records, or a clean end
+//      of the log; a bogus start inside a payload reads a random length and
+//      lands on a non-type byte within a step or two);
+//   2. from the guess it walks the headers (reading ~9 bytes per record, not
+//      the payloads) to the first record start at or past the segment's end:
+//      its EXIT -- or to the chain's end (EOF, or a bad type byte);
+//   3. the guesses are checked all at once: with segment 0 right, every
+//      segment before the first one that ends the chain (jterm) must have its
+//      exit's segment t's guess equal to that exit, and no guessed segment
+//      strictly between them.  By induction along the chain that makes every
+//      guessed segment up to jterm a true entry (and the rest of the log past
+//      jterm irrelevant: the chain ended there).  The first failure is at a
+//      segment whose own entry is right, so its exit is the true entry of t:
+//      a repair rewalks t from it and the check runs again.  After too many
+//      repairs the caller takes the candidate-doubling walk instead;
+//   4. an exclusive scan of the per-segment record counts of the checked
+//      segments places each segment's records; each thread walks its segment
+//      again and emits them.
+// The chain found is the reference's exactly: a record is the one at the
+// previous record's end, its payload cut at EOF as read_to_end on take()
+// does, the chain ending at EOF (or in a truncated header: UnexpectedEof) or
+// at a byte that is not a command type (InvalidCommandType, wal.rs:36).
+#ifndef LSMCK_SEGWALK_H
+#define LSMCK_SEGWALK_H
+#include <stdint.h>
+#include <string.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define LSMCK_HD __host__ __device__ __forceinline__
+#else
+#define LSMCK_HD static inline
+#endif
+
+namespace lsmck {
+namespace seg {
+
+// a segment's outcome (its walk from the guessed entry)
+constexpr uint32_t kNone = 0;  // no entry: the chain passes over the segment (or the guess found none)
+constexpr uint32_t kExit = 1;  // the walk left the segment at a record start `pos`
+constexpr uint32_t kEnd = 2;   // the chain ends in the segment: EOF (or a truncated header)
+constexpr uint32_t kBad = 3;   // the chain ends in the segment: `pos` holds a byte that is not a command type
+constexpr uint64_t kNoGuess = ~0ull;
+constexpr uint32_t kNoSeg = 0xFFFFFFFFu;
+// a guessed entry must lead to this many complete records (or to a clean
+// end of the log) before it is taken: a bogus one passes a step with ~1/128
+// odds on random payloads, so six steps leave ~1e-13 per candidate
+constexpr uint32_t kAccept = 6;
+// per-segment record counts and the guessed-segment count share one u64 in
+// the placement scan: guessed segments in the top 24 bits, records below
+constexpr int kSegShift = 40;
+constexpr uint64_t kRecMask = (1ull << kSegShift) - 1;
+
+struct WalkOut {
+  uint32_t code;  // kExit / kEnd / kBad
+  uint32_t recs;  // records of the chain that start in the segment
+  uint64_t pos;   // kExit: the next record (at or past the segment end); kBad: the bad byte
+};
+
+LSMCK_HD uint32_t rd32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+LSMCK_HD uint32_t hdr_len(uint32_t t) { return t == 1 ? 13u : 9u; }
+
+// what position q is in the chain: 0 = a record start (type byte, header
+// fits), kEnd = EOF at or inside its header (wal.rs:76-77), kBad = not a type
+LSMCK_HD uint32_t classify(const uint8_t* img, uint64_t n, uint64_t q) {
+  if (q >= n) return kEnd;
+  const uint32_t t = img[q];
+  if (t != 1 && t != 2) return kBad;
+  return q + hdr_len(t) > n ? kEnd : 0u;
+}
+
+// the record at p (a record start): where the next one starts -- its payload
+// cut at EOF (wal.rs:130-133) -- and whether the payload is whole.  The
+// length is key_len + val_len in u32, as wal.rs:129 (wrapping).
+LSMCK_HD uint64_t succ(const uint8_t* img, uint64_t n, uint64_t p, bool* whole) {
+  const uint32_t t = img[p];
+  const uint32_t h = hdr_len(t);
+  const uint32_t dlen = rd32(img + p + 5) + (t == 1 ? rd32(img + p + 9) : 0u);
+  const uint64_t avail = n - (p + h);
+  *whole = dlen <= avail;
+  return p + h + (*whole ? (uint64_t)dlen : avail);
+}
+
+// The walk from the record start c through the segment ending at e.
+// forced: c is known to be on the chain (segment 0, a repair): taken as is.
+// Otherwise c is taken when its walk reaches kAccept whole records (past e if
+// need be) or ends cleanly at EOF.  Returns whether c is taken; *o then holds
+// the segment's outcome.
+LSMCK_HD bool walk(const uint8_t* img, uint64_t n, uint64_t c, uint64_t e, bool forced, WalkOut* o) {
+  uint64_t p = c;
+  uint32_t cnt = 0, good = 0;
+  bool out = false;
+  for (;;) {
+    if (!out && p >= e) {
+      out = true;
+      o->code = kExit;
+      o->pos = p;
+      o->recs = cnt;
+    }
+    if (out && (forced || good >= kAccept)) return true;
+    bool whole;
+    const uint64_t q = succ(img, n, p, &whole);
+    cnt += p < e;
+    good += whole;
+    const uint32_t cl = classify(img, n, q);
+    if (cl) {  // the chain ends after the record at p
+      if (!out) {
+        o->code = cl;
+        o->pos = q;
+        o->recs = cnt;
+      }
+      return forced || good >= kAccept || (whole && cl == kEnd);
+    }
+    p = q;
+  }
+}
+
+// bit 8j+7 set where byte j of v is 1 or 2 (exact, no cross-byte carries)
+LSMCK_HD uint32_t type_bytes(uint32_t v) {
+  const uint32_t hi = v & 0xFCFCFCFCu;  // zero iff the byte is < 4
+  const uint32_t z = ~(((hi & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | hi | 0x7F7F7F7Fu);
+  const uint32_t lo = v & 0x03030303u;  // the byte's low two bits: 1 or 2, not 0 or 3
+  return z & (((lo ^ (lo >> 1)) & 0x01010101u) << 7);
+}
+
+// 16 bytes at an address aligned to 16 (device: one vector load)
+LSMCK_HD void load16(const uint8_t* a, uint32_t w[4]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint4 v = *(const uint4*)a;
+  w[0] = v.x;
+  w[1] = v.y;
+  w[2] = v.z;
+  w[3] = v.w;
+#else
+  memcpy(w, a, 16);
+#endif
+}
+
+// The first type byte c in [from, e) whose header fits, or kNoGuess.  Reads
+// the 64-byte block holding `from` (aligned in the address space: vector
+// loads inside the image, byte loads at its two ends) and the ones after it.
+LSMCK_HD uint64_t next_cand(const uint8_t* img, uint64_t n, uint64_t from, uint64_t e) {
+  const uintptr_t base = (uintptr_t)img;
+  for (uintptr_t A = (base + from) & ~(uintptr_t)63;; A += 64) {
+    const int64_t p0 = (int64_t)(A - base);  // image position of the block's first byte (< 0: before the image)
+    if (p0 >= (int64_t)e) return kNoGuess;
+    uint64_t m = 0;
+    if (p0 >= 0 && (uint64_t)p0 + 64 <= n) {
+      uint32_t w[16];
+      load16((const uint8_t*)A, w);
+      load16((const uint8_t*)A + 16, w + 4);
+      load16((const uint8_t*)A + 32, w + 8);
+      load16((const uint8_t*)A + 48, w + 12);
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+      for (int d = 0; d < 16; ++d) {
+        const uint32_t f = type_bytes(w[d]);
+        const uint64_t nib = ((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u);
+        m |= nib << (4 * d);
+      }
+    } else {
+      for (int i = 0; i < 64; ++i) {
+        const int64_t p = p0 + i;
+        if (p >= 0 && (uint64_t)p < n) {
+          const uint32_t t = img[p];
+          if (t == 1 || t == 2) m |= 1ull << i;
+        }
+      }
+    }
+    // only positions in [from, e)
+    const int64_t lo = (int64_t)from - p0, hi = (int64_t)e - p0;
+    if (lo > 0) m &= ~0ull << lo;
+    if (hi < 64) m &= (1ull << hi) - 1ull;
+    while (m) {
+      const int i = __builtin_ctzll(m);
+      m &= m - 1;
+      const uint64_t c = (uint64_t)(p0 + i);
+      if (c + hdr_len(img[c]) <= n) return c;
+    }
+  }
+}
+
+// whether the chain from the record start c passes through position q > c
+LSMCK_HD bool reaches(const uint8_t* img, uint64_t n, uint64_t c, uint64_t q) {
+  uint64_t p = c;
+  while (p < q) {
+    bool whole;
+    p = succ(img, n, p, &whole);
+    if (p < q && classify(img, n, p)) return false;
+  }
+  return p == q;
+}
+
+// The guess of a segment [b, e) (b > start): the first type byte c in it
+// whose header fits and whose walk is taken -- unless a later start inside
+// c's first record has a chain through that record's end, which is then
+// preferred (the same test again from it).  The common wrong guess is a
+// bogus start before the segment's first true record whose random length
+// happens to land on a later true record: its chains merge with the true
+// one, so its walk is taken, but its first "record" covers the true entry,
+// whose chain reaches the merge point.  kNoGuess: no start taken.
+LSMCK_HD uint64_t guess(const uint8_t* img, uint64_t n, uint64_t b, uint64_t e, WalkOut* o) {
+  for (uint64_t c = next_cand(img, n, b, e); c != kNoGuess; c = next_cand(img, n, c + 1, e)) {
+    if (!walk(img, n, c, e, false, o)) continue;
+    for (;;) {
+      bool whole;
+      const uint64_t q1 = succ(img, n, c, &whole), lim = q1 < e ? q1 : e;
+      uint64_t c2 = next_cand(img, n, c + 1, lim);
+      while (c2 != kNoGuess && !reaches(img, n, c2, q1)) c2 = next_cand(img, n, c2 + 1, lim);
+      if (c2 == kNoGuess) return c;
+      c = c2;
+      walk(img, n, c, e, true, o);
+    }
+  }
+  return kNoGuess;
+}
+
+// --- the per-thread steps of the kernels ------------------------------------
+// Per segment k: g[k] (the guessed entry), x[k] (kExit: the exit; kBad: the
+// bad byte), code[k], recs[k].  info: u64 words, see kInfo*.
+enum : int {
+  kInfoJterm = 0,  // u32 at info word 0: the first segment whose walk ends the chain (atomic min)
+  kInfoFail = 1,   // u32 at info word 1: the first segment failing the check (atomic min)
+  kInfoRecs = 2,   // finalize: records of segments 0..jterm
+  kInfoCode = 3,   // finalize: jterm's code (kEnd / kBad)
+  kInfoPos = 4,    // finalize: jterm's bad byte
+  kInfoFailX = 5,  // finalize: the failing segment's exit
+  kInfoNFail = 6,  // u32 at info word 6: how many segments fail the check (atomic add)
+  kInfoWords = 8
+};
+
+struct SegArgs {
+  const uint8_t* img;
+  uint64_t n;
+  uint64_t start;  // the chain's first record
+  uint64_t S;      // segment bytes
+  uint32_t K;      // segments: ceil((n - start) / S)
+  uint64_t* g;
+  uint64_t* x;
+  uint32_t* code;
+  uint32_t* recs;
+  uint64_t* pre;  // K + 1: exclusive scan of the placement words
+  unsigned long long* info;
+};
+
+LSMCK_HD uint64_t seg_begin(const SegArgs& a, uint32_t k) { return a.start + (uint64_t)k * a.S; }
+LSMCK_HD uint64_t seg_end(const SegArgs& a, uint32_t k) {
+  const uint64_t e = a.start + (uint64_t)(k + 1) * a.S;
+  return e < a.n ? e : a.n;
+}
+LSMCK_HD uint32_t seg_of(const SegArgs& a, uint64_t pos) { return (uint32_t)((pos - a.start) / a.S); }
+
+// the forced walk of segment k from its entry c (a position on the chain)
+LSMCK_HD void seg_forced(const SegArgs& a, uint32_t k, uint64_t c) {
+  WalkOut o;
+  const uint32_t cl = classify(a.img, a.n, c);
+  if (cl) {
+    o.code = cl;
+    o.pos = c;
+    o.recs = 0;
+  } else {
+    walk(a.img, a.n, c, seg_end(a, k), true, &o);
+  }
+  a.g[k] = c;
+  a.x[k] = o.pos;
+  a.code[k] = o.code;
+  a.recs[k] = o.recs;
+}
+
+// step 1-2 for segment k
+LSMCK_HD void seg_walk_thread(const SegArgs& a, uint32_t k) {
+  if (k == 0) {
+    seg_forced(a, 0, a.start);
+    return;
+  }
+  WalkOut o;
+  const uint64_t c = guess(a.img, a.n, seg_begin(a, k), seg_end(a, k), &o);
+  a.g[k] = c;
+  if (c == kNoGuess) {
+    a.x[k] = 0;
+    a.code[k] = kNone;
+    a.recs[k] = 0;
+  } else {
+    a.x[k] = o.pos;
+    a.code[k] = o.code;
+    a.recs[k] = o.recs;
+  }
+}
+
+// placement word of segment k (the scan's input): guessed segments up to jterm
+LSMCK_HD uint64_t seg_word(const SegArgs& a, uint32_t k, uint32_t jterm) {
+  return (a.code[k] != kNone && k <= jterm) ? ((1ull << kSegShift) | a.recs[k]) : 0ull;
+}
+
+// step 3 for segment k: whether it fails the check (after the scan)
+LSMCK_HD bool seg_check_fails(const SegArgs& a, uint32_t k, uint32_t jterm) {
+  if (k >= jterm || a.code[k] == kNone) return false;
+  if (a.code[k] != kExit) return true;  // (cannot happen: jterm is the first chain end)
+  const uint32_t t = seg_of(a, a.x[k]);
+  const uint64_t between = (a.pre[t] >> kSegShift) - (a.pre[k + 1] >> kSegShift);
+  return between != 0 || a.g[t] != a.x[k];
+}
+
+// repair after a failure at segment j (whose entry is right): the segments
+// strictly inside its exit's span are cleared, the exit's segment t is walked
+// from that exit, and so on while t's own exit does not meet a consistent
+// guess -- at most `budget` segments rewalked.  One thread.
+LSMCK_HD void seg_repair(const SegArgs& a, uint32_t j, uint32_t budget) {
+  for (uint32_t step = 0; step < budget; ++step) {
+    if (a.code[j] != kExit) return;
+    const uint64_t xe = a.x[j];
+    const uint32_t t = seg_of(a, xe);
+    bool clean = a.g[t] == xe;
+    for (uint32_t u = j + 1; u < t; ++u) {
+      if (a.code[u] != kNone) clean = false;
+      a.g[u] = kNoGuess;
+      a.code[u] = kNone;
+      a.recs[u] = 0;
+    }
+    if (clean) return;
+    seg_forced(a, t, xe);
+    j = t;
+  }
+}
+
+// step 4 for segment k (after the check passed): its records at `at` + its
+// place, as lsmck_wal_rec entries, CRC descriptors and stored CRCs
+template <class Rec>
+LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint64_t at, Rec* recs, uint64_t* poff,
+                              uint32_t* plen, uint32_t* pcrc) {
+  if (k > jterm || a.code[k] == kNone) return;
+  uint64_t i = at + (a.pre[k] & kRecMask);
+  uint64_t p = a.g[k];
+  const uint8_t* img = a.img;
+  for (uint32_t r = 0; r < a.recs[k]; ++r, ++i) {
+    const uint32_t t = img[p];
+    const uint32_t h = hdr_len(t);
+    const uint32_t klen = rd32(img + p + 5), vlen = t == 1 ? rd32(img + p + 9) : 0u;
+    const uint32_t dlen = klen + vlen;
+    const uint64_t avail = a.n - (p + h);
+    const uint32_t got = dlen <= avail ? dlen : (uint32_t)avail;
+    Rec R;
+    R.rec_off = p;
+    R.payload_off = p + h;
+    R.klen = klen;
+    R.vlen = vlen;
+    R.crc = rd32(img + p + 1);
+    R.type = t;
+    recs[i] = R;
+    poff[i] = p + h;
+    plen[i] = got;
+    pcrc[i] = R.crc;
+    p += h + got;
+  }
+}
+
+}  // namespace seg
+}  // namespace lsmck
+#endif

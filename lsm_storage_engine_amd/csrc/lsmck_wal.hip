@@ -25,6 +25,7 @@
 
 #include "lsmck.h"
 #include "lsmck_device.h"
+#include "lsmck_segwalk.h"
 
 namespace lsmck {
 
@@ -314,9 +315,190 @@ __global__ __launch_bounds__(256) void wal_frame_insert(uint8_t* __restrict__ im
   }
 }
 
+// --- the segment walk (lsmck_segwalk.h) ------------------------------------
+// Thread per segment.  The walks are chains of dependent header reads, so
+// the launch wants as many segments in flight as the chip holds: the host
+// sizes segments for ~2^19 of them (lsmk_wal_seg_bytes).
+__global__ __launch_bounds__(256) void wal_seg_walk(seg::SegArgs a) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < a.K) seg::seg_walk_thread(a, k);
+}
+
+__global__ __launch_bounds__(256) void wal_seg_jterm(seg::SegArgs a) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < a.K && (a.code[k] == seg::kEnd || a.code[k] == seg::kBad))
+    atomicMin((unsigned int*)(a.info + seg::kInfoJterm), k);
+}
+
+// exclusive scan of the placement words into pre[0..K] (three passes: block
+// sums, one block over those, per-block rescan), 1024 threads x 4 segments
+#define SSCAN_ITEMS 4u
+#define SSCAN_BLOCK 1024u
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x, uint32_t lane) {
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t o = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += o;
+  }
+  return x;
+}
+__global__ __launch_bounds__(SSCAN_BLOCK) void wal_seg_scan_a(seg::SegArgs a, uint64_t* __restrict__ bsum) {
+  __shared__ uint64_t s[SSCAN_BLOCK / 64];
+  const uint32_t jterm = (uint32_t)a.info[seg::kInfoJterm];
+  const uint64_t i0 = ((uint64_t)blockIdx.x * SSCAN_BLOCK + threadIdx.x) * SSCAN_ITEMS;
+  uint64_t x = 0;
+  for (uint32_t j = 0; j < SSCAN_ITEMS; ++j)
+    if (i0 + j < a.K) x += seg::seg_word(a, (uint32_t)(i0 + j), jterm);
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  if ((threadIdx.x & 63u) == 0) s[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (uint32_t k = 0; k < SSCAN_BLOCK / 64; ++k) t += s[k];
+    bsum[blockIdx.x] = t;
+  }
+}
+__global__ __launch_bounds__(1024) void wal_seg_scan_b(uint64_t* __restrict__ bsum, uint32_t nb) {
+  __shared__ uint64_t ws[16];
+  const uint32_t C = (nb + 1023u) / 1024u, b0 = threadIdx.x * C, b1 = min(nb, b0 + C);
+  uint64_t mine = 0;
+  for (uint32_t b = b0; b < b1; ++b) mine += bsum[b];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t x = wave_incl_scan(mine, lane);
+  if (lane == 63u) ws[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t acc = 0;
+    for (int i = 0; i < 16; ++i) {
+      const uint64_t v = ws[i];
+      ws[i] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+  uint64_t run = ws[threadIdx.x >> 6] + x - mine;
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint64_t v = bsum[b];
+    bsum[b] = run;
+    run += v;
+  }
+}
+__global__ __launch_bounds__(SSCAN_BLOCK) void wal_seg_scan_c(seg::SegArgs a, const uint64_t* __restrict__ bsum) {
+  __shared__ uint64_t s[SSCAN_BLOCK / 64];
+  const uint32_t jterm = (uint32_t)a.info[seg::kInfoJterm];
+  const uint64_t i0 = ((uint64_t)blockIdx.x * SSCAN_BLOCK + threadIdx.x) * SSCAN_ITEMS;
+  uint64_t v[SSCAN_ITEMS], x = 0;
+  for (uint32_t j = 0; j < SSCAN_ITEMS; ++j) {
+    v[j] = i0 + j < a.K ? seg::seg_word(a, (uint32_t)(i0 + j), jterm) : 0ull;
+    x += v[j];
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t inc = wave_incl_scan(x, lane);
+  if (lane == 63u) s[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t acc = 0;
+    for (uint32_t k = 0; k < SSCAN_BLOCK / 64; ++k) {
+      const uint64_t t = s[k];
+      s[k] = acc;
+      acc += t;
+    }
+  }
+  __syncthreads();
+  uint64_t run = bsum[blockIdx.x] + s[threadIdx.x >> 6] + inc - x;
+  for (uint32_t j = 0; j < SSCAN_ITEMS; ++j)
+    if (i0 + j <= a.K) {  // (pre[K]: the total)
+      a.pre[i0 + j] = run;
+      run += v[j];
+    }
+}
+
+__global__ __launch_bounds__(256) void wal_seg_check(seg::SegArgs a) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t jterm = (uint32_t)a.info[seg::kInfoJterm];
+  if (k < a.K && seg::seg_check_fails(a, k, jterm)) {
+    atomicMin((unsigned int*)(a.info + seg::kInfoFail), k);
+    atomicAdd((unsigned int*)(a.info + seg::kInfoNFail), 1u);
+  }
+}
+
+// the round's outcome into info (one thread)
+__global__ void wal_seg_finalize(seg::SegArgs a) {
+  const uint32_t jterm = (uint32_t)a.info[seg::kInfoJterm], fail = (uint32_t)a.info[seg::kInfoFail];
+  a.info[seg::kInfoRecs] = a.pre[a.K] & seg::kRecMask;
+  const bool jt = jterm < a.K;
+  a.info[seg::kInfoCode] = jt ? a.code[jterm] : 0u;
+  a.info[seg::kInfoPos] = jt ? a.x[jterm] : 0ull;
+  a.info[seg::kInfoFailX] = fail < a.K ? a.x[fail] : 0ull;
+}
+
+// a new round: jterm and fail back to "none"
+__global__ void wal_seg_reset(seg::SegArgs a) {
+  a.info[seg::kInfoJterm] = seg::kNoSeg;
+  a.info[seg::kInfoFail] = seg::kNoSeg;
+  a.info[seg::kInfoNFail] = 0;
+}
+
+__global__ void wal_seg_repair(seg::SegArgs a, uint32_t budget) {
+  const uint32_t j = (uint32_t)a.info[seg::kInfoFail];
+  if (j < a.K) seg::seg_repair(a, j, budget);
+}
+
+__global__ __launch_bounds__(256) void wal_seg_emit(seg::SegArgs a, uint64_t at, lsmck_wal_rec* __restrict__ recs,
+                                                     uint64_t* __restrict__ poff, uint32_t* __restrict__ plen,
+                                                     uint32_t* __restrict__ pcrc) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < a.K) seg::seg_emit_thread(a, k, (uint32_t)a.info[seg::kInfoJterm], at, recs, poff, plen, pcrc);
+}
+
 }  // namespace lsmck
 
 using namespace lsmck;
+
+static int launch_err();
+
+// Segment bytes for a walk over `len` bytes: a power of two from 512 B to
+// 16 MiB giving about 2^19 segments (one thread each); `want` overrides.
+extern "C" uint64_t lsmk_wal_seg_bytes(uint64_t len, uint64_t want) {
+  if (want) return want;
+  uint64_t S = 512;
+  while (S < (16ull << 20) && (len + S - 1) / S > (1ull << 19)) S <<= 1;
+  return S;
+}
+extern "C" uint64_t lsmk_wal_seg_scan_blocks(uint32_t K) {
+  return ((uint64_t)K + 1 + SSCAN_BLOCK * SSCAN_ITEMS - 1) / (SSCAN_BLOCK * SSCAN_ITEMS);
+}
+
+// steps 1-2: every segment's guess and walk (a round follows)
+extern "C" int lsmk_wal_seg_walk(const seg::SegArgs* a, hipStream_t st) {
+  hipLaunchKernelGGL(wal_seg_walk, dim3((a->K + 255) / 256), dim3(256), 0, st, *a);
+  return launch_err();
+}
+
+// one check round: jterm, the placement scan, the check, the outcome in info
+// (bsum: lsmk_wal_seg_scan_blocks(K) u64)
+extern "C" int lsmk_wal_seg_round(const seg::SegArgs* a, uint64_t* bsum, hipStream_t st) {
+  const unsigned g = (a->K + 255) / 256;
+  const uint32_t nb = (uint32_t)lsmk_wal_seg_scan_blocks(a->K);
+  hipLaunchKernelGGL(wal_seg_reset, dim3(1), dim3(1), 0, st, *a);
+  hipLaunchKernelGGL(wal_seg_jterm, dim3(g), dim3(256), 0, st, *a);
+  hipLaunchKernelGGL(wal_seg_scan_a, dim3(nb), dim3(SSCAN_BLOCK), 0, st, *a, bsum);
+  hipLaunchKernelGGL(wal_seg_scan_b, dim3(1), dim3(1024), 0, st, bsum, nb);
+  hipLaunchKernelGGL(wal_seg_scan_c, dim3(nb), dim3(SSCAN_BLOCK), 0, st, *a, (const uint64_t*)bsum);
+  hipLaunchKernelGGL(wal_seg_check, dim3(g), dim3(256), 0, st, *a);
+  hipLaunchKernelGGL(wal_seg_finalize, dim3(1), dim3(1), 0, st, *a);
+  return launch_err();
+}
+
+extern "C" int lsmk_wal_seg_repair(const seg::SegArgs* a, uint32_t budget, hipStream_t st) {
+  hipLaunchKernelGGL(wal_seg_repair, dim3(1), dim3(1), 0, st, *a, budget);
+  return launch_err();
+}
+
+extern "C" int lsmk_wal_seg_emit(const seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff,
+                                 uint32_t* plen, uint32_t* pcrc, hipStream_t st) {
+  hipLaunchKernelGGL(wal_seg_emit, dim3((a->K + 255) / 256), dim3(256), 0, st, *a, at, recs, poff, plen, pcrc);
+  return launch_err();
+}
 
 extern "C" int lsmk_wal_frame_insert(uint8_t* img, const uint64_t* off, const uint32_t* len, const uint32_t* crc,
                                      uint64_t n, uint32_t kmax, hipStream_t st) {

@@ -127,6 +127,11 @@ class Context:
     def set_option(self, key, value):
         _lib.check(self.lib.lsmck_ctx_set_option(self.handle, key.encode(), int(value)), f"set_option({key})")
 
+    def get_stat(self, key):
+        v = C.c_long()
+        _lib.check(self.lib.lsmck_ctx_get_stat(self.handle, key.encode(), C.byref(v)), f"get_stat({key})")
+        return v.value
+
     # --- memory -------------------------------------------------------------
     def alloc(self, nbytes):
         return DeviceBuffer(self, nbytes)
@@ -247,7 +252,8 @@ class Context:
                                                          C.byref(nrec), C.byref(bi), C.byref(bc), C.byref(be)),
                         "wal_replay_verify")
         # np.recarray: record fields read as attributes (r.payload_off), like the ctypes struct
-        return recs[:nrec.value].view(np.recarray), rc, (bi.value, bc.value, be.value)
+        # nrec counts the whole log's accepted records; at most cap of them were written
+        return recs[:min(nrec.value, cap)].view(np.recarray), rc, (bi.value, bc.value, be.value)
 
     def checksums_verify_many(self, triples):
         n = len(triples)

@@ -374,3 +374,113 @@ def test_gpu_header_walk_big_binary_log(ctx):
     tail = bytes([1]) + O.crc32(short).to_bytes(4, "little") + (3).to_bytes(4, "little") + \
         (300).to_bytes(4, "little") + short
     assert same(ctx, img + tail, device=True) == 0
+
+
+@pytest.fixture
+def seg_opts(ctx):
+    """Sets segment-walk options for one test, then restores the defaults."""
+    def set_(**kw):
+        for k, v in kw.items():
+            ctx.set_option(k, v)
+    yield set_
+    for k, v in (("wal_seg_bytes", 0), ("wal_seg_rounds", 16), ("wal_seg_walk", 1)):
+        ctx.set_option(k, v)
+
+
+def _binary_log(n, seed, lo=0, hi=600, big_every=0, big=0):
+    rng = np.random.default_rng(seed)
+    blob = O.gen_stream(seed, 0, 1 << 21)
+    parts = []
+    for i in range(n):
+        kl = int(rng.integers(1, 40))
+        vl = big if (big_every and i % big_every == 0) else int(rng.integers(lo, hi))
+        o = int(rng.integers(0, (1 << 21) - 40 - min(vl, 1 << 20)))
+        k = blob[o:o + kl].tobytes()
+        v = blob[o + 40:o + 40 + vl].tobytes() if vl <= (1 << 20) else rng.bytes(vl)
+        parts.append(O.wal_remove(k) if i % 9 == 0 else O.wal_insert(k, v))
+    return b"".join(parts)
+
+
+@pytest.mark.parametrize("seg", [0, 64, 512, 4096])
+@pytest.mark.parametrize("shift", [0, 5])
+def test_segment_walk(ctx, seg_opts, seg, shift):
+    """The segment walk (lsmck_segwalk.h) of device images: random binary
+    payloads (bogus starts everywhere), segments from 64 B (far shorter than
+    the records: most hold no true entry) to auto, the image at an odd
+    address; a bad type byte, a truncated tail, a corrupted payload -- the
+    oracle's records and outcome, and the walk reports the segment path."""
+    seg_opts(wal_seg_bytes=seg)
+    img = _binary_log(20000, 61)
+    assert same(ctx, img, device=True, shift=shift) == 0
+    assert ctx.get_stat("wal_walk_path") == 1
+    if seg in (0, 4096):  # segments longer than every record: no guess to repair
+        assert ctx.get_stat("wal_seg_repairs") == 0
+    st, recs, _ = O.wal_replay(img)
+    b = bytearray(img)
+    b[recs[12345].rec_off] = 0x33
+    assert same(ctx, bytes(b), device=True, shift=shift) == 3
+    same(ctx, img[:recs[17000].payload_off + 3], device=True, shift=shift)
+    b = bytearray(img)
+    b[recs[9999].payload_off] ^= 0x08
+    assert same(ctx, bytes(b), device=True, shift=shift) in (1, 2)
+
+
+def test_segment_walk_long_records(ctx, seg_opts):
+    """Records longer than the auto segments (1 MiB values among small ones):
+    segments inside them hold no true entry, the first check fails many times
+    and the walk re-segments; results stay the oracle's."""
+    img = _binary_log(3000, 62, big_every=7, big=(1 << 20) + 3)
+    assert same(ctx, img, device=True) == 0
+    assert ctx.get_stat("wal_walk_path") in (1, 2)
+
+
+def test_segment_walk_log_of_logs(ctx, seg_opts):
+    """Values that are WAL images themselves: guesses inside them follow
+    plausible chains that are not the log's.  Every wrong guess is caught:
+    repaired (segment walk) or, with no repairs allowed, the walk declines
+    to candidate doubling -- the same records either way."""
+    inner = _binary_log(80, 63, hi=200)
+    rng = np.random.default_rng(64)
+    parts = [O.wal_insert(b"k%d" % i, inner if i % 3 == 0 else rng.bytes(int(rng.integers(0, 400))))
+             for i in range(3000)]
+    img = b"".join(parts)
+    for seg, rounds in ((256, 1024), (4096, 1024), (256, 0)):
+        seg_opts(wal_seg_bytes=seg, wal_seg_rounds=rounds)
+        assert same(ctx, img, device=True) == 0
+        assert ctx.get_stat("wal_walk_path") in (1, 2)
+    seg_opts(wal_seg_walk=0)
+    assert same(ctx, img, device=True) == 0
+    assert ctx.get_stat("wal_walk_path") == 2
+
+
+def test_segment_walk_every_cut(ctx, seg_opts):
+    """Small logs cut at every position (EOF inside a header or a payload),
+    64-byte segments: the tail segment's entry is refused by the guess and
+    repaired."""
+    img = _binary_log(30, 65, hi=120)
+    seg_opts(wal_seg_bytes=64)
+    d = ctx.alloc(len(img) + 8)
+    try:
+        d.upload(np.frombuffer(img, np.uint8))
+        for cut in range(0, len(img) + 1, 3):
+            recs, st, bad = ctx.wal_replay_verify(cut, device_ptr=d.ptr)
+            ost, orecs, obad = O.wal_replay(img[:cut])
+            assert st == ost, cut
+            assert [int(r.rec_off) for r in recs] == [r.rec_off for r in orecs], cut
+    finally:
+        d.free()
+
+
+def test_wal_replay_cap_below_count(ctx):
+    """cap below the record count: exactly cap records come back, also into a
+    records array left larger by an earlier replay (no stale entries)."""
+    img = _binary_log(5000, 66)
+    recs, st, _ = ctx.wal_replay_verify(img)
+    assert st == 0 and len(recs) == 5000
+    del recs
+    small = _binary_log(2000, 67)
+    recs, st, _ = ctx.wal_replay_verify(small, cap=700)
+    ost, orecs, _ = O.wal_replay(small)
+    assert st == ost == 0
+    assert len(recs) == 700
+    assert [int(r.rec_off) for r in recs] == [r.rec_off for r in orecs[:700]]

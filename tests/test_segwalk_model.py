@@ -1,0 +1,190 @@
+"""The segment walk (lsmck_segwalk.h, the GPU WAL header walk's logic) run on
+the host through tools/segwalk_sim.cpp -- the kernels' own per-thread
+functions in the launch order of lsmck_api.cpp -- against a plain chain walk
+of wal.rs:68-84,122-163 (each record at the previous one's end, the payload
+cut at EOF, the chain ending at EOF, in a truncated header, or at a byte that
+is not a command type).  Covers what the GPU suite can afford little of:
+segments far smaller than records, every cut position, bad type bytes, and
+payloads built to fool the guesses (framed records inside values, floods of
+type bytes), where the check must catch every wrong guess and the repairs (or
+the decline to candidate doubling) must leave the chain exact."""
+import ctypes as C
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "lsm_storage_engine_amd", "csrc")
+END, BAD = 2, 3
+
+
+@pytest.fixture(scope="module")
+def sim(tmp_path_factory):
+    so = str(tmp_path_factory.mktemp("segwalk") / "libsegwalk_sim.so")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-I", CSRC, "-o", so,
+                    os.path.join(ROOT, "tools", "segwalk_sim.cpp")], check=True)
+    lib = C.CDLL(so)
+    u64p = C.POINTER(C.c_uint64)
+    lib.segwalk_sim.restype = C.c_int
+    lib.segwalk_sim.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, u64p, C.c_size_t, u64p,
+                                C.POINTER(C.c_uint32), u64p, C.POINTER(C.c_int), u64p, C.POINTER(C.c_uint32)]
+
+    def run(img, S, start=0, rounds=16, shift=0):
+        raw = np.zeros(len(img) + shift + 1, dtype=np.uint8)  # shift: the image at an odd address
+        a = raw[shift:shift + len(img)]
+        a[:] = np.frombuffer(bytes(img), np.uint8)
+        cap = len(img) // 9 + 2
+        offs = (C.c_uint64 * cap)()
+        m, code, pos, rep, K, nf = C.c_uint64(), C.c_uint32(), C.c_uint64(), C.c_int(), C.c_uint64(), C.c_uint32()
+        rc = lib.segwalk_sim(a.ctypes.data, len(img), start, S, rounds, offs, cap, C.byref(m), C.byref(code),
+                             C.byref(pos), C.byref(rep), C.byref(K), C.byref(nf))
+        assert rc in (0, 1), rc
+        if rc == 1:
+            return None
+        return list(offs[:m.value]), code.value, (pos.value if code.value == BAD else 0), rep.value
+    return run
+
+
+def chain(img, start=0):
+    """wal.rs's read loop over the headers alone (no CRCs)."""
+    n, p, offs = len(img), start, []
+    while True:
+        if p >= n:
+            return offs, END, 0
+        t = img[p]
+        if t not in (1, 2):
+            return offs, BAD, p
+        h = 13 if t == 1 else 9
+        if p + h > n:
+            return offs, END, 0
+        klen = struct.unpack_from("<I", img, p + 5)[0]
+        vlen = struct.unpack_from("<I", img, p + 9)[0] if t == 1 else 0
+        dlen = (klen + vlen) & 0xFFFFFFFF
+        offs.append(p)
+        p += h + min(dlen, n - p - h)
+
+
+def rec(key, val=None):
+    if val is None:
+        return struct.pack("<BII", 2, 0x1234, len(key)) + key
+    return struct.pack("<BIII", 1, 0x5678, len(key), len(val)) + key + val
+
+
+def random_log(rng, nrec, lo=0, hi=600, remove_every=9):
+    parts = []
+    for i in range(nrec):
+        kl = int(rng.integers(0, 40))
+        vl = int(rng.integers(lo, hi))
+        k = rng.bytes(kl)
+        parts.append(rec(k) if i % remove_every == 0 else rec(k, rng.bytes(vl)))
+    return bytearray(b"".join(parts))
+
+
+def check(sim, img, S, start=0, shift=0, rounds=16, expect_fast=True):
+    want = chain(bytes(img), start)
+    got = sim(img, S, start=start, rounds=rounds, shift=shift)
+    if got is None:
+        assert not expect_fast, "declined"
+        return None
+    offs, code, pos, rep = got
+    assert code == want[1] and pos == want[2]
+    assert offs == want[0]
+    return rep
+
+
+@pytest.mark.parametrize("S", [64, 100, 512, 4096, 1 << 16])
+@pytest.mark.parametrize("shift", [0, 3])
+def test_random_logs(sim, S, shift):
+    rng = np.random.default_rng(S + shift)
+    img = random_log(rng, 3000)
+    rep = check(sim, img, S, shift=shift)
+    if S >= 1024:  # every segment holds a true record start: no wrong guess to repair
+        assert rep == 0
+
+
+def test_long_records_span_segments(sim):
+    rng = np.random.default_rng(7)
+    parts = [rec(rng.bytes(8), rng.bytes(int(L))) for L in rng.integers(0, 20000, 300)]
+    img = bytearray(b"".join(parts))
+    for S in (64, 1000, 4096):
+        assert check(sim, img, S) is not None
+
+
+def test_every_cut_position(sim):
+    """Truncated logs: EOF inside a header (clean end) or inside a payload
+    (the record kept with a short payload) -- the true entry of the last
+    segment may be refused by the guess, and the check repairs it."""
+    rng = np.random.default_rng(11)
+    img = random_log(rng, 40, hi=200)
+    for cut in range(0, len(img) + 1):
+        check(sim, img[:cut], 128)
+
+
+def test_bad_type_bytes(sim):
+    rng = np.random.default_rng(12)
+    img = random_log(rng, 2000)
+    offs = chain(bytes(img))[0]
+    for i in (0, 1, 500, 1999):
+        b = bytearray(img)
+        b[offs[i]] = 7
+        check(sim, b, 256)
+        check(sim, b, 4096)
+    # garbage after a bad byte that still parses as records (a torn write):
+    # the chain ends at the bad byte, the segments after it do not matter
+    b = bytearray(img)
+    b[offs[700]] = 0
+    check(sim, b, 512)
+
+
+def test_start_offsets(sim):
+    rng = np.random.default_rng(13)
+    img = random_log(rng, 1500)
+    offs = chain(bytes(img))[0]
+    for st in (offs[1], offs[777], offs[-1], len(img)):
+        check(sim, img, 512, start=st)
+
+
+def test_framed_records_inside_values(sim):
+    """Values that are themselves WAL images (a log of logs): inside them the
+    guesses find plausible chains that are not the log's.  The check catches
+    each one; repairs keep the chain exact, and past wal_seg_rounds the walk
+    declines (the caller then takes candidate doubling)."""
+    rng = np.random.default_rng(14)
+    inner = bytes(random_log(rng, 60, hi=120))
+    parts = []
+    for i in range(200):
+        parts.append(rec(b"k%d" % i, inner if i % 3 == 0 else rng.bytes(int(rng.integers(0, 300)))))
+    img = bytearray(b"".join(parts))
+    for S in (256, 1024, 8192):
+        rep = check(sim, img, S, rounds=1024)
+        assert rep is not None
+    # with no repairs allowed it declines rather than return a wrong chain
+    assert sim(img, 256, rounds=0) is None or check(sim, img, 256, rounds=0) == 0
+
+
+def test_type_byte_flood(sim):
+    """Keys and values of 0x01 bytes: every byte a candidate, every false
+    start a long plausible chain."""
+    img = bytearray(b"".join(rec(b"\x01" * 40, b"\x01" * 200) for _ in range(300)))
+    for S in (64, 512, 4096):
+        check(sim, img, S, rounds=1024)
+    img2 = bytearray(b"".join(rec(b"\x02" * 3, b"\x01\x00\x00\x00" * 50) for _ in range(300)))
+    check(sim, img2, 512, rounds=1024)
+
+
+def test_tiny_logs(sim):
+    for img in (b"", b"\x01", b"\x02", b"\x05", rec(b""), rec(b"", b""), rec(b"a", b"b")[:-1],
+                rec(b"key", b"value") + b"\x01\x00", rec(b"k") + b"\x09"):
+        for S in (64, 4096):
+            check(sim, bytearray(img), S)
+
+
+def test_huge_lengths_wrap(sim):
+    """klen + vlen wrapping in u32 (wal.rs:129), and a length past EOF."""
+    r = struct.pack("<BIII", 1, 0, 0xFFFFFFF0, 0x20) + b"x" * 16  # wraps to 16
+    img = bytearray(r * 50 + struct.pack("<BIII", 1, 0, 5, 1 << 30) + b"abc")
+    for S in (64, 200):
+        check(sim, img, S)

@@ -1,0 +1,80 @@
+// segwalk_sim.cpp -- the segment walk of lsmck_segwalk.h run on the host:
+// the same per-thread functions the wal_seg_* kernels run, called in loops in
+// the order lsmck_api.cpp's wal_seg_walk launches them.  Test infrastructure
+// (tests/test_segwalk_model.py builds it with g++): it checks the walk's logic
+// -- guesses, the check, repairs, placement -- against a plain chain walk on
+// logs the GPU suite cannot afford many of (adversarial payloads, tiny
+// segments, every cut position).  Not part of liblsmck.
+#include <stdint.h>
+#include <stddef.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "lsmck_segwalk.h"
+
+namespace sg = lsmck::seg;
+
+struct SimRec {
+  uint64_t rec_off, payload_off;
+  uint32_t klen, vlen, crc, type;
+};
+
+static uint64_t* g_dbg = nullptr;  // debug: the first round's guesses
+extern "C" void segwalk_sim_debug(uint64_t* g) { g_dbg = g; }
+
+extern "C" int segwalk_sim(const uint8_t* img, uint64_t n, uint64_t start, uint64_t S, int max_rounds,
+                           uint64_t* rec_off, size_t cap, uint64_t* m_out, uint32_t* code_out, uint64_t* pos_out,
+                           int* repairs, uint64_t* segments, uint32_t* first_fails) {
+  *first_fails = 0;
+  *repairs = 0;
+  *segments = 0;
+  if (start >= n) {
+    *m_out = 0;
+    *code_out = sg::kEnd;
+    *pos_out = 0;
+    return 0;
+  }
+  const uint32_t K = (uint32_t)((n - start + S - 1) / S);
+  *segments = K;
+  std::vector<uint64_t> g(K + 1), x(K + 1), pre(K + 1);
+  std::vector<uint32_t> code(K + 1), recs(K + 1);
+  unsigned long long info[sg::kInfoWords] = {};
+  sg::SegArgs a{img, n, start, S, K, g.data(), x.data(), code.data(), recs.data(), pre.data(), info};
+  for (uint32_t k = 0; k < K; ++k) sg::seg_walk_thread(a, k);
+  if (g_dbg) std::copy(g.begin(), g.begin() + K, g_dbg);
+  for (int round = 0;; ++round) {
+    uint32_t jterm = sg::kNoSeg, fail = sg::kNoSeg;
+    for (uint32_t k = 0; k < K; ++k)
+      if (code[k] == sg::kEnd || code[k] == sg::kBad) jterm = std::min(jterm, k);
+    uint64_t run = 0;
+    for (uint32_t k = 0; k <= K; ++k) {
+      pre[k] = run;
+      if (k < K) run += sg::seg_word(a, k, jterm);
+    }
+    uint32_t nfail = 0;
+    for (uint32_t k = 0; k < K; ++k)
+      if (sg::seg_check_fails(a, k, jterm)) fail = std::min(fail, k), ++nfail;
+    if (round == 0) *first_fails = nfail;
+    info[sg::kInfoJterm] = jterm;
+    info[sg::kInfoFail] = fail;
+    if (fail == sg::kNoSeg) {
+      if (jterm == sg::kNoSeg) return 2;  // (cannot happen: the last guessed segment would fail)
+      *m_out = pre[K] & sg::kRecMask;
+      *code_out = code[jterm];
+      *pos_out = x[jterm];
+      break;
+    }
+    if (round >= max_rounds) return 1;  // declined: the caller walks by candidate doubling
+    sg::seg_repair(a, fail, 4096);
+    *repairs = round + 1;
+  }
+  const uint64_t m = *m_out;
+  std::vector<SimRec> R(m);
+  std::vector<uint64_t> poff(m);
+  std::vector<uint32_t> plen(m), pcrc(m);
+  for (uint32_t k = 0; k < K; ++k)
+    sg::seg_emit_thread(a, k, (uint32_t)info[sg::kInfoJterm], 0, R.data(), poff.data(), plen.data(), pcrc.data());
+  for (uint64_t i = 0; i < m && i < cap; ++i) rec_off[i] = R[i].rec_off;
+  return 0;
+}

@@ -33,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--records", type=int, default=1 << 26)
+    ap.add_argument("--seg-walk", type=int, default=1, help="0: the candidate-doubling walk (A/B)")
     a = ap.parse_args()
     n = a.records
     ln = gen_zipf_lengths(0x5EED0003, n)
@@ -46,6 +47,7 @@ def main():
             golden = json.load(f)["config3w"]
         assert total == golden["image_bytes"]
     ctx = Context(0)
+    ctx.set_option("wal_seg_walk", a.seg_walk)
     d = ctx.alloc(total + 64)
     d_o, d_l, out = ctx.alloc(off.nbytes), ctx.alloc(ln.nbytes), ctx.alloc(4 * n)
     ctx.gen_stream(d.ptr, 0x5EED0003, 0, total)
@@ -78,6 +80,8 @@ def main():
         "log_bytes": total, "records": n, "ms_median": round(med * 1e3, 2), "ms_best": round(best * 1e3, 2),
         "steps": a.steps, "summary_crc32": summary, "summary_matches_oracle": bool(golden) and True,
         "records_out_bytes": 32 * n,
+        "walk_path": {1: "segment walk", 2: "candidate doubling", 3: "host walk"}.get(ctx.get_stat("wal_walk_path")),
+        "seg_repairs": ctx.get_stat("wal_seg_repairs"), "segments": ctx.get_stat("wal_segments"),
         "workload": "config 3's 2^26 Zipf payloads (64 B-64 KiB) framed as wal.rs Insert records (13-byte headers), "
                     "headers and CRCs written on the device"}))
 
