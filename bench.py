@@ -3,16 +3,22 @@
 "GiB/s device-resident batched record checksum; % of HBM3E read BW").
 
 One step = one pass of the hot path (lsmck_crc32_batch*) over one batch of
-synthetic records already resident in HBM.  Default workload (N = 1) is
+synthetic records already resident in HBM.  Default workload at every N is
 BASELINE config 3, the north_star's "synthetic variable-length KV records
-(64 B-64 KiB)": 2^26 Zipf-length records packed back to back (~97 GiB, the
-largest single-GPU config).  --config 2 runs the fixed 4 KiB blocks (64 GiB),
---config 1 the 256 B WAL payloads.  With --gpus N > 1 the workload is BASELINE
-config 4: one process per GPU, and rank
-r checksums shard r = blocks [r*2^26, (r+1)*2^26) of the same global block
-stream, 2^26 x 4 KiB = 256 GiB per GPU (weak scaling, record-sharded, no
-data-path collective); the control plane (barrier, max of per-rank times, the
-per-rank summary digests) goes over torch.distributed (gloo).
+(64 B-64 KiB) at 1, 2, 4 and 8 MI355X": 2^26 Zipf-length records per GPU
+packed back to back (~97 GiB, the largest single-GPU config).  With --gpus N
+there is one process per GPU and rank r checksums records [r*2^26, (r+1)*2^26)
+of ONE global config-3 stream (its lengths from the counter-based generator
+at record r*2^26, its bytes at the stream offset where rank r-1's end) --
+weak scaling, record-sharded, no data-path collective; the control plane
+(barrier, max of per-rank times, per-rank summary digests against the
+oracle's, tests/golden/summaries.json config3_shards) goes over
+torch.distributed (gloo).  Rank 0's shard is the N = 1 workload itself, so
+the 1 -> N curve is like for like.  Every line also carries BASELINE config 4
+as "config4": the fixed 4 KiB block shard (2^26 blocks = 256 GiB per GPU,
+shard r = blocks [r*2^26, (r+1)*2^26) of config 2's stream), timed the same
+way after the config-3 buffers are freed.  --config 2 / 1 run the fixed 4 KiB
+blocks (64 GiB; config 4's shard at N > 1) / the 256 B WAL payloads.
 
 `python bench.py --gpus N` outside torch.distributed.run starts
 `torch.distributed.run --nproc-per-node N` on itself as a child process
@@ -50,6 +56,7 @@ VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # full-rate VALU issue slots/s: 256 C
 # kernel issued 1,553 instructions per block).
 SHA_OPS_PER_BLOCK = 2238
 METRIC = "GiB/s device-resident batched record checksum; % of HBM3E read BW"
+CONFIG3_SHARDS = {1 << 26: "config3_shards", 1 << 20: "config3_shards_small"}  # records per rank -> golden key
 SEED = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003}
 
 
@@ -59,7 +66,13 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=0, choices=[0, 1, 2, 3],
-                    help="0 (default): config 3 at N = 1, config 4 (config 2's blocks, 2^26 per GPU) at N > 1")
+                    help="0 (default): config 3 (records [r*2^26, (r+1)*2^26) of one global stream per rank); "
+                         "2: config 2's blocks (config 4's 2^26-block shard per rank at N > 1)")
+    ap.add_argument("--no-config4", action="store_true",
+                    help="skip the config-4 block-shard sub-measurement of the config-3 line")
+    ap.add_argument("--c4-blocks", type=int, default=0,
+                    help="blocks per rank of the config-4 sub-measurement (default 2^26; 2^26/N when the ranks "
+                         "share one GPU)")
     ap.add_argument("--blocks-per-gpu", type=int, default=0, help="override the per-GPU record count")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-records", type=int, default=0)
@@ -92,8 +105,9 @@ def parse():
 
 def resolve_config(config, world):
     """--config 0 (default): BASELINE config 3 (north_star's variable-length
-    records) at N = 1; config 4's fixed 4 KiB shard per rank at N > 1."""
-    return config or (2 if world > 1 else 3)
+    records) at every N: rank r takes records [r*2^26, (r+1)*2^26) of one
+    global stream."""
+    return config or 3
 
 
 def traffic_from_profiles(workload_key):
@@ -142,6 +156,89 @@ def golden_summaries():
             return json.load(f)
     except (OSError, ValueError):
         return {}
+
+
+def config3_shard(gen, seed, nrec, rank, gather=None, framed=False, align=1):
+    """Rank r's share of one global config-3 stream: records [r*nrec,
+    (r+1)*nrec) -- their lengths from the counter-based generator `gen` at
+    record r*nrec -- laid out packed (or wal.rs-framed: a 13-byte header before
+    every payload, wal.rs:178-182), and the stream byte offset of the shard's
+    first byte: the sizes of the lower ranks' shards (gather: an all_gather of
+    one value per rank; None at N = 1).  Returns (offs, lens, nbytes, byte_off)."""
+    lens = gen(seed, nrec, first=rank * nrec)
+    offs = np.zeros(nrec, dtype=np.uint64)
+    if framed:
+        offs[:] = 13  # payload i+1 starts len[i] + 13 after payload i
+        offs[1:] += lens[:-1].astype(np.uint64)
+        offs = np.cumsum(offs, dtype=np.uint64)
+    else:
+        slot = ((lens.astype(np.uint64) + (align - 1)) // align) * align  # align 1: packed back to back
+        np.cumsum(slot[:-1], out=offs[1:])
+    nbytes = int(offs[-1]) + int(lens[-1])
+    byte_off = sum(gather(nbytes)[:rank]) if gather else 0
+    return offs, lens, nbytes, byte_off
+
+
+def config4_sub(a, ctx, stream, sptr, world, rank):
+    """BASELINE config 4 on this rank: blocks [r*n4, (r+1)*n4) of config 2's
+    4 KiB block stream (n4 = 2^26: 256 GiB per GPU), W warm-up steps, then K
+    steps between barriers, the max wall time over ranks; per-rank digests
+    against the oracle's (make_summaries.py config4) at full size."""
+    share = bool(os.environ.get("LSMCK_BENCH_SHARE_GPU")) and world > 1
+    n4 = a.c4_blocks or ((1 << 26) // world if share else (1 << 26))
+    L = 4096
+    d4, o4 = ctx.alloc(n4 * L + 64), ctx.alloc(4 * n4)
+    ctx.gen_stream(d4.ptr, SEED[2], rank * n4 * L, n4 * L, sptr)
+
+    def step4():
+        ctx.crc32_fixed_device(d4.ptr, L, L, n4, o4.ptr, sptr)
+    for _ in range(a.warmup):
+        step4()
+    ctx.sync(sptr)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(a.steps):
+        step4()
+    e1.record(stream)
+    ctx.sync(sptr)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    ev_ms = e0.elapsed_time(e1) / a.steps
+    t = torch.tensor([wall], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t[0])
+    import zlib
+    mine = "%08x" % zlib.crc32(o4.download(np.uint8, count=4 * n4).tobytes())
+    mine_t = {"rank": rank, "launch_ms_hip_events": round(ev_ms, 4), "summary_crc32": mine}
+    if world > 1:
+        allr = [None] * world
+        dist.all_gather_object(allr, mine_t)
+    else:
+        allr = [mine_t]
+    d4.free()
+    o4.free()
+    algo = n4 * L + 4 * n4
+    r = {
+        "workload": f"config4: {n4} fixed 4 KiB SSTable blocks per GPU ({n4 * L / GIB:.0f} GiB), rank r = blocks "
+                    f"[r*{n4}, (r+1)*{n4}) of config 2's stream, device-resident",
+        "value": round(world * n4 * L / GIB / (wall_max / a.steps), 2), "unit": "GiB/s",
+        "ms_per_step": round(wall_max * 1e3 / a.steps, 4), "steps": a.steps, "records_per_gpu": n4,
+        "kernel": "crc32_wring_kernel",
+        "frac": round(algo / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "per_rank": allr,
+    }
+    g4 = golden_summaries().get("config4", {}).get("shard_summary_crc32", [])
+    if n4 == (1 << 26) and world <= len(g4):
+        r["summary_matches_oracle"] = [x["summary_crc32"] for x in allr] == g4[:world]
+    return r
 
 
 def main():
@@ -193,25 +290,23 @@ def main():
         workload = f"config1: {nrec} x 256 B WAL payloads per GPU, device-resident"
     else:
         nrec = a.blocks_per_gpu or (1 << 26)
-        lens = gen_zipf_lengths(seed + rank, nrec)
-        offs = np.zeros(nrec, dtype=np.uint64)
         A = max(1, a.pack_align)
-        if a.wal_framed:  # wal.rs:178-182: [u8 1][u32 crc][u32 klen][u32 vlen] in front of every payload
-            offs[:] = 13  # payload i+1 starts len[i] + 13 after payload i
-            offs[1:] += lens[:-1].astype(np.uint64)
-            offs = np.cumsum(offs, dtype=np.uint64)
-        else:
-            slot = ((lens.astype(np.uint64) + (A - 1)) // A) * A  # A = 1: packed back to back
-            np.cumsum(slot[:-1], out=offs[1:])
-        nbytes = int(offs[-1]) + int(lens[-1])
-        byte_off = 0
+        gather = None
+        if world > 1:
+            def gather(x):
+                xs = [None] * world
+                dist.all_gather_object(xs, x)
+                return xs
+        offs, lens, nbytes, byte_off = config3_shard(gen_zipf_lengths, seed, nrec, rank, gather, a.wal_framed, A)
+        shard = (f"; rank r = records [r*{nrec}, (r+1)*{nrec}) of one global stream, bytes at its global offset"
+                 if world > 1 else "")
         if a.wal_framed:
             workload = (f"config3w: {nrec} mixed-length records per GPU (64 B-64 KiB, Zipf s=1.5) framed as wal.rs "
                         f"Insert records: a 13-byte header before every payload, unaligned ({nbytes / GIB:.1f} GiB "
-                        "image), device-resident")
+                        f"image), device-resident{shard}")
         else:
             workload = (f"config3: {nrec} mixed-length records per GPU (64 B-64 KiB, Zipf s=1.5, packed, unaligned; "
-                        f"{nbytes / GIB:.1f} GiB), device-resident")
+                        f"{nbytes / GIB:.1f} GiB), device-resident{shard}")
         if A > 1:
             workload += f" [diagnostic: offsets aligned to {A} B]"
         if a.sorted:
@@ -461,6 +556,11 @@ def main():
             g4 = gold.get("config4", {}).get("shard_summary_crc32", [])
             if cfg == 2 and not sha and nrec == (1 << 26) and world <= len(g4):
                 res["summary_matches_oracle"] = allsum == g4[:world]
+            # config 3's global-stream shards (make_summaries.py config3_shards; a
+            # reduced shard of 2^20 records per rank: config3_shards_small)
+            g3 = gold.get(CONFIG3_SHARDS.get(nrec, ""), {}).get("shard_summary_crc32", [])
+            if cfg == 3 and not sha and not a.wal_framed and a.pack_align <= 1 and world <= len(g3):
+                res["summary_matches_oracle"] = allsum == g3[:world]
         elif not a.blocks_per_gpu and a.pack_align <= 1:
             # against the oracle's full-size value (default layouts only)
             g = gold.get(f"config{cfg}" + ("w" if a.wal_framed and cfg == 3 else ""), {}).get(
@@ -583,6 +683,15 @@ def main():
             "frac_of_ceiling": round(achieved_gbs / ceil_gbs, 4),
             "how": "same kernel with crc_ablate 3: payload loads only (no checksum, no store), same buffer",
         }
+
+    # BASELINE config 4 beside the config-3 line: the per-GPU fixed-block shard
+    # (its own 1 -> N curve from the same runs), after config 3's buffers go
+    if cfg == 3 and not sha and not a.no_config4:
+        data.free()
+        out.free()
+        for b in (d_off, d_len):
+            b.free()
+        res["config4"] = config4_sub(a, ctx, stream, sptr, world, rank)
 
     if rank == 0:
         print(json.dumps(res), flush=True)

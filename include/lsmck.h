@@ -162,9 +162,10 @@ int lsmck_device_count(void);
  *                 declines gets no CRCs).
  *   "crc_ablate"  DIAGNOSTIC ONLY, results are invalid while set: 3 = payload
  *                 loads only (ring, stream and walking kernels: the bench's
- *                 loads-only ceiling), 2 = the stream kernel without payload
- *                 loads; 4..10 = stream kernel ablations (DESIGN.md 3.1
- *                 items 10-11); 0 = off.
+ *                 loads-only ceiling); 0 = off.  2 (the stream kernel without
+ *                 payload loads) and 4..10 (stream kernel ablations,
+ *                 DESIGN.md 3.1 items 10-11) only in A/B builds
+ *                 (-DLSMCK_AB_ABLATIONS, tools/build_ab.sh).
  *   "sha_order"   variable-length SHA-256 batches of >= 2048 messages run in
  *                 decreasing length order (1, default) or batch order (0).
  *                 A/B switch; digests are identical either way.
@@ -401,6 +402,10 @@ int lsmck_stream_sync(lsmck_ctx* ctx, void* stream);
 int lsmck_gen_stream(lsmck_ctx* ctx, uint8_t* dst_dev, uint64_t seed, uint64_t byte_off, size_t n, void* stream);
 /* Zipf(s) lengths on k=1..kmax, L = max(lmin, 64k - j), j ~ U{0..63} (host). */
 void lsmck_gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, size_t n, uint32_t* out);
+/* records [first, first + n) of the same stream (record r's length depends on
+ * (seed, r) alone): one rank's share of a global config-3 stream */
+void lsmck_gen_zipf_lengths_at(uint64_t seed, double s, int kmax, uint32_t lmin, uint64_t first, size_t n,
+                               uint32_t* out);
 
 #ifdef __cplusplus
 }

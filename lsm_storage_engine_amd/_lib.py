@@ -119,6 +119,7 @@ SIGNATURES = [
     ("lsmck_stream_sync", C.c_int, [vp, vp]),
     ("lsmck_gen_stream", C.c_int, [vp, vp, C.c_uint64, C.c_uint64, sz, vp]),
     ("lsmck_gen_zipf_lengths", None, [C.c_uint64, C.c_double, C.c_int, C.c_uint32, sz, vp]),
+    ("lsmck_gen_zipf_lengths_at", None, [C.c_uint64, C.c_double, C.c_int, C.c_uint32, C.c_uint64, sz, vp]),
 ]
 
 _lib = None

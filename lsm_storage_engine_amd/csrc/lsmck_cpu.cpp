@@ -445,7 +445,12 @@ size_t lsmck_wal_encode_remove(const uint8_t* key, uint32_t klen, uint8_t* out) 
 }
 
 void lsmck_gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, size_t n, uint32_t* out) {
-  lsmck_host::gen_zipf_lengths(seed, s, kmax, lmin, n, out);
+  lsmck_host::gen_zipf_lengths(seed, s, kmax, lmin, 0, n, out);
+}
+
+void lsmck_gen_zipf_lengths_at(uint64_t seed, double s, int kmax, uint32_t lmin, uint64_t first, size_t n,
+                               uint32_t* out) {
+  lsmck_host::gen_zipf_lengths(seed, s, kmax, lmin, first, n, out);
 }
 
 }  // extern "C"

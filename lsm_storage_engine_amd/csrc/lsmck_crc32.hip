@@ -1562,6 +1562,15 @@ extern "C" int lsmk_launch_crc32_fixed(const CrcParams* P, int ncu, int variant,
 
 extern "C" uint32_t lsmk_stream_waves(int ncu) { return (uint32_t)ncu * 16u; }
 
+// whether this library carries the stream kernel's diagnostic ablations (crc_ablate 2, 4..10)
+extern "C" int lsmk_ab_ablations() {
+#ifdef LSMCK_AB_ABLATIONS
+  return 1;
+#else
+  return 0;
+#endif
+}
+
 // stream kernel: eligibility flag (trusted: the library's own batch, sorted
 // with its gaps inside one buffer, so no check), per-wave cuts, the kernel.
 // The walking kernel launched after it on the same stream exits when the flag
@@ -1581,6 +1590,9 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   }
   hipLaunchKernelGGL(stream_cuts, dim3((W + 1u + 255u) / 256u), dim3(256), 0, st, *P, W);
   const int ablate = (variant >> 8) & 0xF;
+#ifdef LSMCK_AB_ABLATIONS
+  // the stream kernel's diagnostic ablations: only in the
+  // A/B libraries tools/build_ab.sh builds with EXTRA=-DLSMCK_AB_ABLATIONS
   const void* fn = ablate == 9 ? (const void*)crc32_stream_kernel<9>
                  : ablate == 10 ? (const void*)crc32_stream_kernel<10>
                  : ablate == 4 ? (const void*)crc32_stream_kernel<4>
@@ -1590,6 +1602,11 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
                  : ablate == 8 ? (const void*)crc32_stream_kernel<8>
                  : ablate == 3 ? (const void*)crc32_stream_kernel<3>
                  : ablate == 2 ? (const void*)crc32_stream_kernel<2> : (const void*)crc32_stream_kernel<0>;
+#else
+  // the product library: the kernel and its loads-only twin (the bench's
+  // loads_only_ceiling); lsmck_ctx_set_option refuses the other ablations
+  const void* fn = ablate == 3 ? (const void*)crc32_stream_kernel<3> : (const void*)crc32_stream_kernel<0>;
+#endif
   const size_t lds = LDS_SCRATCH_OFF + LDS_SMAP_BYTES;
   e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return -(int)e;

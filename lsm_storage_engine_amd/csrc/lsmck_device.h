@@ -75,6 +75,7 @@ int lsmk_launch_crc32_walk(const lsmck::CrcParams* P, uint64_t* sb_prefix, int n
 // a caller's batch is checked on the device unless `trusted`: P->sflag;
 // P->scuts holds lsmk_stream_waves(ncu) + 1 entries)
 uint32_t lsmk_stream_waves(int ncu);
+int lsmk_ab_ablations(void);  // 1: built with -DLSMCK_AB_ABLATIONS (tools/build_ab.sh)
 int lsmk_launch_crc32_stream(const lsmck::CrcParams* P, int ncu, int variant, int trusted, hipStream_t st);
 uint64_t lsmk_wal_words(uint64_t n);
 uint64_t lsmk_wal_scan_blocks(uint64_t n);

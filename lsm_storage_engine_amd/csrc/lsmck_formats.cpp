@@ -235,7 +235,7 @@ static uint64_t splitmix64(uint64_t x) {
   return z ^ (z >> 31);
 }
 
-void gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, size_t n, uint32_t* out) {
+void gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, uint64_t first, size_t n, uint32_t* out) {
   std::vector<double> cdf((size_t)kmax);
   double tot = 0.0;
   for (int k = 1; k <= kmax; ++k) tot += pow((double)k, -s);
@@ -245,9 +245,10 @@ void gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, size_t n
     cdf[(size_t)k - 1] = acc / tot;
   }
   cdf[(size_t)kmax - 1] = 1.0;
-  for (size_t r = 0; r < n; ++r) {
-    uint64_t u1 = splitmix64(seed ^ (2 * (uint64_t)r));
-    uint64_t u2 = splitmix64(seed ^ (2 * (uint64_t)r + 1));
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t r = first + i;  // counter-based: record r's length depends on (seed, r) alone
+    uint64_t u1 = splitmix64(seed ^ (2 * r));
+    uint64_t u2 = splitmix64(seed ^ (2 * r + 1));
     double u = (double)(u1 >> 11) * 0x1.0p-53;
     int lo = 0, hi = kmax - 1;
     while (lo < hi) {
@@ -256,7 +257,7 @@ void gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, size_t n
       else lo = mid + 1;
     }
     int64_t L = 64 * (int64_t)(lo + 1) - (int64_t)(u2 & 63);
-    out[r] = L < (int64_t)lmin ? lmin : (uint32_t)L;
+    out[i] = L < (int64_t)lmin ? lmin : (uint32_t)L;
   }
 }
 

@@ -29,6 +29,6 @@ struct TableMeta {
 int read_metadata_json(const char* path, TableMeta* m);
 std::string path_push(const std::string& a, const std::string& b);
 
-void gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, size_t n, uint32_t* out);
+void gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, uint64_t first, size_t n, uint32_t* out);
 }  // namespace lsmck_host
 #endif

@@ -37,13 +37,28 @@
 // command with a missing argument makes the reference's connection task panic
 // (command.rs:27 indexes args[1]); here the connection is closed.  At EOF the
 // reference's read_line loop spins on Ok(0) (server.rs:20); here the
-// connection is closed.  Compaction (db.rs:188-232) is not run: it is not on
-// the checksum path.
+// connection is closed.
+//
+// The compaction tick (server.rs:93-99: tokio interval of 10 s, its first
+// tick at once) runs Db::compact (tokio/db.rs:191-228), whose checksum work
+// is the re-verify: every table of levels 0..3 it keeps is cloned, and
+// SsTable's Clone is SsTable::load (tokio/sstable.rs:274-277), which runs
+// Checksums::verify (checksums.rs:40-62) on it.  Here each tick verifies
+// those tables in one GPU batch (lsmck_checksums_verify_many) while the
+// server serves.  The merge of a level at sstable_level_limit tables is not
+// run (compaction proper is not on the checksum path): such a level keeps its
+// tables and they are re-verified like the clones; the reference's quirk of
+// dropping level 4 from the new levels (db.rs:221-222) is not reproduced.  A
+// table that fails the verify panics the tick as the reference's does (its
+// message, then "Compact failed"): ticks stop, serving goes on (a panicked
+// tokio task does not end the process).
 //
 // Usage: lsmck_server [--base DIR] [--port P] [--bind ADDR] [--device D]
-//                     [--memtable-limit BYTES] [--exit-after-load]
-// Prints one JSON line when loaded ({"event":"loaded",...}) and one when it
-// listens ({"event":"listening","port":P}).
+//                     [--memtable-limit BYTES] [--compact-interval MS]
+//                     [--exit-after-load]
+// Prints one JSON line when loaded ({"event":"loaded",...}), one when it
+// listens ({"event":"listening","port":P}), and one per compaction tick
+// ({"event":"compact",...}; {"event":"compact_failed",...}).
 #include <arpa/inet.h>
 #include <dirent.h>
 #include <errno.h>
@@ -62,6 +77,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -225,7 +241,7 @@ struct MemTable {
 struct SsTable {
   uint64_t id = 0;
   int level = 0;
-  std::string data_path;
+  std::string data_path, index_path, checksum_path;
   std::map<std::string, uint64_t> index;
   uint64_t size = 0;
   mutable std::once_flag last_once;
@@ -358,7 +374,30 @@ struct Config {
   std::string bind = "127.0.0.1";
   int device = 0;
   bool exit_after_load = false;
+  long compact_interval_ms = 10000;  // server.rs:94 (0: no tick)
 };
+
+// the name a panic of Checksums::verify (checksums.rs:49-60) gives: the
+// metadata's data_filename / index_filename (the file name in the table's
+// level directory)
+std::string base_name(const std::string& p) {
+  const size_t s = p.rfind('/');
+  return s == std::string::npos ? p : p.substr(s + 1);
+}
+
+// the reference's panic message for a table whose verify returned `status`
+// (lsmck_checksums_verify_many), or "" for an io::Error (the caller's
+// expect() names it)
+std::string verify_panic(int status, const std::string& data_path, const std::string& index_path) {
+  switch (status) {
+    case LSMCK_DATA_MISMATCH: return "Can't load SSTable from " + base_name(data_path) + ". Checksum is not correct";
+    case LSMCK_INDEX_MISMATCH: return "Can't load SSTable from " + base_name(index_path) + ". Checksum is not correct";
+    case LSMCK_PANIC_OPEN_FILE:
+    case LSMCK_PANIC_OPEN_INDEX: return "Can't open file to calculate checksum";
+    case LSMCK_PANIC_OPEN_CHECKSUM: return "Can't open checksum file";
+    default: return "";
+  }
+}
 
 // ---------------------------------------------------------------------------
 struct Db {
@@ -393,13 +432,13 @@ struct Db {
     double t_index = 0;
     struct Listed {
       Db* db;
-      std::vector<std::string> data, index;
+      std::vector<std::string> data, index, checksum;
       std::vector<uint64_t> id;
       std::vector<int> level;
       std::thread th;
       int* err;
       double* secs;
-    } L{this, {}, {}, {}, {}, {}, &idx_err, &t_index};
+    } L{this, {}, {}, {}, {}, {}, {}, &idx_err, &t_index};
     auto on_listed = [](void* user, const lsmck_table_entry* e, size_t n) {
       Listed& L = *(Listed*)user;
       const double t_idx0 = now_s();
@@ -407,6 +446,7 @@ struct Db {
         if (e[i].status) continue;  // a bad metadata file: the verify reports it (the reference panics)
         L.data.emplace_back(e[i].data_path);
         L.index.emplace_back(e[i].index_path);
+        L.checksum.emplace_back(e[i].checksum_path);
         L.id.push_back(strtoull(e[i].id, nullptr, 10));
         L.level.push_back((int)e[i].level);
       }
@@ -421,6 +461,8 @@ struct Db {
             t->id = L.id[i];
             t->level = L.level[i];
             t->data_path = L.data[i];
+            t->index_path = L.index[i];
+            t->checksum_path = L.checksum[i];
             struct stat st;
             if (stat(t->data_path.c_str(), &st) == 0) t->size = (uint64_t)st.st_size;
             if (!t->load_index(L.index[i])) bad = true;
@@ -610,7 +652,7 @@ struct Db {
           std::string j, fn;
           read_file(rep.first_metadata_path, &j);
           json_field(j, rep.first_status == LSMCK_DATA_MISMATCH ? "data_filename" : "index_filename", &fn);
-          panic_exit("Can't load SSTable from " + fn + ". Checksum is not correct");
+          panic_exit(verify_panic(rep.first_status, fn, fn));
         }
         case LSMCK_PANIC_OPEN_FILE:
         case LSMCK_PANIC_OPEN_INDEX: panic_exit("Can't open file to calculate checksum");
@@ -739,6 +781,69 @@ struct Db {
     return found && !(v->size() == 1 && (*v)[0] == '\0');
   }
 
+  // One compaction tick's checksum work (Db::compact, tokio/db.rs:191-228):
+  // the tables of levels 0..3, each verified as its clone's SsTable::load
+  // would (tokio/sstable.rs:274-277 -> checksums.rs:40-62), in one GPU batch.
+  // Returns false when one fails: the reference's panic is printed and the
+  // tick task is over.
+  bool compact_tick(uint64_t tick) {
+    std::vector<std::shared_ptr<SsTable>> tabs;
+    {
+      std::shared_lock<std::shared_mutex> lk(lv_mu);
+      for (int lv = 0; lv < kMaxLevel - 1; ++lv) tabs.insert(tabs.end(), levels[lv].begin(), levels[lv].end());
+    }
+    const size_t n = tabs.size();
+    std::vector<const char*> d(n), ix(n), c(n);
+    uint64_t bytes = 0;
+    for (size_t i = 0; i < n; ++i) {
+      d[i] = tabs[i]->data_path.c_str();
+      ix[i] = tabs[i]->index_path.c_str();
+      c[i] = tabs[i]->checksum_path.c_str();
+      struct stat st;
+      if (stat(d[i], &st) == 0) bytes += (uint64_t)st.st_size;
+      if (stat(ix[i], &st) == 0) bytes += (uint64_t)st.st_size;
+    }
+    std::vector<int> status(std::max<size_t>(n, 1), 0);
+    const double t0 = now_s();
+    const int rc = n ? lsmck_checksums_verify_many(ctx, d.data(), ix.data(), c.data(), n, status.data()) : 0;
+    const double dt = now_s() - t0;
+    if (rc < 0) {
+      fprintf(stderr, "lsmck_checksums_verify_many: %s\n", lsmck_last_error());
+      return false;
+    }
+    size_t bad = n;
+    for (size_t i = 0; i < n && bad == n; ++i)
+      if (status[i]) bad = i;  // the clone loop's first failing table (level, then id order)
+    if (bad < n) {
+      std::string msg = verify_panic(status[bad], tabs[bad]->data_path, tabs[bad]->index_path);
+      if (msg.empty()) msg = "Can't load sstable file: status " + std::to_string(status[bad]);  // expect() on Err
+      fprintf(stderr, "thread 'tokio-runtime-worker' panicked at '%s'\n", msg.c_str());
+      fprintf(stderr, "thread 'tokio-runtime-worker' panicked at 'Compact failed: JoinError::Panic(...)'\n");
+      fflush(stderr);
+      printf("{\"event\": \"compact_failed\", \"tick\": %llu, \"panic\": %s}\n", (unsigned long long)tick,
+             json_str(msg).c_str());
+      fflush(stdout);
+      return false;
+    }
+    printf("{\"event\": \"compact\", \"tick\": %llu, \"tables\": %zu, \"table_bytes\": %llu, "
+           "\"verify_s\": %.6f, \"GiBps\": %.3f}\n",
+           (unsigned long long)tick, n, (unsigned long long)bytes, dt, dt > 0 ? (double)bytes / dt / 1073741824.0 : 0.0);
+    fflush(stdout);
+    return true;
+  }
+
+  // server.rs:93-99: tokio::time::interval -- the first tick at once, then one
+  // per period (a late tick is not made up twice here: the next waits a period)
+  void compact_loop() {
+    const auto period = std::chrono::milliseconds(cfg.compact_interval_ms);
+    auto next = std::chrono::steady_clock::now();
+    for (uint64_t tick = 0;; ++tick) {
+      std::this_thread::sleep_until(next);
+      if (!compact_tick(tick)) return;
+      next = std::max(next + period, std::chrono::steady_clock::now());
+    }
+  }
+
   // SsTable::from_memtable (tokio/sstable.rs:88-111) + the WAL swap (db.rs:100-121)
   void flush(std::shared_ptr<const MemTable> m) {
     uint64_t id;
@@ -758,6 +863,8 @@ struct Db {
     auto t = std::make_shared<SsTable>();
     t->id = id;
     t->data_path = join(dir, data_fn);
+    t->index_path = join(dir, index_fn);
+    t->checksum_path = join(dir, checksum_fn);
     std::string data, index;
     uint64_t i = 0;
     if (!m->data.empty()) t->set_last(m->data.rbegin()->first);
@@ -983,10 +1090,11 @@ int main(int argc, char** argv) {
     else if (a == "--bind") cfg.bind = val();
     else if (a == "--device") cfg.device = atoi(val());
     else if (a == "--memtable-limit") cfg.memtable_limit = strtoull(val(), nullptr, 10);
+    else if (a == "--compact-interval") cfg.compact_interval_ms = atol(val());
     else if (a == "--exit-after-load") cfg.exit_after_load = true;
     else {
       fprintf(stderr, "usage: %s [--base DIR] [--port P] [--bind ADDR] [--device D] [--memtable-limit B] "
-                      "[--exit-after-load]\n", argv[0]);
+                      "[--compact-interval MS] [--exit-after-load]\n", argv[0]);
       return 2;
     }
   }
@@ -1018,6 +1126,7 @@ int main(int argc, char** argv) {
   getsockname(ls, (struct sockaddr*)&sa, &sl);
   printf("{\"event\": \"listening\", \"port\": %d}\n", ntohs(sa.sin_port));
   fflush(stdout);
+  if (cfg.compact_interval_ms > 0) std::thread(&Db::compact_loop, &db).detach();
   for (;;) {
     int fd = accept4(ls, nullptr, nullptr, SOCK_CLOEXEC);
     if (fd < 0) {

@@ -399,7 +399,8 @@ def device_count():
     return _lib.load().lsmck_device_count()
 
 
-def gen_zipf_lengths(seed, n, s=1.5, kmax=1024, lmin=64):
+def gen_zipf_lengths(seed, n, s=1.5, kmax=1024, lmin=64, first=0):
+    """lengths of records [first, first + n) of the config-3 length stream"""
     out = np.empty(n, dtype=np.uint32)
-    _lib.load().lsmck_gen_zipf_lengths(seed, s, kmax, lmin, n, out.ctypes.data)
+    _lib.load().lsmck_gen_zipf_lengths_at(seed, s, kmax, lmin, first, n, out.ctypes.data)
     return out

@@ -2,7 +2,8 @@
 the loopback server of the reference (src/server.rs; protocol src/command.rs).
 
 ``Server(base, ...)`` starts the binary, waits for its start-up (Db::load: the
-GPU tree verify and WAL replay) and exposes the JSON it reports; ``Client``
+GPU tree verify and WAL replay) and exposes the JSON it reports (later events,
+such as each compaction tick's re-verify, through ``wait_event``); ``Client``
 speaks the newline-terminated protocol: ``insert k v`` / ``update k v`` ->
 "ok", ``delete k`` -> "ok", ``get k`` -> the value or "<k> not found".
 """
@@ -27,13 +28,16 @@ class ServerExited(RuntimeError):
 
 
 class Server:
-    def __init__(self, base, port=0, memtable_limit=4096, device=0, timeout=600, exit_after_load=False):
+    def __init__(self, base, port=0, memtable_limit=4096, device=0, timeout=600, exit_after_load=False,
+                 compact_interval_ms=None):
         if not os.path.exists(BIN):
             raise FileNotFoundError(f"{BIN} is not built (make -C lsm_storage_engine_amd/csrc)")
         cmd = [BIN, "--base", str(base), "--port", str(port), "--memtable-limit", str(memtable_limit),
                "--device", str(device)]
         if exit_after_load:
             cmd.append("--exit-after-load")
+        if compact_interval_ms is not None:  # the server's default is the reference's 10 s tick
+            cmd += ["--compact-interval", str(int(compact_interval_ms))]
         self.proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
         # stderr is drained on its own thread into a bounded tail: an undrained
         # pipe fills at 64 KiB (LSMCK_TREE_TRACE prints a line per round) and
@@ -46,7 +50,7 @@ class Server:
         self.port = None
         # the event lines come through a reader thread (select() on a buffered
         # pipe misses lines already read into the buffer)
-        lines = queue.Queue()
+        self._lines = lines = queue.Queue()
         threading.Thread(target=lambda: [lines.put(x) for x in iter(self.proc.stdout.readline, "")] + [lines.put("")],
                          daemon=True).start()
         deadline = time.time() + timeout
@@ -66,6 +70,21 @@ class Server:
                 self.port = ev["port"]
         if exit_after_load:
             self.proc.wait(timeout=60)
+
+    def wait_event(self, kind, timeout=120):
+        """The next JSON event line of this kind the server prints after start-up
+        (e.g. "compact" / "compact_failed": a compaction tick's re-verify)."""
+        deadline = time.time() + timeout
+        while True:
+            try:
+                line = self._lines.get(timeout=max(0.01, deadline - time.time()))
+            except queue.Empty:
+                raise TimeoutError(f"no {kind!r} event from lsmck_server")
+            if not line:
+                raise ServerExited(self.proc.wait(), self.stderr_tail())
+            ev = json.loads(line)
+            if ev["event"] == kind:
+                return ev
 
     def stderr_tail(self):
         """The last lines the server wrote to stderr (all of them once it has exited)."""

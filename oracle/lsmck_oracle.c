@@ -418,7 +418,11 @@ void oracle_gen_stream(uint64_t seed, uint64_t byte_off, size_t n, uint8_t* out)
   }
 }
 
-void oracle_gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, size_t n, uint32_t* out) {
+/* records [first, first + n) of the counter-based length stream (record r's
+ * length depends on (seed, r) alone: a rank's share of one global stream is
+ * generated without the records before it) */
+void oracle_gen_zipf_lengths_at(uint64_t seed, double s, int kmax, uint32_t lmin, uint64_t first, size_t n,
+                                uint32_t* out) {
   double* cdf = (double*)malloc(sizeof(double) * (size_t)kmax);
   double tot = 0.0;
   for (int k = 1; k <= kmax; ++k) tot += pow((double)k, -s);
@@ -428,9 +432,10 @@ void oracle_gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, s
     cdf[k - 1] = acc / tot;
   }
   cdf[kmax - 1] = 1.0;
-  for (size_t r = 0; r < n; ++r) {
-    uint64_t u1 = oracle_splitmix64(seed ^ (2 * (uint64_t)r));
-    uint64_t u2 = oracle_splitmix64(seed ^ (2 * (uint64_t)r + 1));
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t r = first + i;
+    uint64_t u1 = oracle_splitmix64(seed ^ (2 * r));
+    uint64_t u2 = oracle_splitmix64(seed ^ (2 * r + 1));
     double u = (double)(u1 >> 11) * 0x1.0p-53;
     int lo = 0, hi = kmax - 1;
     while (lo < hi) {
@@ -441,7 +446,11 @@ void oracle_gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, s
         lo = mid + 1;
     }
     int64_t L = 64 * (int64_t)(lo + 1) - (int64_t)(u2 & 63);
-    out[r] = L < (int64_t)lmin ? lmin : (uint32_t)L;
+    out[i] = L < (int64_t)lmin ? lmin : (uint32_t)L;
   }
   free(cdf);
+}
+
+void oracle_gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, size_t n, uint32_t* out) {
+  oracle_gen_zipf_lengths_at(seed, s, kmax, lmin, 0, n, out);
 }

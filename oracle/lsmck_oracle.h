@@ -100,6 +100,8 @@ uint64_t oracle_splitmix64(uint64_t x);
 void oracle_gen_stream(uint64_t seed, uint64_t byte_off, size_t n, uint8_t* out);
 /* Zipf(s) over k in 1..kmax, L = max(lmin, 64k - j), j ~ U{0..63}; SURVEY 8d config 3 */
 void oracle_gen_zipf_lengths(uint64_t seed, double s, int kmax, uint32_t lmin, size_t n, uint32_t* out);
+void oracle_gen_zipf_lengths_at(uint64_t seed, double s, int kmax, uint32_t lmin, uint64_t first, size_t n,
+                                uint32_t* out);
 
 #ifdef __cplusplus
 }

@@ -52,6 +52,7 @@ def lib():
         L.oracle_splitmix64.argtypes = [C.c_uint64]
         L.oracle_gen_stream.argtypes = [C.c_uint64, C.c_uint64, sz, vp]
         L.oracle_gen_zipf_lengths.argtypes = [C.c_uint64, C.c_double, C.c_int, C.c_uint32, sz, vp]
+        L.oracle_gen_zipf_lengths_at.argtypes = [C.c_uint64, C.c_double, C.c_int, C.c_uint32, C.c_uint64, sz, vp]
         _lib = L
     return _lib
 
@@ -150,7 +151,8 @@ def gen_stream(seed, byte_off, n):
     return out
 
 
-def gen_zipf_lengths(seed, n, s=1.5, kmax=1024, lmin=64):
+def gen_zipf_lengths(seed, n, s=1.5, kmax=1024, lmin=64, first=0):
+    """lengths of records [first, first + n) of the config-3 length stream"""
     out = np.empty(n, dtype=np.uint32)
-    lib().oracle_gen_zipf_lengths(seed, s, kmax, lmin, n, out.ctypes.data)
+    lib().oracle_gen_zipf_lengths_at(seed, s, kmax, lmin, first, n, out.ctypes.data)
     return out

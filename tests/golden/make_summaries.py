@@ -21,9 +21,16 @@ with these values; bench.py prints the GPU's as "summary_crc32".
             same seed over the whole image, CRC-32 only (bench.py --wal-framed)
   config 4: 8 per-GPU shards of 2^26 x 4096 B (256 GiB each) of config 2's
             block stream (seed 0x5EED0002): shard r = blocks [r*2^26, (r+1)*2^26),
-            CRC-32 only (bench.py --gpus N: rank r checksums shard r)
+            CRC-32 only (bench.py's config4 sub-measurement: rank r checksums shard r)
+  config3_shards: 8 per-GPU shards of ONE global config-3 stream: shard r =
+            records [r*2^26, (r+1)*2^26) (lengths from the counter-based
+            generator at record r*2^26), packed, its bytes at the global
+            offset where shard r-1 ends (bench.py --gpus N: rank r); shard 0
+            is config 3 itself.  config3_shards_small: the same with 2^20
+            records per shard (the shared-GPU rehearsal in test_gpu_bench.py)
 
-Run:  python3 tests/golden/make_summaries.py [crc|sha|all|config4|config3w]   (updates summaries.json here)
+Run:  python3 tests/golden/make_summaries.py [crc|sha|all|config4|config3w|config3_shards|config3_shards_small]
+      (updates summaries.json here)
 """
 import concurrent.futures as cf
 import json
@@ -108,6 +115,31 @@ def main():
         with open(OUT, "w") as f:
             json.dump(res, f, indent=1)
             f.write("\n")
+        return
+    if what in ("config3_shards", "config3_shards_small"):
+        n = 1 << (26 if what == "config3_shards" else 20)
+        e = res.setdefault(what, {})
+        e.update({"records_per_shard": n, "seed": hex(0x5EED0003),
+                  "layout": "shard r = records [r*n, (r+1)*n) of one global packed config-3 stream, "
+                            "bytes at the stream offset where shard r-1 ends"})
+        shards = e.setdefault("shard_summary_crc32", [])
+        e.setdefault("shard_bytes", [])
+        byte_off = sum(e["shard_bytes"])
+        for r in range(len(shards), 8):
+            lens = O.gen_zipf_lengths(0x5EED0003, n, first=r * n)
+            offs = np.zeros(n, dtype=np.uint64)
+            np.cumsum(lens[:-1].astype(np.uint64), out=offs[1:])
+            nbytes = int(offs[-1]) + int(lens[-1])
+            if r == 0 and n == (1 << 26) and res.get("config3", {}).get("summary_crc32"):
+                shards.append(res["config3"]["summary_crc32"])  # shard 0 is config 3 itself
+            else:
+                shards.append(summary(0x5EED0003, offs, lens, False, byte_off=byte_off))
+            e["shard_bytes"].append(nbytes)
+            byte_off += nbytes
+            print(what, r, shards[-1], nbytes, round(time.time() - t0, 1), flush=True)
+            with open(OUT, "w") as f:
+                json.dump(res, f, indent=1)
+                f.write("\n")
         return
     if what == "config4":
         n, L = 1 << 26, 4096

@@ -65,6 +65,49 @@ def test_two_rank_record_sharding():
     assert cuts[0] == 0 and cuts[-1] == 4000
 
 
+def _config3_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from oracle import oracle as O
+
+    def gather(x):
+        xs = [None] * world
+        dist.all_gather_object(xs, x)
+        return xs
+    n = 3000
+    offs, lens, nbytes, byte_off = bench.config3_shard(O.gen_zipf_lengths, 0x5EED0003, n, rank, gather)
+    mine = O.crc32_batch(O.gen_stream(0x5EED0003, byte_off, nbytes), offs, lens)
+    parts = gather(mine.tolist())
+    if rank == 0:
+        # the one global stream of world * n records, packed
+        L = O.gen_zipf_lengths(0x5EED0003, world * n)
+        off = np.zeros(len(L), dtype=np.uint64)
+        off[1:] = np.cumsum(L[:-1].astype(np.uint64))
+        full = O.crc32_batch(O.gen_stream(0x5EED0003, 0, int(off[-1] + L[-1])), off, L)
+        q.put(bool(np.array_equal(np.concatenate([np.asarray(p, dtype=np.uint32) for p in parts]), full)))
+    dist.destroy_process_group()
+
+
+def test_config3_global_stream_shards():
+    """bench.py's N-rank config 3: rank r's shard (records [r*n, (r+1)*n),
+    bytes at the offset the lower ranks' sizes give) is exactly its slice of
+    the one global stream -- the ranks' outputs concatenated are the
+    one-process output of the whole stream."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_config3_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    ok = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert ok
+
+
 def test_shard_helpers():
     assert [shard_fixed(10, 3, r) for r in range(3)] == [(0, 4), (4, 7), (7, 10)]
     lens = np.array([100, 1, 1, 1, 100, 1, 1, 100], dtype=np.uint32)

@@ -244,3 +244,39 @@ def test_start_merges_a_rotated_log(tmp_path):
             assert c.call(b"get", k) == v, k
     finally:
         srv.kill()
+
+
+def test_compaction_tick_reverifies_and_panics_like_the_reference(tmp_path):
+    """The compaction tick (server.rs:93-99 -> Db::compact, tokio/db.rs:191-228):
+    its first tick comes at once, then one per interval, each re-verifying the
+    tables of levels 0..3 (SsTable::clone = SsTable::load -> Checksums::verify,
+    tokio/sstable.rs:274-277) in one GPU batch while the server serves.  A
+    level-1 data file corrupted after start-up makes the next tick panic with
+    checksums.rs:49-53's message naming that file; the tick task is over but
+    the server still answers."""
+    base = str(tmp_path / "db")
+    tree.synthesize_tree(base, 2 << 20, wal_records=200)
+    metas = tree.list_tables(base)
+    low = [m for m in metas if m.level < 4]
+    srv = Server(base, compact_interval_ms=300)
+    try:
+        ev = srv.wait_event("compact")
+        assert ev["tick"] == 0 and ev["tables"] == len(low)
+        assert ev["table_bytes"] == sum(os.path.getsize(m.data_path()) + os.path.getsize(m.index_path()) for m in low)
+        c = srv.client()
+        assert c.call(b"insert", b"alpha", b"one") == b"ok"  # traffic while the ticks run
+        ev = srv.wait_event("compact")
+        assert ev["tick"] >= 1 and ev["tables"] == len(low)
+        m = next(m for m in low if m.level == 1)
+        with open(m.data_path(), "r+b") as f:
+            f.seek(7)
+            b = f.read(1)
+            f.seek(7)
+            f.write(bytes([b[0] ^ 0x04]))
+        ev = srv.wait_event("compact_failed")
+        assert ev["panic"] == f"Can't load SSTable from {os.path.basename(m.data_path())}. Checksum is not correct"
+        assert "Compact failed" in srv.stderr_tail()
+        assert c.call(b"get", b"alpha") == b"one"  # still serving
+        c.close()
+    finally:
+        srv.kill()

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Build liblsmck.so of a commit (or of the work tree: "WT") into
-# lsm_storage_engine_amd/ab/<name>.so for same-box A/B runs (tools/gpu_ab_libs.sh).
+# lsm_storage_engine_amd/ab/<name>.so for same-box A/B runs (tools/gpu_ab_libs.sh),
+# with the stream kernel's diagnostic ablations (crc_ablate 2, 4..10) compiled in.
 #   [EXTRA=-DFLAG] tools/build_ab.sh <name> <commit|WT>
 set -e
 NAME=$1; REV=$2
@@ -14,5 +15,5 @@ else
   git -C $ROOT archive $REV include lsm_storage_engine_amd/csrc | tar -x -C $D
 fi
 mkdir -p $ROOT/lsm_storage_engine_amd/ab
-make -s -j8 -C $D/lsm_storage_engine_amd/csrc EXTRA="$EXTRA" OUT=$ROOT/lsm_storage_engine_amd/ab/$NAME.so $ROOT/lsm_storage_engine_amd/ab/$NAME.so 2>&1 | grep -v hip-link || true
+make -s -j8 -C $D/lsm_storage_engine_amd/csrc EXTRA="-DLSMCK_AB_ABLATIONS $EXTRA" OUT=$ROOT/lsm_storage_engine_amd/ab/$NAME.so $ROOT/lsm_storage_engine_amd/ab/$NAME.so 2>&1 | grep -v hip-link || true
 ls -la $ROOT/lsm_storage_engine_amd/ab/$NAME.so
