@@ -264,10 +264,14 @@ int lsmck_sha256_batch_fixed(lsmck_ctx* ctx, const uint8_t* base, size_t stride,
 /* WAL replay verify: the batch form of the CommandLog iterator + MemTable::from_log
  * (src/wal.rs:68-84,122-163; src/memtable.rs:28-47) over an in-memory WAL image.
  * Each record's length lives in its own header, so the walk is a dependent
- * chain.  On the GPU (lsmck_wal.hip) it is a speculative parallel parse: every
- * byte that could start a header is a candidate, candidate -> successor links
- * are followed by pointer doubling from offset 0, and the accepted chain's
- * payload CRCs are checked in one batch with the GPU compare.  A device image
+ * chain.  On the GPU (lsmck_wal.hip) it is a speculative parallel parse: the
+ * segment walk (lsmck_segwalk.h: one thread per segment of the log guesses
+ * the segment's first record and walks the headers to the next segment; the
+ * guesses are checked against each other and wrong ones repaired), or, when
+ * its check keeps failing, candidate doubling (every byte that could start a
+ * header is a candidate, candidate -> successor links followed by pointer
+ * doubling from offset 0); the accepted chain's payload CRCs are checked in
+ * one batch with the GPU compare.  A device image
  * never leaves the device; a host image of at least "wal_upload_min" bytes
  * (default 1 MiB) is uploaded whole and walked there; smaller host images
  * (and "wal_upload_min" 0) take the serial host walk with the CRC batches on
@@ -280,7 +284,11 @@ int lsmck_sha256_batch_fixed(lsmck_ctx* ctx, const uint8_t* base, size_t stride,
  *   LSMCK_WAL_REMOVE_PANIC first bad record is a Remove: the reference panics (wal.rs:154-159)
  *   LSMCK_WAL_BAD_TYPE     InvalidCommandType(*bad_crc) at record *bad_index (wal.rs:36)
  * *nrec = records accepted before the stop.  flags: LSMCK_HOST (optionally
- * | LSMCK_HOST_PINNED) or LSMCK_DEVICE for `wal`.  Synchronous. */
+ * | LSMCK_HOST_PINNED) or LSMCK_DEVICE for `wal`, optionally
+ * | LSMCK_RECS_PINNED: `recs` is page-locked (lsmck_host_alloc_pinned), and
+ * the records are DMA'd into it straight from the device (no staging copy).
+ * Synchronous. */
+#define LSMCK_RECS_PINNED 0x8u
 #define LSMCK_WAL_CORRUPTED 1
 #define LSMCK_WAL_REMOVE_PANIC 2
 #define LSMCK_WAL_BAD_TYPE 3

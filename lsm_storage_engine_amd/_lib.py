@@ -38,6 +38,7 @@ DEVICE = 0x1
 HOST = 0x0
 HOST_PINNED = 0x2
 SORTED = 0x4  # LSMCK_SORTED: device descriptors sorted inside one readable span (include/lsmck.h)
+RECS_PINNED = 0x8  # LSMCK_RECS_PINNED: lsmck_wal_replay_verify's records array is page-locked
 
 u8p = C.POINTER(C.c_uint8)
 u32p = C.POINTER(C.c_uint32)

@@ -250,6 +250,7 @@ struct lsmck_ctx {
     unsigned long long* sinfo = nullptr;
     unsigned long long* h_sinfo = nullptr;
   } wd;
+  bool wal_recs_direct = false;  // this replay's records go by DMA into the caller's pinned array (under wal_mu)
   int wal_seg = 1;           // device WAL walk: 1 = the segment walk first (default), 0 = candidate doubling only
   uint64_t wal_seg_bytes = 0;  // segment walk: bytes per segment (0 = auto, ~2^19 segments)
   int wal_seg_rounds = 16;   // segment walk: repairs before it declines to the candidate-doubling walk
@@ -1200,7 +1201,23 @@ static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t ter
   if (m) {
     std::function<int()> copy_out;
     const size_t todo = m - done;
-    if (recs && cap && todo) {
+    const size_t ntake = std::min(m, cap) > done ? std::min(m, cap) - done : 0;  // records for the caller's array
+    if (recs && cap && todo && ctx->wal_recs_direct) {
+      // the caller's array is pinned: the records go there by DMA, on the
+      // staging stream, beside the CRC pass and the compare
+      if ((rc = stage_init(ctx->stage[0]))) return rc;
+      if (!ctx->wal_emit_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_emit_ev, hipEventDisableTiming));
+      if (!ctx->wal_recs_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_recs_ev, hipEventDisableTiming));
+      hipStream_t s2 = ctx->stage[0].s;
+      if (!emit_recorded) HIPCHK(hipEventRecord(ctx->wal_emit_ev, st));
+      HIPCHK(hipStreamWaitEvent(s2, ctx->wal_emit_ev, 0));
+      if (ntake) HIPCHK(hipMemcpyAsync(recs + done, W.recs + done, ntake * sizeof(lsmck_wal_rec), hipMemcpyDeviceToHost, s2));
+      HIPCHK(hipEventRecord(ctx->wal_recs_ev, s2));
+      copy_out = [&]() -> int {
+        HIPCHK(hipEventSynchronize(ctx->wal_recs_ev));
+        return 0;
+      };
+    } else if (recs && cap && todo) {
       if ((rc = ensure_pinned(&ctx->h_wrecs, &ctx->cap_hwrecs, todo)) || (rc = stage_init(ctx->stage[0]))) return rc;
       if (!ctx->wal_emit_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_emit_ev, hipEventDisableTiming));
       if (!ctx->wal_recs_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_recs_ev, hipEventDisableTiming));
@@ -1243,7 +1260,9 @@ static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t ter
     uint32_t got = 0;
     if (recs && cap && first < done)
       r = ctx->h_wrecs1[first];
-    else if (recs && cap && m > done)
+    else if (recs && cap && ctx->wal_recs_direct && first < std::min(m, cap))
+      r = recs[first];
+    else if (recs && cap && m > done && !ctx->wal_recs_direct)
       r = ctx->h_wrecs[first - done];
     else
       HIPCHK(hipMemcpy(&r, W.recs + first, sizeof r, hipMemcpyDeviceToHost));
@@ -1665,8 +1684,17 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
                             size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
+  // LSMCK_RECS_PINNED: the records go by DMA into the caller's pinned array
+  // (the flag is read by wal_finish under wal_mu; the host walk ignores it)
+  struct RecsDirect {  // set while wal_mu is held, cleared on every return
+    bool& f;
+    RecsDirect(bool& f_, bool v) : f(f_) { f = v; }
+    ~RecsDirect() { f = false; }
+  };
+  const bool recs_pinned = (flags & LSMCK_RECS_PINNED) != 0;
   if ((flags & LSMCK_DEVICE) && ctx->wal_gpu_walk) {
     std::lock_guard<std::mutex> wl(ctx->wal_mu);  // the walk's bitmap (ctx->wd) is shared with the upload path
+    RecsDirect rd(ctx->wal_recs_direct, recs_pinned);
     rc = wal_replay_device(ctx, wal, n, recs, cap, nrec, bad_index, bad_crc, bad_expected);
     if (rc != kWalHostWalk) return rc;
     // (the GPU walk declined: the image is copied back and walked on the host below)
@@ -1675,6 +1703,7 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
     // header walk, instead of the serial host walk (~12 GiB/s) -- the records
     // and offsets are the same, they index the caller's image
     std::lock_guard<std::mutex> wl(ctx->wal_mu);
+    RecsDirect rd(ctx->wal_recs_direct, recs_pinned);
     const bool pinned = (flags & LSMCK_HOST_PINNED) != 0;
     rc = ctx->wal_split ? wal_replay_split(ctx, wal, n, pinned, recs, cap, nrec, bad_index, bad_crc, bad_expected)
                         : kWalNoSplit;

@@ -82,6 +82,16 @@ class PinnedBuffer:
             pass
 
 
+class _PinnedRecords:
+    """numpy's view of a PinnedBuffer as lsmck_wal_rec[n]: the arrays made
+    from it keep it (and the page-locked memory) alive."""
+
+    def __init__(self, pb, n):
+        self.pb = pb
+        self.__array_interface__ = {"data": (pb.ptr, False), "shape": (n,), "descr": WAL_REC_DTYPE.descr,
+                                    "version": 3}
+
+
 class Context:
     def __init__(self, device=0):
         lib = _lib.load()
@@ -91,6 +101,7 @@ class Context:
             raise RuntimeError(f"lsmck_ctx_create({device}) failed: {_lib.last_error()}")
         self.device = device
         self._wal_recs = None  # records array of the last WAL replay, reused once nothing refers to it
+        self._wal_pinned = None  # page-locked records array of pinned_recs replays (reused like _wal_recs)
 
     def _wal_recs_buffer(self, cap):
         """An uninitialised WAL_REC_DTYPE array of at least cap entries: the
@@ -107,7 +118,20 @@ class Context:
         self._wal_recs = buf
         return buf
 
+    def _wal_recs_pinned(self, cap):
+        """A page-locked WAL_REC_DTYPE array of at least cap entries (grow-only,
+        reused once no result refers to it): the replay DMAs the records into it
+        (LSMCK_RECS_PINNED).  The array's base is a holder of its PinnedBuffer,
+        so the pinned memory lives as long as any view of it."""
+        arr = self._wal_pinned
+        if arr is not None and len(arr) >= cap and sys.getrefcount(arr) <= 3:
+            return arr
+        arr = np.asarray(_PinnedRecords(PinnedBuffer(self, max(1, cap) * WAL_REC_DTYPE.itemsize), max(1, cap)))
+        self._wal_pinned = arr
+        return arr
+
     def close(self):
+        self._wal_pinned = None
         if self.handle:
             self.lib.lsmck_ctx_destroy(self.handle)
             self.handle = None
@@ -232,11 +256,13 @@ class Context:
         _lib.check(self.lib.lsmck_wal_frame_insert_device(self.handle, img_ptr, off_ptr, len_ptr, crc_ptr, n, kmax,
                                                            stream), "wal_frame_insert_device")
 
-    def wal_replay_verify(self, image, device_ptr=None, cap=None):
+    def wal_replay_verify(self, image, device_ptr=None, cap=None, pinned_recs=False):
         """Returns (records, status, (bad_index, bad_crc, bad_expected)).
         cap: records to return at most (default: the n/9 + 1 a log of n
         bytes can hold; a very large log whose record count is known can ask
-        for fewer -- the status and the count cover the whole log)."""
+        for fewer -- the status and the count cover the whole log).
+        pinned_recs: the records land in a page-locked array by DMA
+        (LSMCK_RECS_PINNED; cap entries stay pinned for the context's life)."""
         if device_ptr is None:
             # any buffer (bytes, bytearray, memoryview, a read-only mmap of the
             # log file) is read in place: no copy of the image
@@ -245,7 +271,11 @@ class Context:
         else:
             ptr, n, flags = device_ptr, image, _lib.DEVICE
         cap = n // 9 + 1 if cap is None else cap  # a record is at least 9 bytes (Remove of an empty key)
-        recs = self._wal_recs_buffer(cap)
+        if pinned_recs:
+            recs = self._wal_recs_pinned(cap)
+            flags |= _lib.RECS_PINNED
+        else:
+            recs = self._wal_recs_buffer(cap)
         nrec = C.c_size_t()
         bi, bc, be = C.c_uint64(), C.c_uint32(), C.c_uint32()
         rc = _lib.check(self.lib.lsmck_wal_replay_verify(self.handle, ptr, n, flags, recs.ctypes.data, cap,

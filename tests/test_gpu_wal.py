@@ -484,3 +484,34 @@ def test_wal_replay_cap_below_count(ctx):
     assert st == ost == 0
     assert len(recs) == 700
     assert [int(r.rec_off) for r in recs] == [r.rec_off for r in orecs[:700]]
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_pinned_records(ctx, device):
+    """LSMCK_RECS_PINNED: the records DMA'd straight into a page-locked array
+    -- the same records and outcome as the oracle (a corrupted Insert's
+    CorruptedData read from that array), also with cap below the count."""
+    img = _binary_log(30000, 71)
+    st, orecs, _ = O.wal_replay(img)
+    b = bytearray(img)
+    r = next(r for r in orecs[20000:] if r.type == 1 and r.klen + r.vlen > 0)
+    b[r.payload_off] ^= 0x20
+    for im in (img, bytes(b)):
+        d = None
+        if device:
+            d = ctx.alloc(len(im))
+            d.upload(np.frombuffer(im, np.uint8))
+        try:
+            for cap in (None, 5000):
+                recs, st, bad = (ctx.wal_replay_verify(len(im), device_ptr=d.ptr, cap=cap, pinned_recs=True) if device
+                                 else ctx.wal_replay_verify(im, cap=cap, pinned_recs=True))
+                ost, orr, obad = O.wal_replay(im)
+                assert st == ost
+                want = [x.rec_off for x in orr][:cap]
+                assert [int(x.rec_off) for x in recs] == want
+                if st:
+                    assert bad[:3] == obad[:3]
+                del recs
+        finally:
+            if d:
+                d.free()

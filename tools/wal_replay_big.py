@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--records", type=int, default=1 << 26)
     ap.add_argument("--seg-walk", type=int, default=1, help="0: the candidate-doubling walk (A/B)")
+    ap.add_argument("--pinned-recs", type=int, default=1,
+                    help="1: the records DMA'd into a page-locked array (LSMCK_RECS_PINNED); 0: staged + copied")
     a = ap.parse_args()
     n = a.records
     ln = gen_zipf_lengths(0x5EED0003, n)
@@ -62,7 +64,7 @@ def main():
     for s in range(a.steps + 1):  # the first replay is a warm-up
         ctx.sync()
         t = time.perf_counter()
-        recs, st, bad = ctx.wal_replay_verify(total, device_ptr=d.ptr, cap=n)
+        recs, st, bad = ctx.wal_replay_verify(total, device_ptr=d.ptr, cap=n, pinned_recs=bool(a.pinned_recs))
         dt = time.perf_counter() - t
         assert st == 0 and len(recs) == n, (st, len(recs), bad)
         summary = "%08x" % zlib.crc32(np.ascontiguousarray(recs.crc).astype("<u4").tobytes())
@@ -79,7 +81,7 @@ def main():
         "value": round(total / GIB / med, 1), "unit": "GiB/s of log",
         "log_bytes": total, "records": n, "ms_median": round(med * 1e3, 2), "ms_best": round(best * 1e3, 2),
         "steps": a.steps, "summary_crc32": summary, "summary_matches_oracle": bool(golden) and True,
-        "records_out_bytes": 32 * n,
+        "records_out_bytes": 32 * n, "pinned_recs": bool(a.pinned_recs),
         "walk_path": {1: "segment walk", 2: "candidate doubling", 3: "host walk"}.get(ctx.get_stat("wal_walk_path")),
         "seg_repairs": ctx.get_stat("wal_seg_repairs"), "segments": ctx.get_stat("wal_segments"),
         "workload": "config 3's 2^26 Zipf payloads (64 B-64 KiB) framed as wal.rs Insert records (13-byte headers), "
