@@ -1450,7 +1450,6 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
   DevGuard g(ctx->dev);
   const WalTrace tr;
   int rc;
-  if ((rc = wal_walk_setup(ctx, n))) return rc;
   ScratchOrder so(ctx, ctx->stream0);
   if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
   hipStream_t st = so.st;
@@ -1462,7 +1461,8 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
                       true);
   }
   if (rc != kWalSegDecline) return rc;
-  ctx->last_walk_path = 2;
+  ctx->last_walk_path = 2;  // candidate doubling: its bitmap, ranks and jump tables
+  if ((rc = wal_walk_setup(ctx, n))) return rc;
   if ((rc = wal_walk_from(ctx, img, n, 0, 0, ctx->wal_part_bytes, marked, st, tr, &P))) return rc;
   return wal_finish(ctx, img, P.m, P.term, P.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr);
 }
