@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=float, default=1.0)
     ap.add_argument("--list-threads", default="", help="comma list of tree_list_threads values to A/B (listing time)")
     ap.add_argument("--ab", default="", help="comma list of active:slice_bytes[:open_files] settings to A/B after the main reps")
+    ap.add_argument("--multi", type=int, default=0,
+                    help="also time lsmck_tree_verify_multi with this many contexts on device 0 against "
+                         "lsmck_tree_verify on one (the multi-GPU split's own cost, measurable on one GPU)")
     a = ap.parse_args()
 
     marker = os.path.join(a.dir, "e2e_tree.json")
@@ -83,6 +86,25 @@ def main():
         lt[v] = round(min(tree.load_verify(ctx, a.dir)[1]["list_s"] for _ in range(2)), 3)
         print(f"list threads {v}: {lt[v]} s", file=sys.stderr, flush=True)
     ctx.set_option("tree_list_threads", 0)
+    multi = None
+    if a.multi > 1:
+        from lsm_storage_engine_amd.device import MultiContext
+        mc = MultiContext(contexts=[Context(0) for _ in range(a.multi)])
+        one, many = [], []
+        for _ in range(3):  # interleaved
+            t = time.perf_counter()
+            r1 = ctx.tree_verify(a.dir)
+            one.append(time.perf_counter() - t)
+            t = time.perf_counter()
+            rm = mc.tree_verify(a.dir)
+            many.append(time.perf_counter() - t)
+            assert r1["bad_tables"] == rm["bad_tables"] == 0 and r1["tables"] == rm["tables"]
+        multi = {"contexts_on_one_gpu": a.multi, "tree_verify_s_one_ctx": [round(x, 3) for x in one],
+                 "tree_verify_multi_s": [round(x, 3) for x in many],
+                 "ratio_median": round(float(np.median(many)) / float(np.median(one)), 3)}
+        print(f"multi: {multi}", file=sys.stderr, flush=True)
+        for c in mc.ctxs:
+            c.close()
     verified = best["table_bytes"] + best["wal_bytes"]
 
     # CPU baseline: the oracle's SHA-256 (= sha2 0.10's algorithm; scalar, no
@@ -120,6 +142,8 @@ def main():
         res["tables_GiBps_by_active_slice"] = ab
     if lt:
         res["list_s_by_threads"] = lt
+    if multi:
+        res["tree_verify_multi_same_gpu"] = multi
     print(json.dumps(res), flush=True)
     ctx.close()
     if not a.keep:
