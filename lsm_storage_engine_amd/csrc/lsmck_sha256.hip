@@ -355,8 +355,8 @@ __global__ __launch_bounds__(256) void sha256_kernel(ShaParams P) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P.nmsg || (P.split && i >= *P.split)) return;  // (the short tail: sha256_short_kernel)
   uint64_t m = P.order ? P.order[i] : i;
-  uint64_t off = P.off ? P.off[m] : m * P.stride;
-  uint64_t len = P.len ? P.len[m] : P.flen;
+  uint64_t off = P.soff ? P.soff[i] : (P.off ? P.off[m] : m * P.stride);
+  uint64_t len = P.slen ? P.slen[i] : (P.len ? P.len[m] : P.flen);
   uint32_t h[8];
   sha256_iv(h);
   sha256_run<PAIR, ABL>(h, P.base, off, len, true, len << 3);
@@ -374,8 +374,8 @@ __global__ __launch_bounds__(256) void sha256_short_kernel(ShaParams P) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P.nmsg || i < *P.split) return;
   const uint64_t m = P.order[i];
-  const uint64_t off = P.off ? P.off[m] : m * P.stride;
-  const uint64_t len = P.len[m];
+  const uint64_t off = P.soff ? P.soff[i] : (P.off ? P.off[m] : m * P.stride);
+  const uint64_t len = P.slen ? P.slen[i] : P.len[m];
   const uintptr_t A = (uintptr_t)(P.base + off);
   const uint64_t nb = (len + 9 + 63) >> 6;
   uint32_t h[8];
