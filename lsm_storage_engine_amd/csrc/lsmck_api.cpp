@@ -1598,7 +1598,9 @@ static int wal_records_early(lsmck_ctx* ctx, size_t m, lsmck_wal_rec* recs, size
 
 constexpr int kWalNoSplit = 0x7FFF0002;  // internal: the image is too small to upload in two parts
 
-// A host image uploaded in two parts ("wal_split", default on from 64 MiB):
+// A host image uploaded in two parts ("wal_split", default on; taken when each
+// half holds at least one upload chunk -- images of two "wal_stage_bytes"
+// chunks and more, 32 MiB at the default 16 MiB chunk):
 // the prefix [0, a) is walked (lsmck_wal.hip's prefix walk: records that end
 // by a) and its CRC pass launched on stream0, on a helper thread, while this
 // thread uploads the rest; the walk then resumes where the prefix stopped

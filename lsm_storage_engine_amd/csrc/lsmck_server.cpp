@@ -505,7 +505,9 @@ struct Db {
       size_t n = 0, nrec = 0;
       double t_verify = 0, t_wal = 0;
     } W;
-    std::thread wal_th([this, &W]() {
+    // own_ctx: the replay's own context (beside the tree verify); otherwise
+    // the given one (the sequential retry below)
+    auto run_wal = [this, &W](lsmck_ctx* use_ctx) {
       const double t1 = now_s();
       const uint8_t* img = nullptr;
       void* map = nullptr;
@@ -533,7 +535,7 @@ struct Db {
         }
       }
       W.n = n;
-      lsmck_ctx* wctx = lsmck_ctx_create(cfg.device);
+      lsmck_ctx* wctx = use_ctx ? use_ctx : lsmck_ctx_create(cfg.device);
       if (!wctx) {
         W.rc = -1;
         W.err = std::string("lsmck_ctx_create: ") + lsmck_last_error();
@@ -550,7 +552,7 @@ struct Db {
         W.rc = lsmck_wal_replay_verify(wctx, img, n, LSMCK_HOST, recs.get(), cap, &nrec, &bad_index, &bad_crc,
                                        &bad_expected);
         if (W.rc < 0) W.err = std::string("lsmck_wal_replay_verify: ") + lsmck_last_error();
-        lsmck_ctx_destroy(wctx);
+        if (!use_ctx) lsmck_ctx_destroy(wctx);
       }
       W.t_verify = now_s() - t1;
       W.nrec = nrec;
@@ -635,7 +637,8 @@ struct Db {
       if (map) munmap(map, n);
       if (rfd >= 0) close(rfd);
       W.t_wal = now_s() - t1;
-    });
+    };
+    std::thread wal_th(run_wal, nullptr);
     lsmck_tree_report rep;
     int rc = lsmck_tree_verify_listed(ctx, cfg.base.c_str(), &rep, on_listed, &L);
     if (L.th.joinable()) L.th.join();
@@ -664,6 +667,14 @@ struct Db {
     }
     const double t_tree = now_s() - t0;
     if (idx_err == 2) panic_exit("Can't open index file");
+    if (W.rc < 0) {
+      // the concurrent replay failed as a call (its context or device memory
+      // beside the tree verify's, not the log's contents): once more, alone,
+      // on the server's context, as a sequential Db::load would have run it
+      fprintf(stderr, "WAL replay beside the tree verify failed (%s); replaying alone\n", W.err.c_str());
+      W = WalLoad();
+      run_wal(ctx);
+    }
     // the WAL's outcome, in from_log's place
     if (W.rc < 0) {
       fprintf(stderr, "%s\n", W.err.c_str());
