@@ -119,6 +119,15 @@ def main():
     d.upload(img)
     ctx.sync()
     res["replay_device_image_s"] = best(lambda: ctx.wal_replay_verify(len(img), device_ptr=d.ptr))
+    # the records DMA'd into a page-locked array (LSMCK_RECS_PINNED), cap = the record count
+    res["replay_device_image_pinned_recs_s"] = best(
+        lambda: ctx.wal_replay_verify(len(img), device_ptr=d.ptr, cap=n, pinned_recs=True))
+    res["device_walk_path"] = ctx.get_stat("wal_walk_path")
+    res["device_segments"] = ctx.get_stat("wal_segments")
+    res["device_seg_repairs"] = ctx.get_stat("wal_seg_repairs")
+    ctx.set_option("wal_seg_walk", 0)  # A/B: candidate doubling
+    res["replay_device_image_doubling_s"] = best(lambda: ctx.wal_replay_verify(len(img), device_ptr=d.ptr))
+    ctx.set_option("wal_seg_walk", 1)
     ctx.set_option("wal_gpu_walk", 0)  # A/B: copy the device image back, host walk
     res["replay_device_image_hostwalk_s"] = best(lambda: ctx.wal_replay_verify(len(img), device_ptr=d.ptr))
     ctx.set_option("wal_gpu_walk", 1)
@@ -126,7 +135,7 @@ def main():
     res["replay_pinned_upload_gpuwalk_s"] = best(
         lambda: (d.upload(pin.array), ctx.wal_replay_verify(len(img), device_ptr=d.ptr)))
     for k in list(res):
-        if k.endswith("_s"):
+        if k.endswith("_s") and isinstance(res[k], float):
             res[k[:-2] + "_GiBps"] = round(len(img) / 2**30 / res[k], 2)
             res[k] = round(res[k], 4)
     print(json.dumps(res))
