@@ -86,6 +86,17 @@ class Server:
             if ev["event"] == kind:
                 return ev
 
+    def drain_events(self, kind):
+        """Every event line of this kind printed so far (no waiting)."""
+        out = []
+        while True:
+            try:
+                line = self._lines.get_nowait()
+            except queue.Empty:
+                return out
+            if line and json.loads(line)["event"] == kind:
+                out.append(json.loads(line))
+
     def stderr_tail(self):
         """The last lines the server wrote to stderr (all of them once it has exited)."""
         if self.proc.poll() is not None:

@@ -104,6 +104,8 @@ def main():
     ap.add_argument("--memtable-limit", type=int, default=4 << 20,
                     help="bytes (the reference's config/default is 4096)")
     ap.add_argument("--cpu-sample-gib", type=float, default=1.0)
+    ap.add_argument("--compact-interval", type=int, default=10000,
+                    help="ms between the server's compaction ticks (server.rs:94; each re-verifies levels 0..3)")
     ap.add_argument("--keep", action="store_true")
     a = ap.parse_args()
 
@@ -119,7 +121,7 @@ def main():
     print(f"tree: {synth}", file=sys.stderr, flush=True)
 
     t0 = time.perf_counter()
-    srv = Server(a.dir, memtable_limit=a.memtable_limit)
+    srv = Server(a.dir, memtable_limit=a.memtable_limit, compact_interval_ms=a.compact_interval)
     start1 = time.perf_counter() - t0
     load1 = srv.loaded
     print(f"first start: {load1}", file=sys.stderr, flush=True)
@@ -127,6 +129,12 @@ def main():
     with cf.ThreadPoolExecutor(a.conns) as ex:
         outs = list(ex.map(lambda k: traffic(srv.port, k, a.ops), range(a.conns)))
     wall = time.perf_counter() - t1
+    # the compaction ticks that ran while the traffic did (the first one at once)
+    ticks = srv.drain_events("compact")
+    if not ticks and a.compact_interval > 0:
+        ticks = [srv.wait_event("compact", timeout=600)]
+    failed = srv.drain_events("compact_failed")
+    print(f"ticks: {ticks} {failed}", file=sys.stderr, flush=True)
     srv.kill()
     model, hist = {}, {}
     for m, h, _ in outs:
@@ -188,6 +196,10 @@ def main():
                     "commands_per_s": round(a.conns * a.ops / wall, 1),
                     "mix": "per connection: 80% insert, 10% get, 10% delete, pipelined 512 per round trip"},
         "restart": {**load2, "process_start_s": round(start2, 3)},
+        "compaction_ticks": {"interval_ms": a.compact_interval, "ticks_during_traffic": len(ticks),
+                             "what": "Db::compact's re-verify of levels 0..3 (SsTable::clone = SsTable::load -> "
+                                     "Checksums::verify) in one GPU batch per tick, beside the traffic",
+                             "ticks": ticks, "failed": failed},
         "readback": {"keys": len(keys), "mismatches": mismatches,
                      "replayed_remove_reads_table_value": resurrected},
         "cpu_baseline": {"value": round(done / GIB / tc, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
