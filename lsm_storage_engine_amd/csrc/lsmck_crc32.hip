@@ -1065,10 +1065,34 @@ __device__ __forceinline__ uint32_t stream_xinv(uint32_t t) {  // x^(-8(4-t))
 // next lane (lane 63 loads it).  The per-wave cuts follow by binary search
 // (stream_cuts, sorted by then).  One record per thread ran 0.18 ms on config
 // 3; a fused check + cuts pass 0.31 ms.
-template <bool VEC>
-__global__ __launch_bounds__(256) void stream_check(CrcParams P) {
+// cut w, w = 0..W: the first record starting at or after off[0] + span*w/W
+// (cut W = n: every record belongs to exactly one wave).  Binary search.
+__device__ __forceinline__ void stream_cut(const CrcParams& P, uint32_t w, uint32_t W) {
   const uint64_t n = P.nrec;
-  const uint64_t i0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
+  if (w == W) {
+    P.scuts[w] = n;
+    return;
+  }
+  const uint64_t o0 = P.off[0], dend = P.off[n - 1] + P.len[n - 1];
+  const uint64_t target = o0 + (dend - o0) * w / W;
+  uint64_t a = 0, b = n;
+  while (a < b) {
+    const uint64_t m = (a + b) >> 1;
+    if (P.off[m] < target) a = m + 1; else b = m;
+  }
+  P.scuts[w] = a;
+}
+
+// The check also computes the cuts, in its first W + 1 threads: their binary
+// searches (dependent loads) run inside the check's own bandwidth-bound pass
+// instead of a launch of their own behind it (the cuts of an ineligible batch
+// are never read: the stream kernel exits on the flag).
+template <bool VEC>
+__global__ __launch_bounds__(256) void stream_check(CrcParams P, uint32_t W) {
+  const uint64_t n = P.nrec;
+  const uint32_t gt = blockIdx.x * 256u + threadIdx.x;
+  if (gt <= W) stream_cut(P, gt, W);
+  const uint64_t i0 = (uint64_t)gt * 4u;  // (threads past the records load record n-1 and find nothing)
   uint64_t o[5];
   uint32_t l[5];
   if (VEC && i0 + 4u <= n) {
@@ -1103,24 +1127,11 @@ __global__ __launch_bounds__(256) void stream_check(CrcParams P) {
   if (bad) *P.sflag = 0u;  // plain stores of one value: no atomic needed
 }
 
-// cut w, w = 0..W: the first record starting at or after off[0] + span*w/W
-// (cut W = n: every record belongs to exactly one wave)
+// the cuts alone (trusted batches: no check)
 __global__ __launch_bounds__(256) void stream_cuts(CrcParams P, uint32_t W) {
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w > W || !*P.sflag) return;
-  const uint64_t n = P.nrec;
-  if (w == W) {
-    P.scuts[w] = n;
-    return;
-  }
-  const uint64_t o0 = P.off[0], dend = P.off[n - 1] + P.len[n - 1];
-  const uint64_t target = o0 + (dend - o0) * w / W;
-  uint64_t a = 0, b = n;
-  while (a < b) {
-    const uint64_t m = (a + b) >> 1;
-    if (P.off[m] < target) a = m + 1; else b = m;
-  }
-  P.scuts[w] = a;
+  stream_cut(P, w, W);
 }
 
 // the tile's 64 chunks: bytes [tb, tb + 8192) from P.base (tb >= -127, the
@@ -1581,14 +1592,15 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
   hipError_t e = hipMemsetAsync(P->sflag, 1, 4, st);
   if (e != hipSuccess) return -(int)e;
   const uint32_t W = lsmk_stream_waves(ncu);
-  if (!trusted)  // a caller's batch: checked first (the cuts below then skip on the flag)
-  {
+  if (!trusted) {  // a caller's batch: checked first, the cuts computed inside the check
     const bool vec = ((uintptr_t)P->off % 16u == 0) && ((uintptr_t)P->len % 16u == 0);
-    const dim3 g((unsigned)((n + 1023) / 1024));
-    if (vec) hipLaunchKernelGGL(stream_check<true>, g, dim3(256), 0, st, *P);
-    else hipLaunchKernelGGL(stream_check<false>, g, dim3(256), 0, st, *P);
+    const uint64_t nb = std::max<uint64_t>((n + 1023) / 1024, (W + 1u + 255u) / 256u);
+    const dim3 g((unsigned)nb);
+    if (vec) hipLaunchKernelGGL(stream_check<true>, g, dim3(256), 0, st, *P, W);
+    else hipLaunchKernelGGL(stream_check<false>, g, dim3(256), 0, st, *P, W);
+  } else {
+    hipLaunchKernelGGL(stream_cuts, dim3((W + 1u + 255u) / 256u), dim3(256), 0, st, *P, W);
   }
-  hipLaunchKernelGGL(stream_cuts, dim3((W + 1u + 255u) / 256u), dim3(256), 0, st, *P, W);
   const int ablate = (variant >> 8) & 0xF;
 #ifdef LSMCK_AB_ABLATIONS
   // the stream kernel's diagnostic ablations: only in the
