@@ -88,8 +88,8 @@ class _PinnedRecords:
 
     def __init__(self, pb, n):
         self.pb = pb
-        self.__array_interface__ = {"data": (pb.ptr, False), "shape": (n,), "descr": WAL_REC_DTYPE.descr,
-                                    "version": 3}
+        self.__array_interface__ = {"data": (pb.ptr, False), "shape": (n,), "typestr": WAL_REC_DTYPE.str,
+                                    "descr": WAL_REC_DTYPE.descr, "version": 3}
 
 
 class Context:

@@ -258,7 +258,7 @@ def test_compaction_tick_reverifies_and_panics_like_the_reference(tmp_path):
     tree.synthesize_tree(base, 2 << 20, wal_records=200)
     metas = tree.list_tables(base)
     low = [m for m in metas if m.level < 4]
-    srv = Server(base, compact_interval_ms=300)
+    srv = Server(base, compact_interval_ms=300, memtable_limit=1 << 30)  # (no flush: the table set stays)
     try:
         ev = srv.wait_event("compact")
         assert ev["tick"] == 0 and ev["tables"] == len(low)

@@ -22,13 +22,16 @@ step() {  # step NAME SECONDS CMD...
   fi
   return 0
 }
-step pytest_wal 500 python -u -m pytest tests/test_gpu_wal.py -x -v --timeout 200 --timeout-method thread
+O=gpurun_out/${R:-r04a}
+mkdir -p $O
+step pytest_wal 500 python -u -m pytest tests/test_gpu_wal.py -v --timeout 200 --timeout-method thread
+step pytest_stream 600 python -u -m pytest tests/test_gpu_stream.py tests/test_gpu_crc.py -x -v --timeout 300 --timeout-method thread
 step wal_big 300 env LSMCK_WAL_TRACE=1 python -u tools/wal_replay_big.py --steps 3
 step wal_diag 240 python -u tools/wal_diag.py
 step pytest_bench 400 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 300 --timeout-method thread
 step bench_default 300 python -u bench.py
-step pytest_server 400 python -u -m pytest tests/test_server.py -x -v --timeout 300 --timeout-method thread
-step sha_ab 300 python -u bench.py --digest sha256 --variants "-,d1" --rounds 3 --steps 5 --warmup 2 --no-cpu-baseline --no-host-roundtrip --no-config4
+step pytest_server 400 python -u -m pytest tests/test_server.py -v --timeout 300 --timeout-method thread
+step sha_ab 300 python -u bench.py --digest sha256 --variants=-,d1 --rounds 3 --steps 5 --warmup 2 --no-cpu-baseline --no-host-roundtrip --no-config4
 step pytest_sha 400 python -u -m pytest tests/test_gpu_sha.py -x -v --timeout 200 --timeout-method thread -k "short_tail or length_sorted"
 step kt_wal_big 300 rocprofv3 --kernel-trace --stats -d $O/kt_wal_big -o run -- python3 tools/wal_replay_big.py --steps 2
 echo done >&2
