@@ -37,6 +37,17 @@ def main():
         recs, st, _ = ctx.wal_replay_verify(len(img), device_ptr=d.ptr)
         ts.append(time.perf_counter() - t)
     out["device_image_ms_best"] = round(min(ts) * 1e3, 3)
+    ts = []  # the records DMA'd into a page-locked array (LSMCK_RECS_PINNED)
+    for _ in range(11):
+        t = time.perf_counter()
+        recs, st, _ = ctx.wal_replay_verify(len(img), device_ptr=d.ptr, cap=500_000, pinned_recs=True)
+        ts.append(time.perf_counter() - t)
+        assert st == 0 and len(recs) == 500_000
+        del recs
+    out["device_image_pinned_recs_ms_best"] = round(min(ts[1:]) * 1e3, 3)
+    out["device_image_pinned_recs_ms_median"] = round(float(np.median(ts[1:])) * 1e3, 3)
+    out["walk"] = {"path": ctx.get_stat("wal_walk_path"), "segments": ctx.get_stat("wal_segments"),
+                   "repairs": ctx.get_stat("wal_seg_repairs")}
     print(out)
     d.free()
     ctx.close()
