@@ -289,6 +289,7 @@ struct lsmck_ctx {
   int sha_pair = 1;  // SHA-256 batches: two blocks per load window (A/B: DESIGN.md 3.2)
   int sha_short_blocks = 12;  // SHA-256 ordered batches: messages of at most this many blocks on the lean kernel (0 = off)
   int sha_sorted_desc = 0;   // SHA-256 ordered batches: descriptors gathered into order first (A/B)
+  int sha_short_pf = 0;      // SHA-256 short-tail kernel: next block's loads before this block's compression (A/B)
   unsigned tree_list_threads = 0;  // lsmck_tree_verify: metadata parsing threads (0 = kListThreads)
   size_t wal_prefetch = 4096;  // lsmck_wal_replay_verify: host walk's prefetch distance in bytes (0 = off)
   uint8_t* wal_host = nullptr;  // lsmck_wal_replay_verify of a device image: pinned host copy (grow-only)
@@ -474,6 +475,7 @@ int sha_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const uint6
   P.pair = (uint32_t)ctx->sha_pair;
   P.split = (order && ctx->sha_short_blocks > 0) ? sc.sha_split : nullptr;
   P.soff = (order && ctx->sha_sorted_desc && off) ? sc.sha_soff : nullptr;
+  P.short_pf = (uint32_t)ctx->sha_short_pf;
   P.slen = P.soff ? sc.sha_slen : nullptr;
   int rc = lsmk_launch_sha256(&P, st);
   return rc ? launch_rc(rc, "sha256 kernel") : 0;
@@ -912,6 +914,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "sha_sorted_desc must be 0 or 1");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->sha_sorted_desc = (int)value;
+    return 0;
+  }
+  if (!strcmp(key, "sha_short_pf")) {  // A/B: the SHA short-tail kernel loads one block ahead
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "sha_short_pf must be 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->sha_short_pf = (int)value;
     return 0;
   }
   if (!strcmp(key, "sha_pair")) {  // A/B: SHA-256 batch kernel loads two blocks (a 128-B line) per window

@@ -44,6 +44,7 @@ struct ShaParams {
   const uint64_t* split;      // device: order index where the short tail starts (lean kernel), null = none
   const uint64_t* soff;       // with order: off[order[i]] / len[order[i]] at i (coalesced), null = gather them
   const uint32_t* slen;
+  uint32_t short_pf;          // the short-tail kernel loads a block ahead (A/B)
 };
 
 // One slice of a message streamed through sha256_slices_kernel.
