@@ -94,36 +94,47 @@ LSMCK_HD uint64_t succ(const uint8_t* img, uint64_t n, uint64_t p, bool* whole) 
   return p + h + (*whole ? (uint64_t)dlen : avail);
 }
 
-// The walk from the record start c through the segment ending at e.
-// forced: c is known to be on the chain (segment 0, a repair): taken as is.
-// Otherwise c is taken when its walk reaches kAccept whole records (past e if
-// need be) or ends cleanly at EOF.  Returns whether c is taken; *o then holds
-// the segment's outcome.
-LSMCK_HD bool walk(const uint8_t* img, uint64_t n, uint64_t c, uint64_t e, bool forced, WalkOut* o) {
+// The segment's outcome from its entry c (a record start on the chain, or
+// the guess): the walk through the segment ending at e, to the first record
+// start at or past e (kExit) or to the chain's end (kEnd / kBad).
+LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, uint64_t e, WalkOut* o) {
   uint64_t p = c;
-  uint32_t cnt = 0, good = 0;
-  bool out = false;
+  uint32_t cnt = 0;
   for (;;) {
-    if (!out && p >= e) {
-      out = true;
+    if (p >= e) {
       o->code = kExit;
       o->pos = p;
       o->recs = cnt;
+      return;
     }
-    if (out && (forced || good >= kAccept)) return true;
     bool whole;
     const uint64_t q = succ(img, n, p, &whole);
-    cnt += p < e;
-    good += whole;
+    ++cnt;
     const uint32_t cl = classify(img, n, q);
     if (cl) {  // the chain ends after the record at p
-      if (!out) {
-        o->code = cl;
-        o->pos = q;
-        o->recs = cnt;
-      }
-      return forced || good >= kAccept || (whole && cl == kEnd);
+      o->code = cl;
+      o->pos = q;
+      o->recs = cnt;
+      return;
     }
+    p = q;
+  }
+}
+
+// Whether a candidate start c (a type byte whose header fits) is plausible:
+// its chain holds kAccept whole records, or ends cleanly at EOF before that.
+// At most kAccept + 1 headers are read, so the lanes of a wave that test
+// candidates stay together; the long walk through the segment runs after the
+// guess, in step across the wave.
+LSMCK_HD bool accept(const uint8_t* img, uint64_t n, uint64_t c) {
+  uint64_t p = c;
+  for (uint32_t good = 0;;) {
+    bool whole;
+    const uint64_t q = succ(img, n, p, &whole);
+    good += whole;
+    if (good >= kAccept) return true;
+    const uint32_t cl = classify(img, n, q);
+    if (cl) return whole && cl == kEnd;
     p = q;
   }
 }
@@ -206,16 +217,16 @@ LSMCK_HD bool reaches(const uint8_t* img, uint64_t n, uint64_t c, uint64_t q) {
 }
 
 // The guess of a segment [b, e) (b > start): the first type byte c in it
-// whose header fits and whose walk is taken -- unless a later start inside
+// whose header fits and which accept() takes -- unless a later start inside
 // c's first record has a chain through that record's end, which is then
 // preferred (the same test again from it).  The common wrong guess is a
 // bogus start before the segment's first true record whose random length
 // happens to land on a later true record: its chains merge with the true
 // one, so its walk is taken, but its first "record" covers the true entry,
 // whose chain reaches the merge point.  kNoGuess: no start taken.
-LSMCK_HD uint64_t guess(const uint8_t* img, uint64_t n, uint64_t b, uint64_t e, WalkOut* o) {
+LSMCK_HD uint64_t guess(const uint8_t* img, uint64_t n, uint64_t b, uint64_t e) {
   for (uint64_t c = next_cand(img, n, b, e); c != kNoGuess; c = next_cand(img, n, c + 1, e)) {
-    if (!walk(img, n, c, e, false, o)) continue;
+    if (!accept(img, n, c)) continue;
     for (;;) {
       bool whole;
       const uint64_t q1 = succ(img, n, c, &whole), lim = q1 < e ? q1 : e;
@@ -223,7 +234,6 @@ LSMCK_HD uint64_t guess(const uint8_t* img, uint64_t n, uint64_t b, uint64_t e, 
       while (c2 != kNoGuess && !reaches(img, n, c2, q1)) c2 = next_cand(img, n, c2 + 1, lim);
       if (c2 == kNoGuess) return c;
       c = c2;
-      walk(img, n, c, e, true, o);
     }
   }
   return kNoGuess;
@@ -273,7 +283,7 @@ LSMCK_HD void seg_forced(const SegArgs& a, uint32_t k, uint64_t c) {
     o.pos = c;
     o.recs = 0;
   } else {
-    walk(a.img, a.n, c, seg_end(a, k), true, &o);
+    walk(a.img, a.n, c, seg_end(a, k), &o);
   }
   a.g[k] = c;
   a.x[k] = o.pos;
@@ -287,17 +297,14 @@ LSMCK_HD void seg_walk_thread(const SegArgs& a, uint32_t k) {
     seg_forced(a, 0, a.start);
     return;
   }
-  WalkOut o;
-  const uint64_t c = guess(a.img, a.n, seg_begin(a, k), seg_end(a, k), &o);
-  a.g[k] = c;
+  const uint64_t c = guess(a.img, a.n, seg_begin(a, k), seg_end(a, k));
   if (c == kNoGuess) {
+    a.g[k] = c;
     a.x[k] = 0;
     a.code[k] = kNone;
     a.recs[k] = 0;
   } else {
-    a.x[k] = o.pos;
-    a.code[k] = o.code;
-    a.recs[k] = o.recs;
+    seg_forced(a, k, c);  // the walk from the guess (every lane of the wave at once)
   }
 }
 
