@@ -57,6 +57,16 @@ constexpr uint32_t kNoSeg = 0xFFFFFFFFu;
 // end of the log) before it is taken: a bogus one passes a step with ~1/128
 // odds on random payloads, so six steps leave ~1e-13 per candidate
 constexpr uint32_t kAccept = 6;
+// ... and its first record must end within this many bytes (or the segment
+// length, if longer).  A bogus start reads a random 32-bit length; on a log
+// past 4 GiB it lands inside the log, and exactly on a true record with odds
+// of (records / bytes), ~1/1,500 for config 3w -- a merge with the true
+// chain that the acceptance test cannot see, and with ~100 bogus starts
+// scanned before a segment's first true record, one segment in ~13 would
+// be guessed wrong.  A first record of at most kHop bytes cuts that by
+// 4 GiB / 64 KiB.  A true first record longer than this is refused and
+// repaired by the check (or the walk re-segments, with longer hops).
+constexpr uint64_t kHop = 65536;
 // per-segment record counts and the guessed-segment count share one u64 in
 // the placement scan: guessed segments in the top 24 bits, records below
 constexpr int kSegShift = 40;
@@ -122,15 +132,17 @@ LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, uint64_t e, WalkO
 }
 
 // Whether a candidate start c (a type byte whose header fits) is plausible:
-// its chain holds kAccept whole records, or ends cleanly at EOF before that.
+// its first record ends within `hop` bytes, and its chain holds kAccept whole
+// records, or ends cleanly at EOF before that.
 // At most kAccept + 1 headers are read, so the lanes of a wave that test
 // candidates stay together; the long walk through the segment runs after the
 // guess, in step across the wave.
-LSMCK_HD bool accept(const uint8_t* img, uint64_t n, uint64_t c) {
+LSMCK_HD bool accept(const uint8_t* img, uint64_t n, uint64_t c, uint64_t hop) {
   uint64_t p = c;
   for (uint32_t good = 0;;) {
     bool whole;
     const uint64_t q = succ(img, n, p, &whole);
+    if (p == c && q - c > hop) return false;  // a first record this long: not taken (kHop)
     good += whole;
     if (good >= kAccept) return true;
     const uint32_t cl = classify(img, n, q);
@@ -206,6 +218,7 @@ LSMCK_HD uint64_t next_cand(const uint8_t* img, uint64_t n, uint64_t from, uint6
 }
 
 // whether the chain from the record start c passes through position q > c
+// (q is at most a hop past the candidate that asks: a bounded walk)
 LSMCK_HD bool reaches(const uint8_t* img, uint64_t n, uint64_t c, uint64_t q) {
   uint64_t p = c;
   while (p < q) {
@@ -224,9 +237,9 @@ LSMCK_HD bool reaches(const uint8_t* img, uint64_t n, uint64_t c, uint64_t q) {
 // happens to land on a later true record: its chains merge with the true
 // one, so its walk is taken, but its first "record" covers the true entry,
 // whose chain reaches the merge point.  kNoGuess: no start taken.
-LSMCK_HD uint64_t guess(const uint8_t* img, uint64_t n, uint64_t b, uint64_t e) {
+LSMCK_HD uint64_t guess(const uint8_t* img, uint64_t n, uint64_t b, uint64_t e, uint64_t hop) {
   for (uint64_t c = next_cand(img, n, b, e); c != kNoGuess; c = next_cand(img, n, c + 1, e)) {
-    if (!accept(img, n, c)) continue;
+    if (!accept(img, n, c, hop)) continue;
     for (;;) {
       bool whole;
       const uint64_t q1 = succ(img, n, c, &whole), lim = q1 < e ? q1 : e;
@@ -297,7 +310,7 @@ LSMCK_HD void seg_walk_thread(const SegArgs& a, uint32_t k) {
     seg_forced(a, 0, a.start);
     return;
   }
-  const uint64_t c = guess(a.img, a.n, seg_begin(a, k), seg_end(a, k));
+  const uint64_t c = guess(a.img, a.n, seg_begin(a, k), seg_end(a, k), a.S > kHop ? a.S : kHop);
   if (c == kNoGuess) {
     a.g[k] = c;
     a.x[k] = 0;
