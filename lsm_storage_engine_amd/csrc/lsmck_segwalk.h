@@ -67,6 +67,10 @@ constexpr uint32_t kAccept = 6;
 // 4 GiB / 64 KiB.  A true first record longer than this is refused and
 // repaired by the check (or the walk re-segments, with longer hops).
 constexpr uint64_t kHop = 65536;
+#ifndef LSMCK_SCAN_BLOCKS
+#define LSMCK_SCAN_BLOCKS 4
+#endif
+constexpr int kScanBlocks = LSMCK_SCAN_BLOCKS;  // 64-byte blocks the guess scan loads per iteration
 // per-segment record counts and the guessed-segment count share one u64 in
 // the placement scan: guessed segments in the top 24 bits, records below
 constexpr int kSegShift = 40;
@@ -176,43 +180,63 @@ LSMCK_HD void load16(const uint8_t* a, uint32_t w[4]) {
 // the 64-byte block holding `from` (aligned in the address space: vector
 // loads inside the image, byte loads at its two ends) and the ones after it.
 LSMCK_HD uint64_t next_cand(const uint8_t* img, uint64_t n, uint64_t from, uint64_t e) {
+  // kScanBlocks 64-byte blocks per iteration: all their loads are in flight
+  // together, so a lane that starts inside a long record waits on a quarter as
+  // many dependent loads (the wave waits for its slowest lane).
   const uintptr_t base = (uintptr_t)img;
-  for (uintptr_t A = (base + from) & ~(uintptr_t)63;; A += 64) {
-    const int64_t p0 = (int64_t)(A - base);  // image position of the block's first byte (< 0: before the image)
+  for (uintptr_t A = (base + from) & ~(uintptr_t)63;; A += 64 * kScanBlocks) {
+    const int64_t p0 = (int64_t)(A - base);  // image position of the chunk's first byte (< 0: before the image)
     if (p0 >= (int64_t)e) return kNoGuess;
-    uint64_t m = 0;
-    if (p0 >= 0 && (uint64_t)p0 + 64 <= n) {
-      uint32_t w[16];
-      load16((const uint8_t*)A, w);
-      load16((const uint8_t*)A + 16, w + 4);
-      load16((const uint8_t*)A + 32, w + 8);
-      load16((const uint8_t*)A + 48, w + 12);
+    uint64_t m[kScanBlocks];
+    if (p0 >= 0 && (uint64_t)p0 + 64 * kScanBlocks <= n) {
+      uint32_t w[16 * kScanBlocks];
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
-      for (int d = 0; d < 16; ++d) {
-        const uint32_t f = type_bytes(w[d]);
-        const uint64_t nib = ((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u);
-        m |= nib << (4 * d);
+      for (int q = 0; q < 4 * kScanBlocks; ++q) load16((const uint8_t*)A + 16 * q, w + 4 * q);
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+      for (int j = 0; j < kScanBlocks; ++j) {
+        uint64_t mj = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int d = 0; d < 16; ++d) {
+          const uint32_t f = type_bytes(w[16 * j + d]);
+          const uint64_t nib = ((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u);
+          mj |= nib << (4 * d);
+        }
+        m[j] = mj;
       }
     } else {
-      for (int i = 0; i < 64; ++i) {
-        const int64_t p = p0 + i;
-        if (p >= 0 && (uint64_t)p < n) {
-          const uint32_t t = img[p];
-          if (t == 1 || t == 2) m |= 1ull << i;
+      for (int j = 0; j < kScanBlocks; ++j) {
+        uint64_t mj = 0;
+        for (int i = 0; i < 64; ++i) {
+          const int64_t p = p0 + 64 * j + i;
+          if (p >= 0 && (uint64_t)p < n) {
+            const uint32_t t = img[p];
+            if (t == 1 || t == 2) mj |= 1ull << i;
+          }
         }
+        m[j] = mj;
       }
     }
-    // only positions in [from, e)
-    const int64_t lo = (int64_t)from - p0, hi = (int64_t)e - p0;
-    if (lo > 0) m &= ~0ull << lo;
-    if (hi < 64) m &= (1ull << hi) - 1ull;
-    while (m) {
-      const int i = __builtin_ctzll(m);
-      m &= m - 1;
-      const uint64_t c = (uint64_t)(p0 + i);
-      if (c + hdr_len(img[c]) <= n) return c;
+    for (int j = 0; j < kScanBlocks; ++j) {
+      // only positions in [from, e)
+      const int64_t pj = p0 + 64 * j;
+      const int64_t lo = (int64_t)from - pj, hi = (int64_t)e - pj;
+      if (hi <= 0) return kNoGuess;
+      uint64_t mj = m[j];
+      if (lo >= 64) continue;
+      if (lo > 0) mj &= ~0ull << lo;
+      if (hi < 64) mj &= (1ull << hi) - 1ull;
+      while (mj) {
+        const int i = __builtin_ctzll(mj);
+        mj &= mj - 1;
+        const uint64_t c = (uint64_t)(pj + i);
+        if (c + hdr_len(img[c]) <= n) return c;
+      }
     }
   }
 }
