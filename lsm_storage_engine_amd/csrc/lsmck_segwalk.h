@@ -82,36 +82,87 @@ struct WalkOut {
   uint64_t pos;   // kExit: the next record (at or past the segment end); kBad: the bad byte
 };
 
-LSMCK_HD uint32_t rd32(const uint8_t* p) {
-  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-}
 LSMCK_HD uint32_t hdr_len(uint32_t t) { return t == 1 ? 13u : 9u; }
-
-// what position q is in the chain: 0 = a record start (type byte, header
-// fits), kEnd = EOF at or inside its header (wal.rs:76-77), kBad = not a type
-LSMCK_HD uint32_t classify(const uint8_t* img, uint64_t n, uint64_t q) {
-  if (q >= n) return kEnd;
-  const uint32_t t = img[q];
-  if (t != 1 && t != 2) return kBad;
-  return q + hdr_len(t) > n ? kEnd : 0u;
+// bytes s .. s+3 of the 8-byte little-endian pair lo, hi (s = 0..3: v_alignbyte)
+LSMCK_HD uint32_t fsh(uint32_t hi, uint32_t lo, uint32_t s) {
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * s));
 }
 
-// the record at p (a record start): where the next one starts -- its payload
-// cut at EOF (wal.rs:130-133) -- and whether the payload is whole.  The
-// length is key_len + val_len in u32, as wal.rs:129 (wrapping).
-LSMCK_HD uint64_t succ(const uint8_t* img, uint64_t n, uint64_t p, bool* whole) {
-  const uint32_t t = img[p];
-  const uint32_t h = hdr_len(t);
-  const uint32_t dlen = rd32(img + p + 5) + (t == 1 ? rd32(img + p + 9) : 0u);
-  const uint64_t avail = n - (p + h);
+// The header at q, read at once: whether q starts a record (cl: 0), or ends
+// the chain -- EOF at or inside the header (kEnd, wal.rs:76-77) or a byte that
+// is not a command type (kBad) -- and the header's fields.  One 16-byte load
+// of the four dwords holding bytes q .. q+12 (address-aligned to 4; the
+// dwords at the image's two ends are read byte by byte instead): a lane's
+// loads are what the walk's time goes to, so one per record, not one per byte.
+struct Head {
+  uint32_t cl;
+  uint32_t t, crc, klen, vlen;  // vlen 0 for Remove
+};
+LSMCK_HD Head head(const uint8_t* img, uint64_t n, uint64_t q) {
+  Head h{};
+  if (q >= n) {
+    h.cl = kEnd;
+    return h;
+  }
+  const uintptr_t A = ((uintptr_t)img + q) & ~(uintptr_t)3;
+  const int64_t a0 = (int64_t)(A - (uintptr_t)img);
+  uint32_t e0, e1, e2, e3;  // bytes q .. q+15
+  if (a0 >= 0 && (uint64_t)a0 + 16 <= n) {
+    uint32_t d[4];
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+    const u32x4a4 v = *(const __attribute__((address_space(1))) u32x4a4*)A;  // global_load_dwordx4
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
+#else
+    memcpy(d, (const void*)A, 16);
+#endif
+    const uint32_t s = (uint32_t)(((uintptr_t)img + q) & 3u);
+    e0 = fsh(d[1], d[0], s);
+    e1 = fsh(d[2], d[1], s);
+    e2 = fsh(d[3], d[2], s);
+    e3 = fsh(0u, d[3], s);
+  } else {
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t i = 0; i < 16u; ++i)
+      if (q + i < n) w[i >> 2] |= (uint32_t)img[q + i] << (8u * (i & 3u));
+    e0 = w[0];
+    e1 = w[1];
+    e2 = w[2];
+    e3 = w[3];
+  }
+  h.t = e0 & 0xFFu;
+  if (h.t != 1u && h.t != 2u) {
+    h.cl = kBad;
+    return h;
+  }
+  if (q + hdr_len(h.t) > n) {
+    h.cl = kEnd;
+    return h;
+  }
+  h.crc = (e0 >> 8) | (e1 << 24);
+  h.klen = (e1 >> 8) | (e2 << 24);
+  h.vlen = h.t == 1u ? ((e2 >> 8) | (e3 << 24)) : 0u;
+  return h;
+}
+
+// the record at p with header h: where the next one starts -- its payload cut
+// at EOF (wal.rs:130-133) -- and whether the payload is whole.  The length is
+// key_len + val_len in u32, as wal.rs:129 (wrapping).
+LSMCK_HD uint64_t next_of(const Head& h, uint64_t n, uint64_t p, bool* whole) {
+  const uint32_t hl = hdr_len(h.t);
+  const uint32_t dlen = h.klen + h.vlen;
+  const uint64_t avail = n - (p + hl);
   *whole = dlen <= avail;
-  return p + h + (*whole ? (uint64_t)dlen : avail);
+  return p + hl + (*whole ? (uint64_t)dlen : avail);
 }
 
 // The segment's outcome from its entry c (a record start on the chain, or
-// the guess): the walk through the segment ending at e, to the first record
-// start at or past e (kExit) or to the chain's end (kEnd / kBad).
-LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, uint64_t e, WalkOut* o) {
+// the guess; h its header): the walk through the segment ending at e, to the
+// first record start at or past e (kExit) or to the chain's end (kEnd / kBad).
+LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, Head h, uint64_t e, WalkOut* o) {
   uint64_t p = c;
   uint32_t cnt = 0;
   for (;;) {
@@ -122,11 +173,11 @@ LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, uint64_t e, WalkO
       return;
     }
     bool whole;
-    const uint64_t q = succ(img, n, p, &whole);
+    const uint64_t q = next_of(h, n, p, &whole);
     ++cnt;
-    const uint32_t cl = classify(img, n, q);
-    if (cl) {  // the chain ends after the record at p
-      o->code = cl;
+    h = head(img, n, q);
+    if (h.cl) {  // the chain ends after the record at p
+      o->code = h.cl;
       o->pos = q;
       o->recs = cnt;
       return;
@@ -143,18 +194,18 @@ LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, uint64_t e, WalkO
 // guess, in step across the wave.
 LSMCK_HD bool accept(const uint8_t* img, uint64_t n, uint64_t c, uint64_t hop) {
   uint64_t p = c;
+  Head h = head(img, n, c);
   for (uint32_t good = 0;;) {
     bool whole;
-    const uint64_t q = succ(img, n, p, &whole);
+    const uint64_t q = next_of(h, n, p, &whole);
     if (p == c && q - c > hop) return false;  // a first record this long: not taken (kHop)
     good += whole;
     if (good >= kAccept) return true;
-    const uint32_t cl = classify(img, n, q);
-    if (cl) return whole && cl == kEnd;
+    h = head(img, n, q);
+    if (h.cl) return whole && h.cl == kEnd;
     p = q;
   }
 }
-
 // bit 8j+7 set where byte j of v is 1 or 2 (exact, no cross-byte carries)
 LSMCK_HD uint32_t type_bytes(uint32_t v) {
   const uint32_t hi = v & 0xFCFCFCFCu;  // zero iff the byte is < 4
@@ -162,11 +213,11 @@ LSMCK_HD uint32_t type_bytes(uint32_t v) {
   const uint32_t lo = v & 0x03030303u;  // the byte's low two bits: 1 or 2, not 0 or 3
   return z & (((lo ^ (lo >> 1)) & 0x01010101u) << 7);
 }
-
 // 16 bytes at an address aligned to 16 (device: one vector load)
 LSMCK_HD void load16(const uint8_t* a, uint32_t w[4]) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  const uint4 v = *(const uint4*)a;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(uintptr_t)a;
   w[0] = v.x;
   w[1] = v.y;
   w[2] = v.z;
@@ -175,51 +226,60 @@ LSMCK_HD void load16(const uint8_t* a, uint32_t w[4]) {
   memcpy(w, a, 16);
 #endif
 }
-
-// The first type byte c in [from, e) whose header fits, or kNoGuess.  Reads
-// the 64-byte block holding `from` (aligned in the address space: vector
-// loads inside the image, byte loads at its two ends) and the ones after it.
-LSMCK_HD uint64_t next_cand(const uint8_t* img, uint64_t n, uint64_t from, uint64_t e) {
-  // kScanBlocks 64-byte blocks per iteration: all their loads are in flight
-  // together, so a lane that starts inside a long record waits on a quarter as
-  // many dependent loads (the wave waits for its slowest lane).
+// The scan's current chunk: kScanBlocks 64-byte blocks, aligned in the
+// address space, and their type-byte masks.  A lane steps through the
+// candidates of a chunk without loading it again.
+constexpr int64_t kNoChunk = INT64_MIN;
+struct Scan {
+  int64_t p0 = kNoChunk;  // image position of the chunk's first byte (< 0: before the image)
+  uint64_t m[kScanBlocks];
+};
+// The first type byte c in [from, e) whose header fits, or kNoGuess.  The
+// chunk holding `from` comes from S when it is the one already loaded (vector
+// loads inside the image, byte loads at its two ends); then the ones after it.
+LSMCK_HD uint64_t next_cand(Scan& S, const uint8_t* img, uint64_t n, uint64_t from, uint64_t e) {
+  // all the chunk's loads are in flight together, so a lane that starts
+  // inside a long record waits on a quarter as many dependent loads (the
+  // wave waits for its slowest lane)
   const uintptr_t base = (uintptr_t)img;
-  for (uintptr_t A = (base + from) & ~(uintptr_t)63;; A += 64 * kScanBlocks) {
-    const int64_t p0 = (int64_t)(A - base);  // image position of the chunk's first byte (< 0: before the image)
+  for (uintptr_t A = (base + from) & ~(uintptr_t)(64 * kScanBlocks - 1);; A += 64 * kScanBlocks) {
+    const int64_t p0 = (int64_t)(A - base);
     if (p0 >= (int64_t)e) return kNoGuess;
-    uint64_t m[kScanBlocks];
-    if (p0 >= 0 && (uint64_t)p0 + 64 * kScanBlocks <= n) {
-      uint32_t w[16 * kScanBlocks];
+    if (p0 != S.p0) {
+      S.p0 = p0;
+      if (p0 >= 0 && (uint64_t)p0 + 64 * kScanBlocks <= n) {
+        uint32_t w[16 * kScanBlocks];
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
-      for (int q = 0; q < 4 * kScanBlocks; ++q) load16((const uint8_t*)A + 16 * q, w + 4 * q);
+        for (int q = 0; q < 4 * kScanBlocks; ++q) load16((const uint8_t*)A + 16 * q, w + 4 * q);
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
-      for (int j = 0; j < kScanBlocks; ++j) {
-        uint64_t mj = 0;
+        for (int j = 0; j < kScanBlocks; ++j) {
+          uint64_t mj = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
-        for (int d = 0; d < 16; ++d) {
-          const uint32_t f = type_bytes(w[16 * j + d]);
-          const uint64_t nib = ((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u);
-          mj |= nib << (4 * d);
-        }
-        m[j] = mj;
-      }
-    } else {
-      for (int j = 0; j < kScanBlocks; ++j) {
-        uint64_t mj = 0;
-        for (int i = 0; i < 64; ++i) {
-          const int64_t p = p0 + 64 * j + i;
-          if (p >= 0 && (uint64_t)p < n) {
-            const uint32_t t = img[p];
-            if (t == 1 || t == 2) mj |= 1ull << i;
+          for (int d = 0; d < 16; ++d) {
+            const uint32_t f = type_bytes(w[16 * j + d]);
+            const uint64_t nib = ((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u);
+            mj |= nib << (4 * d);
           }
+          S.m[j] = mj;
         }
-        m[j] = mj;
+      } else {
+        for (int j = 0; j < kScanBlocks; ++j) {
+          uint64_t mj = 0;
+          for (int i = 0; i < 64; ++i) {
+            const int64_t p = p0 + 64 * j + i;
+            if (p >= 0 && (uint64_t)p < n) {
+              const uint32_t t = img[p];
+              if (t == 1 || t == 2) mj |= 1ull << i;
+            }
+          }
+          S.m[j] = mj;
+        }
       }
     }
     for (int j = 0; j < kScanBlocks; ++j) {
@@ -227,32 +287,33 @@ LSMCK_HD uint64_t next_cand(const uint8_t* img, uint64_t n, uint64_t from, uint6
       const int64_t pj = p0 + 64 * j;
       const int64_t lo = (int64_t)from - pj, hi = (int64_t)e - pj;
       if (hi <= 0) return kNoGuess;
-      uint64_t mj = m[j];
       if (lo >= 64) continue;
+      uint64_t mj = S.m[j];
       if (lo > 0) mj &= ~0ull << lo;
       if (hi < 64) mj &= (1ull << hi) - 1ull;
       while (mj) {
         const int i = __builtin_ctzll(mj);
         mj &= mj - 1;
         const uint64_t c = (uint64_t)(pj + i);
-        if (c + hdr_len(img[c]) <= n) return c;
+        if (c + 13u <= n || c + hdr_len(img[c]) <= n) return c;  // (the byte is read only at the image's end)
       }
     }
   }
 }
-
 // whether the chain from the record start c passes through position q > c
 // (q is at most a hop past the candidate that asks: a bounded walk)
 LSMCK_HD bool reaches(const uint8_t* img, uint64_t n, uint64_t c, uint64_t q) {
   uint64_t p = c;
+  Head h = head(img, n, c);
   while (p < q) {
     bool whole;
-    p = succ(img, n, p, &whole);
-    if (p < q && classify(img, n, p)) return false;
+    p = next_of(h, n, p, &whole);
+    if (p >= q) break;
+    h = head(img, n, p);
+    if (h.cl) return false;
   }
   return p == q;
 }
-
 // The guess of a segment [b, e) (b > start): the first type byte c in it
 // whose header fits and which accept() takes -- unless a later start inside
 // c's first record has a chain through that record's end, which is then
@@ -262,20 +323,20 @@ LSMCK_HD bool reaches(const uint8_t* img, uint64_t n, uint64_t c, uint64_t q) {
 // one, so its walk is taken, but its first "record" covers the true entry,
 // whose chain reaches the merge point.  kNoGuess: no start taken.
 LSMCK_HD uint64_t guess(const uint8_t* img, uint64_t n, uint64_t b, uint64_t e, uint64_t hop) {
-  for (uint64_t c = next_cand(img, n, b, e); c != kNoGuess; c = next_cand(img, n, c + 1, e)) {
+  Scan S;
+  for (uint64_t c = next_cand(S, img, n, b, e); c != kNoGuess; c = next_cand(S, img, n, c + 1, e)) {
     if (!accept(img, n, c, hop)) continue;
     for (;;) {
       bool whole;
-      const uint64_t q1 = succ(img, n, c, &whole), lim = q1 < e ? q1 : e;
-      uint64_t c2 = next_cand(img, n, c + 1, lim);
-      while (c2 != kNoGuess && !reaches(img, n, c2, q1)) c2 = next_cand(img, n, c2 + 1, lim);
+      const uint64_t q1 = next_of(head(img, n, c), n, c, &whole), lim = q1 < e ? q1 : e;
+      uint64_t c2 = next_cand(S, img, n, c + 1, lim);
+      while (c2 != kNoGuess && !reaches(img, n, c2, q1)) c2 = next_cand(S, img, n, c2 + 1, lim);
       if (c2 == kNoGuess) return c;
       c = c2;
     }
   }
   return kNoGuess;
 }
-
 // --- the per-thread steps of the kernels ------------------------------------
 // Per segment k: g[k] (the guessed entry), x[k] (kExit: the exit; kBad: the
 // bad byte), code[k], recs[k].  info: u64 words, see kInfo*.
@@ -314,13 +375,13 @@ LSMCK_HD uint32_t seg_of(const SegArgs& a, uint64_t pos) { return (uint32_t)((po
 // the forced walk of segment k from its entry c (a position on the chain)
 LSMCK_HD void seg_forced(const SegArgs& a, uint32_t k, uint64_t c) {
   WalkOut o;
-  const uint32_t cl = classify(a.img, a.n, c);
-  if (cl) {
-    o.code = cl;
+  const Head h = head(a.img, a.n, c);
+  if (h.cl) {
+    o.code = h.cl;
     o.pos = c;
     o.recs = 0;
   } else {
-    walk(a.img, a.n, c, seg_end(a, k), &o);
+    walk(a.img, a.n, c, h, seg_end(a, k), &o);
   }
   a.g[k] = c;
   a.x[k] = o.pos;
@@ -391,24 +452,23 @@ LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint
   uint64_t p = a.g[k];
   const uint8_t* img = a.img;
   for (uint32_t r = 0; r < a.recs[k]; ++r, ++i) {
-    const uint32_t t = img[p];
-    const uint32_t h = hdr_len(t);
-    const uint32_t klen = rd32(img + p + 5), vlen = t == 1 ? rd32(img + p + 9) : 0u;
-    const uint32_t dlen = klen + vlen;
-    const uint64_t avail = a.n - (p + h);
+    const Head h = head(img, a.n, p);
+    const uint32_t hl = hdr_len(h.t);
+    const uint32_t dlen = h.klen + h.vlen;
+    const uint64_t avail = a.n - (p + hl);
     const uint32_t got = dlen <= avail ? dlen : (uint32_t)avail;
     Rec R;
     R.rec_off = p;
-    R.payload_off = p + h;
-    R.klen = klen;
-    R.vlen = vlen;
-    R.crc = rd32(img + p + 1);
-    R.type = t;
+    R.payload_off = p + hl;
+    R.klen = h.klen;
+    R.vlen = h.vlen;
+    R.crc = h.crc;
+    R.type = h.t;
     recs[i] = R;
-    poff[i] = p + h;
+    poff[i] = p + hl;
     plen[i] = got;
-    pcrc[i] = R.crc;
-    p += h + got;
+    pcrc[i] = h.crc;
+    p += hl + got;
   }
 }
 
