@@ -286,9 +286,14 @@ int lsmck_sha256_batch_fixed(lsmck_ctx* ctx, const uint8_t* base, size_t stride,
  * *nrec = records accepted before the stop.  flags: LSMCK_HOST (optionally
  * | LSMCK_HOST_PINNED) or LSMCK_DEVICE for `wal`, optionally
  * | LSMCK_RECS_PINNED: `recs` is page-locked (lsmck_host_alloc_pinned), and
- * the records are DMA'd into it straight from the device (no staging copy).
- * Synchronous. */
+ * the records are DMA'd into it straight from the device (no staging copy),
+ * or | LSMCK_RECS_DEVICE: `recs` is device memory (cap entries) and the
+ * records stay there -- for a device-resident log whose consumer runs on the
+ * GPU; the segment walk writes them in place when all of them fit, and no
+ * record crosses the host link (any path that walks on the host copies its
+ * records up).  Synchronous. */
 #define LSMCK_RECS_PINNED 0x8u
+#define LSMCK_RECS_DEVICE 0x10u
 #define LSMCK_WAL_CORRUPTED 1
 #define LSMCK_WAL_REMOVE_PANIC 2
 #define LSMCK_WAL_BAD_TYPE 3

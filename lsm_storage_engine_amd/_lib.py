@@ -39,6 +39,7 @@ HOST = 0x0
 HOST_PINNED = 0x2
 SORTED = 0x4  # LSMCK_SORTED: device descriptors sorted inside one readable span (include/lsmck.h)
 RECS_PINNED = 0x8  # LSMCK_RECS_PINNED: lsmck_wal_replay_verify's records array is page-locked
+RECS_DEVICE = 0x10  # LSMCK_RECS_DEVICE: the records array is device memory (include/lsmck.h)
 
 u8p = C.POINTER(C.c_uint8)
 u32p = C.POINTER(C.c_uint32)

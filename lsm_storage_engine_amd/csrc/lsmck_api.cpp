@@ -257,6 +257,12 @@ struct lsmck_ctx {
     unsigned long long* h_sinfo = nullptr;
   } wd;
   bool wal_recs_direct = false;  // this replay's records go by DMA into the caller's pinned array (under wal_mu)
+  // LSMCK_RECS_DEVICE (under wal_mu): the caller's device array and its capacity
+  // (the segment walk emits straight into it when every record fits), and
+  // whether this replay's emit did
+  lsmck_wal_rec* wal_recs_dev = nullptr;
+  size_t wal_recs_dev_cap = 0;
+  bool wal_recs_dev_emitted = false;
   int wal_seg = 1;           // device WAL walk: 1 = the segment walk first (default), 0 = candidate doubling only
   uint64_t wal_seg_bytes = 0;  // segment walk: bytes per segment (0 = auto, ~2^19 segments)
   int wal_seg_rounds = 16;   // segment walk: repairs before it declines to the candidate-doubling walk
@@ -1230,7 +1236,12 @@ static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t ter
     std::function<int()> copy_out;
     const size_t todo = m - done;
     const size_t ntake = std::min(m, cap) > done ? std::min(m, cap) - done : 0;  // records for the caller's array
-    if (recs && cap && todo && ctx->wal_recs_direct) {
+    if (ctx->wal_recs_dev) {
+      // LSMCK_RECS_DEVICE: the records stay on the device (emitted there, or
+      // copied from the walk's own array); nothing crosses the link
+      if (recs && ntake && !ctx->wal_recs_dev_emitted)
+        HIPCHK(hipMemcpyAsync(recs + done, W.recs + done, ntake * sizeof(lsmck_wal_rec), hipMemcpyDeviceToDevice, st));
+    } else if (recs && cap && todo && ctx->wal_recs_direct) {
       // the caller's array is pinned: the records go there by DMA, on the
       // staging stream, beside the CRC pass and the compare
       if ((rc = stage_init(ctx->stage[0]))) return rc;
@@ -1286,7 +1297,9 @@ static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t ter
   if (nbad) {
     lsmck_wal_rec r;
     uint32_t got = 0;
-    if (recs && cap && first < done)
+    if (ctx->wal_recs_dev)
+      HIPCHK(hipMemcpy(&r, (ctx->wal_recs_dev_emitted ? recs : W.recs) + first, sizeof r, hipMemcpyDeviceToHost));
+    else if (recs && cap && first < done)
       r = ctx->h_wrecs1[first];
     else if (recs && cap && ctx->wal_recs_direct && first < std::min(m, cap))
       r = recs[first];
@@ -1454,14 +1467,17 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
   out->tpos = W.h_sinfo[sg::kInfoPos];
   if (m) {
     const size_t tot = at + m;
-    if ((rc = ensure_dev_keep(&W.recs, &W.cap_recs, tot, at, st)) ||
+    // LSMCK_RECS_DEVICE with room for every record: emitted into the caller's array
+    const bool dev = ctx->wal_recs_dev && at == 0 && tot <= ctx->wal_recs_dev_cap;
+    if ((!dev && (rc = ensure_dev_keep(&W.recs, &W.cap_recs, tot, at, st))) ||
         (rc = ensure_dev_keep(&ctx->d_woff, &ctx->cap_woff, tot, at, st)) ||
         (rc = ensure_dev_keep(&ctx->d_wlen, &ctx->cap_wlen, tot, at, st)) ||
         (rc = ensure_dev_keep(&ctx->d_wexp, &ctx->cap_wexp, tot, at, st)) ||
         (rc = ensure_dev_keep(&ctx->d_vcrc, &ctx->cap_vcrc, tot, at, st)))
       return rc;
-    if ((rc = lsmk_wal_seg_emit(&a, at, W.recs, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st)))
+    if ((rc = lsmk_wal_seg_emit(&a, at, dev ? ctx->wal_recs_dev : W.recs, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st)))
       return launch_rc(rc, "wal segment emit kernel");
+    ctx->wal_recs_dev_emitted = dev;
   }
   if (!ctx->wal_emit_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_emit_ev, hipEventDisableTiming));
   HIPCHK(hipEventRecord(ctx->wal_emit_ev, st));
@@ -1722,6 +1738,42 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
     ~RecsDirect() { f = false; }
   };
   const bool recs_pinned = (flags & LSMCK_RECS_PINNED) != 0;
+  if (flags & LSMCK_RECS_DEVICE) {
+    if (recs_pinned) return lsmck_host::set_error(LSMCK_EINVAL, "LSMCK_RECS_DEVICE with LSMCK_RECS_PINNED");
+    struct RecsDev {  // set while wal_mu is held, cleared on every return
+      lsmck_ctx* c;
+      RecsDev(lsmck_ctx* c_, lsmck_wal_rec* r, size_t cap) : c(c_) {
+        c->wal_recs_dev = r;
+        c->wal_recs_dev_cap = r ? cap : 0;
+        c->wal_recs_dev_emitted = false;
+      }
+      ~RecsDev() {
+        c->wal_recs_dev = nullptr;
+        c->wal_recs_dev_cap = 0;
+        c->wal_recs_dev_emitted = false;
+      }
+    };
+    if ((flags & LSMCK_DEVICE) && ctx->wal_gpu_walk) {
+      std::lock_guard<std::mutex> wl(ctx->wal_mu);
+      RecsDev rd(ctx, recs, cap);
+      rc = wal_replay_device(ctx, wal, n, recs, cap, nrec, bad_index, bad_crc, bad_expected);
+      if (rc != kWalHostWalk) return rc;
+    }
+    // any other path makes the records on the host: into a host array, then
+    // copied to the caller's device array
+    std::vector<lsmck_wal_rec> tmp(recs ? std::min<size_t>(cap, n / 9 + 1) : 0);
+    size_t got = 0;
+    rc = lsmck_wal_replay_verify(ctx, wal, n, flags & ~LSMCK_RECS_DEVICE, recs ? tmp.data() : nullptr, tmp.size(),
+                                 &got, bad_index, bad_crc, bad_expected);
+    if (rc < 0) return rc;
+    if (nrec) *nrec = got;
+    const size_t k = std::min(got, tmp.size());
+    if (k) {
+      DevGuard g(ctx->dev);
+      HIPCHK(hipMemcpy(recs, tmp.data(), k * sizeof(lsmck_wal_rec), hipMemcpyHostToDevice));
+    }
+    return rc;
+  }
   if ((flags & LSMCK_DEVICE) && ctx->wal_gpu_walk) {
     std::lock_guard<std::mutex> wl(ctx->wal_mu);  // the walk's bitmap (ctx->wd) is shared with the upload path
     RecsDirect rd(ctx->wal_recs_direct, recs_pinned);

@@ -285,6 +285,23 @@ class Context:
         # nrec counts the whole log's accepted records; at most cap of them were written
         return recs[:min(nrec.value, cap)].view(np.recarray), rc, (bi.value, bc.value, be.value)
 
+    def wal_replay_verify_to_device(self, image, recs_ptr, cap, device_ptr=None):
+        """The replay with its records left in device memory (LSMCK_RECS_DEVICE):
+        recs_ptr is a device array of cap lsmck_wal_rec entries (32 bytes each,
+        WAL_REC_DTYPE).  Returns (nrec, status, (bad_index, bad_crc, bad_expected));
+        min(nrec, cap) records were written."""
+        if device_ptr is None:
+            img = np.frombuffer(image, dtype=np.uint8) if len(image) else np.zeros(1, dtype=np.uint8)[:0]
+            ptr, n, flags = img.ctypes.data, len(img), _lib.HOST
+        else:
+            ptr, n, flags = device_ptr, image, _lib.DEVICE
+        nrec = C.c_size_t()
+        bi, bc, be = C.c_uint64(), C.c_uint32(), C.c_uint32()
+        rc = _lib.check(self.lib.lsmck_wal_replay_verify(self.handle, ptr, n, flags | _lib.RECS_DEVICE, recs_ptr, cap,
+                                                         C.byref(nrec), C.byref(bi), C.byref(bc), C.byref(be)),
+                        "wal_replay_verify")
+        return nrec.value, rc, (bi.value, bc.value, be.value)
+
     def checksums_verify_many(self, triples):
         n = len(triples)
         arr = C.c_char_p * max(n, 1)

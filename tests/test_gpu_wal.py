@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from lsm_storage_engine_amd import _lib, wal
+from lsm_storage_engine_amd.device import WAL_REC_DTYPE
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -512,6 +513,49 @@ def test_pinned_records(ctx, device):
                 if st:
                     assert bad[:3] == obad[:3]
                 del recs
+        finally:
+            if d:
+                d.free()
+
+
+@pytest.mark.parametrize("device", [False, True])
+@pytest.mark.parametrize("seg_walk", [1, 0])
+def test_device_records(ctx, seg_opts, device, seg_walk):
+    """LSMCK_RECS_DEVICE: the records left in a device array -- emitted there
+    by the segment walk when all fit, copied on the device when cap is below
+    the count or the doubling walk ran, copied up after a host walk (host
+    image) -- the oracle's records and outcome in every case, a corrupted
+    Insert's CorruptedData included; entries past the count stay untouched."""
+    seg_opts(wal_seg_walk=seg_walk)
+    img = _binary_log(30000, 72)
+    st, orecs, _ = O.wal_replay(img)
+    b = bytearray(img)
+    r = next(r for r in orecs[20000:] if r.type == 1 and r.klen + r.vlen > 0)
+    b[r.payload_off] ^= 0x20
+    rec_bytes = WAL_REC_DTYPE.itemsize
+    for im in (img, bytes(b)):
+        ost, orr, obad = O.wal_replay(im)
+        d = None
+        if device:
+            d = ctx.alloc(len(im))
+            d.upload(np.frombuffer(im, np.uint8))
+        try:
+            for cap in (40000, 5000):
+                out = ctx.alloc(cap * rec_bytes)
+                try:
+                    out.upload(np.full(cap * rec_bytes, 0xA5, np.uint8))
+                    n, st, bad = (ctx.wal_replay_verify_to_device(len(im), out.ptr, cap, device_ptr=d.ptr) if device
+                                  else ctx.wal_replay_verify_to_device(im, out.ptr, cap))
+                    assert st == ost and n == len(orr)
+                    got = out.download(np.uint8, cap * rec_bytes).view(WAL_REC_DTYPE)
+                    k = min(n, cap)
+                    assert [int(x) for x in got["rec_off"][:k]] == [x.rec_off for x in orr][:k]
+                    assert [int(x) for x in got["crc"][:k]] == [x.crc for x in orr][:k]
+                    assert (got.view(np.uint8)[k * rec_bytes:] == 0xA5).all()
+                    if st:
+                        assert bad[:3] == obad[:3]
+                finally:
+                    out.free()
         finally:
             if d:
                 d.free()

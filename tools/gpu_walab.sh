@@ -5,6 +5,7 @@
 #   LIBS="A B" ROUNDS=2 BIG=16777216 R=r04g bash tools/gpu_walab.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
+export WAL_KT_DEVRECS=${WAL_KT_DEVRECS:-0}  # (builds before LSMCK_RECS_DEVICE would misread the flag)
 O=gpurun_out/${R:-walab}
 mkdir -p $O
 L=lsm_storage_engine_amd
@@ -20,3 +21,13 @@ for r in $(seq 1 ${ROUNDS:-2}); do
   done
 done
 restore
+# then, with KT=1, a kernel trace of the small replay per build
+if [ -n "$KT" ]; then
+  for N in $LIBS; do
+    cp $L/ab/$N.so $L/liblsmck.so
+    timeout -k 10 150 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_small_$N -o kt -- python3 tools/wal_kt.py > $O/kt_small_$N.log 2>&1 || { echo "kt $N failed"; restore; exit 1; }
+    python3 tools/kt_stats.py $O/kt_small_$N > $O/kt_stats_small_$N.txt 2>&1
+    grep -E "wal_seg|crc32_stream|copyBuffer" $O/kt_stats_small_$N.txt | head -8
+  done
+  restore
+fi

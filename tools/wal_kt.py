@@ -46,6 +46,18 @@ def main():
         del recs
     out["device_image_pinned_recs_ms_best"] = round(min(ts[1:]) * 1e3, 3)
     out["device_image_pinned_recs_ms_median"] = round(float(np.median(ts[1:])) * 1e3, 3)
+    from lsm_storage_engine_amd.device import WAL_REC_DTYPE
+    rb = ctx.alloc(500_000 * WAL_REC_DTYPE.itemsize)
+    ts = []  # the records left in device memory (LSMCK_RECS_DEVICE; builds before it: WAL_KT_DEVRECS=0)
+    for _ in range(11 if os.environ.get("WAL_KT_DEVRECS", "1") != "0" else 0):
+        t = time.perf_counter()
+        m, st, _ = ctx.wal_replay_verify_to_device(len(img), rb.ptr, 500_000, device_ptr=d.ptr)
+        ts.append(time.perf_counter() - t)
+        assert st == 0 and m == 500_000
+    rb.free()
+    if ts:
+        out["device_image_device_recs_ms_best"] = round(min(ts[1:]) * 1e3, 3)
+        out["device_image_device_recs_ms_median"] = round(float(np.median(ts[1:])) * 1e3, 3)
     out["walk"] = {"path": ctx.get_stat("wal_walk_path"), "segments": ctx.get_stat("wal_segments"),
                    "repairs": ctx.get_stat("wal_seg_repairs")}
     print(out)

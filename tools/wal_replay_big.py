@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--seg-walk", type=int, default=1, help="0: the candidate-doubling walk (A/B)")
     ap.add_argument("--pinned-recs", type=int, default=1,
                     help="1: the records DMA'd into a page-locked array (LSMCK_RECS_PINNED); 0: staged + copied")
+    ap.add_argument("--device-recs", type=int, default=0,
+                    help="1: then the same replays with the records left in device memory (LSMCK_RECS_DEVICE)")
     a = ap.parse_args()
     n = a.records
     ln = gen_zipf_lengths(0x5EED0003, n)
@@ -74,6 +76,27 @@ def main():
             times.append(dt)
         print(f"replay {s}: {dt * 1e3:.1f} ms", file=sys.stderr, flush=True)
         del recs  # the wrapper reuses its records array once no result refers to it
+    dev = None
+    if a.device_recs:  # the records stay in HBM: the walk, the CRC pass and the compare, no host link
+        from lsm_storage_engine_amd.device import WAL_REC_DTYPE
+        rb = ctx.alloc(n * WAL_REC_DTYPE.itemsize)
+        dts = []
+        for s in range(a.steps + 1):
+            ctx.sync()
+            t = time.perf_counter()
+            m, st, bad = ctx.wal_replay_verify_to_device(total, rb.ptr, n, device_ptr=d.ptr)
+            dt = time.perf_counter() - t
+            assert st == 0 and m == n, (st, m, bad)
+            if s:
+                dts.append(dt)
+            print(f"replay (records on the device) {s}: {dt * 1e3:.1f} ms", file=sys.stderr, flush=True)
+        crc = rb.download(np.uint8, n * WAL_REC_DTYPE.itemsize).view(WAL_REC_DTYPE)["crc"]
+        dsum = "%08x" % zlib.crc32(np.ascontiguousarray(crc).astype("<u4").tobytes())
+        rb.free()
+        dmed = float(np.median(dts))
+        dev = {"ms_median": round(dmed * 1e3, 2), "ms_best": round(min(dts) * 1e3, 2),
+               "value": round(total / GIB / dmed, 1), "summary_crc32": dsum,
+               "summary_matches_oracle": bool(golden) and dsum == golden["summary_crc32"]}
     d.free()
     best, med = min(times), float(np.median(times))
     print(json.dumps({
@@ -84,6 +107,7 @@ def main():
         "records_out_bytes": 32 * n, "pinned_recs": bool(a.pinned_recs),
         "walk_path": {1: "segment walk", 2: "candidate doubling", 3: "host walk"}.get(ctx.get_stat("wal_walk_path")),
         "seg_repairs": ctx.get_stat("wal_seg_repairs"), "segments": ctx.get_stat("wal_segments"),
+        "records_on_device": dev,
         "workload": "config 3's 2^26 Zipf payloads (64 B-64 KiB) framed as wal.rs Insert records (13-byte headers), "
                     "headers and CRCs written on the device"}))
 
