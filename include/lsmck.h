@@ -177,6 +177,18 @@ int lsmck_device_count(void);
  *                 compression blocks run on a lean kernel with more waves per
  *                 SIMD (default 12; 0 = every message on the window kernel).
  *                 Digests are identical either way.
+ *   "sha_short_conc"  1: that lean kernel runs on a second stream, beside the
+ *                 window kernel instead of after it (default 0).  A/B switch;
+ *                 digests are identical either way.
+ *   "sha_short_pf"  1: that lean kernel issues a block's loads before the
+ *                 previous block's compression (default 0).  A/B switch.
+ *   "sha_sorted_desc"  1: an ordered batch's descriptors are gathered into
+ *                 order first, so lanes read them contiguously (default 0).
+ *                 A/B switch.
+ *   "sha_pair"    the window kernel loads two blocks (a 128-B line) per window
+ *                 (1, default) or one (0); 2 and 3 are diagnostics (no payload
+ *                 loads: digests invalid / line-aligned loads realigned
+ *                 through LDS).
  *   "tree_active_files" / "tree_slice_bytes"  lsmck_checksums_verify_many's
  *                 files in flight (0 = 8192) and bytes of a file per round
  *                 (0 = 128 KiB; a multiple of 64).  Tests use small values.
@@ -192,6 +204,9 @@ int lsmck_device_count(void);
  *                 on the GPU (default), 0 = read back and walk on the host.
  *   "wal_upload_min"  host images of at least this many bytes are uploaded and
  *                 walked on the GPU (default 1 MiB; 0 = always the host walk).
+ *   "wal_split"   an uploaded host image is walked in two parts, the first
+ *                 behind the upload of the second (1, default; taken when each
+ *                 half holds one "wal_stage_bytes" chunk), or whole after it (0).
  *   "wal_stage_bytes"  an uploaded host WAL image moves in chunks of this many
  *                 bytes (pageable: copied into a pinned slot, then DMA'd; each
  *                 chunk's candidate marking runs behind its DMA); a multiple

@@ -70,7 +70,7 @@ struct ShaSliceParams {
 
 extern "C" {
 int lsmk_launch_crc32_fixed(const lsmck::CrcParams* P, int ncu, int variant, hipStream_t st);
-int lsmk_launch_sha256(const lsmck::ShaParams* P, hipStream_t st);
+int lsmk_launch_sha256(const lsmck::ShaParams* P, hipStream_t st, hipStream_t st2 = nullptr);
 int lsmk_launch_sha256_slices(const lsmck::ShaSliceParams* P, hipStream_t st);
 uint64_t lsmk_walk_sb_count(uint64_t n);
 int lsmk_launch_crc32_walk(const lsmck::CrcParams* P, uint64_t* sb_prefix, int ncu, int variant, hipStream_t st);

@@ -493,7 +493,8 @@ __global__ __launch_bounds__(256) void gen_stream_kernel(unsigned char* dst, uin
 
 using namespace lsmck;
 
-extern "C" int lsmk_launch_sha256(const ShaParams* P, hipStream_t st) {
+// st2 (or null: st): the stream of the short-tail kernel (the caller orders it)
+extern "C" int lsmk_launch_sha256(const ShaParams* P, hipStream_t st, hipStream_t st2) {
   if (P->nmsg == 0) return 0;
   uint64_t blocks = (P->nmsg + 255) / 256;
   if (P->pair == 2)  // diagnostic: the pair kernel without its payload loads
@@ -505,10 +506,11 @@ extern "C" int lsmk_launch_sha256(const ShaParams* P, hipStream_t st) {
   else
     hipLaunchKernelGGL(sha256_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, *P);
   if (P->split && P->order && P->len) {  // the short tail of the order (its start on the device)
+    hipStream_t s = st2 ? st2 : st;
     if (P->short_pf)
-      hipLaunchKernelGGL(sha256_short_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, *P);
+      hipLaunchKernelGGL(sha256_short_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, *P);
     else
-      hipLaunchKernelGGL(sha256_short_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, *P);
+      hipLaunchKernelGGL(sha256_short_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, *P);
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
