@@ -1411,17 +1411,20 @@ static int wal_walk_from(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t 
   }
 }
 
-// The segment walk (lsmck_segwalk.h) of the chain from `start` to the end of
-// the image: every segment's guess and walk, check rounds (one host sync
-// each; a failure is repaired on the device and checked again), then the
-// records emitted after the `at` already there, the emit's completion
-// recorded on ctx->wal_emit_ev (the records' read-back waits for that, not
-// for the CRC pass behind it).  kWalSegDecline: more failures than
-// wal_seg_rounds -- payloads that look like framed records along the chain;
-// the caller walks by candidate doubling instead.
+// The segment walk (lsmck_segwalk.h) of the chain from `start`: the records
+// that start in [start, lim) (lim = n: to the end of the image) -- every
+// segment's guess and walk, check rounds (one host sync each; a failure is
+// repaired on the device and checked again), then the records emitted after
+// the `at` already there, the emit's completion recorded on
+// ctx->wal_emit_ev (the records' read-back waits for that, not for the CRC
+// pass behind it).  out->term: END / kWalBad where the chain ends, or
+// kWalStop with out->tpos = the first record start at or past lim (the next
+// prefix starts there).  kWalSegDecline: more failures than wal_seg_rounds --
+// payloads that look like framed records along the chain; the caller walks
+// by candidate doubling instead.
 constexpr int kWalSegDecline = 0x7FFF0004;
-static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t start, size_t at, hipStream_t st,
-                        const WalTrace& tr, WalPart* out) {
+static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t start, uint64_t lim, size_t at,
+                        hipStream_t st, const WalTrace& tr, WalPart* out) {
   namespace sg = lsmck::seg;
   auto& W = ctx->wd;
   int rc;
@@ -1434,12 +1437,13 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
     out->tpos = 0;
     return 0;
   }
-  uint64_t S = lsmk_wal_seg_bytes(n - start, ctx->wal_seg_bytes);
+  if (lim > n || lim <= start) lim = n;
+  uint64_t S = lsmk_wal_seg_bytes(lim - start, ctx->wal_seg_bytes);
   sg::SegArgs a{};
   int resegs = 0;
   for (int round = 0;; ++round) {
     if (round == 0) {  // (re)segment and walk every segment
-      const uint64_t K64 = (n - start + S - 1) / S;
+      const uint64_t K64 = (lim - start + S - 1) / S;
       if (K64 >= (1ull << 31)) return kWalSegDecline;  // (tiny forced segments over a huge log)
       const uint32_t K = (uint32_t)K64;
       ctx->last_segments = K;
@@ -1460,7 +1464,7 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
       }
       if (!W.sinfo) HIPCHK(hipMalloc((void**)&W.sinfo, sg::kInfoWords * 8));
       if (!W.h_sinfo) HIPCHK(hipHostMalloc((void**)&W.h_sinfo, sg::kInfoWords * 8, hipHostMallocDefault));
-      a = sg::SegArgs{img, n, start, S, K, W.sg, W.sx, W.scode, W.srecs, W.spre, W.sinfo};
+      a = sg::SegArgs{img, n, start, S, K, W.sg, W.sx, W.scode, W.srecs, W.spre, W.sinfo, lim};
       if ((rc = lsmk_wal_seg_walk(&a, st))) return launch_rc(rc, "wal segment walk kernel");
     }
     if ((rc = lsmk_wal_seg_round(&a, W.sbsum, st))) return launch_rc(rc, "wal segment check kernels");
@@ -1490,7 +1494,8 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
   }
   const uint64_t m = W.h_sinfo[sg::kInfoRecs];
   out->m = at + m;
-  out->term = W.h_sinfo[sg::kInfoCode] == sg::kBad ? kWalBad : 0xFFFFFFFFu;
+  const uint64_t code = W.h_sinfo[sg::kInfoCode];
+  out->term = code == sg::kBad ? kWalBad : (code == sg::kExit ? kWalStop : 0xFFFFFFFFu);
   out->tpos = W.h_sinfo[sg::kInfoPos];
   if (m) {
     const size_t tot = at + m;
@@ -1525,7 +1530,7 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
   if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
   hipStream_t st = so.st;
   WalPart P;
-  rc = ctx->wal_seg && !ctx->wal_part_bytes ? wal_seg_walk(ctx, img, n, 0, 0, st, tr, &P) : kWalSegDecline;
+  rc = ctx->wal_seg && !ctx->wal_part_bytes ? wal_seg_walk(ctx, img, n, 0, n, 0, st, tr, &P) : kWalSegDecline;
   if (rc == 0) {  // the CRC pass over every record, then the compare and the records
     if ((rc = wal_crc_part(ctx, img, 0, P.m, st))) return rc;
     return wal_finish(ctx, img, P.m, P.term, P.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr, 0,
@@ -1727,7 +1732,7 @@ static int wal_replay_split(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool p
   // (in parts, when the rest's scratch would not fit)
   const uint64_t r = P1.tpos;
   if (ctx->wal_seg && !ctx->wal_part_bytes) {
-    rc = wal_seg_walk(ctx, d, n, r, P1.m, st, tr, &P2);
+    rc = wal_seg_walk(ctx, d, n, r, n, P1.m, st, tr, &P2);
     if (rc == 0) {
       if ((rc = wal_crc_part(ctx, d, P1.m, P2.m - P1.m, st))) return rc;
       return wal_finish(ctx, d, P2.m, P2.term, P2.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr,

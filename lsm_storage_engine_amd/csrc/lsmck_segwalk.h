@@ -348,29 +348,37 @@ enum : int {
   kInfoPos = 4,    // finalize: jterm's bad byte
   kInfoFailX = 5,  // finalize: the failing segment's exit
   kInfoNFail = 6,  // u32 at info word 6: how many segments fail the check (atomic add)
+  kInfoLast = 7,   // u32 at info word 7: 1 + the last guessed segment whose exit is at or past lim (atomic max)
   kInfoWords = 8
 };
 
+// The walk covers the records that start in [start, lim) (lim <= n: a prefix
+// of the rest of the log; the next prefix resumes at the first record start
+// at or past lim, its records emitted after these).
 struct SegArgs {
   const uint8_t* img;
   uint64_t n;
   uint64_t start;  // the chain's first record
   uint64_t S;      // segment bytes
-  uint32_t K;      // segments: ceil((n - start) / S)
+  uint32_t K;      // segments: ceil((lim - start) / S)
   uint64_t* g;
   uint64_t* x;
   uint32_t* code;
   uint32_t* recs;
   uint64_t* pre;  // K + 1: exclusive scan of the placement words
   unsigned long long* info;
+  uint64_t lim;   // the prefix end
 };
 
 LSMCK_HD uint64_t seg_begin(const SegArgs& a, uint32_t k) { return a.start + (uint64_t)k * a.S; }
 LSMCK_HD uint64_t seg_end(const SegArgs& a, uint32_t k) {
   const uint64_t e = a.start + (uint64_t)(k + 1) * a.S;
-  return e < a.n ? e : a.n;
+  return e < a.lim ? e : a.lim;
 }
-LSMCK_HD uint32_t seg_of(const SegArgs& a, uint64_t pos) { return (uint32_t)((pos - a.start) / a.S); }
+// the segment holding pos; K for a position at or past lim (beyond the prefix)
+LSMCK_HD uint32_t seg_of(const SegArgs& a, uint64_t pos) {
+  return pos >= a.lim ? a.K : (uint32_t)((pos - a.start) / a.S);
+}
 
 // the forced walk of segment k from its entry c (a position on the chain)
 LSMCK_HD void seg_forced(const SegArgs& a, uint32_t k, uint64_t c) {
@@ -417,7 +425,7 @@ LSMCK_HD bool seg_check_fails(const SegArgs& a, uint32_t k, uint32_t jterm) {
   if (a.code[k] != kExit) return true;  // (cannot happen: jterm is the first chain end)
   const uint32_t t = seg_of(a, a.x[k]);
   const uint64_t between = (a.pre[t] >> kSegShift) - (a.pre[k + 1] >> kSegShift);
-  return between != 0 || a.g[t] != a.x[k];
+  return between != 0 || (t < a.K && a.g[t] != a.x[k]);  // (t == K: the exit leaves the prefix)
 }
 
 // repair after a failure at segment j (whose entry is right): the segments
@@ -429,7 +437,7 @@ LSMCK_HD void seg_repair(const SegArgs& a, uint32_t j, uint32_t budget) {
     if (a.code[j] != kExit) return;
     const uint64_t xe = a.x[j];
     const uint32_t t = seg_of(a, xe);
-    bool clean = a.g[t] == xe;
+    bool clean = t == a.K || a.g[t] == xe;  // (t == K: the exit leaves the prefix)
     for (uint32_t u = j + 1; u < t; ++u) {
       if (a.code[u] != kNone) clean = false;
       a.g[u] = kNoGuess;

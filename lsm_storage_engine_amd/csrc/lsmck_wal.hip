@@ -419,6 +419,10 @@ __global__ __launch_bounds__(256) void wal_seg_check(seg::SegArgs a) {
     atomicMin((unsigned int*)(a.info + seg::kInfoFail), k);
     atomicAdd((unsigned int*)(a.info + seg::kInfoNFail), 1u);
   }
+  // the chain's way out of a prefix (lim < n): the last guessed segment whose
+  // exit lies at or past lim (once the check passes, the only one)
+  if (k < a.K && k < jterm && a.code[k] == seg::kExit && a.x[k] >= a.lim)
+    atomicMax((unsigned int*)(a.info + seg::kInfoLast), k + 1u);
 }
 
 // the round's outcome into info (one thread)
@@ -426,8 +430,9 @@ __global__ void wal_seg_finalize(seg::SegArgs a) {
   const uint32_t jterm = (uint32_t)a.info[seg::kInfoJterm], fail = (uint32_t)a.info[seg::kInfoFail];
   a.info[seg::kInfoRecs] = a.pre[a.K] & seg::kRecMask;
   const bool jt = jterm < a.K;
-  a.info[seg::kInfoCode] = jt ? a.code[jterm] : 0u;
-  a.info[seg::kInfoPos] = jt ? a.x[jterm] : 0ull;
+  const uint32_t last = (uint32_t)a.info[seg::kInfoLast];  // (no chain end in the prefix: its way out)
+  a.info[seg::kInfoCode] = jt ? a.code[jterm] : (last ? seg::kExit : 0u);
+  a.info[seg::kInfoPos] = jt ? a.x[jterm] : (last ? a.x[last - 1u] : 0ull);
   a.info[seg::kInfoFailX] = fail < a.K ? a.x[fail] : 0ull;
 }
 
@@ -436,6 +441,7 @@ __global__ void wal_seg_reset(seg::SegArgs a) {
   a.info[seg::kInfoJterm] = seg::kNoSeg;
   a.info[seg::kInfoFail] = seg::kNoSeg;
   a.info[seg::kInfoNFail] = 0;
+  a.info[seg::kInfoLast] = 0;
 }
 
 __global__ void wal_seg_repair(seg::SegArgs a, uint32_t budget) {

@@ -45,6 +45,23 @@ def sim(tmp_path_factory):
         if rc == 1:
             return None
         return list(offs[:m.value]), code.value, (pos.value if code.value == BAD else 0), rep.value
+    lib.segwalk_sim_prefix.restype = C.c_int
+    lib.segwalk_sim_prefix.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, u64p,
+                                       C.c_size_t, u64p, C.POINTER(C.c_uint32), u64p, C.POINTER(C.c_int), u64p,
+                                       C.POINTER(C.c_uint32)]
+
+    def prefix(img, start, lim, S, rounds=16):
+        """(records starting in [start, lim), code, pos): pos is where the
+        next prefix starts when code is EXIT (1), the bad byte for BAD"""
+        a = np.frombuffer(bytes(img), np.uint8)
+        cap = len(img) // 9 + 2
+        offs = (C.c_uint64 * cap)()
+        m, code, pos, rep, K, nf = C.c_uint64(), C.c_uint32(), C.c_uint64(), C.c_int(), C.c_uint64(), C.c_uint32()
+        rc = lib.segwalk_sim_prefix(a.ctypes.data, len(img), start, lim, S, rounds, offs, cap, C.byref(m),
+                                    C.byref(code), C.byref(pos), C.byref(rep), C.byref(K), C.byref(nf))
+        assert rc in (0, 1), rc
+        return None if rc == 1 else (list(offs[:m.value]), code.value, pos.value)
+    run.prefix = prefix
     return run
 
 
@@ -188,3 +205,47 @@ def test_huge_lengths_wrap(sim):
     img = bytearray(r * 50 + struct.pack("<BIII", 1, 0, 5, 1 << 30) + b"abc")
     for S in (64, 200):
         check(sim, img, S)
+
+
+@pytest.mark.parametrize("S", [64, 512, 4096])
+@pytest.mark.parametrize("parts", [2, 5, 17])
+def test_prefix_walks_chain_to_the_whole(sim, S, parts):
+    """The walk in prefixes (lim < n: the records that start before lim, and
+    the first record start at or past lim as the next prefix's start), as the
+    pipelined device replay runs it: the prefixes' records in order are the
+    whole chain's, whatever the cut points -- inside headers, payloads, long
+    records that cross several prefixes -- and the chain's end (clean EOF,
+    truncated tail, bad type byte) lands in the right prefix."""
+    rng = np.random.default_rng(S * 31 + parts)
+    img = bytearray(random_log(rng, 3000, hi=900))
+    for variant in range(3):
+        im = bytes(img)
+        if variant == 1:
+            im = im[:len(im) - 7]  # EOF inside a payload or a header
+        if variant == 2:
+            want, _, _ = chain(im)
+            b = bytearray(im)
+            b[want[2222]] = 0x77  # bad type byte
+            im = bytes(b)
+        want = chain(im)
+        n = len(im)
+        cuts = sorted(set(int(c) for c in rng.integers(1, n, size=parts - 1)))
+        r, got, end = 0, [], None
+        for lim in cuts + [n]:
+            if lim <= r:
+                continue
+            res = sim.prefix(im, r, lim, S)
+            assert res is not None
+            offs, code, pos = res
+            assert all(r <= o < lim for o in offs)
+            got += offs
+            if code != 1:  # the chain ended in this prefix
+                end = (code, pos if code == BAD else 0)
+                break
+            assert pos >= lim
+            r = pos
+        if end is None:  # the last prefix stopped exactly at n
+            assert r >= n
+            end = (END, 0)
+        assert got == want[0]
+        assert end == (want[1], want[2])

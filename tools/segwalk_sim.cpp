@@ -23,9 +23,11 @@ struct SimRec {
 static uint64_t* g_dbg = nullptr;  // debug: the first round's guesses
 extern "C" void segwalk_sim_debug(uint64_t* g) { g_dbg = g; }
 
-extern "C" int segwalk_sim(const uint8_t* img, uint64_t n, uint64_t start, uint64_t S, int max_rounds,
-                           uint64_t* rec_off, size_t cap, uint64_t* m_out, uint32_t* code_out, uint64_t* pos_out,
-                           int* repairs, uint64_t* segments, uint32_t* first_fails) {
+// the records starting in [start, lim): code_out kExit with pos_out the first
+// record start at or past lim when the chain goes on past the prefix
+extern "C" int segwalk_sim_prefix(const uint8_t* img, uint64_t n, uint64_t start, uint64_t lim, uint64_t S,
+                                  int max_rounds, uint64_t* rec_off, size_t cap, uint64_t* m_out, uint32_t* code_out,
+                                  uint64_t* pos_out, int* repairs, uint64_t* segments, uint32_t* first_fails) {
   *first_fails = 0;
   *repairs = 0;
   *segments = 0;
@@ -35,12 +37,13 @@ extern "C" int segwalk_sim(const uint8_t* img, uint64_t n, uint64_t start, uint6
     *pos_out = 0;
     return 0;
   }
-  const uint32_t K = (uint32_t)((n - start + S - 1) / S);
+  if (lim > n || lim <= start) lim = n;
+  const uint32_t K = (uint32_t)((lim - start + S - 1) / S);
   *segments = K;
   std::vector<uint64_t> g(K + 1), x(K + 1), pre(K + 1);
   std::vector<uint32_t> code(K + 1), recs(K + 1);
   unsigned long long info[sg::kInfoWords] = {};
-  sg::SegArgs a{img, n, start, S, K, g.data(), x.data(), code.data(), recs.data(), pre.data(), info};
+  sg::SegArgs a{img, n, start, S, K, g.data(), x.data(), code.data(), recs.data(), pre.data(), info, lim};
   for (uint32_t k = 0; k < K; ++k) sg::seg_walk_thread(a, k);
   if (g_dbg) std::copy(g.begin(), g.begin() + K, g_dbg);
   for (int round = 0;; ++round) {
@@ -59,10 +62,18 @@ extern "C" int segwalk_sim(const uint8_t* img, uint64_t n, uint64_t start, uint6
     info[sg::kInfoJterm] = jterm;
     info[sg::kInfoFail] = fail;
     if (fail == sg::kNoSeg) {
-      if (jterm == sg::kNoSeg) return 2;  // (cannot happen: the last guessed segment would fail)
       *m_out = pre[K] & sg::kRecMask;
-      *code_out = code[jterm];
-      *pos_out = x[jterm];
+      if (jterm != sg::kNoSeg) {
+        *code_out = code[jterm];
+        *pos_out = x[jterm];
+        break;
+      }
+      uint32_t last = 0;  // the chain's way out of the prefix (wal_seg_check's kInfoLast)
+      for (uint32_t k = 0; k < K; ++k)
+        if (code[k] == sg::kExit && x[k] >= lim) last = k + 1;
+      if (!last) return 2;  // (cannot happen: the chain ends in the prefix or leaves it)
+      *code_out = sg::kExit;
+      *pos_out = x[last - 1];
       break;
     }
     if (round >= max_rounds) return 1;  // declined: the caller walks by candidate doubling
@@ -77,4 +88,11 @@ extern "C" int segwalk_sim(const uint8_t* img, uint64_t n, uint64_t start, uint6
     sg::seg_emit_thread(a, k, (uint32_t)info[sg::kInfoJterm], 0, R.data(), poff.data(), plen.data(), pcrc.data());
   for (uint64_t i = 0; i < m && i < cap; ++i) rec_off[i] = R[i].rec_off;
   return 0;
+}
+
+extern "C" int segwalk_sim(const uint8_t* img, uint64_t n, uint64_t start, uint64_t S, int max_rounds,
+                           uint64_t* rec_off, size_t cap, uint64_t* m_out, uint32_t* code_out, uint64_t* pos_out,
+                           int* repairs, uint64_t* segments, uint32_t* first_fails) {
+  return segwalk_sim_prefix(img, n, start, n, S, max_rounds, rec_off, cap, m_out, code_out, pos_out, repairs, segments,
+                            first_fails);
 }
