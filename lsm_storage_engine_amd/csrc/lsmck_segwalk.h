@@ -68,7 +68,7 @@ constexpr uint32_t kAccept = 6;
 // repaired by the check (or the walk re-segments, with longer hops).
 constexpr uint64_t kHop = 65536;
 #ifndef LSMCK_SCAN_BLOCKS
-#define LSMCK_SCAN_BLOCKS 4
+#define LSMCK_SCAN_BLOCKS 1
 #endif
 constexpr int kScanBlocks = LSMCK_SCAN_BLOCKS;  // 64-byte blocks the guess scan loads per iteration
 // per-segment record counts and the guessed-segment count share one u64 in

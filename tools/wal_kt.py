@@ -54,6 +54,17 @@ def main():
         m, st, _ = ctx.wal_replay_verify_to_device(len(img), rb.ptr, 500_000, device_ptr=d.ptr)
         ts.append(time.perf_counter() - t)
         assert st == 0 and m == 500_000
+    for sb in [int(x) for x in os.environ.get("WAL_KT_SEGS", "").split(",") if x]:  # A/B: segment sizes
+        ctx.set_option("wal_seg_bytes", sb)
+        tt = []
+        for _ in range(11):
+            t = time.perf_counter()
+            m, st, _ = ctx.wal_replay_verify_to_device(len(img), rb.ptr, 500_000, device_ptr=d.ptr)
+            tt.append(time.perf_counter() - t)
+            assert st == 0 and m == 500_000
+        out[f"device_recs_seg{sb}_ms_median"] = round(float(np.median(tt[1:])) * 1e3, 3)
+        out[f"device_recs_seg{sb}_repairs"] = ctx.get_stat("wal_seg_repairs")
+    ctx.set_option("wal_seg_bytes", 0)
     rb.free()
     if ts:
         out["device_image_device_recs_ms_best"] = round(min(ts[1:]) * 1e3, 3)

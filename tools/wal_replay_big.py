@@ -38,6 +38,8 @@ def main():
                     help="1: the records DMA'd into a page-locked array (LSMCK_RECS_PINNED); 0: staged + copied")
     ap.add_argument("--device-recs", type=int, default=0,
                     help="1: then the same replays with the records left in device memory (LSMCK_RECS_DEVICE)")
+    ap.add_argument("--seg-sweep", default="",
+                    help="comma list of wal_seg_bytes: the records-on-device replay per segment size (A/B)")
     a = ap.parse_args()
     n = a.records
     ln = gen_zipf_lengths(0x5EED0003, n)
@@ -90,13 +92,29 @@ def main():
             if s:
                 dts.append(dt)
             print(f"replay (records on the device) {s}: {dt * 1e3:.1f} ms", file=sys.stderr, flush=True)
+        sweep = {}
+        for sb in [int(x) for x in a.seg_sweep.split(",") if x]:
+            ctx.set_option("wal_seg_bytes", sb)
+            ts = []
+            for s in range(a.steps + 1):
+                ctx.sync()
+                t = time.perf_counter()
+                m, st, bad = ctx.wal_replay_verify_to_device(total, rb.ptr, n, device_ptr=d.ptr)
+                dt = time.perf_counter() - t
+                assert st == 0 and m == n, (st, m, bad)
+                if s:
+                    ts.append(dt)
+            sweep[sb] = {"ms_median": round(float(np.median(ts)) * 1e3, 2), "segments": ctx.get_stat("wal_segments"),
+                         "repairs": ctx.get_stat("wal_seg_repairs"), "path": ctx.get_stat("wal_walk_path")}
+            print(f"wal_seg_bytes {sb}: {sweep[sb]}", file=sys.stderr, flush=True)
+        ctx.set_option("wal_seg_bytes", 0)
         crc = rb.download(np.uint8, n * WAL_REC_DTYPE.itemsize).view(WAL_REC_DTYPE)["crc"]
         dsum = "%08x" % zlib.crc32(np.ascontiguousarray(crc).astype("<u4").tobytes())
         rb.free()
         dmed = float(np.median(dts))
         dev = {"ms_median": round(dmed * 1e3, 2), "ms_best": round(min(dts) * 1e3, 2),
                "value": round(total / GIB / dmed, 1), "summary_crc32": dsum,
-               "summary_matches_oracle": bool(golden) and dsum == golden["summary_crc32"]}
+               "summary_matches_oracle": bool(golden) and dsum == golden["summary_crc32"], "seg_sweep": sweep}
     d.free()
     best, med = min(times), float(np.median(times))
     print(json.dumps({
