@@ -306,7 +306,8 @@ int lsmck_sha256_batch_fixed(lsmck_ctx* ctx, const uint8_t* base, size_t stride,
  * records stay there -- for a device-resident log whose consumer runs on the
  * GPU; the segment walk writes them in place when all of them fit, and no
  * record crosses the host link (any path that walks on the host copies its
- * records up).  Synchronous. */
+ * records up).  In either array, entries past *nrec up to the walked record
+ * count (records after a failed CRC) may be written too.  Synchronous. */
 #define LSMCK_RECS_PINNED 0x8u
 #define LSMCK_RECS_DEVICE 0x10u
 #define LSMCK_WAL_CORRUPTED 1

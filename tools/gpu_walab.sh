@@ -16,8 +16,8 @@ for r in $(seq 1 ${ROUNDS:-2}); do
     cp $L/ab/$N.so $L/liblsmck.so
     timeout -k 10 150 python3 -u tools/wal_kt.py > $O/small_${N}_$r.log 2>&1 || { echo "small $N failed rc=$?"; tail -5 $O/small_${N}_$r.log; restore; exit 1; }
     echo "$N round $r small: $(tail -1 $O/small_${N}_$r.log)"
-    timeout -k 10 200 python3 -u tools/wal_replay_big.py --steps 3 --records ${BIG:-16777216} > $O/big_${N}_$r.log 2>&1 || { echo "big $N failed rc=$?"; tail -5 $O/big_${N}_$r.log; restore; exit 1; }
-    echo "$N round $r big: $(tail -1 $O/big_${N}_$r.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_median"], d["value"], d["summary_matches_oracle"], d["seg_repairs"])')"
+    timeout -k 10 300 python3 -u tools/wal_replay_big.py --steps 3 --records ${BIG:-16777216} $BIG_ARGS > $O/big_${N}_$r.log 2>&1 || { echo "big $N failed rc=$?"; tail -5 $O/big_${N}_$r.log; restore; exit 1; }
+    echo "$N round $r big: $(tail -1 $O/big_${N}_$r.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_median"], d["value"], d["summary_matches_oracle"], d["seg_repairs"], d.get("records_on_device"))')"
   done
 done
 restore
