@@ -234,81 +234,70 @@ struct Scan {
   int64_t p0 = kNoChunk;  // image position of the chunk's first byte (< 0: before the image)
   uint64_t m[kScanBlocks];
 };
-constexpr uint64_t kChunk = 64 * kScanBlocks;
-// image position of the chunk holding `from` (chunks are aligned in the
-// address space; < 0: the chunk begins before the image)
-LSMCK_HD int64_t chunk_of(const uint8_t* img, uint64_t from) {
+// The first type byte c in [from, e) whose header fits, or kNoGuess.  The
+// chunk holding `from` comes from S when it is the one already loaded (vector
+// loads inside the image, byte loads at its two ends); then the ones after it.
+LSMCK_HD uint64_t next_cand(Scan& S, const uint8_t* img, uint64_t n, uint64_t from, uint64_t e) {
+  // all the chunk's loads are in flight together, so a lane that starts
+  // inside a long record waits on a quarter as many dependent loads (the
+  // wave waits for its slowest lane)
   const uintptr_t base = (uintptr_t)img;
-  return (int64_t)(((base + from) & ~(uintptr_t)(kChunk - 1)) - base);
-}
-// S := the chunk at p0 and its type-byte masks (vector loads inside the
-// image, byte loads at its two ends)
-LSMCK_HD void load_chunk(Scan& S, const uint8_t* img, uint64_t n, int64_t p0) {
-  S.p0 = p0;
-  if (p0 >= 0 && (uint64_t)p0 + kChunk <= n) {
-    uint32_t w[16 * kScanBlocks];
+  for (uintptr_t A = (base + from) & ~(uintptr_t)(64 * kScanBlocks - 1);; A += 64 * kScanBlocks) {
+    const int64_t p0 = (int64_t)(A - base);
+    if (p0 >= (int64_t)e) return kNoGuess;
+    if (p0 != S.p0) {
+      S.p0 = p0;
+      if (p0 >= 0 && (uint64_t)p0 + 64 * kScanBlocks <= n) {
+        uint32_t w[16 * kScanBlocks];
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
-    for (int q = 0; q < 4 * kScanBlocks; ++q) load16(img + p0 + 16 * q, w + 4 * q);
+        for (int q = 0; q < 4 * kScanBlocks; ++q) load16((const uint8_t*)A + 16 * q, w + 4 * q);
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
-    for (int j = 0; j < kScanBlocks; ++j) {
-      uint64_t mj = 0;
+        for (int j = 0; j < kScanBlocks; ++j) {
+          uint64_t mj = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
-      for (int d = 0; d < 16; ++d) {
-        const uint32_t f = type_bytes(w[16 * j + d]);
-        const uint64_t nib = ((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u);
-        mj |= nib << (4 * d);
-      }
-      S.m[j] = mj;
-    }
-  } else {
-    for (int j = 0; j < kScanBlocks; ++j) {
-      uint64_t mj = 0;
-      for (int i = 0; i < 64; ++i) {
-        const int64_t p = p0 + 64 * j + i;
-        if (p >= 0 && (uint64_t)p < n) {
-          const uint32_t t = img[p];
-          if (t == 1 || t == 2) mj |= 1ull << i;
+          for (int d = 0; d < 16; ++d) {
+            const uint32_t f = type_bytes(w[16 * j + d]);
+            const uint64_t nib = ((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u);
+            mj |= nib << (4 * d);
+          }
+          S.m[j] = mj;
+        }
+      } else {
+        for (int j = 0; j < kScanBlocks; ++j) {
+          uint64_t mj = 0;
+          for (int i = 0; i < 64; ++i) {
+            const int64_t p = p0 + 64 * j + i;
+            if (p >= 0 && (uint64_t)p < n) {
+              const uint32_t t = img[p];
+              if (t == 1 || t == 2) mj |= 1ull << i;
+            }
+          }
+          S.m[j] = mj;
         }
       }
-      S.m[j] = mj;
     }
-  }
-}
-// the first type byte c in [from, e) of the loaded chunk S whose header fits,
-// or kNoGuess (none in this chunk)
-LSMCK_HD uint64_t scan_chunk(const Scan& S, const uint8_t* img, uint64_t n, uint64_t from, uint64_t e) {
-  for (int j = 0; j < kScanBlocks; ++j) {
-    const int64_t pj = S.p0 + 64 * j;
-    const int64_t lo = (int64_t)from - pj, hi = (int64_t)e - pj;
-    if (hi <= 0) return kNoGuess;
-    if (lo >= 64) continue;
-    uint64_t mj = S.m[j];
-    if (lo > 0) mj &= ~0ull << lo;
-    if (hi < 64) mj &= (1ull << hi) - 1ull;
-    while (mj) {
-      const int i = __builtin_ctzll(mj);
-      mj &= mj - 1;
-      const uint64_t c = (uint64_t)(pj + i);
-      if (c + 13u <= n || c + hdr_len(img[c]) <= n) return c;  // (the byte is read only at the image's end)
+    for (int j = 0; j < kScanBlocks; ++j) {
+      // only positions in [from, e)
+      const int64_t pj = p0 + 64 * j;
+      const int64_t lo = (int64_t)from - pj, hi = (int64_t)e - pj;
+      if (hi <= 0) return kNoGuess;
+      if (lo >= 64) continue;
+      uint64_t mj = S.m[j];
+      if (lo > 0) mj &= ~0ull << lo;
+      if (hi < 64) mj &= (1ull << hi) - 1ull;
+      while (mj) {
+        const int i = __builtin_ctzll(mj);
+        mj &= mj - 1;
+        const uint64_t c = (uint64_t)(pj + i);
+        if (c + 13u <= n || c + hdr_len(img[c]) <= n) return c;  // (the byte is read only at the image's end)
+      }
     }
-  }
-  return kNoGuess;
-}
-// The first type byte c in [from, e) whose header fits, or kNoGuess.  The
-// chunk holding `from` comes from S when it is the one already loaded; then
-// the ones after it.
-LSMCK_HD uint64_t next_cand(Scan& S, const uint8_t* img, uint64_t n, uint64_t from, uint64_t e) {
-  for (int64_t p0 = chunk_of(img, from);; p0 += (int64_t)kChunk) {
-    if (p0 >= (int64_t)e) return kNoGuess;
-    if (p0 != S.p0) load_chunk(S, img, n, p0);
-    const uint64_t c = scan_chunk(S, img, n, from, e);
-    if (c != kNoGuess) return c;
   }
 }
 // whether the chain from the record start c passes through position q > c
@@ -408,11 +397,8 @@ LSMCK_HD void seg_forced(const SegArgs& a, uint32_t k, uint64_t c) {
   a.recs[k] = o.recs;
 }
 
-// step 1-2 for segment k, as nested loops: the guess (scan, acceptance walk
-// per candidate, the later-start rule), then the walk from it.  Kept as the
-// reference form of seg_walk_thread (A/B option "wal_seg_flat" 0, and the
-// host model checks that both give the same segments).
-LSMCK_HD void seg_walk_thread_nested(const SegArgs& a, uint32_t k) {
+// step 1-2 for segment k
+LSMCK_HD void seg_walk_thread(const SegArgs& a, uint32_t k) {
   if (k == 0) {
     seg_forced(a, 0, a.start);
     return;
@@ -425,132 +411,6 @@ LSMCK_HD void seg_walk_thread_nested(const SegArgs& a, uint32_t k) {
     a.recs[k] = 0;
   } else {
     seg_forced(a, k, c);  // the walk from the guess (every lane of the wave at once)
-  }
-}
-
-// step 1-2 for segment k: the same guess and walk as one flat loop with one
-// load per step -- a scan chunk or a header.  In the nested form a wave runs
-// each inner loop as long as its slowest lane (an acceptance walk of
-// kAccept + 1 headers for every candidate a lane rejects after one), so its
-// steps add up over the candidates; here a lane goes on to its next
-// candidate, the later-start test or the walk while the others are still
-// busy, and the wave takes as many steps as its busiest lane.
-enum : uint32_t { kStScan, kStAccept, kStLater, kStReach, kStWalk };
-LSMCK_HD void seg_walk_thread(const SegArgs& a, uint32_t k) {
-  const uint8_t* img = a.img;
-  const uint64_t n = a.n, e = seg_end(a, k), hop = a.S > kHop ? a.S : kHop;
-  Scan S;
-  uint32_t st = k == 0 ? kStWalk : kStScan;
-  uint64_t c = a.start, p = a.start;  // the candidate (the guess, once taken); the position of the next header
-  uint64_t from = seg_begin(a, k);    // scans: the next byte to look at
-  uint64_t q1 = 0, lim = 0;           // the taken candidate's first record end; the later-start scan's end
-  uint64_t c2 = 0, q2 = 0;            // a later start under test; its first record's end
-  uint32_t good = 0, cnt = 0;
-  bool lastwhole = false;
-  for (;;) {
-    // the scans settle on the loaded chunk: a candidate, the end of the
-    // scan, or the next chunk to load
-    int64_t want = kNoChunk;
-    while (st == kStScan || st == kStLater) {
-      const uint64_t end = st == kStScan ? e : lim;
-      const int64_t p0 = chunk_of(img, from);
-      if (p0 >= (int64_t)end || from >= end) {
-        if (st == kStScan) {  // no start taken in the segment
-          a.g[k] = kNoGuess;
-          a.x[k] = 0;
-          a.code[k] = kNone;
-          a.recs[k] = 0;
-          return;
-        }
-        st = kStWalk;  // no later start: c is the guess
-        p = c;
-        break;
-      }
-      if (p0 != S.p0) {
-        want = p0;
-        break;
-      }
-      const uint64_t cand = scan_chunk(S, img, n, from, end);
-      if (cand == kNoGuess) {
-        from = (uint64_t)(p0 + (int64_t)kChunk);
-        continue;
-      }
-      if (st == kStScan) {
-        c = p = cand;
-        good = 0;
-        st = kStAccept;
-      } else {
-        c2 = p = cand;
-        st = kStReach;
-      }
-      break;
-    }
-    if (want != kNoChunk) {
-      load_chunk(S, img, n, want);
-      continue;
-    }
-    const Head h = head(img, n, p);
-    bool whole;
-    if (st == kStAccept) {  // accept(c), one header per step
-      int verdict = 0;        // 1 taken, -1 refused
-      if (p != c && h.cl) {
-        verdict = (lastwhole && h.cl == kEnd) ? 1 : -1;
-      } else {
-        const uint64_t q = next_of(h, n, p, &whole);
-        if (p == c) q1 = q;
-        if (p == c && q - c > hop) {
-          verdict = -1;
-        } else {
-          good += whole;
-          if (good >= kAccept) {
-            verdict = 1;
-          } else {
-            p = q;
-            lastwhole = whole;
-          }
-        }
-      }
-      if (verdict < 0) {
-        st = kStScan;
-        from = c + 1;
-      } else if (verdict > 0) {
-        st = kStLater;
-        from = c + 1;
-        lim = q1 < e ? q1 : e;
-      }
-    } else if (st == kStReach) {  // reaches(c2, q1), one header per step
-      int verdict = 0;
-      if (p != c2 && h.cl) {
-        verdict = -1;
-      } else {
-        const uint64_t q = next_of(h, n, p, &whole);
-        if (p == c2) q2 = q;
-        if (q >= q1)
-          verdict = q == q1 ? 1 : -1;
-        else
-          p = q;
-      }
-      if (verdict < 0) {
-        st = kStLater;
-        from = c2 + 1;
-      } else if (verdict > 0) {  // the later start is preferred: the same test again from it
-        c = c2;
-        q1 = q2;
-        lim = q1 < e ? q1 : e;
-        from = c + 1;
-        st = kStLater;
-      }
-    } else {  // kStWalk: seg_forced(a, k, c)
-      if (h.cl || p >= e) {
-        a.g[k] = c;
-        a.x[k] = p;
-        a.code[k] = h.cl ? h.cl : kExit;
-        a.recs[k] = cnt;
-        return;
-      }
-      p = next_of(h, n, p, &whole);
-      ++cnt;
-    }
   }
 }
 
