@@ -227,7 +227,7 @@ int lsmck_device_count(void);
  *                 lsmck_segwalk.h), falling back to candidate doubling when
  *                 its check keeps failing; 0 = candidate doubling only.
  *   "wal_seg_bytes"  segment walk: bytes per segment (0 = auto, default:
- *                 ~2^19 segments; else 64..2^30).  Tests use small segments.
+ *                 ~2^16 segments; else 64..2^30).  Tests use small segments.
  *   "wal_seg_rounds"  segment walk: check failures repaired before it
  *                 declines to candidate doubling (default 16).
  * Returns 0, or LSMCK_EINVAL for an unknown key / value. */

@@ -264,7 +264,7 @@ struct lsmck_ctx {
   size_t wal_recs_dev_cap = 0;
   bool wal_recs_dev_emitted = false;
   int wal_seg = 1;           // device WAL walk: 1 = the segment walk first (default), 0 = candidate doubling only
-  uint64_t wal_seg_bytes = 0;  // segment walk: bytes per segment (0 = auto, ~2^19 segments)
+  uint64_t wal_seg_bytes = 0;  // segment walk: bytes per segment (0 = auto, ~2^16 segments)
   int wal_seg_rounds = 16;   // segment walk: repairs before it declines to the candidate-doubling walk
   // what the last device-walked replay did (lsmck_ctx_get_stat "wal_walk_path" / "wal_seg_repairs" / "wal_segments")
   int last_walk_path = 0;

@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256) void wal_frame_insert(uint8_t* __restrict__ im
 // --- the segment walk (lsmck_segwalk.h) ------------------------------------
 // Thread per segment.  The walks are chains of dependent header reads, so
 // the launch wants as many segments in flight as the chip holds: the host
-// sizes segments for ~2^19 of them (lsmk_wal_seg_bytes).
+// sizes segments for ~2^16 of them (lsmk_wal_seg_bytes).
 __global__ __launch_bounds__(256) void wal_seg_walk(seg::SegArgs a) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < a.K) seg::seg_walk_thread(a, k);
@@ -463,11 +463,15 @@ using namespace lsmck;
 static int launch_err();
 
 // Segment bytes for a walk over `len` bytes: a power of two from 512 B to
-// 16 MiB giving about 2^19 segments (one thread each); `want` overrides.
+// 16 MiB giving about 2^16 segments (one thread each; same-box sweeps, profiles/r04/j:
+// 2 MiB segments walk the 97.8 GiB log in 34.7 ms against 43.1 at 256 KiB and
+// 38.0 at 4 MiB, 4 KiB the 0.24 GB one in 0.41 ms against 0.56 at 512 B --
+// fewer, longer segments pay the per-segment scan to the first record fewer
+// times); `want` overrides.
 extern "C" uint64_t lsmk_wal_seg_bytes(uint64_t len, uint64_t want) {
   if (want) return want;
   uint64_t S = 512;
-  while (S < (16ull << 20) && (len + S - 1) / S > (1ull << 19)) S <<= 1;
+  while (S < (16ull << 20) && (len + S - 1) / S > (1ull << 16)) S <<= 1;
   return S;
 }
 extern "C" uint64_t lsmk_wal_seg_scan_blocks(uint32_t K) {
