@@ -39,9 +39,9 @@ if has c3pmc; then  # HBM bytes per launch of the stream kernel (separate FETCH_
   done
   python3 tools/pmc_summary.py $O/pmc_c3_FETCH_SIZE $O/pmc_c3_WRITE_SIZE config3 > $O/pmc_summary_c3.json 2>&1
 fi
-has walbig && step walbig 300 env LSMCK_WAL_TRACE=1 python3 -u tools/wal_replay_big.py --steps 3
+has walbig && step walbig 300 env LSMCK_WAL_TRACE=1 python3 -u tools/wal_replay_big.py --steps 3 --device-recs 1
 if has walbigkt; then
-  step walbigkt 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_walbig -o kt -- python3 tools/wal_replay_big.py --steps 2
+  step walbigkt 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_walbig -o kt -- python3 tools/wal_replay_big.py --steps 2 --device-recs 1
   python3 tools/kt_stats.py $O/kt_walbig > $O/kt_stats_walbig.txt 2>&1
 fi
 if has waldiag; then
@@ -50,7 +50,7 @@ if has waldiag; then
   python3 tools/kt_stats.py $O/kt_waldev > $O/kt_stats_waldev.txt 2>&1
 fi
 has sha && step sha 400 python3 bench.py --digest sha256 --steps 5 --warmup 1 --no-config4
-has shaab && step shaab 600 python3 bench.py --digest sha256 --variants=-,d1,q1,d1+q1 --rounds 3 --steps 3 --warmup 1 --no-cpu-baseline --no-host-roundtrip --no-config4
+has shaab && step shaab 600 python3 bench.py --digest sha256 --variants=-,c1,c1+q1,d1+c1 --rounds 3 --steps 3 --warmup 1 --no-cpu-baseline --no-host-roundtrip --no-config4
 has tree && step tree 900 python3 -u tools/e2e_tree.py --gib 16 --reps 2 --multi 2 --dir /dev/shm/lsm_e2e_r04
 has server && step server 1100 python3 -u tools/e2e_server.py --gib 100 --dir /dev/shm/lsm_e2e_server_r04
 echo "== done" >&2
