@@ -368,7 +368,7 @@ def main():
             for v in vs:
                 opts = dict(defaults)
                 for part in ([] if v == "-" else v.split("+")):
-                    m = re.fullmatch(r"([sapbftdq])(\d+)", part)
+                    m = re.fullmatch(r"([sapbftdqc])(\d+)", part)
                     if not m:
                         raise SystemExit(f"bad variant {v!r}")
                     opts[keys[m.group(1)]] = int(m.group(2))
