@@ -228,10 +228,6 @@ int lsmck_device_count(void);
  *                 its check keeps failing; 0 = candidate doubling only.
  *   "wal_seg_bytes"  segment walk: bytes per segment (0 = auto, default:
  *                 ~2^16 segments; else 64..2^30).  Tests use small segments.
- *   "wal_seg_parts"  a device image replayed with LSMCK_RECS_PINNED: the
- *                 segment walk in this many prefixes of the log, each part's
- *                 records read back while the later parts are walked (0 =
- *                 by size: one part per 8 GiB, up to 8; 1 = whole).
  *   "wal_seg_rounds"  segment walk: check failures repaired before it
  *                 declines to candidate doubling (default 16).
  * Returns 0, or LSMCK_EINVAL for an unknown key / value. */

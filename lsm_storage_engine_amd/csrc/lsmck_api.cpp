@@ -255,14 +255,7 @@ struct lsmck_ctx {
     size_t cap_sbsum = 0;
     unsigned long long* sinfo = nullptr;
     unsigned long long* h_sinfo = nullptr;
-    // the walk in parts with the records read back part by part (wal_seg_parts):
-    // two part record buffers, each part's emit and read-back events
-    lsmck_wal_rec* prec[2] = {nullptr, nullptr};
-    size_t cap_prec[2] = {0, 0};
-    hipEvent_t pemit[2] = {nullptr, nullptr}, pdone[2] = {nullptr, nullptr};
-    bool pbusy[2] = {false, false};  // a read-back from the buffer may still run
   } wd;
-  int wal_seg_parts = 0;  // records to a pinned host array: the walk in this many parts (0 = by size, 1 = whole)
   bool wal_recs_direct = false;  // this replay's records go by DMA into the caller's pinned array (under wal_mu)
   // LSMCK_RECS_DEVICE (under wal_mu): the caller's device array and its capacity
   // (the segment walk emits straight into it when every record fits), and
@@ -270,7 +263,6 @@ struct lsmck_ctx {
   lsmck_wal_rec* wal_recs_dev = nullptr;
   size_t wal_recs_dev_cap = 0;
   bool wal_recs_dev_emitted = false;
-  bool wal_parts_done = false;  // wal_replay_parts: every record already read back (wal_finish's error path)
   int wal_seg = 1;           // device WAL walk: 1 = the segment walk first (default), 0 = candidate doubling only
   uint64_t wal_seg_bytes = 0;  // segment walk: bytes per segment (0 = auto, ~2^16 segments)
   int wal_seg_rounds = 16;   // segment walk: repairs before it declines to the candidate-doubling walk
@@ -917,13 +909,7 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->wal_seg_rounds = (int)value;
     return 0;
-  }  if (!strcmp(key, "wal_seg_parts")) {  // records to a pinned array: the segment walk in parts (0 = by size)
-    if (value < 0 || value > 64) return lsmck_host::set_error(LSMCK_EINVAL, "wal_seg_parts: 0..64");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->wal_seg_parts = (int)value;
-    return 0;
   }
-
   if (!strcmp(key, "wal_prefetch")) {  // A/B: bytes the WAL header walk prefetches ahead (0 = off)
     if (value < 0 || value > (1l << 24)) return lsmck_host::set_error(LSMCK_EINVAL, "wal_prefetch: 0..16 MiB");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1032,11 +1018,6 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
                   (void*)ctx->wd.srecs, (void*)ctx->wd.sbsum, (void*)ctx->wd.sinfo})
     if (p) (void)hipFree(p);
   if (ctx->wd.h_sinfo) (void)hipHostFree(ctx->wd.h_sinfo);
-  for (int b = 0; b < 2; ++b) {
-    if (ctx->wd.prec[b]) (void)hipFree(ctx->wd.prec[b]);
-    if (ctx->wd.pemit[b]) (void)hipEventDestroy(ctx->wd.pemit[b]);
-    if (ctx->wd.pdone[b]) (void)hipEventDestroy(ctx->wd.pdone[b]);
-  }
   for (void* p : {(void*)ctx->d_vcrc, (void*)ctx->d_woff, (void*)ctx->d_wlen, (void*)ctx->d_wexp})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)ctx->h_woff, (void*)ctx->h_wlen, (void*)ctx->h_wexp})
@@ -1343,32 +1324,16 @@ static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t ter
   if (nbad) {
     lsmck_wal_rec r;
     uint32_t got = 0;
-    if (ctx->wal_recs_dev) {
+    if (ctx->wal_recs_dev)
       HIPCHK(hipMemcpy(&r, (ctx->wal_recs_dev_emitted ? recs : W.recs) + first, sizeof r, hipMemcpyDeviceToHost));
-    } else if (recs && cap && ctx->wal_recs_direct && first < std::min(m, cap)) {
-      r = recs[first];
-    } else if (recs && cap && first < done) {
+    else if (recs && cap && first < done)
       r = ctx->h_wrecs1[first];
-    } else if (recs && cap && m > done && !ctx->wal_recs_direct) {
+    else if (recs && cap && ctx->wal_recs_direct && first < std::min(m, cap))
+      r = recs[first];
+    else if (recs && cap && m > done && !ctx->wal_recs_direct)
       r = ctx->h_wrecs[first - done];
-    } else if (ctx->wal_parts_done) {
-      // past the caller's array, and no whole records array on the device:
-      // the record starts where the one before it ends (payload offset +
-      // length, wal.rs's chain); its type byte from the image, its stored
-      // CRC from the compare's input
-      uint64_t o = 0;
-      uint32_t l = 0;
-      if (first) {
-        HIPCHK(hipMemcpy(&o, ctx->d_woff + first - 1, 8, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(&l, ctx->d_wlen + first - 1, 4, hipMemcpyDeviceToHost));
-      }
-      uint8_t t = 0;
-      HIPCHK(hipMemcpy(&t, img + o + l, 1, hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(&r.crc, ctx->d_wexp + first, 4, hipMemcpyDeviceToHost));
-      r.type = t;
-    } else {
+    else
       HIPCHK(hipMemcpy(&r, W.recs + first, sizeof r, hipMemcpyDeviceToHost));
-    }
     HIPCHK(hipMemcpy(&got, ctx->d_vcrc + first, 4, hipMemcpyDeviceToHost));
     if (bad_index) *bad_index = first;
     if (bad_expected) *bad_expected = r.crc;
@@ -1458,10 +1423,8 @@ static int wal_walk_from(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t 
 // payloads that look like framed records along the chain; the caller walks
 // by candidate doubling instead.
 constexpr int kWalSegDecline = 0x7FFF0004;
-// pbuf >= 0: the records go to the part buffer W.prec[pbuf] (record at + j at
-// index j) instead of the walk's own array.
 static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t start, uint64_t lim, size_t at,
-                        hipStream_t st, const WalTrace& tr, WalPart* out, int pbuf = -1) {
+                        hipStream_t st, const WalTrace& tr, WalPart* out) {
   namespace sg = lsmck::seg;
   auto& W = ctx->wd;
   int rc;
@@ -1537,109 +1500,20 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
   if (m) {
     const size_t tot = at + m;
     // LSMCK_RECS_DEVICE with room for every record: emitted into the caller's array
-    const bool part = pbuf >= 0;
-    const bool dev = !part && ctx->wal_recs_dev && at == 0 && tot <= ctx->wal_recs_dev_cap;
-    lsmck_wal_rec* dst = dev ? ctx->wal_recs_dev : W.recs;
-    if (part) {
-      if (W.cap_prec[pbuf] < m) {  // (its last read-back finished first: the buffer is freed)
-        if (W.pbusy[pbuf]) HIPCHK(hipEventSynchronize(W.pdone[pbuf]));
-        W.pbusy[pbuf] = false;
-        const size_t c = std::max<size_t>(m, W.cap_prec[pbuf] * 3 / 2);
-        if (W.prec[pbuf]) HIPCHK(hipFree(W.prec[pbuf]));
-        W.prec[pbuf] = nullptr;
-        W.cap_prec[pbuf] = 0;
-        HIPCHK(hipMalloc((void**)&W.prec[pbuf], c * sizeof(lsmck_wal_rec)));
-        W.cap_prec[pbuf] = c;
-      }
-      dst = W.prec[pbuf];
-    }
-    if ((!dev && !part && (rc = ensure_dev_keep(&W.recs, &W.cap_recs, tot, at, st))) ||
+    const bool dev = ctx->wal_recs_dev && at == 0 && tot <= ctx->wal_recs_dev_cap;
+    if ((!dev && (rc = ensure_dev_keep(&W.recs, &W.cap_recs, tot, at, st))) ||
         (rc = ensure_dev_keep(&ctx->d_woff, &ctx->cap_woff, tot, at, st)) ||
         (rc = ensure_dev_keep(&ctx->d_wlen, &ctx->cap_wlen, tot, at, st)) ||
         (rc = ensure_dev_keep(&ctx->d_wexp, &ctx->cap_wexp, tot, at, st)) ||
         (rc = ensure_dev_keep(&ctx->d_vcrc, &ctx->cap_vcrc, tot, at, st)))
       return rc;
-    if (!part) dst = dev ? ctx->wal_recs_dev : W.recs;  // (W.recs may have moved)
-    if ((rc = lsmk_wal_seg_emit(&a, at, part ? at : 0, dst, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st)))
+    if ((rc = lsmk_wal_seg_emit(&a, at, dev ? ctx->wal_recs_dev : W.recs, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st)))
       return launch_rc(rc, "wal segment emit kernel");
     ctx->wal_recs_dev_emitted = dev;
   }
   if (!ctx->wal_emit_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_emit_ev, hipEventDisableTiming));
   HIPCHK(hipEventRecord(ctx->wal_emit_ev, st));
   return 0;
-}
-
-// Records to a pinned host array (LSMCK_RECS_PINNED) from a device image:
-// the segment walk in `parts` prefixes of the log.  Each part's records are
-// emitted into one of two part buffers and read back on the staging stream
-// while the next parts are walked and every part's CRC pass runs: the
-// read-back (PCIe-bound, 2 GB for config 3w's 2^26 records) then overlaps the
-// device work instead of following it.  A part that declines hands the rest
-// of the log to candidate doubling.  Caller holds wal_mu and ctx->mu.
-static int wal_replay_parts(lsmck_ctx* ctx, const uint8_t* img, size_t n, size_t parts, lsmck_wal_rec* recs,
-                            size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected,
-                            hipStream_t st, const WalTrace& tr) {
-  auto& W = ctx->wd;
-  int rc;
-  if ((rc = stage_init(ctx->stage[0]))) return rc;
-  for (int b = 0; b < 2; ++b) {
-    if (!W.pemit[b]) HIPCHK(hipEventCreateWithFlags(&W.pemit[b], hipEventDisableTiming));
-    if (!W.pdone[b]) HIPCHK(hipEventCreateWithFlags(&W.pdone[b], hipEventDisableTiming));
-  }
-  hipStream_t s2 = ctx->stage[0].s;
-  // every read-back queued so far ahead of the stream's end (the final sync,
-  // and any return, waits for it)
-  auto join = [&]() -> int {
-    for (int b = 0; b < 2; ++b)
-      if (W.pbusy[b]) HIPCHK(hipStreamWaitEvent(st, W.pdone[b], 0));
-    return 0;
-  };
-  const uint64_t per = (n + parts - 1) / parts;
-  uint64_t r = 0;
-  size_t at = 0;
-  WalPart P{};
-  for (int i = 0;; ++i) {
-    const uint64_t lim = n - r > per + per / 4 ? r + per : n;  // (the last part takes a short tail)
-    const int b = i & 1;
-    if (W.pbusy[b]) HIPCHK(hipStreamWaitEvent(st, W.pdone[b], 0));  // part i-2's read-back from this buffer
-    rc = wal_seg_walk(ctx, img, n, r, lim, at, st, tr, &P, b);
-    if (rc == kWalSegDecline) {  // the rest by candidate doubling, its records read back by wal_finish
-      int jr = join();
-      if (jr) return jr;
-      ctx->last_walk_path = 2;
-      if ((rc = wal_walk_setup(ctx, n))) return rc;
-      if ((rc = wal_walk_from(ctx, img, n, r, at, ctx->wal_part_bytes, false, st, tr, &P))) return rc;
-      return wal_finish(ctx, img, P.m, P.term, P.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr,
-                        at);
-    }
-    if (rc) {
-      (void)join();
-      return rc;
-    }
-    const size_t mi = P.m - at;
-    if (mi) {
-      const size_t take = at < cap ? std::min(mi, cap - at) : 0;
-      HIPCHK(hipEventRecord(W.pemit[b], st));
-      HIPCHK(hipStreamWaitEvent(s2, W.pemit[b], 0));
-      if (take) HIPCHK(hipMemcpyAsync(recs + at, W.prec[b], take * sizeof(lsmck_wal_rec), hipMemcpyDeviceToHost, s2));
-      HIPCHK(hipEventRecord(W.pdone[b], s2));
-      W.pbusy[b] = true;
-      if ((rc = wal_crc_part(ctx, img, at, mi, st))) {
-        (void)join();
-        return rc;
-      }
-    }
-    at = P.m;
-    if (P.term != kWalStop) break;
-    r = P.tpos;
-  }
-  if ((rc = join())) return rc;
-  ctx->wal_parts_done = true;  // (wal_finish: every record is in the caller's array already)
-  rc = wal_finish(ctx, img, P.m, P.term, P.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr, P.m,
-                  true);
-  ctx->wal_parts_done = false;
-  W.pbusy[0] = W.pbusy[1] = false;  // (wal_finish synchronized the stream, which waited for them)
-  return rc;
 }
 
 // A device-resident image (or an uploaded one: `marked`, its candidate bitmap
@@ -1656,14 +1530,6 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
   if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
   hipStream_t st = so.st;
   WalPart P;
-  if (ctx->wal_seg && !ctx->wal_part_bytes && ctx->wal_recs_direct && recs && cap && !marked) {
-    // records to a pinned array: the walk in parts, each part's read-back
-    // beside the work after it (by size: one part per 8 GiB, up to 8)
-    const size_t parts = ctx->wal_seg_parts ? (size_t)ctx->wal_seg_parts
-                                            : std::min<size_t>(8, std::max<size_t>(1, (size_t)(n >> 33)));
-    if (parts > 1)
-      return wal_replay_parts(ctx, img, n, parts, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr);
-  }
   rc = ctx->wal_seg && !ctx->wal_part_bytes ? wal_seg_walk(ctx, img, n, 0, n, 0, st, tr, &P) : kWalSegDecline;
   if (rc == 0) {  // the CRC pass over every record, then the compare and the records
     if ((rc = wal_crc_part(ctx, img, 0, P.m, st))) return rc;

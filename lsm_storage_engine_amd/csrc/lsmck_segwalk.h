@@ -558,11 +558,10 @@ LSMCK_HD void seg_repair(const SegArgs& a, uint32_t j, uint32_t budget) {
 }
 
 // step 4 for segment k (after the check passed): its records at `at` + its
-// place, as lsmck_wal_rec entries, CRC descriptors and stored CRCs (record i
-// goes to recs[i - rbase]: a part's own array when the walk runs in parts)
+// place, as lsmck_wal_rec entries, CRC descriptors and stored CRCs
 template <class Rec>
-LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint64_t at, uint64_t rbase, Rec* recs,
-                              uint64_t* poff, uint32_t* plen, uint32_t* pcrc) {
+LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint64_t at, Rec* recs, uint64_t* poff,
+                              uint32_t* plen, uint32_t* pcrc) {
   if (k > jterm || a.code[k] == kNone) return;
   uint64_t i = at + (a.pre[k] & kRecMask);
   uint64_t p = a.g[k];
@@ -580,7 +579,7 @@ LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint
     R.vlen = h.vlen;
     R.crc = h.crc;
     R.type = h.t;
-    recs[i - rbase] = R;
+    recs[i] = R;
     poff[i] = p + hl;
     plen[i] = got;
     pcrc[i] = h.crc;

@@ -449,12 +449,11 @@ __global__ void wal_seg_repair(seg::SegArgs a, uint32_t budget) {
   if (j < a.K) seg::seg_repair(a, j, budget);
 }
 
-__global__ __launch_bounds__(256) void wal_seg_emit(seg::SegArgs a, uint64_t at, uint64_t rbase,
-                                                     lsmck_wal_rec* __restrict__ recs,
+__global__ __launch_bounds__(256) void wal_seg_emit(seg::SegArgs a, uint64_t at, lsmck_wal_rec* __restrict__ recs,
                                                      uint64_t* __restrict__ poff, uint32_t* __restrict__ plen,
                                                      uint32_t* __restrict__ pcrc) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < a.K) seg::seg_emit_thread(a, k, (uint32_t)a.info[seg::kInfoJterm], at, rbase, recs, poff, plen, pcrc);
+  if (k < a.K) seg::seg_emit_thread(a, k, (uint32_t)a.info[seg::kInfoJterm], at, recs, poff, plen, pcrc);
 }
 
 }  // namespace lsmck
@@ -505,10 +504,9 @@ extern "C" int lsmk_wal_seg_repair(const seg::SegArgs* a, uint32_t budget, hipSt
   return launch_err();
 }
 
-// records at at.. ; record i into recs[i - rbase]
-extern "C" int lsmk_wal_seg_emit(const seg::SegArgs* a, uint64_t at, uint64_t rbase, lsmck_wal_rec* recs,
-                                 uint64_t* poff, uint32_t* plen, uint32_t* pcrc, hipStream_t st) {
-  hipLaunchKernelGGL(wal_seg_emit, dim3((a->K + 255) / 256), dim3(256), 0, st, *a, at, rbase, recs, poff, plen, pcrc);
+extern "C" int lsmk_wal_seg_emit(const seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff,
+                                 uint32_t* plen, uint32_t* pcrc, hipStream_t st) {
+  hipLaunchKernelGGL(wal_seg_emit, dim3((a->K + 255) / 256), dim3(256), 0, st, *a, at, recs, poff, plen, pcrc);
   return launch_err();
 }
 

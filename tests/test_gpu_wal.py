@@ -562,58 +562,3 @@ def test_device_records(ctx, seg_opts, device, seg_walk):
         finally:
             if d:
                 d.free()
-
-
-@pytest.mark.parametrize("parts", [2, 3, 7])
-def test_pinned_records_in_parts(ctx, seg_opts, parts):
-    """The device replay in parts (wal_seg_parts): each part's records read
-    back into the pinned array while the next parts are walked -- the
-    oracle's records and outcome, a bad CRC inside a later part (its record
-    read from the pinned array, or rebuilt from the device arrays when it lies
-    past cap), a bad type byte, a truncated tail, and a part that declines to
-    candidate doubling (log of logs, no repairs allowed)."""
-    seg_opts(wal_seg_parts=parts)
-    try:
-        img = _binary_log(30000, 73, big_every=997, big=70000)
-        st, orecs, _ = O.wal_replay(img)
-        cases = [img]
-        b = bytearray(img)
-        r = next(r for r in orecs[25000:] if r.type == 1 and r.klen + r.vlen > 0)
-        b[r.payload_off] ^= 0x20
-        cases.append(bytes(b))
-        b = bytearray(img)
-        b[orecs[21000].rec_off] = 0x09
-        cases.append(bytes(b))
-        cases.append(img[:orecs[28000].payload_off + 2])
-        for im in cases:
-            d = ctx.alloc(len(im))
-            d.upload(np.frombuffer(im, np.uint8))
-            try:
-                for cap in (None, 20000):
-                    recs, st, bad = ctx.wal_replay_verify(len(im), device_ptr=d.ptr, cap=cap, pinned_recs=True)
-                    ost, orr, obad = O.wal_replay(im)
-                    assert st == ost
-                    assert [int(x.rec_off) for x in recs] == [x.rec_off for x in orr][:cap]
-                    if st:
-                        assert bad[:3] == obad[:3]
-                    assert ctx.get_stat("wal_walk_path") == 1
-                    del recs
-            finally:
-                d.free()
-        # a log of logs with no repairs allowed: a part declines, the rest by candidate doubling
-        inner = _binary_log(80, 63, hi=200)
-        rng = np.random.default_rng(74)
-        lol = b"".join(O.wal_insert(b"k%d" % i, inner if i % 3 == 0 else rng.bytes(int(rng.integers(0, 400))))
-                       for i in range(3000))
-        seg_opts(wal_seg_bytes=256, wal_seg_rounds=0)
-        d = ctx.alloc(len(lol))
-        d.upload(np.frombuffer(lol, np.uint8))
-        try:
-            recs, st, bad = ctx.wal_replay_verify(len(lol), device_ptr=d.ptr, pinned_recs=True)
-            ost, orr, _ = O.wal_replay(lol)
-            assert st == ost == 0
-            assert [int(x.rec_off) for x in recs] == [x.rec_off for x in orr]
-        finally:
-            d.free()
-    finally:
-        ctx.set_option("wal_seg_parts", 0)

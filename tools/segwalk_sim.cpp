@@ -85,7 +85,7 @@ extern "C" int segwalk_sim_prefix(const uint8_t* img, uint64_t n, uint64_t start
   std::vector<uint64_t> poff(m);
   std::vector<uint32_t> plen(m), pcrc(m);
   for (uint32_t k = 0; k < K; ++k)
-    sg::seg_emit_thread(a, k, (uint32_t)info[sg::kInfoJterm], 0, 0, R.data(), poff.data(), plen.data(), pcrc.data());
+    sg::seg_emit_thread(a, k, (uint32_t)info[sg::kInfoJterm], 0, R.data(), poff.data(), plen.data(), pcrc.data());
   for (uint64_t i = 0; i < m && i < cap; ++i) rec_off[i] = R[i].rec_off;
   return 0;
 }

@@ -4,13 +4,15 @@
 Config 3's 2^26 Zipf payloads framed as wal.rs Insert records (a 13-byte
 header before each, CRCs written on the device: lsmck_wal_frame_insert_device),
 a 97.8 GiB log resident in HBM, replayed by lsmck_wal_replay_verify: the
-header walk on the GPU (in parts: its jump tables for the whole log would not
-fit), the payload CRC pass on the stream kernel, the compare, and the 2^26
-record descriptors copied back to the host.  Every step checks the record
-count and the CRC summary against the oracle's (tests/golden/summaries.json
-config3w), then prints one JSON line with the replay rate.
+segment walk of the headers on the GPU (lsmck_segwalk.h), the payload CRC
+pass on the stream kernel, the compare, and the 2^26 record descriptors
+copied back to the host (into a page-locked array: LSMCK_RECS_PINNED).
+--device-recs 1 adds the same replays with the records left in HBM
+(LSMCK_RECS_DEVICE), --seg-sweep a segment-size A/B of those.  Every step
+checks the record count and the CRC summary against the oracle's
+(tests/golden/summaries.json config3w), then prints one JSON line.
 
-  python3 tools/wal_replay_big.py [--steps 3] [--records 67108864]
+  python3 tools/wal_replay_big.py [--steps 3] [--records 67108864] [--device-recs 1]
 (LSMCK_WAL_TRACE=1 prints the replay's phases to stderr.)"""
 import argparse
 import json
@@ -38,8 +40,6 @@ def main():
                     help="1: the records DMA'd into a page-locked array (LSMCK_RECS_PINNED); 0: staged + copied")
     ap.add_argument("--device-recs", type=int, default=0,
                     help="1: then the same replays with the records left in device memory (LSMCK_RECS_DEVICE)")
-    ap.add_argument("--parts-sweep", default="",
-                    help="comma list of wal_seg_parts: the records-to-host replay per part count (A/B)")
     ap.add_argument("--seg-sweep", default="",
                     help="comma list of wal_seg_bytes: the records-on-device replay per segment size (A/B)")
     a = ap.parse_args()
@@ -80,24 +80,6 @@ def main():
             times.append(dt)
         print(f"replay {s}: {dt * 1e3:.1f} ms", file=sys.stderr, flush=True)
         del recs  # the wrapper reuses its records array once no result refers to it
-    parts = {}
-    for pc in [int(x) for x in a.parts_sweep.split(",") if x]:  # the walk in parts, records read back per part
-        ctx.set_option("wal_seg_parts", pc)
-        ts = []
-        for s in range(a.steps + 1):
-            ctx.sync()
-            t = time.perf_counter()
-            recs, st, bad = ctx.wal_replay_verify(total, device_ptr=d.ptr, cap=n, pinned_recs=bool(a.pinned_recs))
-            dt = time.perf_counter() - t
-            assert st == 0 and len(recs) == n, (st, len(recs), bad)
-            psum = "%08x" % zlib.crc32(np.ascontiguousarray(recs.crc).astype("<u4").tobytes())
-            del recs
-            if s:
-                ts.append(dt)
-        parts[pc] = {"ms_median": round(float(np.median(ts)) * 1e3, 2), "summary_crc32": psum,
-                     "summary_matches_oracle": bool(golden) and psum == golden["summary_crc32"]}
-        print(f"wal_seg_parts {pc}: {parts[pc]}", file=sys.stderr, flush=True)
-    ctx.set_option("wal_seg_parts", 0)
     dev = None
     if a.device_recs:  # the records stay in HBM: the walk, the CRC pass and the compare, no host link
         from lsm_storage_engine_amd.device import WAL_REC_DTYPE
@@ -145,7 +127,7 @@ def main():
         "records_out_bytes": 32 * n, "pinned_recs": bool(a.pinned_recs),
         "walk_path": {1: "segment walk", 2: "candidate doubling", 3: "host walk"}.get(ctx.get_stat("wal_walk_path")),
         "seg_repairs": ctx.get_stat("wal_seg_repairs"), "segments": ctx.get_stat("wal_segments"),
-        "records_on_device": dev, "parts_sweep": parts,
+        "records_on_device": dev,
         "workload": "config 3's 2^26 Zipf payloads (64 B-64 KiB) framed as wal.rs Insert records (13-byte headers), "
                     "headers and CRCs written on the device"}))
 
