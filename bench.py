@@ -80,8 +80,7 @@ def parse():
                     help="comma list of A/B variants timed in interleaved rounds, each a '+' list of "
                          "s<n> (crc_stream: 0 walking kernel only, 1 default), a<n> (crc_ablate: 3 payload "
                          "loads only, 2 stream kernel without loads), p<n> (sha_pair), b<n> (sha_bucket_shift), t<n> (sha_short_blocks), "
-                         "f<n> (sha_bucket_from), d<n> (sha_sorted_desc), q<n> (sha_short_pf), c<n> (sha_short_conc); "
-                         "'-' is the default")
+                         "f<n> (sha_bucket_from); '-' is the default")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--no-stream-ceiling", action="store_true",
                     help="skip the loads-only ceiling run of the same kernel (roofline.loads_only_ceiling)")
@@ -359,16 +358,14 @@ def main():
         ab = {v: [] for v in vs}
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         defaults = {"crc_stream": 1, "crc_ablate": 0, "sha_pair": 1, "sha_bucket_shift": 2, "sha_bucket_from": 128,
-                    "sha_short_blocks": 12, "sha_sorted_desc": 0, "sha_short_pf": 0,
-                    "sha_short_conc": 0}
+                    "sha_short_blocks": 12}
         keys = {"s": "crc_stream", "a": "crc_ablate", "p": "sha_pair", "b": "sha_bucket_shift", "f": "sha_bucket_from",
-                "t": "sha_short_blocks", "d": "sha_sorted_desc", "q": "sha_short_pf",
-                "c": "sha_short_conc"}
+                "t": "sha_short_blocks"}
         for _ in range(a.rounds):
             for v in vs:
                 opts = dict(defaults)
                 for part in ([] if v == "-" else v.split("+")):
-                    m = re.fullmatch(r"([sapbftdqc])(\d+)", part)
+                    m = re.fullmatch(r"([sapbft])(\d+)", part)
                     if not m:
                         raise SystemExit(f"bad variant {v!r}")
                     opts[keys[m.group(1)]] = int(m.group(2))

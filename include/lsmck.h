@@ -177,14 +177,6 @@ int lsmck_device_count(void);
  *                 compression blocks run on a lean kernel with more waves per
  *                 SIMD (default 12; 0 = every message on the window kernel).
  *                 Digests are identical either way.
- *   "sha_short_conc"  1: that lean kernel runs on a second stream, beside the
- *                 window kernel instead of after it (default 0).  A/B switch;
- *                 digests are identical either way.
- *   "sha_short_pf"  1: that lean kernel issues a block's loads before the
- *                 previous block's compression (default 0).  A/B switch.
- *   "sha_sorted_desc"  1: an ordered batch's descriptors are gathered into
- *                 order first, so lanes read them contiguously (default 0).
- *                 A/B switch.
  *   "sha_pair"    the window kernel loads two blocks (a 128-B line) per window
  *                 (1, default) or one (0); 2 and 3 are diagnostics (no payload
  *                 loads: digests invalid / line-aligned loads realigned

@@ -126,10 +126,6 @@ struct DescScratch {
   size_t cap_tmp = 0;
   uint64_t* sha_split = nullptr;  // device, 1 u64: where the order's short tail starts
   size_t cap_split = 0;
-  uint64_t* sha_soff = nullptr;  // the ordered batch's descriptors in order ("sha_sorted_desc")
-  size_t cap_soff = 0;
-  uint32_t* sha_slen = nullptr;
-  size_t cap_slen = 0;
   // stream kernel (lsmck_crc32.hip): eligibility flag, per-wave boundary cuts
   uint32_t* sflag = nullptr;
   uint64_t* scuts = nullptr;
@@ -143,8 +139,6 @@ struct DescScratch {
     if (sha_order) (void)hipFree(sha_order);
     if (sort_tmp) (void)hipFree(sort_tmp);
     if (sha_split) (void)hipFree(sha_split);
-    if (sha_soff) (void)hipFree(sha_soff);
-    if (sha_slen) (void)hipFree(sha_slen);
     *this = DescScratch();
   }
 };
@@ -294,11 +288,6 @@ struct lsmck_ctx {
   int sha_bucket_from = 128;
   int sha_pair = 1;  // SHA-256 batches: two blocks per load window (A/B: DESIGN.md 3.2)
   int sha_short_blocks = 12;  // SHA-256 ordered batches: messages of at most this many blocks on the lean kernel (0 = off)
-  int sha_sorted_desc = 0;   // SHA-256 ordered batches: descriptors gathered into order first (A/B)
-  int sha_short_pf = 0;      // SHA-256 short-tail kernel: next block's loads before this block's compression (A/B)
-  int sha_short_conc = 0;    // SHA-256 short-tail kernel on a second stream, beside the window kernel (A/B)
-  hipStream_t sha_s2 = nullptr;
-  hipEvent_t sha_ev_a = nullptr, sha_ev_b = nullptr;
   unsigned tree_list_threads = 0;  // lsmck_tree_verify: metadata parsing threads (0 = kListThreads)
   size_t wal_prefetch = 4096;  // lsmck_wal_replay_verify: host walk's prefetch distance in bytes (0 = off)
   uint8_t* wal_host = nullptr;  // lsmck_wal_replay_verify of a device image: pinned host copy (grow-only)
@@ -461,11 +450,6 @@ int sha_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const uint6
     rc = lsmk_sha_order(len, n, sc.sha_keys, sc.sha_order, sc.sort_tmp, &tmp, ctx->sha_bucket_shift, ctx->sha_bucket_from, st);
     if (rc) return launch_rc(rc, "sha order (radix sort)");
     order = sc.sha_order;
-    if (ctx->sha_sorted_desc && off) {
-      if ((rc = ensure_dev(&sc.sha_soff, &sc.cap_soff, n)) || (rc = ensure_dev(&sc.sha_slen, &sc.cap_slen, n))) return rc;
-      rc = lsmk_sha_gather_desc(order, off, len, n, sc.sha_soff, sc.sha_slen, st);
-      if (rc) return launch_rc(rc, "sha descriptor gather");
-    }
     if (ctx->sha_short_blocks > 0) {
       if ((rc = ensure_dev(&sc.sha_split, &sc.cap_split, 1))) return rc;
       rc = lsmk_sha_split(sc.sha_keys, n, (uint32_t)ctx->sha_short_blocks, sc.sha_split, st);
@@ -483,25 +467,7 @@ int sha_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const uint6
   P.out = out32;
   P.pair = (uint32_t)ctx->sha_pair;
   P.split = (order && ctx->sha_short_blocks > 0) ? sc.sha_split : nullptr;
-  P.soff = (order && ctx->sha_sorted_desc && off) ? sc.sha_soff : nullptr;
-  P.short_pf = (uint32_t)ctx->sha_short_pf;
-  P.slen = P.soff ? sc.sha_slen : nullptr;
-  // the short tail on a second stream: its latency-bound lanes run beside
-  // the window kernel's VALU-bound ones instead of after them
-  hipStream_t s2 = nullptr;
-  if (ctx->sha_short_conc && P.split && P.order && P.len) {
-    if (!ctx->sha_s2) HIPCHK(hipStreamCreateWithFlags(&ctx->sha_s2, hipStreamNonBlocking));
-    if (!ctx->sha_ev_a) HIPCHK(hipEventCreateWithFlags(&ctx->sha_ev_a, hipEventDisableTiming));
-    if (!ctx->sha_ev_b) HIPCHK(hipEventCreateWithFlags(&ctx->sha_ev_b, hipEventDisableTiming));
-    s2 = ctx->sha_s2;
-    HIPCHK(hipEventRecord(ctx->sha_ev_a, st));
-    HIPCHK(hipStreamWaitEvent(s2, ctx->sha_ev_a, 0));
-  }
-  int rc = lsmk_launch_sha256(&P, st, s2);
-  if (s2) {
-    HIPCHK(hipEventRecord(ctx->sha_ev_b, s2));
-    HIPCHK(hipStreamWaitEvent(st, ctx->sha_ev_b, 0));
-  }
+  int rc = lsmk_launch_sha256(&P, st);
   return rc ? launch_rc(rc, "sha256 kernel") : 0;
 }
 
@@ -934,24 +900,9 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->sha_short_blocks = (int)value;
     return 0;
   }
-  if (!strcmp(key, "sha_sorted_desc")) {  // A/B: ordered SHA batches read their descriptors gathered into order
-    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "sha_sorted_desc must be 0 or 1");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->sha_sorted_desc = (int)value;
-    return 0;
-  }
-  if (!strcmp(key, "sha_short_pf")) {  // A/B: the SHA short-tail kernel loads one block ahead
-    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "sha_short_pf must be 0 or 1");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->sha_short_pf = (int)value;
-    return 0;
-  }
-  if (!strcmp(key, "sha_short_conc")) {  // A/B: the SHA short-tail kernel on a second stream
-    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "sha_short_conc must be 0 or 1");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->sha_short_conc = (int)value;
-    return 0;
-  }
+
+
+
   if (!strcmp(key, "sha_pair")) {  // A/B: SHA-256 batch kernel loads two blocks (a 128-B line) per window
     // 2: diagnostic, the pair kernel's main loop without payload loads (digests invalid);
     // 3: line-aligned loads realigned through LDS rows
@@ -1025,9 +976,6 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   if (ctx->h_verify) (void)hipHostFree(ctx->h_verify);
   if (ctx->h_wrecs) (void)hipHostFree(ctx->h_wrecs);
   if (ctx->wal_emit_ev) (void)hipEventDestroy(ctx->wal_emit_ev);
-  if (ctx->sha_ev_a) (void)hipEventDestroy(ctx->sha_ev_a);
-  if (ctx->sha_ev_b) (void)hipEventDestroy(ctx->sha_ev_b);
-  if (ctx->sha_s2) (void)hipStreamDestroy(ctx->sha_s2);
   if (ctx->wal_recs_ev) (void)hipEventDestroy(ctx->wal_recs_ev);
   if (ctx->h_wrecs1) (void)hipHostFree(ctx->h_wrecs1);
   if (ctx->wal_emit1_ev) (void)hipEventDestroy(ctx->wal_emit1_ev);

@@ -42,9 +42,6 @@ struct ShaParams {
   unsigned char* out;         // 32 bytes per message
   uint32_t pair;              // 1: two blocks per load window (A/B, lsmck_sha256.hip ShaWin2)
   const uint64_t* split;      // device: order index where the short tail starts (lean kernel), null = none
-  const uint64_t* soff;       // with order: off[order[i]] / len[order[i]] at i (coalesced), null = gather them
-  const uint32_t* slen;
-  uint32_t short_pf;          // the short-tail kernel loads a block ahead (A/B)
 };
 
 // One slice of a message streamed through sha256_slices_kernel.
@@ -70,7 +67,7 @@ struct ShaSliceParams {
 
 extern "C" {
 int lsmk_launch_crc32_fixed(const lsmck::CrcParams* P, int ncu, int variant, hipStream_t st);
-int lsmk_launch_sha256(const lsmck::ShaParams* P, hipStream_t st, hipStream_t st2 = nullptr);
+int lsmk_launch_sha256(const lsmck::ShaParams* P, hipStream_t st);
 int lsmk_launch_sha256_slices(const lsmck::ShaSliceParams* P, hipStream_t st);
 uint64_t lsmk_walk_sb_count(uint64_t n);
 int lsmk_launch_crc32_walk(const lsmck::CrcParams* P, uint64_t* sb_prefix, int ncu, int variant, hipStream_t st);
@@ -108,8 +105,6 @@ int lsmk_launch_crc32_compare(const uint32_t* crc, const uint32_t* expected, uin
 int lsmk_sha_order(const uint32_t* len, size_t n, uint16_t* keys_out, uint32_t* order, void* tmp, size_t* tmp_bytes,
                    int coarse, int from, hipStream_t st);
 int lsmk_sha_split(const uint16_t* keys, size_t n, uint32_t t, uint64_t* split, hipStream_t st);
-int lsmk_sha_gather_desc(const uint32_t* order, const uint64_t* off, const uint32_t* len, size_t n, uint64_t* soff,
-                         uint32_t* slen, hipStream_t st);
 int lsmk_launch_gen_stream(unsigned char* dst, uint64_t seed, uint64_t byte_off, uint64_t n, hipStream_t st);
 }
 #endif

@@ -70,29 +70,6 @@ __global__ void sha_split_kernel(const uint16_t* keys, uint64_t n, uint32_t t, u
   *split = lo;
 }
 
-// The ordered batch's descriptors in order (soff[i] = off[order[i]], slen[i]
-// = len[order[i]]): the kernels then read them coalesced, one dependent
-// round trip (order -> descriptor) fewer per message.
-__global__ __launch_bounds__(256) void sha_gather_desc_kernel(const uint32_t* __restrict__ order,
-                                                              const uint64_t* __restrict__ off,
-                                                              const uint32_t* __restrict__ len, uint64_t n,
-                                                              uint64_t* __restrict__ soff, uint32_t* __restrict__ slen) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t m = order[i];
-  soff[i] = off[m];
-  slen[i] = len[m];
-}
-
-extern "C" int lsmk_sha_gather_desc(const uint32_t* order, const uint64_t* off, const uint32_t* len, size_t n,
-                                    uint64_t* soff, uint32_t* slen, hipStream_t st) {
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(sha_gather_desc_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, order, off, len,
-                     (uint64_t)n, soff, slen);
-  hipError_t e = hipGetLastError();
-  return e == hipSuccess ? 0 : -(int)e;
-}
-
 extern "C" int lsmk_sha_split(const uint16_t* keys, size_t n, uint32_t t, uint64_t* split, hipStream_t st) {
   hipLaunchKernelGGL(sha_split_kernel, dim3(1), dim3(1), 0, st, keys, (uint64_t)n, t, split);
   hipError_t e = hipGetLastError();

@@ -355,8 +355,8 @@ __global__ __launch_bounds__(256) void sha256_kernel(ShaParams P) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P.nmsg || (P.split && i >= *P.split)) return;  // (the short tail: sha256_short_kernel)
   uint64_t m = P.order ? P.order[i] : i;
-  uint64_t off = P.soff ? P.soff[i] : (P.off ? P.off[m] : m * P.stride);
-  uint64_t len = P.slen ? P.slen[i] : (P.len ? P.len[m] : P.flen);
+  uint64_t off = P.off ? P.off[m] : m * P.stride;
+  uint64_t len = P.len ? P.len[m] : P.flen;
   uint32_t h[8];
   sha256_iv(h);
   sha256_run<PAIR, ABL>(h, P.base, off, len, true, len << 3);
@@ -370,59 +370,36 @@ __global__ __launch_bounds__(256) void sha256_kernel(ShaParams P) {
 // window kernel 65.3; messages of <= 3 / 6 / 12 / 16 / 32 blocks here 64.6 /
 // 64.4 / 64.2 / 64.3 / 64.9 (default 12: "sha_short_blocks").  Compiled for 5
 // waves (96 VGPRs, 4 spilled) it ran 64.4 against 64.2.
-// block b of a short message: mask past the end, pad, length in the last block
-__device__ __forceinline__ void short_block(uint32_t (&h)[8], uint32_t (&w)[16], uint64_t len, uint64_t b, uint64_t nb) {
-  const uint64_t p0 = b << 6;
-  if (p0 + 64 > len) {
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      int64_t c = (int64_t)len - (int64_t)(p0 + 4 * t);
-      uint32_t mask = c >= 4 ? 0xFFFFFFFFu : (c <= 0 ? 0u : ((1u << (8 * c)) - 1u));
-      uint32_t pad = (c >= 0 && c < 4) ? (0x80u << (8 * c)) : 0u;
-      w[t] = (w[t] & mask) | pad;
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < 16; ++t) w[t] = __builtin_bswap32(w[t]);
-  if (b == nb - 1) {
-    w[14] = (uint32_t)(len >> 29);
-    w[15] = (uint32_t)(len << 3);
-  }
-  sha256_compress(h, w);
-}
-
-// PF (option "sha_short_pf", A/B): the next block's loads are issued before
-// this block is compressed (two 16-word slots, alternating)
-template <bool PF>
 __global__ __launch_bounds__(256) void sha256_short_kernel(ShaParams P) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P.nmsg || i < *P.split) return;
   const uint64_t m = P.order[i];
-  const uint64_t off = P.soff ? P.soff[i] : (P.off ? P.off[m] : m * P.stride);
-  const uint64_t len = P.slen ? P.slen[i] : P.len[m];
+  const uint64_t off = P.off ? P.off[m] : m * P.stride;
+  const uint64_t len = P.len[m];
   const uintptr_t A = (uintptr_t)(P.base + off);
   const uint64_t nb = (len + 9 + 63) >> 6;
   uint32_t h[8];
   sha256_iv(h);
-  if (PF) {
-    uint32_t wa[16], wb[16];
-    load_block(A, len, 0, wa);
-    uint64_t b = 0;
-    for (; b + 2 <= nb; b += 2) {
-      load_block(A, len, (b + 1) << 6, wb);
-      __builtin_amdgcn_sched_barrier(0);
-      short_block(h, wa, len, b, nb);
-      if (b + 2 < nb) load_block(A, len, (b + 2) << 6, wa);
-      __builtin_amdgcn_sched_barrier(0);
-      short_block(h, wb, len, b + 1, nb);
+  for (uint64_t b = 0; b < nb; ++b) {
+    const uint64_t p0 = b << 6;
+    uint32_t w[16];
+    load_block(A, len, p0, w);
+    if (p0 + 64 > len) {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        int64_t c = (int64_t)len - (int64_t)(p0 + 4 * t);
+        uint32_t mask = c >= 4 ? 0xFFFFFFFFu : (c <= 0 ? 0u : ((1u << (8 * c)) - 1u));
+        uint32_t pad = (c >= 0 && c < 4) ? (0x80u << (8 * c)) : 0u;
+        w[t] = (w[t] & mask) | pad;
+      }
     }
-    if (b < nb) short_block(h, wa, len, b, nb);
-  } else {
-    for (uint64_t b = 0; b < nb; ++b) {
-      uint32_t w[16];
-      load_block(A, len, b << 6, w);
-      short_block(h, w, len, b, nb);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) w[t] = __builtin_bswap32(w[t]);
+    if (b == nb - 1) {
+      w[14] = (uint32_t)(len >> 29);
+      w[15] = (uint32_t)(len << 3);
     }
+    sha256_compress(h, w);
   }
   store_digest(P.out + 32 * m, h);
 }
@@ -493,8 +470,7 @@ __global__ __launch_bounds__(256) void gen_stream_kernel(unsigned char* dst, uin
 
 using namespace lsmck;
 
-// st2 (or null: st): the stream of the short-tail kernel (the caller orders it)
-extern "C" int lsmk_launch_sha256(const ShaParams* P, hipStream_t st, hipStream_t st2) {
+extern "C" int lsmk_launch_sha256(const ShaParams* P, hipStream_t st) {
   if (P->nmsg == 0) return 0;
   uint64_t blocks = (P->nmsg + 255) / 256;
   if (P->pair == 2)  // diagnostic: the pair kernel without its payload loads
@@ -505,13 +481,8 @@ extern "C" int lsmk_launch_sha256(const ShaParams* P, hipStream_t st, hipStream_
     hipLaunchKernelGGL(sha256_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, *P);
   else
     hipLaunchKernelGGL(sha256_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, *P);
-  if (P->split && P->order && P->len) {  // the short tail of the order (its start on the device)
-    hipStream_t s = st2 ? st2 : st;
-    if (P->short_pf)
-      hipLaunchKernelGGL(sha256_short_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, *P);
-    else
-      hipLaunchKernelGGL(sha256_short_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, *P);
-  }
+  if (P->split && P->order && P->len)  // the short tail of the order (its start on the device)
+    hipLaunchKernelGGL(sha256_short_kernel, dim3((unsigned)blocks), dim3(256), 0, st, *P);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
 }

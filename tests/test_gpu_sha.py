@@ -174,15 +174,12 @@ def test_length_sorted_batch(ctx, order, shift, start):
     assert np.array_equal(got, O.sha256_batch(data, off, ln, threads=8))
 
 
-@pytest.mark.parametrize("short,sorted_desc,pf", [(0, 0, 0), (1, 0, 0), (3, 0, 0), (8, 0, 0), (12, 0, 0), (127, 0, 0),
-                                                  (0, 1, 0), (12, 1, 0), (127, 1, 0), (12, 0, 1), (127, 1, 1),
-                                                  (3, 1, 1)])
-def test_short_tail_on_the_lean_kernel(ctx, short, sorted_desc, pf):
+@pytest.mark.parametrize("short", [0, 1, 3, 8, 12, 127])
+def test_short_tail_on_the_lean_kernel(ctx, short):
     """"sha_short_blocks" N: in a length-ordered batch, the messages of at most
     N compression blocks (the order's tail, found on the device) run on the
     lean kernel, the rest on the window kernel; every digest at its message's
-    index, identical to the oracle.  Host and device batches; with
-    "sha_sorted_desc" the descriptors are gathered into order first."""
+    index, identical to the oracle.  Host and device batches."""
     rng = np.random.default_rng(78 + short)
     n = 5000
     ln = O.gen_zipf_lengths(0x5EED0033, n).astype(np.uint32)
@@ -194,8 +191,6 @@ def test_short_tail_on_the_lean_kernel(ctx, short, sorted_desc, pf):
     data = O.gen_stream(0x5EED0034, 0, total + 8)
     want = O.sha256_batch(data, off, ln, threads=8)
     ctx.set_option("sha_short_blocks", short)
-    ctx.set_option("sha_sorted_desc", sorted_desc)
-    ctx.set_option("sha_short_pf", pf)
     try:
         assert np.array_equal(ctx.sha256(data, off, ln), want)
         d, d_o, d_l, out = ctx.alloc(total + 8), ctx.alloc(8 * n), ctx.alloc(4 * n), ctx.alloc(32 * n)
@@ -211,8 +206,6 @@ def test_short_tail_on_the_lean_kernel(ctx, short, sorted_desc, pf):
                 b.free()
     finally:
         ctx.set_option("sha_short_blocks", 12)
-        ctx.set_option("sha_sorted_desc", 0)
-        ctx.set_option("sha_short_pf", 0)
 
 
 def _summaries():

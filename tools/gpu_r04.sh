@@ -51,7 +51,7 @@ if has waldiag; then
   python3 tools/kt_stats.py $O/kt_waldev > $O/kt_stats_waldev.txt 2>&1
 fi
 has sha && step sha 400 python3 bench.py --digest sha256 --steps 5 --warmup 1 --no-config4
-has shaab && step shaab 600 python3 bench.py --digest sha256 --variants=-,c1,c1+q1,d1+c1 --rounds 3 --steps 3 --warmup 1 --no-cpu-baseline --no-host-roundtrip --no-config4
+has shaab && step shaab 600 python3 bench.py --digest sha256 --variants=-,t6,t16 --rounds 3 --steps 3 --warmup 1 --no-cpu-baseline --no-host-roundtrip --no-config4
 has tree && step tree 900 python3 -u tools/e2e_tree.py --gib 16 --reps 2 --multi 2 --dir /dev/shm/lsm_e2e_r04
 has server && step server 1100 python3 -u tools/e2e_server.py --gib 100 --dir /dev/shm/lsm_e2e_server_r04
 echo "== done" >&2
