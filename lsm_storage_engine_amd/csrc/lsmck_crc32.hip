@@ -1374,14 +1374,8 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
       if (src >= 64u) {  // the new entries only
         const uint64_t i2 = bt + lane;
         const uint64_t ic = i2 < n ? i2 : n - 1u;
-#ifdef LSMCK_STREAM_WPRIO  // (A/B build: the window's reloads at the top wave priority too)
-        __builtin_amdgcn_s_setprio(3);
-#endif
         Wo = P.off[ic];
         Wl = P.len[ic];
-#ifdef LSMCK_STREAM_WPRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
       }
     }
     // then the payload one tile ahead: after the window, so that waiting for

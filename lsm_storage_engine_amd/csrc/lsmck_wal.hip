@@ -321,11 +321,7 @@ __global__ __launch_bounds__(256) void wal_frame_insert(uint8_t* __restrict__ im
 // sizes segments for ~2^16 of them (lsmk_wal_seg_bytes).
 __global__ __launch_bounds__(256) void wal_seg_walk(seg::SegArgs a) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-#ifdef LSMCK_SEG_REF  // (A/B build: accept() and the walk apart)
-  if (k < a.K) seg::seg_walk_thread_ref(a, k);
-#else
   if (k < a.K) seg::seg_walk_thread(a, k);
-#endif
 }
 
 __global__ __launch_bounds__(256) void wal_seg_jterm(seg::SegArgs a) {
