@@ -162,8 +162,9 @@ LSMCK_HD uint64_t next_of(const Head& h, uint64_t n, uint64_t p, bool* whole) {
 // The segment's outcome from its entry c (a record start on the chain, or
 // the guess; h its header): the walk through the segment ending at e, to the
 // first record start at or past e (kExit) or to the chain's end (kEnd / kBad).
-LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, Head h, uint64_t e, WalkOut* o, uint32_t cnt = 0) {
+LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, Head h, uint64_t e, WalkOut* o) {
   uint64_t p = c;
+  uint32_t cnt = 0;
   for (;;) {
     if (p >= e) {
       o->code = kExit;
@@ -396,116 +397,8 @@ LSMCK_HD void seg_forced(const SegArgs& a, uint32_t k, uint64_t c) {
   a.recs[k] = o.recs;
 }
 
-// The acceptance walk of a candidate c fused with the start of its walk
-// through the segment [.., e): accept()'s verdict, and the walk's state after
-// it -- its outcome when the walk ended (an exit at or past e, or the chain's
-// end), else where it stands after at least kFused records.  A true entry's
-// first records are then read once, not by accept() and again by the walk
-// (segments of a few records: most of their walk); the bound keeps long walks
-// out of the candidate loop, where a wave would wait on each lane's in turn.
-constexpr uint32_t kFused = 16;
-struct Trial {
-  uint64_t q1;    // c's first record end
-  uint64_t p;     // (walk not ended) a record start on c's chain, before e
-  Head h;         // its header
-  uint32_t cnt;   // records of the chain that start in [c, e) so far
-  bool ended;
-  WalkOut o;      // (ended) the walk's outcome
-};
-LSMCK_HD bool trial(const uint8_t* img, uint64_t n, uint64_t c, uint64_t e, uint64_t hop, Trial& T) {
-  uint64_t p = c;
-  Head h = head(img, n, c);
-  uint32_t good = 0, cnt = 0;
-  T.ended = false;
-  for (uint32_t step = 0;; ++step) {
-    if (!T.ended && p >= e) {
-      T.ended = true;
-      T.o.code = kExit;
-      T.o.pos = p;
-      T.o.recs = cnt;
-    }
-    if (good >= kAccept && (T.ended || step >= kFused)) {
-      T.p = p;
-      T.h = h;
-      T.cnt = cnt;
-      return true;
-    }
-    bool whole;
-    const uint64_t q = next_of(h, n, p, &whole);
-    if (p == c) {
-      T.q1 = q;
-      if (q - c > hop) return false;  // a first record this long: not taken (kHop)
-    }
-    if (!T.ended) ++cnt;
-    good += whole;
-    h = head(img, n, q);
-    if (h.cl) {  // the chain ends after the record at p
-      if (!T.ended) {
-        T.ended = true;
-        T.o.code = h.cl;
-        T.o.pos = q;
-        T.o.recs = cnt;
-      }
-      return good >= kAccept || (whole && h.cl == kEnd);
-    }
-    p = q;
-  }
-}
-
-// guess() with trial() for accept(): the guess, and whether T is its walk's
-// state (not when a later start replaced the candidate the trial took)
-LSMCK_HD uint64_t guess_fused(const uint8_t* img, uint64_t n, uint64_t b, uint64_t e, uint64_t hop, Trial& T,
-                              bool* valid) {
-  Scan S;
-  *valid = false;
-  for (uint64_t c = next_cand(S, img, n, b, e); c != kNoGuess; c = next_cand(S, img, n, c + 1, e)) {
-    if (!trial(img, n, c, e, hop, T)) continue;
-    *valid = true;
-    uint64_t q1 = T.q1;
-    for (;;) {
-      const uint64_t lim = q1 < e ? q1 : e;
-      uint64_t c2 = next_cand(S, img, n, c + 1, lim);
-      while (c2 != kNoGuess && !reaches(img, n, c2, q1)) c2 = next_cand(S, img, n, c2 + 1, lim);
-      if (c2 == kNoGuess) return c;
-      c = c2;
-      *valid = false;
-      bool whole;
-      q1 = next_of(head(img, n, c), n, c, &whole);
-    }
-  }
-  return kNoGuess;
-}
-
 // step 1-2 for segment k
 LSMCK_HD void seg_walk_thread(const SegArgs& a, uint32_t k) {
-  if (k == 0) {
-    seg_forced(a, 0, a.start);
-    return;
-  }
-  const uint64_t e = seg_end(a, k);
-  Trial T;
-  bool valid;
-  const uint64_t c = guess_fused(a.img, a.n, seg_begin(a, k), e, a.S > kHop ? a.S : kHop, T, &valid);
-  if (c == kNoGuess) {
-    a.g[k] = c;
-    a.x[k] = 0;
-    a.code[k] = kNone;
-    a.recs[k] = 0;
-  } else if (!valid) {
-    seg_forced(a, k, c);
-  } else {
-    WalkOut o = T.o;
-    if (!T.ended) walk(a.img, a.n, T.p, T.h, e, &o, T.cnt);  // the rest of the walk (every lane of the wave at once)
-    a.g[k] = c;
-    a.x[k] = o.pos;
-    a.code[k] = o.code;
-    a.recs[k] = o.recs;
-  }
-}
-
-// the same steps with accept() and the walk apart (the form the fused one
-// restates; tools/segwalk_sim.cpp checks that both give the same segments)
-LSMCK_HD void seg_walk_thread_ref(const SegArgs& a, uint32_t k) {
   if (k == 0) {
     seg_forced(a, 0, a.start);
     return;
@@ -517,7 +410,7 @@ LSMCK_HD void seg_walk_thread_ref(const SegArgs& a, uint32_t k) {
     a.code[k] = kNone;
     a.recs[k] = 0;
   } else {
-    seg_forced(a, k, c);
+    seg_forced(a, k, c);  // the walk from the guess (every lane of the wave at once)
   }
 }
 

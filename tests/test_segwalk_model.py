@@ -62,15 +62,6 @@ def sim(tmp_path_factory):
         assert rc in (0, 1), rc
         return None if rc == 1 else (list(offs[:m.value]), code.value, pos.value)
     run.prefix = prefix
-    lib.segwalk_sim_vs_ref.restype = C.c_uint64
-    lib.segwalk_sim_vs_ref.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64]
-
-    def vs_ref(img, S, start=0, shift=0):
-        raw = np.zeros(len(img) + shift + 1, dtype=np.uint8)
-        a = raw[shift:shift + len(img)]
-        a[:] = np.frombuffer(bytes(img), np.uint8)
-        return lib.segwalk_sim_vs_ref(a.ctypes.data, len(img), start, S)
-    run.vs_ref = vs_ref
     return run
 
 
@@ -258,28 +249,3 @@ def test_prefix_walks_chain_to_the_whole(sim, S, parts):
             end = (END, 0)
         assert got == want[0]
         assert end == (want[1], want[2])
-
-
-@pytest.mark.parametrize("S", [64, 200, 512, 4096, 65536])
-def test_fused_acceptance_equals_reference(sim, S):
-    """The kernel's walk (acceptance fused with the start of the walk through
-    the segment) gives every segment the guess, exit, code and record count of
-    the form with accept() and the walk apart -- on random binary logs at odd
-    addresses, records longer than the segments, logs of logs, type-byte
-    floods, cuts inside headers and bad type bytes."""
-    rng = np.random.default_rng(S + 7)
-    logs = [random_log(rng, 2000, hi=900), random_log(rng, 300, lo=2000, hi=9000), random_log(rng, 3000, hi=40)]
-    inner = random_log(rng, 40, hi=200)
-    logs.append(b"".join(rec(b"k%d" % i, inner if i % 3 == 0 else rng.bytes(int(rng.integers(0, 300))))
-                         for i in range(400)))
-    logs.append(bytes([1]) * 3000 + random_log(rng, 50))
-    logs.append(bytes([2, 0, 0, 0, 0]) * 700)
-    base = random_log(rng, 300)
-    logs.append(base[:len(base) - 5])
-    b = bytearray(base)
-    b[len(b) // 2] = 0x44
-    logs.append(bytes(b))
-    for i, img in enumerate(logs):
-        for shift in (0, 3):
-            for start in (0, 1, 17):
-                assert sim.vs_ref(img, S, start=start, shift=shift) == 0, (i, shift, start)

@@ -96,24 +96,3 @@ extern "C" int segwalk_sim(const uint8_t* img, uint64_t n, uint64_t start, uint6
   return segwalk_sim_prefix(img, n, start, n, S, max_rounds, rec_off, cap, m_out, code_out, pos_out, repairs, segments,
                             first_fails);
 }
-
-// The kernel's walk (seg_walk_thread: acceptance fused with the walk's start)
-// against the form it restates (seg_walk_thread_ref) over every segment of
-// [start, n): the number of segments whose guess, exit, code or record count
-// differ.
-extern "C" uint64_t segwalk_sim_vs_ref(const uint8_t* img, uint64_t n, uint64_t start, uint64_t S) {
-  if (start >= n) return 0;
-  const uint32_t K = (uint32_t)((n - start + S - 1) / S);
-  std::vector<uint64_t> g1(K), x1(K), g2(K), x2(K), pre(K + 1);
-  std::vector<uint32_t> c1(K), r1(K), c2(K), r2(K);
-  unsigned long long info[sg::kInfoWords] = {};
-  sg::SegArgs a1{img, n, start, S, K, g1.data(), x1.data(), c1.data(), r1.data(), pre.data(), info, n};
-  sg::SegArgs a2{img, n, start, S, K, g2.data(), x2.data(), c2.data(), r2.data(), pre.data(), info, n};
-  uint64_t bad = 0;
-  for (uint32_t k = 0; k < K; ++k) {
-    sg::seg_walk_thread(a1, k);
-    sg::seg_walk_thread_ref(a2, k);
-    bad += g1[k] != g2[k] || c1[k] != c2[k] || (c1[k] != sg::kNone && (x1[k] != x2[k] || r1[k] != r2[k]));
-  }
-  return bad;
-}
