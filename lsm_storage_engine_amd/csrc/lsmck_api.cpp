@@ -249,6 +249,9 @@ struct lsmck_ctx {
     size_t cap_sbsum = 0;
     unsigned long long* sinfo = nullptr;
     unsigned long long* h_sinfo = nullptr;
+    uint64_t* scpp = nullptr;  // the emit's checkpoints (segments of 128 KiB and more)
+    uint32_t* scpc = nullptr;
+    size_t cap_cp = 0;
   } wd;
   bool wal_recs_direct = false;  // this replay's records go by DMA into the caller's pinned array (under wal_mu)
   // LSMCK_RECS_DEVICE (under wal_mu): the caller's device array and its capacity
@@ -966,7 +969,8 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
     if (p) (void)hipFree(p);
   if (ctx->wd.h_info) (void)hipHostFree(ctx->wd.h_info);
   for (void* p : {(void*)ctx->wd.sg, (void*)ctx->wd.sx, (void*)ctx->wd.spre, (void*)ctx->wd.scode,
-                  (void*)ctx->wd.srecs, (void*)ctx->wd.sbsum, (void*)ctx->wd.sinfo})
+                  (void*)ctx->wd.srecs, (void*)ctx->wd.sbsum, (void*)ctx->wd.sinfo, (void*)ctx->wd.scpp,
+                  (void*)ctx->wd.scpc})
     if (p) (void)hipFree(p);
   if (ctx->wd.h_sinfo) (void)hipHostFree(ctx->wd.h_sinfo);
   for (void* p : {(void*)ctx->d_vcrc, (void*)ctx->d_woff, (void*)ctx->d_wlen, (void*)ctx->d_wexp})
@@ -1412,7 +1416,22 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
       }
       if (!W.sinfo) HIPCHK(hipMalloc((void**)&W.sinfo, sg::kInfoWords * 8));
       if (!W.h_sinfo) HIPCHK(hipHostMalloc((void**)&W.h_sinfo, sg::kInfoWords * 8, hipHostMallocDefault));
-      a = sg::SegArgs{img, n, start, S, K, W.sg, W.sx, W.scode, W.srecs, W.spre, W.sinfo, lim};
+      // the emit from checkpoints every 64 KiB (up to 32 per segment): its
+      // walks run 32x as many threads, each a 32nd as long
+      const uint32_t nsub = S >= (128u << 10) ? (uint32_t)std::min<uint64_t>(32, S >> 16) : 1u;
+      if (nsub > 1 && W.cap_cp < (size_t)K * nsub) {
+        for (void* p : {(void*)W.scpp, (void*)W.scpc})
+          if (p) (void)hipFree(p);
+        W.scpp = nullptr;
+        W.scpc = nullptr;
+        W.cap_cp = 0;
+        const size_t c = (size_t)K * nsub;
+        HIPCHK(hipMalloc((void**)&W.scpp, c * 8));
+        HIPCHK(hipMalloc((void**)&W.scpc, c * 4));
+        W.cap_cp = c;
+      }
+      a = sg::SegArgs{img, n, start, S, K, W.sg, W.sx, W.scode, W.srecs, W.spre, W.sinfo, lim,
+                      nsub, S / nsub, nsub > 1 ? W.scpp : nullptr, nsub > 1 ? W.scpc : nullptr};
       if ((rc = lsmk_wal_seg_walk(&a, st))) return launch_rc(rc, "wal segment walk kernel");
     }
     if ((rc = lsmk_wal_seg_round(&a, W.sbsum, st))) return launch_rc(rc, "wal segment check kernels");

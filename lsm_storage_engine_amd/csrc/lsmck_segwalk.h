@@ -368,6 +368,15 @@ struct SegArgs {
   uint64_t* pre;  // K + 1: exclusive scan of the placement words
   unsigned long long* info;
   uint64_t lim;   // the prefix end
+  // emit checkpoints (nsub > 1): segment k's walk notes, for each of its
+  // nsub sub-segments j (bytes [begin + j*sub, ..)), the first chain record
+  // starting at or past the sub-segment's start (cpp) and how many of the
+  // segment's records come before it (cpc) -- the emit then runs one thread
+  // per sub-segment instead of one per segment
+  uint32_t nsub;
+  uint64_t sub;
+  uint64_t* cpp;  // K * nsub
+  uint32_t* cpc;
 };
 
 LSMCK_HD uint64_t seg_begin(const SegArgs& a, uint32_t k) { return a.start + (uint64_t)k * a.S; }
@@ -381,6 +390,46 @@ LSMCK_HD uint32_t seg_of(const SegArgs& a, uint64_t pos) {
 }
 
 // the forced walk of segment k from its entry c (a position on the chain)
+// walk() of segment k from its entry c (header h), noting the emit
+// checkpoints as it passes each sub-segment's start
+LSMCK_HD void walk_cp(const SegArgs& a, uint32_t k, uint64_t c, Head h, WalkOut* o) {
+  const uint8_t* img = a.img;
+  const uint64_t n = a.n, e = seg_end(a, k), b0 = seg_begin(a, k);
+  uint64_t* cpp = a.cpp + (uint64_t)k * a.nsub;
+  uint32_t* cpc = a.cpc + (uint64_t)k * a.nsub;
+  uint32_t j = 0;
+  uint64_t p = c;
+  uint32_t cnt = 0;
+  for (;;) {
+    for (; j < a.nsub && b0 + j * a.sub <= p; ++j) {  // sub-segments whose start p is the first record at or past
+      cpp[j] = p;
+      cpc[j] = cnt;
+    }
+    if (p >= e) {
+      o->code = kExit;
+      o->pos = p;
+      o->recs = cnt;
+      break;
+    }
+    bool whole;
+    const uint64_t q = next_of(h, n, p, &whole);
+    ++cnt;
+    h = head(img, n, q);
+    if (h.cl) {
+      o->code = h.cl;
+      o->pos = q;
+      o->recs = cnt;
+      p = q;
+      break;
+    }
+    p = q;
+  }
+  for (; j < a.nsub; ++j) {  // past the chain's end or the exit: no records there
+    cpp[j] = p;
+    cpc[j] = cnt;
+  }
+}
+
 LSMCK_HD void seg_forced(const SegArgs& a, uint32_t k, uint64_t c) {
   WalkOut o;
   const Head h = head(a.img, a.n, c);
@@ -388,6 +437,12 @@ LSMCK_HD void seg_forced(const SegArgs& a, uint32_t k, uint64_t c) {
     o.code = h.cl;
     o.pos = c;
     o.recs = 0;
+    for (uint32_t j = 0; a.nsub > 1 && j < a.nsub; ++j) {  // no records in any sub-segment
+      a.cpp[(uint64_t)k * a.nsub + j] = c;
+      a.cpc[(uint64_t)k * a.nsub + j] = 0;
+    }
+  } else if (a.nsub > 1) {
+    walk_cp(a, k, c, h, &o);
   } else {
     walk(a.img, a.n, c, h, seg_end(a, k), &o);
   }
@@ -452,14 +507,23 @@ LSMCK_HD void seg_repair(const SegArgs& a, uint32_t j, uint32_t budget) {
 
 // step 4 for segment k (after the check passed): its records at `at` + its
 // place, as lsmck_wal_rec entries, CRC descriptors and stored CRCs
+// (sub-segment j of segment k when a.nsub > 1: its records only, from the
+// checkpoint the walk noted)
 template <class Rec>
 LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint64_t at, Rec* recs, uint64_t* poff,
-                              uint32_t* plen, uint32_t* pcrc) {
+                              uint32_t* plen, uint32_t* pcrc, uint32_t j = 0) {
   if (k > jterm || a.code[k] == kNone) return;
-  uint64_t i = at + (a.pre[k] & kRecMask);
-  uint64_t p = a.g[k];
+  uint32_t r = 0, rend = a.recs[k];
+  uint64_t p = a.g[k], pend = ~0ull;
+  if (a.nsub > 1) {
+    const uint64_t t = (uint64_t)k * a.nsub + j;
+    p = a.cpp[t];
+    r = a.cpc[t];
+    if (j + 1 < a.nsub) pend = seg_begin(a, k) + (uint64_t)(j + 1) * a.sub;
+  }
+  uint64_t i = at + (a.pre[k] & kRecMask) + r;
   const uint8_t* img = a.img;
-  for (uint32_t r = 0; r < a.recs[k]; ++r, ++i) {
+  for (; r < rend && p < pend; ++r, ++i) {
     const Head h = head(img, a.n, p);
     const uint32_t hl = hdr_len(h.t);
     const uint32_t dlen = h.klen + h.vlen;

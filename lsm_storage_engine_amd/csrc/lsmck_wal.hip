@@ -452,8 +452,10 @@ __global__ void wal_seg_repair(seg::SegArgs a, uint32_t budget) {
 __global__ __launch_bounds__(256) void wal_seg_emit(seg::SegArgs a, uint64_t at, lsmck_wal_rec* __restrict__ recs,
                                                      uint64_t* __restrict__ poff, uint32_t* __restrict__ plen,
                                                      uint32_t* __restrict__ pcrc) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < a.K) seg::seg_emit_thread(a, k, (uint32_t)a.info[seg::kInfoJterm], at, recs, poff, plen, pcrc);
+  // one thread per sub-segment (a.nsub per segment; 1: per segment)
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = (uint32_t)(t / a.nsub), j = (uint32_t)(t % a.nsub);
+  if (k < a.K) seg::seg_emit_thread(a, k, (uint32_t)a.info[seg::kInfoJterm], at, recs, poff, plen, pcrc, j);
 }
 
 }  // namespace lsmck
@@ -506,7 +508,9 @@ extern "C" int lsmk_wal_seg_repair(const seg::SegArgs* a, uint32_t budget, hipSt
 
 extern "C" int lsmk_wal_seg_emit(const seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff,
                                  uint32_t* plen, uint32_t* pcrc, hipStream_t st) {
-  hipLaunchKernelGGL(wal_seg_emit, dim3((a->K + 255) / 256), dim3(256), 0, st, *a, at, recs, poff, plen, pcrc);
+  const uint64_t threads = (uint64_t)a->K * a->nsub;
+  hipLaunchKernelGGL(wal_seg_emit, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, *a, at, recs, poff, plen,
+                     pcrc);
   return launch_err();
 }
 

@@ -402,19 +402,20 @@ def _binary_log(n, seed, lo=0, hi=600, big_every=0, big=0):
     return b"".join(parts)
 
 
-@pytest.mark.parametrize("seg", [0, 64, 512, 4096])
+@pytest.mark.parametrize("seg", [0, 64, 512, 4096, 262144])
 @pytest.mark.parametrize("shift", [0, 5])
 def test_segment_walk(ctx, seg_opts, seg, shift):
     """The segment walk (lsmck_segwalk.h) of device images: random binary
     payloads (bogus starts everywhere), segments from 64 B (far shorter than
     the records: most hold no true entry) to auto, the image at an odd
     address; a bad type byte, a truncated tail, a corrupted payload -- the
-    oracle's records and outcome, and the walk reports the segment path."""
+    oracle's records and outcome, and the walk reports the segment path.
+    256 KiB segments emit from the walk's checkpoints (4 sub-segments each)."""
     seg_opts(wal_seg_bytes=seg)
     img = _binary_log(20000, 61)
     assert same(ctx, img, device=True, shift=shift) == 0
     assert ctx.get_stat("wal_walk_path") == 1
-    if seg in (0, 4096):  # segments longer than every record: no guess to repair
+    if seg in (0, 4096, 262144):  # segments longer than every record: no guess to repair
         assert ctx.get_stat("wal_seg_repairs") == 0
     st, recs, _ = O.wal_replay(img)
     b = bytearray(img)

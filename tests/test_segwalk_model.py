@@ -62,6 +62,8 @@ def sim(tmp_path_factory):
         assert rc in (0, 1), rc
         return None if rc == 1 else (list(offs[:m.value]), code.value, pos.value)
     run.prefix = prefix
+    lib.segwalk_sim_set_nsub.argtypes = [C.c_uint32]
+    run.set_nsub = lib.segwalk_sim_set_nsub
     return run
 
 
@@ -249,3 +251,26 @@ def test_prefix_walks_chain_to_the_whole(sim, S, parts):
             end = (END, 0)
         assert got == want[0]
         assert end == (want[1], want[2])
+
+
+@pytest.mark.parametrize("nsub", [2, 4, 32])
+@pytest.mark.parametrize("S", [256, 4096, 65536])
+def test_emit_by_sub_segments(sim, S, nsub):
+    """The emit from the walk's checkpoints, one thread per sub-segment: the
+    same records as the chain walk -- records longer than sub-segments and
+    segments, entries after a sub-segment start, repairs (which rewalk and
+    re-note the checkpoints), a bad type byte and a cut inside a record."""
+    sim.set_nsub(nsub)
+    try:
+        rng = np.random.default_rng(S * 3 + nsub)
+        for img in (random_log(rng, 1500, hi=900), random_log(rng, 200, lo=1000, hi=30000),
+                    random_log(rng, 3000, hi=30)):
+            check(sim, img, S)  # (asserts the records, the code and the bad byte)
+            check(sim, img, S, start=1, shift=3)
+            want, _, _ = chain(img)
+            b = bytearray(img)
+            b[want[len(want) // 2]] = 0x55
+            check(sim, bytes(b), S)
+            check(sim, img[:len(img) - 11], S)
+    finally:
+        sim.set_nsub(1)

@@ -22,6 +22,8 @@ struct SimRec {
 
 static uint64_t* g_dbg = nullptr;  // debug: the first round's guesses
 extern "C" void segwalk_sim_debug(uint64_t* g) { g_dbg = g; }
+static uint32_t g_nsub = 1;  // emit checkpoints: sub-segments per segment (1 = none)
+extern "C" void segwalk_sim_set_nsub(uint32_t v) { g_nsub = v ? v : 1; }
 
 // the records starting in [start, lim): code_out kExit with pos_out the first
 // record start at or past lim when the chain goes on past the prefix
@@ -43,7 +45,10 @@ extern "C" int segwalk_sim_prefix(const uint8_t* img, uint64_t n, uint64_t start
   std::vector<uint64_t> g(K + 1), x(K + 1), pre(K + 1);
   std::vector<uint32_t> code(K + 1), recs(K + 1);
   unsigned long long info[sg::kInfoWords] = {};
-  sg::SegArgs a{img, n, start, S, K, g.data(), x.data(), code.data(), recs.data(), pre.data(), info, lim};
+  std::vector<uint64_t> cpp((size_t)K * g_nsub);
+  std::vector<uint32_t> cpc((size_t)K * g_nsub);
+  sg::SegArgs a{img, n, start, S, K, g.data(), x.data(), code.data(), recs.data(), pre.data(), info, lim,
+                g_nsub, (S + g_nsub - 1) / g_nsub, cpp.data(), cpc.data()};
   for (uint32_t k = 0; k < K; ++k) sg::seg_walk_thread(a, k);
   if (g_dbg) std::copy(g.begin(), g.begin() + K, g_dbg);
   for (int round = 0;; ++round) {
@@ -85,7 +90,8 @@ extern "C" int segwalk_sim_prefix(const uint8_t* img, uint64_t n, uint64_t start
   std::vector<uint64_t> poff(m);
   std::vector<uint32_t> plen(m), pcrc(m);
   for (uint32_t k = 0; k < K; ++k)
-    sg::seg_emit_thread(a, k, (uint32_t)info[sg::kInfoJterm], 0, R.data(), poff.data(), plen.data(), pcrc.data());
+    for (uint32_t j = 0; j < a.nsub; ++j)
+      sg::seg_emit_thread(a, k, (uint32_t)info[sg::kInfoJterm], 0, R.data(), poff.data(), plen.data(), pcrc.data(), j);
   for (uint64_t i = 0; i < m && i < cap; ++i) rec_off[i] = R[i].rec_off;
   return 0;
 }
