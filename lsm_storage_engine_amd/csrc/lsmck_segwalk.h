@@ -56,7 +56,10 @@ constexpr uint32_t kNoSeg = 0xFFFFFFFFu;
 // a guessed entry must lead to this many complete records (or to a clean
 // end of the log) before it is taken: a bogus one passes a step with ~1/128
 // odds on random payloads, so six steps leave ~1e-13 per candidate
-constexpr uint32_t kAccept = 6;
+#ifndef LSMCK_SEG_ACCEPT
+#define LSMCK_SEG_ACCEPT 6
+#endif
+constexpr uint32_t kAccept = LSMCK_SEG_ACCEPT;
 // ... and its first record must end within this many bytes (or the segment
 // length, if longer).  A bogus start reads a random 32-bit length; on a log
 // past 4 GiB it lands inside the log, and exactly on a true record with odds
@@ -326,6 +329,9 @@ LSMCK_HD uint64_t guess(const uint8_t* img, uint64_t n, uint64_t b, uint64_t e, 
   Scan S;
   for (uint64_t c = next_cand(S, img, n, b, e); c != kNoGuess; c = next_cand(S, img, n, c + 1, e)) {
     if (!accept(img, n, c, hop)) continue;
+#ifdef LSMCK_SEG_C2_MIN_HOP  // (A/B build: the later-start rule only where first records may be this long)
+    if (hop < LSMCK_SEG_C2_MIN_HOP) return c;
+#endif
     for (;;) {
       bool whole;
       const uint64_t q1 = next_of(head(img, n, c), n, c, &whole), lim = q1 < e ? q1 : e;
