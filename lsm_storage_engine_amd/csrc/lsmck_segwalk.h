@@ -54,12 +54,12 @@ constexpr uint32_t kBad = 3;   // the chain ends in the segment: `pos` holds a b
 constexpr uint64_t kNoGuess = ~0ull;
 constexpr uint32_t kNoSeg = 0xFFFFFFFFu;
 // a guessed entry must lead to this many complete records (or to a clean
-// end of the log) before it is taken: a bogus one passes a step with ~1/128
-// odds on random payloads, so six steps leave ~1e-13 per candidate
-#ifndef LSMCK_SEG_ACCEPT
-#define LSMCK_SEG_ACCEPT 6
-#endif
-constexpr uint32_t kAccept = LSMCK_SEG_ACCEPT;
+// end of the log) before it is taken: a bogus one passes its first step only
+// with a first record of at most the hop (below), and then each further one
+// with ~1/128 odds on random payloads -- ~1e-11 per candidate for a 64 KiB
+// hop.  (Six ran the 0.24 GB log's walk 3% slower and caught nothing more,
+// profiles/r04/o; a wrong guess that passes is caught by the check anyway.)
+constexpr uint32_t kAccept = 4;
 // ... and its first record must end within this many bytes (or the segment
 // length, if longer).  A bogus start reads a random 32-bit length; on a log
 // past 4 GiB it lands inside the log, and exactly on a true record with odds
@@ -70,6 +70,13 @@ constexpr uint32_t kAccept = LSMCK_SEG_ACCEPT;
 // 4 GiB / 64 KiB.  A true first record longer than this is refused and
 // repaired by the check (or the walk re-segments, with longer hops).
 constexpr uint64_t kHop = 65536;
+// The later-start rule (guess()) where a first record may be this long or
+// longer: a bogus start's random length lands on a true record inside a
+// window of hop bytes with odds hop / 2^32 x (1 / record spacing) -- ~3e-8
+// per candidate for 64 KiB, no repair in practice, but one segment in a few
+// thousand for 2 MiB segments.  Below it the rule's scan of the first
+// record's payload is skipped (0.24 GB log: 0.33 vs 0.42 ms, profiles/r04/o).
+constexpr uint64_t kLaterMinHop = 131072;
 #ifndef LSMCK_SCAN_BLOCKS
 #define LSMCK_SCAN_BLOCKS 1
 #endif
@@ -324,14 +331,13 @@ LSMCK_HD bool reaches(const uint8_t* img, uint64_t n, uint64_t c, uint64_t q) {
 // bogus start before the segment's first true record whose random length
 // happens to land on a later true record: its chains merge with the true
 // one, so its walk is taken, but its first "record" covers the true entry,
-// whose chain reaches the merge point.  kNoGuess: no start taken.
+// whose chain reaches the merge point (the rule runs where the hop is at
+// least kLaterMinHop).  kNoGuess: no start taken.
 LSMCK_HD uint64_t guess(const uint8_t* img, uint64_t n, uint64_t b, uint64_t e, uint64_t hop) {
   Scan S;
   for (uint64_t c = next_cand(S, img, n, b, e); c != kNoGuess; c = next_cand(S, img, n, c + 1, e)) {
     if (!accept(img, n, c, hop)) continue;
-#ifdef LSMCK_SEG_C2_MIN_HOP  // (A/B build: the later-start rule only where first records may be this long)
-    if (hop < LSMCK_SEG_C2_MIN_HOP) return c;
-#endif
+    if (hop < kLaterMinHop) return c;
     for (;;) {
       bool whole;
       const uint64_t q1 = next_of(head(img, n, c), n, c, &whole), lim = q1 < e ? q1 : e;
