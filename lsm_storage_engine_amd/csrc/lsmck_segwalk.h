@@ -70,13 +70,15 @@ constexpr uint32_t kAccept = 4;
 // 4 GiB / 64 KiB.  A true first record longer than this is refused and
 // repaired by the check (or the walk re-segments, with longer hops).
 constexpr uint64_t kHop = 65536;
-// The later-start rule (guess()) where a first record may be this long or
-// longer: a bogus start's random length lands on a true record inside a
-// window of hop bytes with odds hop / 2^32 x (1 / record spacing) -- ~3e-8
-// per candidate for 64 KiB, no repair in practice, but one segment in a few
-// thousand for 2 MiB segments.  Below it the rule's scan of the first
-// record's payload is skipped (0.24 GB log: 0.33 vs 0.42 ms, profiles/r04/o).
-constexpr uint64_t kLaterMinHop = 131072;
+// The later-start rule (guess()) is skipped for segments of 4 KiB up to (not
+// including) 128 KiB: there a wrong guess that merges with the chain is rare
+// (none in the host model's logs: tools/segwalk_sim.cpp over wal_diag-like,
+// binary-payload and Zipf logs, 4 to 64 KiB segments), and the rule's scan of
+// the accepted record's payload is most of a small segment's guess (0.24 GB
+// log: 0.33 vs 0.42 ms, profiles/r04/o).  Segments shorter than records
+// (under 4 KiB) often hold no true start, and long hops (2 MiB segments)
+// let bogus lengths land on a true record: the rule stays for both.
+constexpr uint64_t kLaterSkipFrom = 4096, kLaterSkipTo = 131072;
 #ifndef LSMCK_SCAN_BLOCKS
 #define LSMCK_SCAN_BLOCKS 1
 #endif
@@ -331,13 +333,13 @@ LSMCK_HD bool reaches(const uint8_t* img, uint64_t n, uint64_t c, uint64_t q) {
 // bogus start before the segment's first true record whose random length
 // happens to land on a later true record: its chains merge with the true
 // one, so its walk is taken, but its first "record" covers the true entry,
-// whose chain reaches the merge point (the rule runs where the hop is at
-// least kLaterMinHop).  kNoGuess: no start taken.
-LSMCK_HD uint64_t guess(const uint8_t* img, uint64_t n, uint64_t b, uint64_t e, uint64_t hop) {
+// whose chain reaches the merge point (`later`: the rule runs; see
+// kLaterSkipFrom).  kNoGuess: no start taken.
+LSMCK_HD uint64_t guess(const uint8_t* img, uint64_t n, uint64_t b, uint64_t e, uint64_t hop, bool later = true) {
   Scan S;
   for (uint64_t c = next_cand(S, img, n, b, e); c != kNoGuess; c = next_cand(S, img, n, c + 1, e)) {
     if (!accept(img, n, c, hop)) continue;
-    if (hop < kLaterMinHop) return c;
+    if (!later) return c;
     for (;;) {
       bool whole;
       const uint64_t q1 = next_of(head(img, n, c), n, c, &whole), lim = q1 < e ? q1 : e;
@@ -470,7 +472,12 @@ LSMCK_HD void seg_walk_thread(const SegArgs& a, uint32_t k) {
     seg_forced(a, 0, a.start);
     return;
   }
-  const uint64_t c = guess(a.img, a.n, seg_begin(a, k), seg_end(a, k), a.S > kHop ? a.S : kHop);
+  const uint64_t c = guess(a.img, a.n, seg_begin(a, k), seg_end(a, k), a.S > kHop ? a.S : kHop,
+#ifdef LSMCK_SEG_LATER_ALWAYS  // (host model A/B, tools/segwalk_repairs.py)
+                           true);
+#else
+                           a.S < kLaterSkipFrom || a.S >= kLaterSkipTo);
+#endif
   if (c == kNoGuess) {
     a.g[k] = c;
     a.x[k] = 0;
