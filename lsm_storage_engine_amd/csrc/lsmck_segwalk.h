@@ -238,48 +238,6 @@ LSMCK_HD void load16(const uint8_t* a, uint32_t w[4]) {
   memcpy(w, a, 16);
 #endif
 }
-// word d (0..15) of a 64-byte block in registers, by a tree of bitwise
-// blends (no per-lane register indexing on the GPU; written with ?: hipcc
-// turned the tree back into an indexed scratch array)
-LSMCK_HD uint32_t blend(uint32_t x, uint32_t y, uint32_t m) { return (x & ~m) | (y & m); }
-LSMCK_HD uint32_t sel16(const uint32_t* w, uint32_t d) {
-  const uint32_t m0 = 0u - (d & 1u), m1 = 0u - ((d >> 1) & 1u), m2 = 0u - ((d >> 2) & 1u), m3 = 0u - ((d >> 3) & 1u);
-  const uint32_t a0 = blend(w[0], w[1], m0), a1 = blend(w[2], w[3], m0), a2 = blend(w[4], w[5], m0),
-                 a3 = blend(w[6], w[7], m0), a4 = blend(w[8], w[9], m0), a5 = blend(w[10], w[11], m0),
-                 a6 = blend(w[12], w[13], m0), a7 = blend(w[14], w[15], m0);
-  const uint32_t b0 = blend(a0, a1, m1), b1 = blend(a2, a3, m1), b2 = blend(a4, a5, m1), b3 = blend(a6, a7, m1);
-  return blend(blend(b0, b1, m2), blend(b2, b3, m2), m3);
-}
-#ifndef LSMCK_SCAN_QUICK
-#define LSMCK_SCAN_QUICK 1
-#endif
-// Candidates of a block whose first record ends more than `hop` bytes on
-// (accept() refuses them, and reaches() cannot take them) dropped from its
-// mask while the block is in registers: the record length comes from the
-// block's own words (headers inside the block), not from a load per
-// candidate.  p: the block's image position.
-LSMCK_HD uint64_t quick_drop(uint64_t m, const uint32_t* w, uint64_t p, uint64_t n, uint64_t hop) {
-  uint64_t keep = 0;
-  while (m) {
-    const uint32_t i = (uint32_t)__builtin_ctzll(m);
-    m &= m - 1;
-    if (i <= 51u) {  // bytes i .. i+12 in the block
-      const uint32_t t = (sel16(w, i >> 2) >> (8u * (i & 3u))) & 0xFFu;
-      const uint32_t d = (i + 5u) >> 2, sh = (i + 5u) & 3u;
-      const uint32_t w0 = sel16(w, d), w1 = sel16(w, d + 1u), w2 = sel16(w, d + 2u < 16u ? d + 2u : 15u);
-      const uint32_t klen = fsh(w1, w0, sh), vlen = t == 1u ? fsh(w2, w1, sh) : 0u;
-      const uint32_t hl = hdr_len(t), dlen = klen + vlen;
-      const uint64_t c = p + i;
-      if (c + hl <= n) {
-        const uint64_t avail = n - (c + hl);
-        const uint64_t q = hl + (dlen <= avail ? (uint64_t)dlen : avail);
-        if (q > hop) continue;
-      }
-    }
-    keep |= 1ull << i;
-  }
-  return keep;
-}
 // The scan's current chunk: kScanBlocks 64-byte blocks, aligned in the
 // address space, and their type-byte masks.  A lane steps through the
 // candidates of a chunk without loading it again.
@@ -291,7 +249,7 @@ struct Scan {
 // The first type byte c in [from, e) whose header fits, or kNoGuess.  The
 // chunk holding `from` comes from S when it is the one already loaded (vector
 // loads inside the image, byte loads at its two ends); then the ones after it.
-LSMCK_HD uint64_t next_cand(Scan& S, const uint8_t* img, uint64_t n, uint64_t from, uint64_t e, uint64_t hop) {
+LSMCK_HD uint64_t next_cand(Scan& S, const uint8_t* img, uint64_t n, uint64_t from, uint64_t e) {
   // all the chunk's loads are in flight together, so a lane that starts
   // inside a long record waits on a quarter as many dependent loads (the
   // wave waits for its slowest lane)
@@ -320,7 +278,7 @@ LSMCK_HD uint64_t next_cand(Scan& S, const uint8_t* img, uint64_t n, uint64_t fr
             const uint64_t nib = ((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u);
             mj |= nib << (4 * d);
           }
-          S.m[j] = LSMCK_SCAN_QUICK ? quick_drop(mj, w + 16 * j, (uint64_t)(p0 + 64 * j), n, hop) : mj;
+          S.m[j] = mj;
         }
       } else {
         for (int j = 0; j < kScanBlocks; ++j) {
@@ -379,14 +337,14 @@ LSMCK_HD bool reaches(const uint8_t* img, uint64_t n, uint64_t c, uint64_t q) {
 // kLaterSkipFrom).  kNoGuess: no start taken.
 LSMCK_HD uint64_t guess(const uint8_t* img, uint64_t n, uint64_t b, uint64_t e, uint64_t hop, bool later = true) {
   Scan S;
-  for (uint64_t c = next_cand(S, img, n, b, e, hop); c != kNoGuess; c = next_cand(S, img, n, c + 1, e, hop)) {
+  for (uint64_t c = next_cand(S, img, n, b, e); c != kNoGuess; c = next_cand(S, img, n, c + 1, e)) {
     if (!accept(img, n, c, hop)) continue;
     if (!later) return c;
     for (;;) {
       bool whole;
       const uint64_t q1 = next_of(head(img, n, c), n, c, &whole), lim = q1 < e ? q1 : e;
-      uint64_t c2 = next_cand(S, img, n, c + 1, lim, hop);
-      while (c2 != kNoGuess && !reaches(img, n, c2, q1)) c2 = next_cand(S, img, n, c2 + 1, lim, hop);
+      uint64_t c2 = next_cand(S, img, n, c + 1, lim);
+      while (c2 != kNoGuess && !reaches(img, n, c2, q1)) c2 = next_cand(S, img, n, c2 + 1, lim);
       if (c2 == kNoGuess) return c;
       c = c2;
     }
