@@ -80,7 +80,7 @@ constexpr uint64_t kHop = 65536;
 // let bogus lengths land on a true record: the rule stays for both.
 constexpr uint64_t kLaterSkipFrom = 4096, kLaterSkipTo = 131072;
 #ifndef LSMCK_SCAN_BLOCKS
-#define LSMCK_SCAN_BLOCKS 1
+#define LSMCK_SCAN_BLOCKS 4
 #endif
 constexpr int kScanBlocks = LSMCK_SCAN_BLOCKS;  // 64-byte blocks the guess scan loads per iteration
 // per-segment record counts and the guessed-segment count share one u64 in
