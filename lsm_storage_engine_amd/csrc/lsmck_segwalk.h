@@ -12,7 +12,7 @@
 //      whose own walk is plausible (kAccept complete records, or a clean end
 //      of the log; a bogus start inside a payload reads a random length and
 //      lands on a non-type byte within a step or two);
-//   2. from the guess it walks the headers (reading ~9 bytes per record, not
+//   2. from the guess it walks the headers (one 16-byte load per record, not
 //      the payloads) to the first record start at or past the segment's end:
 //      its EXIT -- or to the chain's end (EOF, or a bad type byte);
 //   3. the guesses are checked all at once: with segment 0 right, every
