@@ -190,6 +190,12 @@ int lsmck_device_count(void);
  *                 instead of a GPU lane (0 = 16 MiB).
  *   "wal_prefetch"  bytes lsmck_wal_replay_verify's header walk prefetches
  *                 ahead of its position (default 4096; 0 = off).  A/B switch.
+ *   "stage_numa"  where host-memory batches stage: -2 (default) the
+ *                 device's NUMA node when the host has several -- pinned
+ *                 buffers allocated there (lsmck_host_alloc_pinned too) and the
+ *                 copy threads on its CPUs; -1 HIP's default placement and
+ *                 unpinned threads; >= 0 that node.  Applies to buffers
+ *                 allocated after the call.
  *   "stage_threads"  host-memory batches: threads that copy a pageable chunk
  *                 into its pinned staging slot (default 8; 1 = one memcpy).
  *   "wal_gpu_walk"  lsmck_wal_replay_verify of a device image: 1 = header walk
@@ -232,6 +238,9 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
  *                    3 = host walk.
  *   "wal_seg_repairs"  its segment walk's repaired check failures.
  *   "wal_segments"   its segment walk's segment count.
+ *   "numa_node"      the device's NUMA node (sysfs of its PCI function; -1
+ *                    unknown), and "stage_numa_node" the node the context's
+ *                    pinned buffers and copy threads are placed on (-1: none).
  * Returns 0 and *value, or LSMCK_EINVAL for an unknown key. */
 int lsmck_ctx_get_stat(lsmck_ctx* ctx, const char* key, long* value);
 

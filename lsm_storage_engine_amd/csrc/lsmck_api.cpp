@@ -31,6 +31,11 @@
 #include <thread>
 #include <vector>
 
+#include <pthread.h>
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include "lsmck.h"
 #include "lsmck_device.h"
 #include "lsmck_internal.h"
@@ -83,6 +88,85 @@ int ensure_dev(T** p, size_t* cap, size_t need) {
   return 0;
 }
 
+// --- NUMA: the staging buffers and threads next to the device --
+// On a node with several sockets each GPU hangs off one socket's PCIe root;
+// pinned staging on the other socket's memory, or copy threads on its cores,
+// cross the socket link on the way to the device.
+constexpr int kMaxDevs = 64;
+std::atomic<int> g_pin_node[kMaxDevs];  // per device: the node its pinned buffers go to (-1: HIP's choice)
+struct PinNodeInit {
+  PinNodeInit() {
+    for (auto& v : g_pin_node) v.store(-1);
+  }
+} g_pin_node_init;
+
+int read_int_file(const std::string& path, int dflt) {
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return dflt;
+  int v = dflt;
+  if (fscanf(f, "%d", &v) != 1) v = dflt;
+  fclose(f);
+  return v;
+}
+// the device's NUMA node (sysfs of its PCI function), -1 if unknown
+int device_numa_node(int dev) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, dev) != hipSuccess) return -1;
+  std::string b(bus);
+  for (auto& c : b) c = (char)tolower((unsigned char)c);
+  return read_int_file("/sys/bus/pci/devices/" + b + "/numa_node", -1);
+}
+int numa_node_count() {
+  int n = 0;
+  while (n < 1024 && access(("/sys/devices/system/node/node" + std::to_string(n)).c_str(), F_OK) == 0) ++n;
+  return n;
+}
+// the CPUs of a node ("0-7,16-23" in sysfs)
+bool node_cpus(int node, cpu_set_t* set) {
+  FILE* f = fopen(("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist").c_str(), "r");
+  if (!f) return false;
+  char buf[4096] = {0};
+  const bool got = fgets(buf, sizeof buf, f) != nullptr;
+  fclose(f);
+  if (!got) return false;
+  CPU_ZERO(set);
+  int n = 0;
+  for (char* s = buf; *s && *s != '\n';) {
+    char* e = nullptr;
+    const long a = strtol(s, &e, 10);
+    if (e == s) break;
+    long b = a;
+    if (*e == '-') b = strtol(e + 1, &e, 10);
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET((int)c, set), ++n;
+    s = *e == ',' ? e + 1 : e;
+  }
+  return n > 0;
+}
+constexpr int kMpolDefault = 0, kMpolPreferred = 1;
+// pinned host memory, on the current device's node when one is set: the
+// calling thread's policy prefers that node while HIP allocates and pins
+// the pages (hipHostMallocNumaUser), then goes back to what it was
+hipError_t host_malloc_near(void** p, size_t bytes) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const int node = dev >= 0 && dev < kMaxDevs ? g_pin_node[dev].load() : -1;
+  if (node < 0 || node >= 1024) return hipHostMalloc(p, bytes, hipHostMallocDefault);
+  int old_mode = kMpolDefault;
+  unsigned long old_mask[16] = {0};
+  const bool have_old = syscall(SYS_get_mempolicy, &old_mode, old_mask, 16 * 64, nullptr, 0) == 0;
+  unsigned long mask[16] = {0};
+  mask[node / 64] |= 1ul << (node % 64);
+  const bool set = syscall(SYS_set_mempolicy, kMpolPreferred, mask, 16 * 64) == 0;
+  const hipError_t e = hipHostMalloc(p, bytes, set ? hipHostMallocNumaUser : hipHostMallocDefault);
+  if (set) {
+    if (have_old && old_mode != kMpolDefault)
+      (void)syscall(SYS_set_mempolicy, old_mode, old_mask, 16 * 64);
+    else
+      (void)syscall(SYS_set_mempolicy, kMpolDefault, nullptr, 0);
+  }
+  return e;
+}
+
 template <typename T>
 int ensure_pinned(T** p, size_t* cap, size_t need) {
   if (*cap >= need && *p) return 0;
@@ -91,7 +175,7 @@ int ensure_pinned(T** p, size_t* cap, size_t need) {
   if (*p) (void)hipHostFree(*p);
   *p = nullptr;
   *cap = 0;
-  HIPCHK(hipHostMalloc((void**)p, want * sizeof(T), hipHostMallocDefault));
+  HIPCHK(host_malloc_near((void**)p, want * sizeof(T)));
   *cap = want;
   return 0;
 }
@@ -263,6 +347,9 @@ struct lsmck_ctx {
   int wal_seg = 1;           // device WAL walk: 1 = the segment walk first (default), 0 = candidate doubling only
   uint64_t wal_seg_bytes = 0;  // segment walk: bytes per segment (0 = auto, ~2^16 segments)
   int wal_seg_rounds = 16;   // segment walk: repairs before it declines to the candidate-doubling walk
+  int numa_node = -1;    // the device's NUMA node (sysfs), -1 unknown
+  int stage_numa = -2;   // option "stage_numa": -2 the device's node on a multi-node host, -1 off, >= 0 that node
+  int pin_node = -1;     // in effect: pinned buffers and copy threads on this node (-1: none)
   // what the last device-walked replay did (lsmck_ctx_get_stat "wal_walk_path" / "wal_seg_repairs" / "wal_segments")
   int last_walk_path = 0;
   int last_seg_repairs = 0;
@@ -500,8 +587,25 @@ int stage_init(Stage& S) {
 // the PCIe link the slot then feeds; large chunks are split over `threads`
 // (contiguous byte ranges, 4 KiB-aligned cuts).
 lsmck_host::HostPool& host_pool(lsmck_ctx* ctx) {
-  if (!ctx->pool) ctx->pool.reset(new lsmck_host::HostPool());
+  if (!ctx->pool) {
+    ctx->pool.reset(new lsmck_host::HostPool());
+    cpu_set_t set;
+    if (ctx->pin_node >= 0 && node_cpus(ctx->pin_node, &set)) ctx->pool->set_cpus(set);
+  }
   return *ctx->pool;
+}
+
+// the context's NUMA placement from its option (ctx->mu held or not yet shared)
+void apply_numa(lsmck_ctx* ctx) {
+  ctx->pin_node = ctx->stage_numa == -2 ? (numa_node_count() > 1 ? ctx->numa_node : -1) : ctx->stage_numa;
+  if (ctx->dev >= 0 && ctx->dev < kMaxDevs) g_pin_node[ctx->dev].store(ctx->pin_node);
+  if (ctx->pool) {
+    cpu_set_t set;
+    if (ctx->pin_node >= 0 && node_cpus(ctx->pin_node, &set))
+      ctx->pool->set_cpus(set);
+    else
+      ctx->pool->clear_cpus();
+  }
 }
 
 void stage_copy(lsmck_ctx* ctx, uint8_t* dst, const uint8_t* src, size_t n, unsigned threads) {
@@ -727,6 +831,8 @@ lsmck_ctx* lsmck_ctx_create(int device) {
   lsmck_ctx* ctx = new lsmck_ctx();
   ctx->dev = device;
   ctx->ncu = pr.multiProcessorCount;
+  ctx->numa_node = device_numa_node(device);
+  apply_numa(ctx);
   // combination tables
   std::vector<uint32_t> master(4096), kseg(65536), khi(65536), tinit(130, 0u);
   const uint32_t* T = lsmck_host::crc_tables();
@@ -873,6 +979,13 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->wal_seg_bytes = (uint64_t)value;
     return 0;
   }
+  if (!strcmp(key, "stage_numa")) {  // pinned staging and copy threads: -2 auto (device's node), -1 off, >= 0 a node
+    if (value < -2 || value > 1023) return lsmck_host::set_error(LSMCK_EINVAL, "stage_numa: -2..1023");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->stage_numa = (int)value;
+    apply_numa(ctx);
+    return 0;
+  }
   if (!strcmp(key, "wal_seg_rounds")) {  // segment walk: repair rounds before declining (0 = decline on any failure)
     if (value < 0 || value > 1024) return lsmck_host::set_error(LSMCK_EINVAL, "wal_seg_rounds: 0..1024");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -943,6 +1056,10 @@ int lsmck_ctx_get_stat(lsmck_ctx* ctx, const char* key, long* value) {
     *value = ctx->last_seg_repairs;
   } else if (!strcmp(key, "wal_segments")) {
     *value = (long)ctx->last_segments;
+  } else if (!strcmp(key, "numa_node")) {
+    *value = ctx->numa_node;
+  } else if (!strcmp(key, "stage_numa_node")) {
+    *value = ctx->pin_node;
   } else {
     return lsmck_host::set_error(LSMCK_EINVAL, "unknown stat");
   }
@@ -2723,7 +2840,7 @@ void* lsmck_host_alloc_pinned(lsmck_ctx* ctx, size_t bytes) {
   if (!ctx) return nullptr;
   DevGuard g(ctx->dev);
   void* p = nullptr;
-  hipError_t e = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault);
+  hipError_t e = host_malloc_near(&p, bytes ? bytes : 1);  // (on the device's node: see stage_numa)
   if (e != hipSuccess) {
     hip_error(e, "hipHostMalloc");
     return nullptr;

@@ -1,5 +1,8 @@
 // lsmck_pool.h -- a small persistent host thread pool (header-only, no HIP).
 #pragma once
+#include <pthread.h>
+#include <sched.h>
+
 #include <condition_variable>
 #include <cstdint>
 #include <functional>
@@ -23,6 +26,22 @@ class HostPool {
     }
     cv_.notify_all();
     for (auto& t : th_) t.join();
+  }
+  // the workers' CPUs (the device's NUMA node), for the ones running and the
+  // ones to come; clear_cpus: any CPU again
+  void set_cpus(const cpu_set_t& set) {
+    std::lock_guard<std::mutex> one(run_mu_);
+    cpus_ = set;
+    pinned_ = true;
+    for (auto& t : th_) (void)pthread_setaffinity_np(t.native_handle(), sizeof cpus_, &cpus_);
+  }
+  void clear_cpus() {
+    std::lock_guard<std::mutex> one(run_mu_);
+    if (!pinned_) return;
+    pinned_ = false;
+    CPU_ZERO(&cpus_);
+    for (int c = 0; c < CPU_SETSIZE; ++c) CPU_SET(c, &cpus_);
+    for (auto& t : th_) (void)pthread_setaffinity_np(t.native_handle(), sizeof cpus_, &cpus_);
   }
   void run(unsigned T, const std::function<void(unsigned)>& f) {
     if (T <= 1) {
@@ -55,6 +74,7 @@ class HostPool {
     while (th_.size() < n) {
       const unsigned idx = (unsigned)th_.size() + 1;
       th_.emplace_back([this, idx, g] { loop(idx, g); });
+      if (pinned_) (void)pthread_setaffinity_np(th_.back().native_handle(), sizeof cpus_, &cpus_);
     }
   }
   void loop(unsigned idx, uint64_t seen) {
@@ -80,6 +100,8 @@ class HostPool {
   unsigned want_ = 0, pending_ = 0;
   uint64_t gen_ = 0;
   bool stop_ = false;
+  cpu_set_t cpus_{};     // (under run_mu_)
+  bool pinned_ = false;
 };
 
 }  // namespace lsmck_host
