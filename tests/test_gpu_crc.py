@@ -424,3 +424,38 @@ def test_empty_batches_every_entry_point(ctx):
     ctx.crc32_fixed_device(d.ptr, 16, 16, 0, out.ptr)
     ctx.sha256_fixed_device(d.ptr, 16, 16, 0, out.ptr)
     ctx.sync()
+
+
+def test_stage_numa_host_batches():
+    """Staging placement (stage_numa): the device's node in effect by default
+    on a multi-node host (none on a single-node one), every node and "off"
+    accepted, a host batch's CRCs the oracle's under each -- pageable
+    (staged on the pool's threads) and pinned (lsmck_host_alloc_pinned,
+    allocated under the placement); out-of-range values refused."""
+    import os
+    from lsm_storage_engine_amd.device import Context
+    nodes = len([d for d in os.listdir("/sys/devices/system/node") if d.startswith("node") and d[4:].isdigit()])
+    rng = np.random.default_rng(11)
+    data = rng.integers(0, 256, size=(20 << 20) + 777, dtype=np.uint8)
+    off = np.sort(rng.integers(0, len(data) - 5000, size=3000)).astype(np.uint64)
+    ln = rng.integers(0, 5000, size=3000).astype(np.uint32)
+    want = np.array([O.crc32(data[int(o):int(o) + int(n)].tobytes()) for o, n in zip(off, ln)], dtype=np.uint32)
+    for mode in [-2, -1] + list(range(nodes)):
+        ctx = Context(0)
+        try:
+            dev_node = ctx.get_stat("numa_node")
+            ctx.set_option("stage_numa", mode)
+            eff = ctx.get_stat("stage_numa_node")
+            if mode == -2:
+                assert eff == (dev_node if nodes > 1 else -1)
+            else:
+                assert eff == mode
+            assert (ctx.crc32(data, off, ln) == want).all()
+            pb = ctx.alloc_pinned(len(data))
+            pb.array[:] = data
+            assert (ctx.crc32(pb.array, off, ln, pinned=True) == want).all()
+            pb.free()
+            with pytest.raises(_lib.LsmckError):
+                ctx.set_option("stage_numa", -3)
+        finally:
+            ctx.close()
