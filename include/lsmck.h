@@ -228,6 +228,10 @@ int lsmck_device_count(void);
  *                 ~2^16 segments; else 64..2^30).  Tests use small segments.
  *   "wal_seg_rounds"  segment walk: check failures repaired before it
  *                 declines to candidate doubling (default 16).
+ *   "wal_seg_pack"  segment walk: 1 = the CRC pass runs over packed spans,
+ *                 each payload with the next record's header, the header
+ *                 then taken back out of the CRC (default); 0 = over the
+ *                 payloads alone.  A/B; results are the same.
  * Returns 0, or LSMCK_EINVAL for an unknown key / value. */
 int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
 

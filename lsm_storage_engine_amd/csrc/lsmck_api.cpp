@@ -346,6 +346,7 @@ struct lsmck_ctx {
   bool wal_recs_dev_emitted = false;
   int wal_seg = 1;           // device WAL walk: 1 = the segment walk first (default), 0 = candidate doubling only
   uint64_t wal_seg_bytes = 0;  // segment walk: bytes per segment (0 = auto, ~2^16 segments)
+  bool wal_seg_pack = true;  // segment walk: packed CRC spans (seg::Pack) for the CRC pass
   int wal_seg_rounds = 16;   // segment walk: repairs before it declines to the candidate-doubling walk
   int numa_node = -1;    // the device's NUMA node (sysfs), -1 unknown
   int stage_numa = -2;   // option "stage_numa": -2 the device's node on a multi-node host, -1 off, >= 0 that node
@@ -986,6 +987,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     apply_numa(ctx);
     return 0;
   }
+  if (!strcmp(key, "wal_seg_pack")) {  // A/B: the segment walk's packed CRC spans (1, default) or payloads alone (0)
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "wal_seg_pack: 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_seg_pack = value != 0;
+    return 0;
+  }
   if (!strcmp(key, "wal_seg_rounds")) {  // segment walk: repair rounds before declining (0 = decline on any failure)
     if (value < 0 || value > 1024) return lsmck_host::set_error(LSMCK_EINVAL, "wal_seg_rounds: 0..1024");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1241,6 +1248,7 @@ struct WalPart {
   uint32_t term = 0;   // terminal code (WAL_END / BAD / STOP / STOPSELF, lsmck_wal.hip)
   uint64_t tpos = 0;   // BAD position, or where a prefix walk resumes
   double over = 0;     // kWalTooBig: the scratch it needed over the budget (ratio)
+  bool packed = false; // the segment walk emitted packed CRC spans (seg::Pack) from `at` on
 };
 constexpr uint32_t kWalBad = 0xFFFFFFFEu, kWalStop = 0xFFFFFFFDu, kWalStopSelf = 0xFFFFFFFCu;
 
@@ -1309,8 +1317,9 @@ static int wal_walk_part(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t 
   return 0;
 }
 
-// The CRC pass over records [at, at + m): their payloads in log order (the
-// stream kernel, no eligibility check), CRCs into d_vcrc + at.  Asynchronous.
+// The CRC pass over records [at, at + m): their spans in log order (the
+// stream kernel, no eligibility check), CRCs into d_vcrc + at.  (Packed spans,
+// seg::Pack, are taken apart by the compare, wal_finish.)  Asynchronous.
 static int wal_crc_part(lsmck_ctx* ctx, const uint8_t* img, size_t at, size_t m, hipStream_t st) {
   if (!m) return 0;
   return crc_desc_device(ctx, ctx->scratch, img, ctx->d_woff + at, ctx->d_wlen + at, m, ctx->d_vcrc + at, st, true);
@@ -1322,9 +1331,13 @@ static int wal_crc_part(lsmck_ctx* ctx, const uint8_t* img, size_t at, size_t m,
 // order, or a bad type byte after the last record at badq).
 // done: records [0, done) are already in the caller's array (the split
 // replay's first part, from ctx->h_wrecs1); the rest land in ctx->h_wrecs.
-static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t term, uint64_t badq, lsmck_wal_rec* recs,
-                      size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected,
-                      hipStream_t st, const WalTrace& tr, size_t done = 0, bool emit_recorded = false) {
+// pack_from: records [pack_from, m) have packed CRC spans (the segment walk's
+// emit, seg::Pack): their compare takes the next header out of each CRC and
+// reads the stored CRCs from the records.
+static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t term, uint64_t badq,
+                      lsmck_wal_rec* recs, size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc,
+                      uint32_t* bad_expected, hipStream_t st, const WalTrace& tr, size_t done = 0,
+                      bool emit_recorded = false, size_t pack_from = ~(size_t)0) {
   auto& W = ctx->wd;
   int rc;
   uint64_t nbad = 0, first = m;
@@ -1374,7 +1387,11 @@ static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t ter
     }
     HIPCHK(hipMemsetAsync(ctx->d_verify, 0, 8, st));         // n_bad
     HIPCHK(hipMemsetAsync(ctx->d_verify + 1, 0xFF, 8, st));  // first_bad = ~0
-    rc = lsmk_launch_crc32_compare(ctx->d_vcrc, ctx->d_wexp, m, ctx->d_verify, ctx->d_verify + 1, st);
+    const size_t plain = std::min(m, pack_from);
+    rc = lsmk_launch_crc32_compare(ctx->d_vcrc, ctx->d_wexp, plain, ctx->d_verify, ctx->d_verify + 1, st);
+    if (!rc && plain < m)
+      rc = lsmk_wal_compare_packed(ctx->d_vcrc, ctx->wal_recs_dev_emitted ? ctx->wal_recs_dev : W.recs, plain, m,
+                                   ctx->d_verify, ctx->d_verify + 1, st);
     if (rc) {
       if (copy_out) (void)hipEventSynchronize(ctx->wal_recs_ev);
       return launch_rc(rc, "compare kernel");
@@ -1591,8 +1608,14 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
         (rc = ensure_dev_keep(&ctx->d_wexp, &ctx->cap_wexp, tot, at, st)) ||
         (rc = ensure_dev_keep(&ctx->d_vcrc, &ctx->cap_vcrc, tot, at, st)))
       return rc;
-    if ((rc = lsmk_wal_seg_emit(&a, at, dev ? ctx->wal_recs_dev : W.recs, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st)))
-      return launch_rc(rc, "wal segment emit kernel");
+    lsmck_wal_rec* to = dev ? ctx->wal_recs_dev : W.recs;
+    if (ctx->wal_seg_pack) {
+      rc = lsmk_wal_seg_emit_packed(&a, at, to, ctx->d_woff, ctx->d_wlen, tot, st);
+    } else {
+      rc = lsmk_wal_seg_emit(&a, at, to, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st);
+    }
+    if (rc) return launch_rc(rc, "wal segment emit kernel");
+    out->packed = ctx->wal_seg_pack;
     ctx->wal_recs_dev_emitted = dev;
   }
   if (!ctx->wal_emit_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_emit_ev, hipEventDisableTiming));
@@ -1618,7 +1641,7 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck
   if (rc == 0) {  // the CRC pass over every record, then the compare and the records
     if ((rc = wal_crc_part(ctx, img, 0, P.m, st))) return rc;
     return wal_finish(ctx, img, P.m, P.term, P.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr, 0,
-                      true);
+                      true, P.packed ? 0 : ~(size_t)0);
   }
   if (rc != kWalSegDecline) return rc;
   ctx->last_walk_path = 2;  // candidate doubling: its bitmap, ranks and jump tables
@@ -1820,7 +1843,7 @@ static int wal_replay_split(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool p
     if (rc == 0) {
       if ((rc = wal_crc_part(ctx, d, P1.m, P2.m - P1.m, st))) return rc;
       return wal_finish(ctx, d, P2.m, P2.term, P2.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr,
-                        done, true);
+                        done, true, P2.packed ? P1.m : ~(size_t)0);
     }
     if (rc != kWalSegDecline) return rc;
   }

@@ -524,13 +524,55 @@ LSMCK_HD void seg_repair(const SegArgs& a, uint32_t j, uint32_t budget) {
   }
 }
 
+// The raw CRC-32 register after a header's bytes [t][crc][klen]([vlen]) fed
+// from register 0, by the four slicing tables T (T0..T3, 256 words each).
+LSMCK_HD uint32_t hdr_reg(const Head& h, const uint32_t* T) {
+  auto sl4 = [T](uint32_t x) {
+    return T[768 + (x & 0xFFu)] ^ T[512 + ((x >> 8) & 0xFFu)] ^ T[256 + ((x >> 16) & 0xFFu)] ^ T[x >> 24];
+  };
+  uint32_t r = T[h.t & 0xFFu];
+  r = sl4(r ^ h.crc);
+  r = sl4(r ^ h.klen);
+  if (h.t == 1) r = sl4(r ^ h.vlen);
+  return r;
+}
+
+// Packed CRC spans (Pack non-null): record i's CRC-pass span is its payload
+// and the NEXT record's header, [payload_i | header_i+1), so the spans tile
+// the log and the stream kernel runs on them as on config 3's packed objects.
+// The last record of the emit (iend: at + records walked) keeps its payload
+// alone, and so does a payload within a header of 4 GiB (pack_fits).  The
+// header comes back out of the CRC by linearity (unpack_crc): the compare
+// reads it from record i+1's fields.  The stored CRCs (pcrc) are not written:
+// the compare reads them from the records too.
+struct Pack {
+  uint64_t iend;
+};
+LSMCK_HD bool pack_fits(uint32_t got, uint32_t hl) { return got <= 0xFFFFFFFFu - hl; }
+
+// c(x) * b(x) mod P(x), reflected (bit 31 is x^0): 32 steps, no branch
+LSMCK_HD uint32_t gf2_mul(uint32_t c, uint32_t b) {
+  uint32_t p = 0;
+  for (int i = 31; i >= 0; --i) {
+    p ^= b & (0u - ((c >> i) & 1u));
+    b = (b >> 1) ^ (0xEDB88320u & (0u - (b & 1u)));
+  }
+  return p;
+}
+// The CRC of a payload P from the CRC c of its packed span P | H, H the next
+// record's header nh:  crc(P) = ~( x^(-8|H|) * (~c ^ hdr_reg(H)) ) mod P(x),
+// x^-104 and x^-72 the constants (tests/test_segwalk_model.py checks them).
+LSMCK_HD uint32_t unpack_crc(uint32_t c, const Head& nh, const uint32_t* T) {
+  return ~gf2_mul(~c ^ hdr_reg(nh, T), nh.t == 1 ? 0x525983aau : 0x2fb98a7du);
+}
+
 // step 4 for segment k (after the check passed): its records at `at` + its
 // place, as lsmck_wal_rec entries, CRC descriptors and stored CRCs
 // (sub-segment j of segment k when a.nsub > 1: its records only, from the
 // checkpoint the walk noted)
 template <class Rec>
 LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint64_t at, Rec* recs, uint64_t* poff,
-                              uint32_t* plen, uint32_t* pcrc, uint32_t j = 0) {
+                              uint32_t* plen, uint32_t* pcrc, uint32_t j = 0, const Pack* pk = nullptr) {
   if (k > jterm || a.code[k] == kNone) return;
   uint32_t r = 0, rend = a.recs[k];
   uint64_t p = a.g[k], pend = ~0ull;
@@ -542,12 +584,15 @@ LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint
   }
   uint64_t i = at + (a.pre[k] & kRecMask) + r;
   const uint8_t* img = a.img;
+  uint64_t pi = ~0ull;  // packed: the previous record, its span closed by this one's header
+  uint32_t pgot = 0;
   for (; r < rend && p < pend; ++r, ++i) {
     const Head h = head(img, a.n, p);
     const uint32_t hl = hdr_len(h.t);
     const uint32_t dlen = h.klen + h.vlen;
     const uint64_t avail = a.n - (p + hl);
     const uint32_t got = dlen <= avail ? dlen : (uint32_t)avail;
+    if (pk && pi != ~0ull) plen[pi] = pack_fits(pgot, hl) ? pgot + hl : pgot;
     Rec R;
     R.rec_off = p;
     R.payload_off = p + hl;
@@ -557,9 +602,19 @@ LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint
     R.type = h.t;
     recs[i] = R;
     poff[i] = p + hl;
-    plen[i] = got;
-    pcrc[i] = h.crc;
+    if (pk) {
+      pi = i;
+      pgot = got;
+    } else {
+      plen[i] = got;
+      pcrc[i] = h.crc;
+    }
     p += hl + got;
+  }
+  if (pk && pi != ~0ull) {  // the last record here: the next one's header is at p (another thread's first)
+    uint32_t hl = 0;
+    if (i < pk->iend) hl = hdr_len(head(img, a.n, p).t);
+    plen[pi] = hl && pack_fits(pgot, hl) ? pgot + hl : pgot;
   }
 }
 

@@ -458,6 +458,81 @@ __global__ __launch_bounds__(256) void wal_seg_emit(seg::SegArgs a, uint64_t at,
   if (k < a.K) seg::seg_emit_thread(a, k, (uint32_t)a.info[seg::kInfoJterm], at, recs, poff, plen, pcrc, j);
 }
 
+// The same with packed CRC spans (seg::Pack): span lengths only, no stored CRCs.
+__global__ __launch_bounds__(256) void wal_seg_emit_packed(seg::SegArgs a, uint64_t at, lsmck_wal_rec* __restrict__ recs,
+                                                            uint64_t* __restrict__ poff, uint32_t* __restrict__ plen,
+                                                            uint64_t iend) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = (uint32_t)(t / a.nsub), j = (uint32_t)(t % a.nsub);
+  const seg::Pack pk{iend};
+  if (k < a.K)
+    seg::seg_emit_thread(a, k, (uint32_t)a.info[seg::kInfoJterm], at, recs, poff, plen, (uint32_t*)nullptr, j, &pk);
+}
+
+// The compare over packed spans, records [i0, m) of recs (the emit's): record
+// i's CRC (of [payload_i | header_i+1) unless i is the last or its span did
+// not fit) back to its payload's by seg::unpack_crc with header i+1 read from
+// record i+1's fields, against the stored CRC in record i.  A mismatch counts
+// as crc32_compare_kernel's do and writes the payload's CRC back (the bad
+// record's report reads it).  The CRC-32 slicing tables T0..T3 in LDS first
+// (T0 bitwise, Tk[b] = T(k-1)[b] >> 8 ^ T0[T(k-1)[b] & 0xFF]).
+__global__ __launch_bounds__(256) void wal_compare_packed(uint32_t* __restrict__ crc,
+                                                          const lsmck_wal_rec* __restrict__ recs, uint64_t i0,
+                                                          uint64_t m, unsigned long long* __restrict__ n_bad,
+                                                          unsigned long long* __restrict__ first_bad) {
+  __shared__ uint32_t T[1024];
+  const uint32_t b = threadIdx.x;
+  uint32_t c = b;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+  T[b] = c;
+  __syncthreads();
+#pragma unroll
+  for (int q = 1; q < 4; ++q) {
+    c = (c >> 8) ^ T[c & 0xFFu];
+    T[q * 256 + b] = c;
+  }
+  __syncthreads();
+  // a wave's 64 lanes take 64 consecutive records: each loads its record's
+  // klen, vlen, crc, type (one 16-byte load) and takes record i+1's from the
+  // next lane (lane 63 loads it).  A record with a successor was not cut at
+  // EOF: its span's payload is klen + vlen bytes.
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  unsigned long long bad = 0, first = ~0ull;
+  for (uint64_t w = i0 + (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); w < m; w += stride) {
+    const uint64_t i = w + lane;
+    u32x4 f = {0u, 0u, 0u, 0u};
+    if (i < m) f = *(const u32x4*)&recs[i].klen;
+    seg::Head nh{};
+    nh.klen = __shfl_down(f.x, 1);
+    nh.vlen = __shfl_down(f.y, 1);
+    nh.crc = __shfl_down(f.z, 1);
+    nh.t = __shfl_down(f.w, 1);
+    if (lane == 63u && i + 1 < m) {
+      const u32x4 g = *(const u32x4*)&recs[i + 1].klen;
+      nh.klen = g.x;
+      nh.vlen = g.y;
+      nh.crc = g.z;
+      nh.t = g.w;
+    }
+    if (i < m) {
+      uint32_t v = crc[i];
+      if (i + 1 < m && seg::pack_fits(f.x + f.y, seg::hdr_len(nh.t))) v = seg::unpack_crc(v, nh, T);
+      if (v != f.z) {
+        ++bad;
+        if (i < first) first = i;
+        crc[i] = v;
+      }
+    }
+  }
+  if (bad) {
+    atomicAdd(n_bad, bad);
+    atomicMin(first_bad, first);
+  }
+}
+
 }  // namespace lsmck
 
 using namespace lsmck;
@@ -511,6 +586,22 @@ extern "C" int lsmk_wal_seg_emit(const seg::SegArgs* a, uint64_t at, lsmck_wal_r
   const uint64_t threads = (uint64_t)a->K * a->nsub;
   hipLaunchKernelGGL(wal_seg_emit, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, *a, at, recs, poff, plen,
                      pcrc);
+  return launch_err();
+}
+
+extern "C" int lsmk_wal_seg_emit_packed(const seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff,
+                                        uint32_t* plen, uint64_t iend, hipStream_t st) {
+  const uint64_t threads = (uint64_t)a->K * a->nsub;
+  hipLaunchKernelGGL(wal_seg_emit_packed, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, *a, at, recs, poff,
+                     plen, iend);
+  return launch_err();
+}
+
+extern "C" int lsmk_wal_compare_packed(uint32_t* crc, const lsmck_wal_rec* recs, uint64_t i0, uint64_t m,
+                                       unsigned long long* n_bad, unsigned long long* first_bad, hipStream_t st) {
+  if (m <= i0) return 0;
+  const uint64_t blocks = (m - i0 + 255) / 256 < 8192 ? (m - i0 + 255) / 256 : 8192;
+  hipLaunchKernelGGL(wal_compare_packed, dim3((unsigned)blocks), dim3(256), 0, st, crc, recs, i0, m, n_bad, first_bad);
   return launch_err();
 }
 

@@ -384,7 +384,7 @@ def seg_opts(ctx):
         for k, v in kw.items():
             ctx.set_option(k, v)
     yield set_
-    for k, v in (("wal_seg_bytes", 0), ("wal_seg_rounds", 16), ("wal_seg_walk", 1)):
+    for k, v in (("wal_seg_bytes", 0), ("wal_seg_rounds", 16), ("wal_seg_walk", 1), ("wal_seg_pack", 1)):
         ctx.set_option(k, v)
 
 
@@ -425,6 +425,37 @@ def test_segment_walk(ctx, seg_opts, seg, shift):
     b = bytearray(img)
     b[recs[9999].payload_off] ^= 0x08
     assert same(ctx, bytes(b), device=True, shift=shift) in (1, 2)
+
+
+@pytest.mark.parametrize("pack", [1, 0])
+@pytest.mark.parametrize("seg", [0, 512, 262144])
+def test_segment_walk_packed_spans(ctx, seg_opts, pack, seg):
+    """The CRC pass over packed spans ([payload | next header), the headers
+    taken back out by wal_compare_packed) against payload-only spans: empty keys
+    and values (spans of a header alone), Removes next to Inserts, a corrupted
+    payload and header CRC (the computed CRC it reports is the payload's own),
+    and a log cut inside the last payload (its span the payload alone)."""
+    seg_opts(wal_seg_bytes=seg, wal_seg_pack=pack)
+    rng = np.random.default_rng(63)
+    parts = []
+    for i in range(6000):
+        kl, vl = int(rng.integers(0, 3)) * int(rng.integers(0, 40)), int(rng.integers(0, 4)) * int(rng.integers(0, 300))
+        k, v = rng.bytes(kl), rng.bytes(vl)
+        parts.append(O.wal_remove(k) if rng.integers(0, 4) == 0 else O.wal_insert(k, v))
+    img = b"".join(parts)
+    assert same(ctx, img, device=True) == 0
+    assert ctx.get_stat("wal_walk_path") == 1
+    st, recs, _ = O.wal_replay(img)
+    for i in (0, 1, 2500, len(recs) - 2, len(recs) - 1):
+        b = bytearray(img)
+        r = recs[i]
+        if r.klen + r.vlen:
+            b[r.payload_off] ^= 0x40
+        else:
+            b[r.rec_off + 1] ^= 0x40  # (the stored CRC)
+        assert same(ctx, bytes(b), device=True) in (1, 2)
+    big = [r for r in recs if r.vlen > 8]
+    same(ctx, img[:big[-1].payload_off + 5], device=True)
 
 
 def test_segment_walk_long_records(ctx, seg_opts):

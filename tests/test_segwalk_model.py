@@ -64,6 +64,23 @@ def sim(tmp_path_factory):
     run.prefix = prefix
     lib.segwalk_sim_set_nsub.argtypes = [C.c_uint32]
     run.set_nsub = lib.segwalk_sim_set_nsub
+    lib.segwalk_sim_pack.argtypes = [u64p, C.POINTER(C.c_uint32), C.c_size_t]
+    lib.segwalk_sim_unpack.restype = C.c_uint32
+    lib.segwalk_sim_unpack.argtypes = [C.c_uint32] * 5
+
+    def packed(img, S):
+        """the walk's packed CRC spans (seg::Pack): (offs, lens)"""
+        cap = len(img) // 9 + 2
+        po, pl = (C.c_uint64 * cap)(), (C.c_uint32 * cap)()
+        lib.segwalk_sim_pack(po, pl, cap)
+        try:
+            res = run(img, S)
+        finally:
+            lib.segwalk_sim_pack(None, None, 0)
+        m = len(res[0])
+        return list(po[:m]), list(pl[:m])
+    run.unpack = lib.segwalk_sim_unpack
+    run.packed = packed
     return run
 
 
@@ -272,5 +289,77 @@ def test_emit_by_sub_segments(sim, S, nsub):
             b[want[len(want) // 2]] = 0x55
             check(sim, bytes(b), S)
             check(sim, img[:len(img) - 11], S)
+    finally:
+        sim.set_nsub(1)
+
+
+def _mulmod(a, b):
+    """a(x) * b(x) mod P(x), reflected (zlib's multmodp)."""
+    m, p = 1 << 31, 0
+    while True:
+        if a & m:
+            p ^= b
+            if (a & (m - 1)) == 0:
+                return p
+        m >>= 1
+        b = (b >> 1) ^ 0xEDB88320 if b & 1 else b >> 1
+
+
+def test_unpack_constants():
+    """wal_crc_unpack's constants are x^-72 and x^-104 mod P(x): times x^72
+    (x^104) they give x^0."""
+    x8inv = 0x6567cb95  # x^-8: times x^8 (bit 23) is x^0 (bit 31)
+    assert _mulmod(x8inv, 1 << 23) == 1 << 31
+    r = 1 << 31
+    pw = {}
+    for k in range(1, 14):
+        r = _mulmod(r, x8inv)
+        pw[k] = r
+    assert pw[9] == 0x2fb98a7d and pw[13] == 0x525983aa
+
+
+@pytest.mark.parametrize("nsub", [1, 4])
+@pytest.mark.parametrize("S", [512, 4096, 65536])
+def test_packed_crc_spans(sim, S, nsub):
+    """The emit's packed CRC spans: record i's span is its payload and the next
+    record's header (the last one's its payload alone), so the spans tile the
+    log; seg::unpack_crc (wal_compare_packed's) takes the header back out of
+    the span's CRC (zlib's here) to the payload's own, and so does the
+    restatement of the algebra in Python."""
+    import zlib
+    M = 0xFFFFFFFF
+    sim.set_nsub(nsub)
+    try:
+        rng = np.random.default_rng(S + nsub)
+        for img in (random_log(rng, 1500, hi=900), random_log(rng, 300, lo=1000, hi=30000),
+                    random_log(rng, 2000, hi=30, remove_every=3)):
+            cut = bytearray(img[:len(img) - 7])
+            bad = bytearray(img)
+            want0, _, _ = chain(img)
+            bad[want0[len(want0) // 2]] = 0x55
+            for im in (img, bytes(cut), bytes(bad)):
+                offs, _, _ = chain(im)
+                po, pl = sim.packed(im, S)
+                assert len(po) == len(offs)
+                for i, q in enumerate(offs):
+                    hl = 13 if im[q] == 1 else 9
+                    klen, vlen = struct.unpack_from("<II", im, q + 5)
+                    if hl == 9:
+                        vlen = 0
+                    plen = min((klen + vlen) & M, len(im) - q - hl)
+                    assert po[i] == q + hl
+                    span = zlib.crc32(im[po[i]:po[i] + pl[i]])
+                    if i + 1 < len(offs):
+                        nq = offs[i + 1]
+                        nh = 13 if im[nq] == 1 else 9
+                        assert po[i] + pl[i] == nq + nh
+                        t, crc, k2 = struct.unpack_from("<BII", im, nq)
+                        v2 = struct.unpack_from("<I", im, nq + 9)[0] if nh == 13 else 0
+                        got = sim.unpack(span, t, crc, k2, v2)
+                        g = ~zlib.crc32(im[nq:nq + nh], M) & M
+                        alg = ~_mulmod(~span & M ^ g, 0x525983aa if nh == 13 else 0x2fb98a7d) & M
+                        assert got == alg == zlib.crc32(im[q + hl:q + hl + plen]), i
+                    else:
+                        assert pl[i] == plen and span == zlib.crc32(im[q + hl:q + hl + plen])
     finally:
         sim.set_nsub(1)

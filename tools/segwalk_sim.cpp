@@ -24,6 +24,41 @@ static uint64_t* g_dbg = nullptr;  // debug: the first round's guesses
 extern "C" void segwalk_sim_debug(uint64_t* g) { g_dbg = g; }
 static uint32_t g_nsub = 1;  // emit checkpoints: sub-segments per segment (1 = none)
 extern "C" void segwalk_sim_set_nsub(uint32_t v) { g_nsub = v ? v : 1; }
+// packed CRC spans (seg::Pack): when set, the next walk emits them here --
+// span offsets and lengths
+static uint64_t* g_poff = nullptr;
+static uint32_t* g_plen = nullptr;
+static size_t g_pcap = 0;
+extern "C" void segwalk_sim_pack(uint64_t* poff, uint32_t* plen, size_t cap) {
+  g_poff = poff;
+  g_plen = plen;
+  g_pcap = poff ? cap : 0;
+}
+// seg::unpack_crc with wal_compare_packed's tables: the payload CRC from a
+// packed span's CRC c and the next header's fields
+static const uint32_t* crc_tables4() {  // T0..T3, as wal_compare_packed builds them in LDS
+  static uint32_t T[1024];
+  static bool done = false;
+  if (!done) {
+    for (uint32_t b = 0; b < 256; ++b) {
+      uint32_t c = b;
+      for (int i = 0; i < 8; ++i) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+      T[b] = c;
+    }
+    for (int q = 1; q < 4; ++q)
+      for (uint32_t b = 0; b < 256; ++b) T[q * 256 + b] = (T[(q - 1) * 256 + b] >> 8) ^ T[T[(q - 1) * 256 + b] & 0xFFu];
+    done = true;
+  }
+  return T;
+}
+extern "C" uint32_t segwalk_sim_unpack(uint32_t c, uint32_t t, uint32_t crc, uint32_t klen, uint32_t vlen) {
+  sg::Head h{};
+  h.t = t;
+  h.crc = crc;
+  h.klen = klen;
+  h.vlen = vlen;
+  return sg::unpack_crc(c, h, crc_tables4());
+}
 
 // the records starting in [start, lim): code_out kExit with pos_out the first
 // record start at or past lim when the chain goes on past the prefix
@@ -89,10 +124,16 @@ extern "C" int segwalk_sim_prefix(const uint8_t* img, uint64_t n, uint64_t start
   std::vector<SimRec> R(m);
   std::vector<uint64_t> poff(m);
   std::vector<uint32_t> plen(m), pcrc(m);
+  const sg::Pack pk{m};
   for (uint32_t k = 0; k < K; ++k)
     for (uint32_t j = 0; j < a.nsub; ++j)
-      sg::seg_emit_thread(a, k, (uint32_t)info[sg::kInfoJterm], 0, R.data(), poff.data(), plen.data(), pcrc.data(), j);
+      sg::seg_emit_thread(a, k, (uint32_t)info[sg::kInfoJterm], 0, R.data(), poff.data(), plen.data(), pcrc.data(), j,
+                          g_pcap ? &pk : nullptr);
   for (uint64_t i = 0; i < m && i < cap; ++i) rec_off[i] = R[i].rec_off;
+  for (uint64_t i = 0; i < m && i < g_pcap; ++i) {
+    g_poff[i] = poff[i];
+    g_plen[i] = plen[i];
+  }
   return 0;
 }
 
