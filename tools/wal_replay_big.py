@@ -43,6 +43,9 @@ def main():
                     help="1: then the same replays with the records left in device memory (LSMCK_RECS_DEVICE)")
     ap.add_argument("--seg-sweep", default="",
                     help="comma list of wal_seg_bytes: the records-on-device replay per segment size (A/B)")
+    ap.add_argument("--raw-reps", type=int, default=0,
+                    help="A/B: time the plain batch CRC (lsmck_crc32_device) over the framed log's packed spans "
+                         "and over its payloads alone, this many times each, before the replays")
     a = ap.parse_args()
     n = a.records
     ln = gen_zipf_lengths(0x5EED0003, n)
@@ -66,8 +69,24 @@ def main():
     ctx.crc32_device(d.ptr, d_o.ptr, d_l.ptr, n, out.ptr)
     ctx.wal_frame_insert_device(d.ptr, d_o.ptr, d_l.ptr, out.ptr, n, 16)
     ctx.sync()
-    for b in (d_o, d_l, out):
-        b.free()
+    raw = {}
+    lp = ln.astype(np.uint32).copy()
+    lp[:-1] += 13  # [payload | next header)
+
+    def raw_batch(name, lens, key):
+        d_l.upload(lens)
+        ts = []
+        for _ in range(a.raw_reps + 1):
+            ctx.sync()
+            t = time.perf_counter()
+            ctx.crc32_device(d.ptr, d_o.ptr, d_l.ptr, n, out.ptr)
+            ctx.sync()
+            ts.append(time.perf_counter() - t)
+        raw[key] = round(float(np.median(ts[1:])) * 1e3, 2)
+        print(f"raw batch CRC over {name}: {raw[key]} ms", file=sys.stderr, flush=True)
+    if a.raw_reps:
+        raw_batch("packed spans", lp, "packed_spans")
+        raw_batch("payloads", ln, "payloads")
     times = []
     for s in range(a.steps + 1):  # the first replay is a warm-up
         ctx.sync()
@@ -112,6 +131,8 @@ def main():
                          "repairs": ctx.get_stat("wal_seg_repairs"), "path": ctx.get_stat("wal_walk_path")}
             print(f"wal_seg_bytes {sb}: {sweep[sb]}", file=sys.stderr, flush=True)
         ctx.set_option("wal_seg_bytes", 0)
+        if a.raw_reps:  # the same batch again after the replays (order effects)
+            raw_batch("packed spans, after the replays", lp, "packed_spans_after")
         crc = rb.download(np.uint8, n * WAL_REC_DTYPE.itemsize).view(WAL_REC_DTYPE)["crc"]
         dsum = "%08x" % zlib.crc32(np.ascontiguousarray(crc).astype("<u4").tobytes())
         rb.free()
@@ -119,6 +140,8 @@ def main():
         dev = {"ms_median": round(dmed * 1e3, 2), "ms_best": round(min(dts) * 1e3, 2),
                "value": round(total / GIB / dmed, 1), "summary_crc32": dsum,
                "summary_matches_oracle": bool(golden) and dsum == golden["summary_crc32"], "seg_sweep": sweep}
+    for b in (d_o, d_l, out):
+        b.free()
     d.free()
     best, med = min(times), float(np.median(times))
     print(json.dumps({
@@ -129,7 +152,7 @@ def main():
         "records_out_bytes": 32 * n, "pinned_recs": bool(a.pinned_recs),
         "walk_path": {1: "segment walk", 2: "candidate doubling", 3: "host walk"}.get(ctx.get_stat("wal_walk_path")),
         "seg_repairs": ctx.get_stat("wal_seg_repairs"), "segments": ctx.get_stat("wal_segments"),
-        "records_on_device": dev,
+        "records_on_device": dev, "raw_batch_crc_ms": raw,
         "workload": "config 3's 2^26 Zipf payloads (64 B-64 KiB) framed as wal.rs Insert records (13-byte headers), "
                     "headers and CRCs written on the device"}))
 
