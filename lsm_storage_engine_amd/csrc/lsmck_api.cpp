@@ -336,6 +336,8 @@ struct lsmck_ctx {
     uint64_t* scpp = nullptr;  // the emit's checkpoints (segments of 128 KiB and more)
     uint32_t* scpc = nullptr;
     size_t cap_cp = 0;
+    lsmck::seg::StageRec* sst = nullptr;  // walk-time staged records (K * scap)
+    size_t cap_sst = 0;
   } wd;
   bool wal_recs_direct = false;  // this replay's records go by DMA into the caller's pinned array (under wal_mu)
   // LSMCK_RECS_DEVICE (under wal_mu): the caller's device array and its capacity
@@ -347,6 +349,7 @@ struct lsmck_ctx {
   int wal_seg = 1;           // device WAL walk: 1 = the segment walk first (default), 0 = candidate doubling only
   uint64_t wal_seg_bytes = 0;  // segment walk: bytes per segment (0 = auto, ~2^16 segments)
   bool wal_seg_pack = true;  // segment walk: packed CRC spans (seg::Pack) for the CRC pass
+  long wal_seg_stage = 1;    // segment walk: staged records (seg::StageRec): 0 off, 1 auto slots, else slots per segment
   int wal_seg_rounds = 16;   // segment walk: repairs before it declines to the candidate-doubling walk
   int numa_node = -1;    // the device's NUMA node (sysfs), -1 unknown
   int stage_numa = -2;   // option "stage_numa": -2 the device's node on a multi-node host, -1 off, >= 0 that node
@@ -987,6 +990,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     apply_numa(ctx);
     return 0;
   }
+  if (!strcmp(key, "wal_seg_stage")) {  // segment walk: records staged by the walk (1 auto, 0 off, >= 2 slots/segment)
+    if (value < 0 || value > (1l << 24)) return lsmck_host::set_error(LSMCK_EINVAL, "wal_seg_stage: 0..2^24");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_seg_stage = value;
+    return 0;
+  }
   if (!strcmp(key, "wal_seg_pack")) {  // A/B: the segment walk's packed CRC spans (1, default) or payloads alone (0)
     if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "wal_seg_pack: 0 or 1");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1094,7 +1103,7 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   if (ctx->wd.h_info) (void)hipHostFree(ctx->wd.h_info);
   for (void* p : {(void*)ctx->wd.sg, (void*)ctx->wd.sx, (void*)ctx->wd.spre, (void*)ctx->wd.scode,
                   (void*)ctx->wd.srecs, (void*)ctx->wd.sbsum, (void*)ctx->wd.sinfo, (void*)ctx->wd.scpp,
-                  (void*)ctx->wd.scpc})
+                  (void*)ctx->wd.scpc, (void*)ctx->wd.sst})
     if (p) (void)hipFree(p);
   if (ctx->wd.h_sinfo) (void)hipHostFree(ctx->wd.h_sinfo);
   for (void* p : {(void*)ctx->d_vcrc, (void*)ctx->d_woff, (void*)ctx->d_wlen, (void*)ctx->d_wexp})
@@ -1564,8 +1573,24 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
         HIPCHK(hipMalloc((void**)&W.scpc, c * 4));
         W.cap_cp = c;
       }
+      // the walk stages each segment's records in scap slots (auto: an
+      // eighth of the walked bytes, 64 MiB .. 8 GiB, over the segments; at
+      // most the records a segment can hold); a segment with more is emitted
+      // by a second walk of its headers
+      uint32_t scap = 0;
+      if (ctx->wal_seg_stage) {
+        const uint64_t most = S / 9 + 1;
+        const uint64_t budget = std::min<uint64_t>(std::max<uint64_t>((lim - start) / 8, 64ull << 20), 8ull << 30);
+        const uint64_t c = std::min<uint64_t>(most, ctx->wal_seg_stage >= 2 ? (uint64_t)ctx->wal_seg_stage
+                                                                               : budget / (sizeof(sg::StageRec) * K));
+        if (c >= 1) {
+          scap = (uint32_t)c;
+          if ((rc = ensure_dev(&W.sst, &W.cap_sst, (size_t)K * scap))) return rc;
+        }
+      }
       a = sg::SegArgs{img, n, start, S, K, W.sg, W.sx, W.scode, W.srecs, W.spre, W.sinfo, lim,
-                      nsub, S / nsub, nsub > 1 ? W.scpp : nullptr, nsub > 1 ? W.scpc : nullptr};
+                      nsub, S / nsub, nsub > 1 ? W.scpp : nullptr, nsub > 1 ? W.scpc : nullptr,
+                      scap ? W.sst : nullptr, scap};
       if ((rc = lsmk_wal_seg_walk(&a, st))) return launch_rc(rc, "wal segment walk kernel");
     }
     if ((rc = lsmk_wal_seg_round(&a, W.sbsum, st))) return launch_rc(rc, "wal segment check kernels");
@@ -1615,6 +1640,9 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
       rc = lsmk_wal_seg_emit(&a, at, to, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st);
     }
     if (rc) return launch_rc(rc, "wal segment emit kernel");
+    if ((rc = lsmk_wal_seg_place(&a, at, to, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, tot, ctx->wal_seg_pack ? 1 : 0,
+                                 st)))
+      return launch_rc(rc, "wal segment place kernel");
     out->packed = ctx->wal_seg_pack;
     ctx->wal_recs_dev_emitted = dev;
   }

@@ -171,10 +171,34 @@ LSMCK_HD uint64_t next_of(const Head& h, uint64_t n, uint64_t p, bool* whole) {
   return p + hl + (*whole ? (uint64_t)dlen : avail);
 }
 
+// A record as the walk stages it (the lsmck_wal_rec layout): segment k's
+// walk writes its records to its own slots [k * scap, k * scap + scap) as it
+// passes them, so the records need no second walk of the headers when they
+// all fit (seg_place_thread copies them out); a segment with more records
+// than slots is emitted by its second walk as before (seg_emit_thread).
+struct StageRec {
+  uint64_t rec_off, payload_off;
+  uint32_t klen, vlen, crc, type;
+};
+LSMCK_HD void stage_put(StageRec* st, uint32_t cap, uint32_t cnt, uint64_t p, const Head& h) {
+  if (st && cnt < cap) {
+    StageRec R;
+    R.rec_off = p;
+    R.payload_off = p + hdr_len(h.t);
+    R.klen = h.klen;
+    R.vlen = h.vlen;
+    R.crc = h.crc;
+    R.type = h.t;
+    st[cnt] = R;
+  }
+}
+
 // The segment's outcome from its entry c (a record start on the chain, or
 // the guess; h its header): the walk through the segment ending at e, to the
 // first record start at or past e (kExit) or to the chain's end (kEnd / kBad).
-LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, Head h, uint64_t e, WalkOut* o) {
+// st: the segment's staging slots (scap of them), or none.
+LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, Head h, uint64_t e, WalkOut* o,
+                   StageRec* st = nullptr, uint32_t scap = 0) {
   uint64_t p = c;
   uint32_t cnt = 0;
   for (;;) {
@@ -186,6 +210,7 @@ LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, Head h, uint64_t 
     }
     bool whole;
     const uint64_t q = next_of(h, n, p, &whole);
+    stage_put(st, scap, cnt, p, h);
     ++cnt;
     h = head(img, n, q);
     if (h.cl) {  // the chain ends after the record at p
@@ -391,7 +416,13 @@ struct SegArgs {
   uint64_t sub;
   uint64_t* cpp;  // K * nsub
   uint32_t* cpc;
+  // walk-time staging (StageRec): scap slots per segment, 0 = none
+  StageRec* srec;
+  uint32_t scap;
 };
+LSMCK_HD StageRec* seg_stage(const SegArgs& a, uint32_t k) {
+  return a.scap ? a.srec + (uint64_t)k * a.scap : nullptr;
+}
 
 LSMCK_HD uint64_t seg_begin(const SegArgs& a, uint32_t k) { return a.start + (uint64_t)k * a.S; }
 LSMCK_HD uint64_t seg_end(const SegArgs& a, uint32_t k) {
@@ -411,6 +442,7 @@ LSMCK_HD void walk_cp(const SegArgs& a, uint32_t k, uint64_t c, Head h, WalkOut*
   const uint64_t n = a.n, e = seg_end(a, k), b0 = seg_begin(a, k);
   uint64_t* cpp = a.cpp + (uint64_t)k * a.nsub;
   uint32_t* cpc = a.cpc + (uint64_t)k * a.nsub;
+  StageRec* st = seg_stage(a, k);
   uint32_t j = 0;
   uint64_t p = c;
   uint32_t cnt = 0;
@@ -427,6 +459,7 @@ LSMCK_HD void walk_cp(const SegArgs& a, uint32_t k, uint64_t c, Head h, WalkOut*
     }
     bool whole;
     const uint64_t q = next_of(h, n, p, &whole);
+    stage_put(st, a.scap, cnt, p, h);
     ++cnt;
     h = head(img, n, q);
     if (h.cl) {
@@ -458,7 +491,7 @@ LSMCK_HD void seg_forced(const SegArgs& a, uint32_t k, uint64_t c) {
   } else if (a.nsub > 1) {
     walk_cp(a, k, c, h, &o);
   } else {
-    walk(a.img, a.n, c, h, seg_end(a, k), &o);
+    walk(a.img, a.n, c, h, seg_end(a, k), &o, seg_stage(a, k), a.scap);
   }
   a.g[k] = c;
   a.x[k] = o.pos;
@@ -574,6 +607,7 @@ template <class Rec>
 LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint64_t at, Rec* recs, uint64_t* poff,
                               uint32_t* plen, uint32_t* pcrc, uint32_t j = 0, const Pack* pk = nullptr) {
   if (k > jterm || a.code[k] == kNone) return;
+  if (a.scap && a.recs[k] <= a.scap) return;  // staged: seg_place_thread
   uint32_t r = 0, rend = a.recs[k];
   uint64_t p = a.g[k], pend = ~0ull;
   if (a.nsub > 1) {
@@ -616,6 +650,40 @@ LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint
     if (i < pk->iend) hl = hdr_len(head(img, a.n, p).t);
     plen[pi] = hl && pack_fits(pgot, hl) ? pgot + hl : pgot;
   }
+}
+
+// Record r of staged segment k (every record it walked fit its slots): the
+// staged record to `at` + its place, its CRC span -- packed (pk: the next
+// record's type from the next slot, or the byte at the segment's exit) or
+// the payload alone -- and, unpacked, its stored CRC.  The payload is cut at
+// EOF only for the last record of the walk (no successor).
+template <class Rec>
+LSMCK_HD void seg_place_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint64_t at, Rec* recs, uint64_t* poff,
+                               uint32_t* plen, uint32_t* pcrc, uint32_t r, const Pack* pk = nullptr) {
+  const StageRec* st = a.srec + (uint64_t)k * a.scap;
+  const StageRec R = st[r];
+  const uint64_t i = at + (a.pre[k] & kRecMask) + r;
+  Rec O;
+  O.rec_off = R.rec_off;
+  O.payload_off = R.payload_off;
+  O.klen = R.klen;
+  O.vlen = R.vlen;
+  O.crc = R.crc;
+  O.type = R.type;
+  recs[i] = O;
+  poff[i] = R.payload_off;
+  const uint32_t dlen = R.klen + R.vlen;
+  const uint64_t avail = a.n - R.payload_off;
+  const uint32_t got = dlen <= avail ? dlen : (uint32_t)avail;
+  if (pk) {
+    uint32_t hl = 0;
+    if (i + 1 < pk->iend) hl = hdr_len(r + 1 < a.recs[k] ? st[r + 1].type : (uint32_t)a.img[a.x[k]]);
+    plen[i] = hl && pack_fits(got, hl) ? got + hl : got;
+  } else {
+    plen[i] = got;
+    pcrc[i] = R.crc;
+  }
+  (void)jterm;
 }
 
 }  // namespace seg

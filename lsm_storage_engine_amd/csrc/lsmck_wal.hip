@@ -469,6 +469,23 @@ __global__ __launch_bounds__(256) void wal_seg_emit_packed(seg::SegArgs a, uint6
     seg::seg_emit_thread(a, k, (uint32_t)a.info[seg::kInfoJterm], at, recs, poff, plen, (uint32_t*)nullptr, j, &pk);
 }
 
+// The staged segments' records out (seg::seg_place_thread): one wave per
+// segment, its slots read in order -- the second walk of the headers that
+// seg_emit_thread makes for a segment with more records than slots.
+template <bool PACK>
+__global__ __launch_bounds__(64) void wal_seg_place(seg::SegArgs a, uint64_t at, lsmck_wal_rec* __restrict__ recs,
+                                                    uint64_t* __restrict__ poff, uint32_t* __restrict__ plen,
+                                                    uint32_t* __restrict__ pcrc, uint64_t iend) {
+  const uint32_t k = blockIdx.x;
+  const uint32_t jterm = (uint32_t)a.info[seg::kInfoJterm];
+  if (k > jterm || a.code[k] == seg::kNone) return;
+  const uint32_t cnt = a.recs[k];
+  if (cnt > a.scap) return;  // (emitted by wal_seg_emit*)
+  const seg::Pack pk{iend};
+  for (uint32_t r = threadIdx.x; r < cnt; r += 64u)
+    seg::seg_place_thread(a, k, jterm, at, recs, poff, plen, pcrc, r, PACK ? &pk : nullptr);
+}
+
 // The compare over packed spans, records [i0, m) of recs (the emit's): record
 // i's CRC (of [payload_i | header_i+1) unless i is the last or its span did
 // not fit) back to its payload's by seg::unpack_crc with header i+1 read from
@@ -594,6 +611,16 @@ extern "C" int lsmk_wal_seg_emit_packed(const seg::SegArgs* a, uint64_t at, lsmc
   const uint64_t threads = (uint64_t)a->K * a->nsub;
   hipLaunchKernelGGL(wal_seg_emit_packed, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, *a, at, recs, poff,
                      plen, iend);
+  return launch_err();
+}
+
+extern "C" int lsmk_wal_seg_place(const seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff,
+                                  uint32_t* plen, uint32_t* pcrc, uint64_t iend, int packed, hipStream_t st) {
+  if (!a->scap || !a->K) return 0;
+  if (packed)
+    hipLaunchKernelGGL(wal_seg_place<true>, dim3(a->K), dim3(64), 0, st, *a, at, recs, poff, plen, pcrc, iend);
+  else
+    hipLaunchKernelGGL(wal_seg_place<false>, dim3(a->K), dim3(64), 0, st, *a, at, recs, poff, plen, pcrc, iend);
   return launch_err();
 }
 

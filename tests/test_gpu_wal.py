@@ -384,7 +384,8 @@ def seg_opts(ctx):
         for k, v in kw.items():
             ctx.set_option(k, v)
     yield set_
-    for k, v in (("wal_seg_bytes", 0), ("wal_seg_rounds", 16), ("wal_seg_walk", 1), ("wal_seg_pack", 1)):
+    for k, v in (("wal_seg_bytes", 0), ("wal_seg_rounds", 16), ("wal_seg_walk", 1), ("wal_seg_pack", 1),
+                 ("wal_seg_stage", 1)):
         ctx.set_option(k, v)
 
 
@@ -427,15 +428,18 @@ def test_segment_walk(ctx, seg_opts, seg, shift):
     assert same(ctx, bytes(b), device=True, shift=shift) in (1, 2)
 
 
+@pytest.mark.parametrize("stage", [1, 0, 3])
 @pytest.mark.parametrize("pack", [1, 0])
 @pytest.mark.parametrize("seg", [0, 512, 262144])
-def test_segment_walk_packed_spans(ctx, seg_opts, pack, seg):
+def test_segment_walk_packed_spans(ctx, seg_opts, pack, seg, stage):
     """The CRC pass over packed spans ([payload | next header), the headers
     taken back out by wal_compare_packed) against payload-only spans: empty keys
     and values (spans of a header alone), Removes next to Inserts, a corrupted
     payload and header CRC (the computed CRC it reports is the payload's own),
-    and a log cut inside the last payload (its span the payload alone)."""
-    seg_opts(wal_seg_bytes=seg, wal_seg_pack=pack)
+    and a log cut inside the last payload (its span the payload alone).
+    stage: the walk's record staging -- auto, off, and 3 slots per segment
+    (most segments emitted by a second walk, the rest placed from slots)."""
+    seg_opts(wal_seg_bytes=seg, wal_seg_pack=pack, wal_seg_stage=stage)
     rng = np.random.default_rng(63)
     parts = []
     for i in range(6000):

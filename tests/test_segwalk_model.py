@@ -64,6 +64,8 @@ def sim(tmp_path_factory):
     run.prefix = prefix
     lib.segwalk_sim_set_nsub.argtypes = [C.c_uint32]
     run.set_nsub = lib.segwalk_sim_set_nsub
+    lib.segwalk_sim_set_stage.argtypes = [C.c_uint32]
+    run.set_stage = lib.segwalk_sim_set_stage
     lib.segwalk_sim_pack.argtypes = [u64p, C.POINTER(C.c_uint32), C.c_size_t]
     lib.segwalk_sim_unpack.restype = C.c_uint32
     lib.segwalk_sim_unpack.argtypes = [C.c_uint32] * 5
@@ -270,14 +272,18 @@ def test_prefix_walks_chain_to_the_whole(sim, S, parts):
         assert end == (want[1], want[2])
 
 
+@pytest.mark.parametrize("stage", [0, 1, 6, 100000])
 @pytest.mark.parametrize("nsub", [2, 4, 32])
 @pytest.mark.parametrize("S", [256, 4096, 65536])
-def test_emit_by_sub_segments(sim, S, nsub):
+def test_emit_by_sub_segments(sim, S, nsub, stage):
     """The emit from the walk's checkpoints, one thread per sub-segment: the
     same records as the chain walk -- records longer than sub-segments and
     segments, entries after a sub-segment start, repairs (which rewalk and
-    re-note the checkpoints), a bad type byte and a cut inside a record."""
+    re-note the checkpoints), a bad type byte and a cut inside a record.
+    stage: the walk's staging slots per segment (seg::StageRec) -- segments
+    that fit are placed from their slots, the rest emitted, mixed in one walk."""
     sim.set_nsub(nsub)
+    sim.set_stage(stage)
     try:
         rng = np.random.default_rng(S * 3 + nsub)
         for img in (random_log(rng, 1500, hi=900), random_log(rng, 200, lo=1000, hi=30000),
@@ -291,6 +297,7 @@ def test_emit_by_sub_segments(sim, S, nsub):
             check(sim, img[:len(img) - 11], S)
     finally:
         sim.set_nsub(1)
+        sim.set_stage(0)
 
 
 def _mulmod(a, b):
@@ -318,9 +325,10 @@ def test_unpack_constants():
     assert pw[9] == 0x2fb98a7d and pw[13] == 0x525983aa
 
 
+@pytest.mark.parametrize("stage", [0, 3, 100000])
 @pytest.mark.parametrize("nsub", [1, 4])
 @pytest.mark.parametrize("S", [512, 4096, 65536])
-def test_packed_crc_spans(sim, S, nsub):
+def test_packed_crc_spans(sim, S, nsub, stage):
     """The emit's packed CRC spans: record i's span is its payload and the next
     record's header (the last one's its payload alone), so the spans tile the
     log; seg::unpack_crc (wal_compare_packed's) takes the header back out of
@@ -329,6 +337,7 @@ def test_packed_crc_spans(sim, S, nsub):
     import zlib
     M = 0xFFFFFFFF
     sim.set_nsub(nsub)
+    sim.set_stage(stage)
     try:
         rng = np.random.default_rng(S + nsub)
         for img in (random_log(rng, 1500, hi=900), random_log(rng, 300, lo=1000, hi=30000),
@@ -363,3 +372,4 @@ def test_packed_crc_spans(sim, S, nsub):
                         assert pl[i] == plen and span == zlib.crc32(im[q + hl:q + hl + plen])
     finally:
         sim.set_nsub(1)
+        sim.set_stage(0)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 evidence in one GPU call.  Steps picked by STEPS (space list), run in this order:
-#   pywal smoke pytest bench benchkt c3pmc walbig walbig0 walbigkt waldiag sha shaab tree server
+#   pywal smoke pytest bench benchkt c3pmc walbig walbigs0 walbig0 walbigkt waldiag sha shaab tree server
 # A test failure goes on to the next step; a timeout / abort / crash ends the call.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -41,6 +41,7 @@ if has c3pmc; then  # HBM bytes per launch of the stream kernel (separate FETCH_
   python3 tools/pmc_summary.py $O/pmc_c3_FETCH_SIZE $O/pmc_c3_WRITE_SIZE config3 > $O/pmc_summary_c3.json 2>&1
 fi
 has walbig && step walbig 300 env LSMCK_WAL_TRACE=1 python3 -u tools/wal_replay_big.py --steps 3 --device-recs 1
+has walbigs0 && step walbigs0 300 env LSMCK_WAL_TRACE=1 python3 -u tools/wal_replay_big.py --steps 3 --device-recs 1 --seg-stage 0
 has walbig0 && step walbig0 300 env LSMCK_WAL_TRACE=1 python3 -u tools/wal_replay_big.py --steps 3 --device-recs 1 --seg-pack 0
 if has walbigkt; then
   step walbigkt 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_walbig -o kt -- python3 tools/wal_replay_big.py --steps 2 --device-recs 1

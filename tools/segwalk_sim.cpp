@@ -24,6 +24,8 @@ static uint64_t* g_dbg = nullptr;  // debug: the first round's guesses
 extern "C" void segwalk_sim_debug(uint64_t* g) { g_dbg = g; }
 static uint32_t g_nsub = 1;  // emit checkpoints: sub-segments per segment (1 = none)
 extern "C" void segwalk_sim_set_nsub(uint32_t v) { g_nsub = v ? v : 1; }
+static uint32_t g_scap = 0;  // walk-time staging: slots per segment (0 = none)
+extern "C" void segwalk_sim_set_stage(uint32_t v) { g_scap = v; }
 // packed CRC spans (seg::Pack): when set, the next walk emits them here --
 // span offsets and lengths
 static uint64_t* g_poff = nullptr;
@@ -82,8 +84,10 @@ extern "C" int segwalk_sim_prefix(const uint8_t* img, uint64_t n, uint64_t start
   unsigned long long info[sg::kInfoWords] = {};
   std::vector<uint64_t> cpp((size_t)K * g_nsub);
   std::vector<uint32_t> cpc((size_t)K * g_nsub);
+  const uint32_t scap = (uint32_t)std::min<uint64_t>(g_scap, S / 9 + 1);  // (as wal_seg_walk caps it)
+  std::vector<sg::StageRec> st((size_t)K * scap);
   sg::SegArgs a{img, n, start, S, K, g.data(), x.data(), code.data(), recs.data(), pre.data(), info, lim,
-                g_nsub, (S + g_nsub - 1) / g_nsub, cpp.data(), cpc.data()};
+                g_nsub, (S + g_nsub - 1) / g_nsub, cpp.data(), cpc.data(), scap ? st.data() : nullptr, scap};
   for (uint32_t k = 0; k < K; ++k) sg::seg_walk_thread(a, k);
   if (g_dbg) std::copy(g.begin(), g.begin() + K, g_dbg);
   for (int round = 0;; ++round) {
@@ -129,6 +133,11 @@ extern "C" int segwalk_sim_prefix(const uint8_t* img, uint64_t n, uint64_t start
     for (uint32_t j = 0; j < a.nsub; ++j)
       sg::seg_emit_thread(a, k, (uint32_t)info[sg::kInfoJterm], 0, R.data(), poff.data(), plen.data(), pcrc.data(), j,
                           g_pcap ? &pk : nullptr);
+  const uint32_t jt = (uint32_t)info[sg::kInfoJterm];
+  for (uint32_t k = 0; scap && k < K; ++k)  // wal_seg_place: the staged segments
+    if (k <= jt && code[k] != sg::kNone && recs[k] <= scap)
+      for (uint32_t r = 0; r < recs[k]; ++r)
+        sg::seg_place_thread(a, k, jt, 0, R.data(), poff.data(), plen.data(), pcrc.data(), r, g_pcap ? &pk : nullptr);
   for (uint64_t i = 0; i < m && i < cap; ++i) rec_off[i] = R[i].rec_off;
   for (uint64_t i = 0; i < m && i < g_pcap; ++i) {
     g_poff[i] = poff[i];

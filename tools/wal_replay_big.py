@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--records", type=int, default=1 << 26)
     ap.add_argument("--seg-walk", type=int, default=1, help="0: the candidate-doubling walk (A/B)")
     ap.add_argument("--seg-pack", type=int, default=1, help="0: the CRC pass over payloads alone (A/B)")
+    ap.add_argument("--seg-stage", type=int, default=1,
+                    help="0: no record staging in the walk (the emit walks the headers again; A/B)")
     ap.add_argument("--pinned-recs", type=int, default=1,
                     help="1: the records DMA'd into a page-locked array (LSMCK_RECS_PINNED); 0: staged + copied")
     ap.add_argument("--device-recs", type=int, default=0,
@@ -61,6 +63,7 @@ def main():
     ctx = Context(0)
     ctx.set_option("wal_seg_walk", a.seg_walk)
     ctx.set_option("wal_seg_pack", a.seg_pack)
+    ctx.set_option("wal_seg_stage", a.seg_stage)
     d = ctx.alloc(total + 64)
     d_o, d_l, out = ctx.alloc(off.nbytes), ctx.alloc(ln.nbytes), ctx.alloc(4 * n)
     ctx.gen_stream(d.ptr, 0x5EED0003, 0, total)
