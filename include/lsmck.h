@@ -232,6 +232,10 @@ int lsmck_device_count(void);
  *                 each payload with the next record's header, the header
  *                 then taken back out of the CRC (default); 0 = over the
  *                 payloads alone.  A/B; results are the same.
+ *   "wal_seg_stage"  segment walk: the walk stages the records it passes so
+ *                 they need no second walk of the headers: 1 = auto slots
+ *                 per segment (default), 0 = off (A/B), N >= 2 = N slots
+ *                 (tests).  A segment with more records is walked again.
  * Returns 0, or LSMCK_EINVAL for an unknown key / value. */
 int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
 

@@ -652,16 +652,15 @@ LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint
   }
 }
 
-// Record r of staged segment k (every record it walked fit its slots): the
-// staged record to `at` + its place, its CRC span -- packed (pk: the next
-// record's type from the next slot, or the byte at the segment's exit) or
-// the payload alone -- and, unpacked, its stored CRC.  The payload is cut at
-// EOF only for the last record of the walk (no successor).
+// Record r of staged segment k (every record it walked fit its slots), R
+// its staged form: the record to `at` + its place, its CRC span -- packed
+// (pk) or the payload alone -- and, unpacked, its stored CRC.  nt: the type
+// byte of the record after it (the next slot's, or the byte at the segment's
+// exit for its last record), read only when the walk has a record after it.
+// The payload is cut at EOF only for the walk's last record.
 template <class Rec>
-LSMCK_HD void seg_place_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint64_t at, Rec* recs, uint64_t* poff,
-                               uint32_t* plen, uint32_t* pcrc, uint32_t r, const Pack* pk = nullptr) {
-  const StageRec* st = a.srec + (uint64_t)k * a.scap;
-  const StageRec R = st[r];
+LSMCK_HD void seg_place_rec(const SegArgs& a, uint32_t k, uint64_t at, Rec* recs, uint64_t* poff, uint32_t* plen,
+                            uint32_t* pcrc, uint32_t r, const StageRec& R, uint32_t nt, const Pack* pk) {
   const uint64_t i = at + (a.pre[k] & kRecMask) + r;
   Rec O;
   O.rec_off = R.rec_off;
@@ -676,14 +675,16 @@ LSMCK_HD void seg_place_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uin
   const uint64_t avail = a.n - R.payload_off;
   const uint32_t got = dlen <= avail ? dlen : (uint32_t)avail;
   if (pk) {
-    uint32_t hl = 0;
-    if (i + 1 < pk->iend) hl = hdr_len(r + 1 < a.recs[k] ? st[r + 1].type : (uint32_t)a.img[a.x[k]]);
+    const uint32_t hl = i + 1 < pk->iend ? hdr_len(nt) : 0u;
     plen[i] = hl && pack_fits(got, hl) ? got + hl : got;
   } else {
     plen[i] = got;
     pcrc[i] = R.crc;
   }
-  (void)jterm;
+}
+// the next record's type byte for record r of staged segment k (see above)
+LSMCK_HD uint32_t seg_place_next_type(const SegArgs& a, uint32_t k, uint32_t r) {
+  return r + 1 < a.recs[k] ? a.srec[(uint64_t)k * a.scap + r + 1].type : (uint32_t)a.img[a.x[k]];
 }
 
 }  // namespace seg

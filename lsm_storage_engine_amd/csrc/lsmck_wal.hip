@@ -469,21 +469,32 @@ __global__ __launch_bounds__(256) void wal_seg_emit_packed(seg::SegArgs a, uint6
     seg::seg_emit_thread(a, k, (uint32_t)a.info[seg::kInfoJterm], at, recs, poff, plen, (uint32_t*)nullptr, j, &pk);
 }
 
-// The staged segments' records out (seg::seg_place_thread): one wave per
-// segment, its slots read in order -- the second walk of the headers that
-// seg_emit_thread makes for a segment with more records than slots.
+// The staged segments' records out (seg::seg_place_rec): one wave per
+// segment, four per workgroup, its slots read in order -- instead of the
+// second walk of the headers seg_emit_thread makes for a segment with more
+// records than slots.  A lane takes the next record's type from the next
+// lane (lane 63 and the segment's last record read it).
 template <bool PACK>
-__global__ __launch_bounds__(64) void wal_seg_place(seg::SegArgs a, uint64_t at, lsmck_wal_rec* __restrict__ recs,
-                                                    uint64_t* __restrict__ poff, uint32_t* __restrict__ plen,
-                                                    uint32_t* __restrict__ pcrc, uint64_t iend) {
-  const uint32_t k = blockIdx.x;
+__global__ __launch_bounds__(256) void wal_seg_place(seg::SegArgs a, uint64_t at, lsmck_wal_rec* __restrict__ recs,
+                                                     uint64_t* __restrict__ poff, uint32_t* __restrict__ plen,
+                                                     uint32_t* __restrict__ pcrc, uint64_t iend) {
+  const uint32_t k = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (k >= a.K) return;
   const uint32_t jterm = (uint32_t)a.info[seg::kInfoJterm];
   if (k > jterm || a.code[k] == seg::kNone) return;
   const uint32_t cnt = a.recs[k];
   if (cnt > a.scap) return;  // (emitted by wal_seg_emit*)
+  const seg::StageRec* st = a.srec + (uint64_t)k * a.scap;
+  const uint64_t i0 = at + (a.pre[k] & seg::kRecMask);
   const seg::Pack pk{iend};
-  for (uint32_t r = threadIdx.x; r < cnt; r += 64u)
-    seg::seg_place_thread(a, k, jterm, at, recs, poff, plen, pcrc, r, PACK ? &pk : nullptr);
+  for (uint32_t r0 = 0; r0 < cnt; r0 += 64u) {  // (wave-uniform)
+    const uint32_t r = r0 + lane;
+    seg::StageRec R{};
+    if (r < cnt) R = st[r];
+    uint32_t nt = __shfl_down(R.type, 1);
+    if (r < cnt && (lane == 63u || r + 1u == cnt) && i0 + r + 1u < iend) nt = seg::seg_place_next_type(a, k, r);
+    if (r < cnt) seg::seg_place_rec(a, k, at, recs, poff, plen, pcrc, r, R, nt, PACK ? &pk : nullptr);
+  }
 }
 
 // The compare over packed spans, records [i0, m) of recs (the emit's): record
@@ -618,9 +629,11 @@ extern "C" int lsmk_wal_seg_place(const seg::SegArgs* a, uint64_t at, lsmck_wal_
                                   uint32_t* plen, uint32_t* pcrc, uint64_t iend, int packed, hipStream_t st) {
   if (!a->scap || !a->K) return 0;
   if (packed)
-    hipLaunchKernelGGL(wal_seg_place<true>, dim3(a->K), dim3(64), 0, st, *a, at, recs, poff, plen, pcrc, iend);
+    hipLaunchKernelGGL(wal_seg_place<true>, dim3((a->K + 3u) / 4u), dim3(256), 0, st, *a, at, recs, poff, plen, pcrc,
+                       iend);
   else
-    hipLaunchKernelGGL(wal_seg_place<false>, dim3(a->K), dim3(64), 0, st, *a, at, recs, poff, plen, pcrc, iend);
+    hipLaunchKernelGGL(wal_seg_place<false>, dim3((a->K + 3u) / 4u), dim3(256), 0, st, *a, at, recs, poff, plen, pcrc,
+                       iend);
   return launch_err();
 }
 

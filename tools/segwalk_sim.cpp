@@ -136,8 +136,12 @@ extern "C" int segwalk_sim_prefix(const uint8_t* img, uint64_t n, uint64_t start
   const uint32_t jt = (uint32_t)info[sg::kInfoJterm];
   for (uint32_t k = 0; scap && k < K; ++k)  // wal_seg_place: the staged segments
     if (k <= jt && code[k] != sg::kNone && recs[k] <= scap)
-      for (uint32_t r = 0; r < recs[k]; ++r)
-        sg::seg_place_thread(a, k, jt, 0, R.data(), poff.data(), plen.data(), pcrc.data(), r, g_pcap ? &pk : nullptr);
+      for (uint32_t r = 0; r < recs[k]; ++r) {
+        const uint64_t i = (pre[k] & sg::kRecMask) + r;
+        const uint32_t nt = i + 1 < m ? sg::seg_place_next_type(a, k, r) : 0u;
+        sg::seg_place_rec(a, k, 0, R.data(), poff.data(), plen.data(), pcrc.data(), r, st[(size_t)k * scap + r], nt,
+                          g_pcap ? &pk : nullptr);
+      }
   for (uint64_t i = 0; i < m && i < cap; ++i) rec_off[i] = R[i].rec_off;
   for (uint64_t i = 0; i < m && i < g_pcap; ++i) {
     g_poff[i] = poff[i];
