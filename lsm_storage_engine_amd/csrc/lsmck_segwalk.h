@@ -78,7 +78,10 @@ constexpr uint64_t kHop = 65536;
 // log: 0.33 vs 0.42 ms, profiles/r04/o).  Segments shorter than records
 // (under 4 KiB) often hold no true start, and long hops (2 MiB segments)
 // let bogus lengths land on a true record: the rule stays for both.
-constexpr uint64_t kLaterSkipFrom = 4096, kLaterSkipTo = 131072;
+#ifndef LSMCK_LATER_SKIP_TO
+#define LSMCK_LATER_SKIP_TO 131072
+#endif
+constexpr uint64_t kLaterSkipFrom = 4096, kLaterSkipTo = LSMCK_LATER_SKIP_TO;
 #ifndef LSMCK_SCAN_BLOCKS
 #define LSMCK_SCAN_BLOCKS 4
 #endif
