@@ -133,7 +133,7 @@ def check(sim, img, S, start=0, shift=0, rounds=16, expect_fast=True):
     return rep
 
 
-@pytest.mark.parametrize("S", [64, 100, 512, 4096, 1 << 16])
+@pytest.mark.parametrize("S", [64, 100, 512, 4096, 1 << 16, 1 << 17, 1 << 19])
 @pytest.mark.parametrize("shift", [0, 3])
 def test_random_logs(sim, S, shift):
     rng = np.random.default_rng(S + shift)
