@@ -43,6 +43,11 @@
 #define LSMCK_HD static inline
 #endif
 
+// diagnostic builds (LSMCK_SEG_CLOCK, lsmck_wal.hip): per-segment clock marks
+#ifndef LSMCK_SEG_CLOCK_MARK
+#define LSMCK_SEG_CLOCK_MARK(k, slot)
+#endif
+
 namespace lsmck {
 namespace seg {
 
@@ -519,6 +524,7 @@ LSMCK_HD void seg_forced(const SegArgs& a, uint32_t k, uint64_t c) {
 
 // step 1-2 for segment k
 LSMCK_HD void seg_walk_thread(const SegArgs& a, uint32_t k) {
+  LSMCK_SEG_CLOCK_MARK(k, 0);
   if (k == 0) {
     seg_forced(a, 0, a.start);
     return;
@@ -529,6 +535,7 @@ LSMCK_HD void seg_walk_thread(const SegArgs& a, uint32_t k) {
 #else
                            a.S < kLaterSkipFrom || a.S >= kLaterSkipTo, a.S >= kLaterSkipTo ? kLaterMin : 0);
 #endif
+  LSMCK_SEG_CLOCK_MARK(k, 1);
   if (c == kNoGuess) {
     a.g[k] = c;
     a.x[k] = 0;
@@ -537,6 +544,7 @@ LSMCK_HD void seg_walk_thread(const SegArgs& a, uint32_t k) {
   } else {
     seg_forced(a, k, c);  // the walk from the guess (every lane of the wave at once)
   }
+  LSMCK_SEG_CLOCK_MARK(k, 2);
 }
 
 // placement word of segment k (the scan's input): guessed segments up to jterm

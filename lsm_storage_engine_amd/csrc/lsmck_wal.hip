@@ -23,6 +23,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifdef LSMCK_SEG_CLOCK  // diagnostic builds only: the segment walk's clock marks per segment
+__device__ uint64_t g_seg_clock[3 * 131072];
+#define LSMCK_SEG_CLOCK_MARK(k, slot) \
+  do {                                  \
+    if ((k) < 131072u) g_seg_clock[3u * (k) + (slot)] = wall_clock64(); \
+  } while (0)
+#endif
+
 #include "lsmck.h"
 #include "lsmck_device.h"
 #include "lsmck_segwalk.h"
@@ -731,3 +739,13 @@ extern "C" int lsmk_wal_emit(const uint8_t* img, uint64_t n, const uint32_t* cha
                      pcrc);
   return launch_err();
 }
+
+#ifdef LSMCK_SEG_CLOCK
+// (diagnostic) the last segment walk's marks: 3 per segment (start, after
+// the guess, after the walk), wall_clock64 ticks (100 MHz)
+extern "C" int lsmck_diag_seg_clock(uint64_t* out, size_t n) {
+  if (n > 3u * 131072u) n = 3u * 131072u;
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seg_clock), n * 8, 0, hipMemcpyDeviceToHost);
+  return e == hipSuccess ? 0 : -(int)e;
+}
+#endif
