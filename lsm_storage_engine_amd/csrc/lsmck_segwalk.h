@@ -380,22 +380,26 @@ LSMCK_HD bool reaches(const uint8_t* img, uint64_t n, uint64_t c, uint64_t q) {
 // one, so its walk is taken, but its first "record" covers the true entry,
 // whose chain reaches the merge point (`later`: the rule runs; see
 // kLaterSkipFrom).  kNoGuess: no start taken.
+// the later-start rule from an accepted start c (see guess())
+LSMCK_HD uint64_t later_rule(Scan& S, const uint8_t* img, uint64_t n, uint64_t c, uint64_t e, uint64_t later_min) {
+  for (;;) {
+    bool whole;
+    const Head hc = head(img, n, c);
+    const uint64_t q1 = next_of(hc, n, c, &whole), lim = q1 < e ? q1 : e;
+    if (later_min && q1 - c - hdr_len(hc.t) <= later_min) return c;  // (kLaterMin)
+    uint64_t c2 = next_cand(S, img, n, c + 1, lim);
+    while (c2 != kNoGuess && !reaches(img, n, c2, q1)) c2 = next_cand(S, img, n, c2 + 1, lim);
+    if (c2 == kNoGuess) return c;
+    c = c2;
+  }
+}
 LSMCK_HD uint64_t guess(const uint8_t* img, uint64_t n, uint64_t b, uint64_t e, uint64_t hop, bool later = true,
                         uint64_t later_min = 0) {
   Scan S;
   for (uint64_t c = next_cand(S, img, n, b, e); c != kNoGuess; c = next_cand(S, img, n, c + 1, e)) {
     if (!accept(img, n, c, hop)) continue;
     if (!later) return c;
-    for (;;) {
-      bool whole;
-      const Head hc = head(img, n, c);
-      const uint64_t q1 = next_of(hc, n, c, &whole), lim = q1 < e ? q1 : e;
-      if (later_min && q1 - c - hdr_len(hc.t) <= later_min) return c;  // (kLaterMin)
-      uint64_t c2 = next_cand(S, img, n, c + 1, lim);
-      while (c2 != kNoGuess && !reaches(img, n, c2, q1)) c2 = next_cand(S, img, n, c2 + 1, lim);
-      if (c2 == kNoGuess) return c;
-      c = c2;
-    }
+    return later_rule(S, img, n, c, e, later_min);
   }
   return kNoGuess;
 }
@@ -523,19 +527,38 @@ LSMCK_HD void seg_forced(const SegArgs& a, uint32_t k, uint64_t c) {
 }
 
 // step 1-2 for segment k
+// the guess's parameters for the walk's segments
+LSMCK_HD uint64_t seg_hop(const SegArgs& a) { return a.S > kHop ? a.S : kHop; }
+LSMCK_HD bool seg_later(const SegArgs& a) {
+#ifdef LSMCK_SEG_LATER_ALWAYS  // (host model A/B, tools/segwalk_repairs.py)
+  (void)a;
+  return true;
+#else
+  return a.S < kLaterSkipFrom || a.S >= kLaterSkipTo;
+#endif
+}
+LSMCK_HD uint64_t seg_later_min(const SegArgs& a) {
+#ifdef LSMCK_SEG_LATER_ALWAYS
+  (void)a;
+  return 0;
+#else
+  return a.S >= kLaterSkipTo ? kLaterMin : 0;
+#endif
+}
+LSMCK_HD void seg_take_guess(const SegArgs& a, uint32_t k, uint64_t c);
 LSMCK_HD void seg_walk_thread(const SegArgs& a, uint32_t k) {
   LSMCK_SEG_CLOCK_MARK(k, 0);
   if (k == 0) {
     seg_forced(a, 0, a.start);
     return;
   }
-  const uint64_t c = guess(a.img, a.n, seg_begin(a, k), seg_end(a, k), a.S > kHop ? a.S : kHop,
-#ifdef LSMCK_SEG_LATER_ALWAYS  // (host model A/B, tools/segwalk_repairs.py)
-                           true);
-#else
-                           a.S < kLaterSkipFrom || a.S >= kLaterSkipTo, a.S >= kLaterSkipTo ? kLaterMin : 0);
-#endif
+  const uint64_t c = guess(a.img, a.n, seg_begin(a, k), seg_end(a, k), seg_hop(a), seg_later(a), seg_later_min(a));
   LSMCK_SEG_CLOCK_MARK(k, 1);
+  seg_take_guess(a, k, c);
+  LSMCK_SEG_CLOCK_MARK(k, 2);
+}
+// segment k from its guess c: its walk, or no entry
+LSMCK_HD void seg_take_guess(const SegArgs& a, uint32_t k, uint64_t c) {
   if (c == kNoGuess) {
     a.g[k] = c;
     a.x[k] = 0;
@@ -544,7 +567,6 @@ LSMCK_HD void seg_walk_thread(const SegArgs& a, uint32_t k) {
   } else {
     seg_forced(a, k, c);  // the walk from the guess (every lane of the wave at once)
   }
-  LSMCK_SEG_CLOCK_MARK(k, 2);
 }
 
 // placement word of segment k (the scan's input): guessed segments up to jterm

@@ -332,6 +332,64 @@ __global__ __launch_bounds__(256) void wal_seg_walk(seg::SegArgs a) {
   if (k < a.K) seg::seg_walk_thread(a, k);
 }
 
+// The guess by a group of G consecutive lanes: lane j of the group scans the
+// segment's scan chunks j, j + G, ... in rounds, each taking the first start
+// in its chunk that accept() takes; after each round the group keeps the
+// lowest one found (all chunks before it held none), so the result is the
+// one seg::guess finds -- before its later-start rule, which the group's
+// first lane then runs.  A wave's time in the guess is its slowest lane's
+// (a segment that starts inside a long record scans tens of KB at about one
+// wave per SIMD); G lanes cut that lane's serial candidate iterations G-fold.
+template <int G>
+__device__ __forceinline__ uint64_t guess_group(const seg::SegArgs& a, uint32_t k, uint32_t j) {
+  using namespace seg;
+  const uint64_t b = seg_begin(a, k), e = seg_end(a, k), hop = seg_hop(a);
+  constexpr uint64_t CH = 64u * kScanBlocks;
+  const uintptr_t base = (uintptr_t)a.img;
+  const uintptr_t A0 = (base + b) & ~(uintptr_t)(CH - 1);
+  for (uint32_t r = 0;; ++r) {
+    const int64_t cs = (int64_t)(A0 + ((uint64_t)r * G + j) * CH - base);
+    const bool act = cs < (int64_t)e;
+    uint64_t f = kNoGuess;
+    if (act) {
+      const uint64_t lo = cs > (int64_t)b ? (uint64_t)cs : b;
+      const uint64_t hi = (uint64_t)(cs + (int64_t)CH) < e ? (uint64_t)(cs + (int64_t)CH) : e;
+      Scan S;
+      for (uint64_t c = next_cand(S, a.img, a.n, lo, hi); c != kNoGuess; c = next_cand(S, a.img, a.n, c + 1, hi))
+        if (accept(a.img, a.n, c, hop)) {
+          f = c;
+          break;
+        }
+    }
+    uint32_t any = act ? 1u : 0u;
+#pragma unroll
+    for (int s = 1; s < G; s <<= 1) {  // (the group's lanes run these rounds together)
+      const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)f, s), hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(f >> 32), s);
+      const uint64_t o = ((uint64_t)hi32 << 32) | lo32;
+      f = o < f ? o : f;
+      any |= (uint32_t)__shfl_xor((int)any, s);
+    }
+    if (f != kNoGuess || !any) return f;
+  }
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void wal_seg_walk_group(seg::SegArgs a) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, k = t / G, j = t % G;
+  if (k >= a.K) return;  // (the whole group)
+  if (k == 0) {
+    if (j == 0) seg::seg_forced(a, 0, a.start);
+    return;
+  }
+  uint64_t c = guess_group<G>(a, k, j);
+  if (j != 0) return;
+  if (c != seg::kNoGuess && seg::seg_later(a)) {
+    seg::Scan S;
+    c = seg::later_rule(S, a.img, a.n, c, seg::seg_end(a, k), seg::seg_later_min(a));
+  }
+  seg::seg_take_guess(a, k, c);
+}
+
 __global__ __launch_bounds__(256) void wal_seg_jterm(seg::SegArgs a) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < a.K && (a.code[k] == seg::kEnd || a.code[k] == seg::kBad))
@@ -592,8 +650,17 @@ extern "C" uint64_t lsmk_wal_seg_scan_blocks(uint32_t K) {
 }
 
 // steps 1-2: every segment's guess and walk (a round follows)
+#ifndef LSMCK_SEG_GUESS_LANES
+#define LSMCK_SEG_GUESS_LANES 4
+#endif
 extern "C" int lsmk_wal_seg_walk(const seg::SegArgs* a, hipStream_t st) {
-  hipLaunchKernelGGL(wal_seg_walk, dim3((a->K + 255) / 256), dim3(256), 0, st, *a);
+  constexpr int G = LSMCK_SEG_GUESS_LANES;
+  if (G == 1) {
+    hipLaunchKernelGGL(wal_seg_walk, dim3((a->K + 255) / 256), dim3(256), 0, st, *a);
+  } else {
+    const uint64_t threads = (uint64_t)a->K * G;
+    hipLaunchKernelGGL(wal_seg_walk_group<G>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, *a);
+  }
   return launch_err();
 }
 
