@@ -650,6 +650,9 @@ extern "C" uint64_t lsmk_wal_seg_scan_blocks(uint32_t K) {
 }
 
 // steps 1-2: every segment's guess and walk (a round follows)
+#if defined(LSMCK_SEG_CLOCK) && !defined(LSMCK_SEG_GUESS_LANES)
+#define LSMCK_SEG_GUESS_LANES 1  // (the clock marks are in the one-lane walk)
+#endif
 #ifndef LSMCK_SEG_GUESS_LANES
 #define LSMCK_SEG_GUESS_LANES 4
 #endif
