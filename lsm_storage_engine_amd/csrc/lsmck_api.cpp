@@ -1341,8 +1341,8 @@ static int wal_crc_part(lsmck_ctx* ctx, const uint8_t* img, size_t at, size_t m,
 // done: records [0, done) are already in the caller's array (the split
 // replay's first part, from ctx->h_wrecs1); the rest land in ctx->h_wrecs.
 // pack_from: records [pack_from, m) have packed CRC spans (the segment walk's
-// emit, seg::Pack): their compare takes the next header out of each CRC and
-// reads the stored CRCs from the records.
+// emit, seg::Pack): their expected CRCs are the spans' (seg::pack_crc), and a
+// bad one's computed CRC is taken back to its payload's for the report.
 static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t term, uint64_t badq,
                       lsmck_wal_rec* recs, size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc,
                       uint32_t* bad_expected, hipStream_t st, const WalTrace& tr, size_t done = 0,
@@ -1396,11 +1396,7 @@ static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t ter
     }
     HIPCHK(hipMemsetAsync(ctx->d_verify, 0, 8, st));         // n_bad
     HIPCHK(hipMemsetAsync(ctx->d_verify + 1, 0xFF, 8, st));  // first_bad = ~0
-    const size_t plain = std::min(m, pack_from);
-    rc = lsmk_launch_crc32_compare(ctx->d_vcrc, ctx->d_wexp, plain, ctx->d_verify, ctx->d_verify + 1, st);
-    if (!rc && plain < m)
-      rc = lsmk_wal_compare_packed(ctx->d_vcrc, ctx->wal_recs_dev_emitted ? ctx->wal_recs_dev : W.recs, plain, m,
-                                   ctx->d_verify, ctx->d_verify + 1, st);
+    rc = lsmk_launch_crc32_compare(ctx->d_vcrc, ctx->d_wexp, m, ctx->d_verify, ctx->d_verify + 1, st);
     if (rc) {
       if (copy_out) (void)hipEventSynchronize(ctx->wal_recs_ev);
       return launch_rc(rc, "compare kernel");
@@ -1430,6 +1426,20 @@ static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t ter
     else
       HIPCHK(hipMemcpy(&r, W.recs + first, sizeof r, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(&got, ctx->d_vcrc + first, 4, hipMemcpyDeviceToHost));
+    if (first >= pack_from && first + 1 < m) {  // a packed span's CRC: the next header taken back out
+      namespace sg = lsmck::seg;
+      lsmck_wal_rec rn;
+      HIPCHK(hipMemcpy(&rn, (ctx->wal_recs_dev && ctx->wal_recs_dev_emitted ? recs : W.recs) + first + 1, sizeof rn,
+                       hipMemcpyDeviceToHost));
+      if (sg::pack_fits(r.klen + r.vlen, sg::hdr_len(rn.type))) {
+        sg::Head nh{};
+        nh.t = rn.type;
+        nh.crc = rn.crc;
+        nh.klen = rn.klen;
+        nh.vlen = rn.vlen;
+        got = sg::unpack_crc(got, nh, lsmck_host::crc_tables());
+      }
+    }
     if (bad_index) *bad_index = first;
     if (bad_expected) *bad_expected = r.crc;
     if (bad_crc) *bad_crc = got;
@@ -1635,7 +1645,7 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
       return rc;
     lsmck_wal_rec* to = dev ? ctx->wal_recs_dev : W.recs;
     if (ctx->wal_seg_pack) {
-      rc = lsmk_wal_seg_emit_packed(&a, at, to, ctx->d_woff, ctx->d_wlen, tot, st);
+      rc = lsmk_wal_seg_emit_packed(&a, at, to, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, tot, st);
     } else {
       rc = lsmk_wal_seg_emit(&a, at, to, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st);
     }

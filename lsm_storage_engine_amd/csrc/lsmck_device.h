@@ -101,11 +101,9 @@ int lsmk_wal_seg_repair(const lsmck::seg::SegArgs* a, uint32_t budget, hipStream
 int lsmk_wal_seg_emit(const lsmck::seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff, uint32_t* plen,
                       uint32_t* pcrc, hipStream_t st);
 int lsmk_wal_seg_emit_packed(const lsmck::seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff,
-                             uint32_t* plen, uint64_t iend, hipStream_t st);
+                             uint32_t* plen, uint32_t* pcrc, uint64_t iend, hipStream_t st);
 int lsmk_wal_seg_place(const lsmck::seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff, uint32_t* plen,
                        uint32_t* pcrc, uint64_t iend, int packed, hipStream_t st);
-int lsmk_wal_compare_packed(uint32_t* crc, const lsmck_wal_rec* recs, uint64_t i0, uint64_t m,
-                            unsigned long long* n_bad, unsigned long long* first_bad, hipStream_t st);
 int lsmk_launch_crc32_compare(const uint32_t* crc, const uint32_t* expected, uint64_t n,
                                unsigned long long* n_bad, unsigned long long* first_bad, hipStream_t st);
 int lsmk_sha_order(const uint32_t* len, size_t n, uint16_t* keys_out, uint32_t* order, void* tmp, size_t* tmp_bytes,

@@ -623,11 +623,13 @@ LSMCK_HD uint32_t hdr_reg(const Head& h, const uint32_t* T) {
 // the log and the stream kernel runs on them as on config 3's packed objects.
 // The last record of the emit (iend: at + records walked) keeps its payload
 // alone, and so does a payload within a header of 4 GiB (pack_fits).  The
-// header comes back out of the CRC by linearity (unpack_crc): the compare
-// reads it from record i+1's fields.  The stored CRCs (pcrc) are not written:
-// the compare reads them from the records too.
+// expected CRC written for a packed span is the stored CRC carried over the
+// next header by linearity (pack_crc), so the compare is the plain one; a
+// bad record's computed CRC is taken back to its payload's (unpack_crc) for
+// the report.
 struct Pack {
   uint64_t iend;
+  const uint32_t* T;  // CRC-32 slicing tables T0..T3 (hdr_reg)
 };
 LSMCK_HD bool pack_fits(uint32_t got, uint32_t hl) { return got <= 0xFFFFFFFFu - hl; }
 
@@ -645,6 +647,12 @@ LSMCK_HD uint32_t gf2_mul(uint32_t c, uint32_t b) {
 // x^-104 and x^-72 the constants (tests/test_segwalk_model.py checks them).
 LSMCK_HD uint32_t unpack_crc(uint32_t c, const Head& nh, const uint32_t* T) {
   return ~gf2_mul(~c ^ hdr_reg(nh, T), nh.t == 1 ? 0x525983aau : 0x2fb98a7du);
+}
+// ... and the other way: what crc(P | H) is when crc(P) is the stored CRC
+// `crc` -- the expected value the emit writes for a packed span, so that the
+// compare is the plain one:  ~( x^(8|H|) * ~crc ^ hdr_reg(H) ),  x^104 / x^72.
+LSMCK_HD uint32_t pack_crc(uint32_t crc, const Head& nh, const uint32_t* T) {
+  return ~(gf2_mul(~crc, nh.t == 1 ? 0xe6050901u : 0x1eb014d8u) ^ hdr_reg(nh, T));
 }
 
 // step 4 for segment k (after the check passed): its records at `at` + its
@@ -667,14 +675,18 @@ LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint
   uint64_t i = at + (a.pre[k] & kRecMask) + r;
   const uint8_t* img = a.img;
   uint64_t pi = ~0ull;  // packed: the previous record, its span closed by this one's header
-  uint32_t pgot = 0;
+  uint32_t pgot = 0, pcv = 0;
   for (; r < rend && p < pend; ++r, ++i) {
     const Head h = head(img, a.n, p);
     const uint32_t hl = hdr_len(h.t);
     const uint32_t dlen = h.klen + h.vlen;
     const uint64_t avail = a.n - (p + hl);
     const uint32_t got = dlen <= avail ? dlen : (uint32_t)avail;
-    if (pk && pi != ~0ull) plen[pi] = pack_fits(pgot, hl) ? pgot + hl : pgot;
+    if (pk && pi != ~0ull) {
+      const bool fit = pack_fits(pgot, hl);
+      plen[pi] = fit ? pgot + hl : pgot;
+      pcrc[pi] = fit ? pack_crc(pcv, h, pk->T) : pcv;
+    }
     Rec R;
     R.rec_off = p;
     R.payload_off = p + hl;
@@ -687,6 +699,7 @@ LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint
     if (pk) {
       pi = i;
       pgot = got;
+      pcv = h.crc;
     } else {
       plen[i] = got;
       pcrc[i] = h.crc;
@@ -694,21 +707,27 @@ LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint
     p += hl + got;
   }
   if (pk && pi != ~0ull) {  // the last record here: the next one's header is at p (another thread's first)
-    uint32_t hl = 0;
-    if (i < pk->iend) hl = hdr_len(head(img, a.n, p).t);
-    plen[pi] = hl && pack_fits(pgot, hl) ? pgot + hl : pgot;
+    bool fit = false;
+    Head h{};
+    if (i < pk->iend) {
+      h = head(img, a.n, p);
+      fit = pack_fits(pgot, hdr_len(h.t));
+    }
+    plen[pi] = fit ? pgot + hdr_len(h.t) : pgot;
+    pcrc[pi] = fit ? pack_crc(pcv, h, pk->T) : pcv;
   }
 }
 
 // Record r of staged segment k (every record it walked fit its slots), R
 // its staged form: the record to `at` + its place, its CRC span -- packed
-// (pk) or the payload alone -- and, unpacked, its stored CRC.  nt: the type
-// byte of the record after it (the next slot's, or the byte at the segment's
-// exit for its last record), read only when the walk has a record after it.
-// The payload is cut at EOF only for the walk's last record.
+// (pk; its expected CRC then pack_crc's) or the payload alone -- and its
+// expected CRC.  nh: the header of the record after it (the next slot's, or
+// the one at the segment's exit for its last record), used only when the
+// walk has a record after it.  The payload is cut at EOF only for the walk's
+// last record.
 template <class Rec>
 LSMCK_HD void seg_place_rec(const SegArgs& a, uint32_t k, uint64_t at, Rec* recs, uint64_t* poff, uint32_t* plen,
-                            uint32_t* pcrc, uint32_t r, const StageRec& R, uint32_t nt, const Pack* pk) {
+                            uint32_t* pcrc, uint32_t r, const StageRec& R, const Head& nh, const Pack* pk) {
   const uint64_t i = at + (a.pre[k] & kRecMask) + r;
   Rec O;
   O.rec_off = R.rec_off;
@@ -722,17 +741,22 @@ LSMCK_HD void seg_place_rec(const SegArgs& a, uint32_t k, uint64_t at, Rec* recs
   const uint32_t dlen = R.klen + R.vlen;
   const uint64_t avail = a.n - R.payload_off;
   const uint32_t got = dlen <= avail ? dlen : (uint32_t)avail;
-  if (pk) {
-    const uint32_t hl = i + 1 < pk->iend ? hdr_len(nt) : 0u;
-    plen[i] = hl && pack_fits(got, hl) ? got + hl : got;
-  } else {
-    plen[i] = got;
-    pcrc[i] = R.crc;
-  }
+  const bool fit = pk && i + 1 < pk->iend && pack_fits(got, hdr_len(nh.t));
+  plen[i] = fit ? got + hdr_len(nh.t) : got;
+  pcrc[i] = fit ? pack_crc(R.crc, nh, pk->T) : R.crc;
 }
-// the next record's type byte for record r of staged segment k (see above)
-LSMCK_HD uint32_t seg_place_next_type(const SegArgs& a, uint32_t k, uint32_t r) {
-  return r + 1 < a.recs[k] ? a.srec[(uint64_t)k * a.scap + r + 1].type : (uint32_t)a.img[a.x[k]];
+// the header of the record after record r of staged segment k (see above)
+LSMCK_HD Head seg_place_next_head(const SegArgs& a, uint32_t k, uint32_t r) {
+  if (r + 1 < a.recs[k]) {
+    const StageRec& N = a.srec[(uint64_t)k * a.scap + r + 1];
+    Head h{};
+    h.t = N.type;
+    h.crc = N.crc;
+    h.klen = N.klen;
+    h.vlen = N.vlen;
+    return h;
+  }
+  return head(a.img, a.n, a.x[k]);
 }
 
 }  // namespace seg

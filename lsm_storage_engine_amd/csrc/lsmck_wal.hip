@@ -524,57 +524,9 @@ __global__ __launch_bounds__(256) void wal_seg_emit(seg::SegArgs a, uint64_t at,
   if (k < a.K) seg::seg_emit_thread(a, k, (uint32_t)a.info[seg::kInfoJterm], at, recs, poff, plen, pcrc, j);
 }
 
-// The same with packed CRC spans (seg::Pack): span lengths only, no stored CRCs.
-__global__ __launch_bounds__(256) void wal_seg_emit_packed(seg::SegArgs a, uint64_t at, lsmck_wal_rec* __restrict__ recs,
-                                                            uint64_t* __restrict__ poff, uint32_t* __restrict__ plen,
-                                                            uint64_t iend) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t k = (uint32_t)(t / a.nsub), j = (uint32_t)(t % a.nsub);
-  const seg::Pack pk{iend};
-  if (k < a.K)
-    seg::seg_emit_thread(a, k, (uint32_t)a.info[seg::kInfoJterm], at, recs, poff, plen, (uint32_t*)nullptr, j, &pk);
-}
-
-// The staged segments' records out (seg::seg_place_rec): one wave per
-// segment, four per workgroup, its slots read in order -- instead of the
-// second walk of the headers seg_emit_thread makes for a segment with more
-// records than slots.  A lane takes the next record's type from the next
-// lane (lane 63 and the segment's last record read it).
-template <bool PACK>
-__global__ __launch_bounds__(256) void wal_seg_place(seg::SegArgs a, uint64_t at, lsmck_wal_rec* __restrict__ recs,
-                                                     uint64_t* __restrict__ poff, uint32_t* __restrict__ plen,
-                                                     uint32_t* __restrict__ pcrc, uint64_t iend) {
-  const uint32_t k = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
-  if (k >= a.K) return;
-  const uint32_t jterm = (uint32_t)a.info[seg::kInfoJterm];
-  if (k > jterm || a.code[k] == seg::kNone) return;
-  const uint32_t cnt = a.recs[k];
-  if (cnt > a.scap) return;  // (emitted by wal_seg_emit*)
-  const seg::StageRec* st = a.srec + (uint64_t)k * a.scap;
-  const uint64_t i0 = at + (a.pre[k] & seg::kRecMask);
-  const seg::Pack pk{iend};
-  for (uint32_t r0 = 0; r0 < cnt; r0 += 64u) {  // (wave-uniform)
-    const uint32_t r = r0 + lane;
-    seg::StageRec R{};
-    if (r < cnt) R = st[r];
-    uint32_t nt = __shfl_down(R.type, 1);
-    if (r < cnt && (lane == 63u || r + 1u == cnt) && i0 + r + 1u < iend) nt = seg::seg_place_next_type(a, k, r);
-    if (r < cnt) seg::seg_place_rec(a, k, at, recs, poff, plen, pcrc, r, R, nt, PACK ? &pk : nullptr);
-  }
-}
-
-// The compare over packed spans, records [i0, m) of recs (the emit's): record
-// i's CRC (of [payload_i | header_i+1) unless i is the last or its span did
-// not fit) back to its payload's by seg::unpack_crc with header i+1 read from
-// record i+1's fields, against the stored CRC in record i.  A mismatch counts
-// as crc32_compare_kernel's do and writes the payload's CRC back (the bad
-// record's report reads it).  The CRC-32 slicing tables T0..T3 in LDS first
-// (T0 bitwise, Tk[b] = T(k-1)[b] >> 8 ^ T0[T(k-1)[b] & 0xFF]).
-__global__ __launch_bounds__(256) void wal_compare_packed(uint32_t* __restrict__ crc,
-                                                          const lsmck_wal_rec* __restrict__ recs, uint64_t i0,
-                                                          uint64_t m, unsigned long long* __restrict__ n_bad,
-                                                          unsigned long long* __restrict__ first_bad) {
-  __shared__ uint32_t T[1024];
+// the CRC-32 slicing tables T0..T3 in LDS (T0 bitwise, Tk[b] = T(k-1)[b] >> 8
+// ^ T0[T(k-1)[b] & 0xFF]), by a 256-thread block, for seg::hdr_reg
+__device__ __forceinline__ void build_crc_tables(uint32_t* T) {
   const uint32_t b = threadIdx.x;
   uint32_t c = b;
 #pragma unroll
@@ -587,43 +539,54 @@ __global__ __launch_bounds__(256) void wal_compare_packed(uint32_t* __restrict__
     T[q * 256 + b] = c;
   }
   __syncthreads();
-  // a wave's 64 lanes take 64 consecutive records: each loads its record's
-  // klen, vlen, crc, type (one 16-byte load) and takes record i+1's from the
-  // next lane (lane 63 loads it).  A record with a successor was not cut at
-  // EOF: its span's payload is klen + vlen bytes.
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint32_t lane = threadIdx.x & 63u;
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  unsigned long long bad = 0, first = ~0ull;
-  for (uint64_t w = i0 + (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); w < m; w += stride) {
-    const uint64_t i = w + lane;
-    u32x4 f = {0u, 0u, 0u, 0u};
-    if (i < m) f = *(const u32x4*)&recs[i].klen;
+}
+
+// The same with packed CRC spans (seg::Pack): the expected CRC of each span
+// from its record's stored CRC and the next header (seg::pack_crc).
+__global__ __launch_bounds__(256) void wal_seg_emit_packed(seg::SegArgs a, uint64_t at, lsmck_wal_rec* __restrict__ recs,
+                                                            uint64_t* __restrict__ poff, uint32_t* __restrict__ plen,
+                                                            uint32_t* __restrict__ pcrc, uint64_t iend) {
+  __shared__ uint32_t T[1024];
+  build_crc_tables(T);
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = (uint32_t)(t / a.nsub), j = (uint32_t)(t % a.nsub);
+  const seg::Pack pk{iend, T};
+  if (k < a.K) seg::seg_emit_thread(a, k, (uint32_t)a.info[seg::kInfoJterm], at, recs, poff, plen, pcrc, j, &pk);
+}
+
+// The staged segments' records out (seg::seg_place_rec): one wave per
+// segment, four per workgroup, its slots read in order -- instead of the
+// second walk of the headers seg_emit_thread makes for a segment with more
+// records than slots.  A lane takes the next record's header fields from the
+// next lane (lane 63 and the segment's last record read them).
+template <bool PACK>
+__global__ __launch_bounds__(256) void wal_seg_place(seg::SegArgs a, uint64_t at, lsmck_wal_rec* __restrict__ recs,
+                                                     uint64_t* __restrict__ poff, uint32_t* __restrict__ plen,
+                                                     uint32_t* __restrict__ pcrc, uint64_t iend) {
+  __shared__ uint32_t T[1024];
+  if (PACK) build_crc_tables(T);
+  const uint32_t k = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (k >= a.K) return;
+  const uint32_t jterm = (uint32_t)a.info[seg::kInfoJterm];
+  if (k > jterm || a.code[k] == seg::kNone) return;
+  const uint32_t cnt = a.recs[k];
+  if (cnt > a.scap) return;  // (emitted by wal_seg_emit*)
+  const seg::StageRec* st = a.srec + (uint64_t)k * a.scap;
+  const uint64_t i0 = at + (a.pre[k] & seg::kRecMask);
+  const seg::Pack pk{iend, T};
+  for (uint32_t r0 = 0; r0 < cnt; r0 += 64u) {  // (wave-uniform)
+    const uint32_t r = r0 + lane;
+    seg::StageRec R{};
+    if (r < cnt) R = st[r];
     seg::Head nh{};
-    nh.klen = __shfl_down(f.x, 1);
-    nh.vlen = __shfl_down(f.y, 1);
-    nh.crc = __shfl_down(f.z, 1);
-    nh.t = __shfl_down(f.w, 1);
-    if (lane == 63u && i + 1 < m) {
-      const u32x4 g = *(const u32x4*)&recs[i + 1].klen;
-      nh.klen = g.x;
-      nh.vlen = g.y;
-      nh.crc = g.z;
-      nh.t = g.w;
+    if (PACK) {
+      nh.t = __shfl_down(R.type, 1);
+      nh.crc = __shfl_down(R.crc, 1);
+      nh.klen = __shfl_down(R.klen, 1);
+      nh.vlen = __shfl_down(R.vlen, 1);
+      if (r < cnt && (lane == 63u || r + 1u == cnt) && i0 + r + 1u < iend) nh = seg::seg_place_next_head(a, k, r);
     }
-    if (i < m) {
-      uint32_t v = crc[i];
-      if (i + 1 < m && seg::pack_fits(f.x + f.y, seg::hdr_len(nh.t))) v = seg::unpack_crc(v, nh, T);
-      if (v != f.z) {
-        ++bad;
-        if (i < first) first = i;
-        crc[i] = v;
-      }
-    }
-  }
-  if (bad) {
-    atomicAdd(n_bad, bad);
-    atomicMin(first_bad, first);
+    if (r < cnt) seg::seg_place_rec(a, k, at, recs, poff, plen, pcrc, r, R, nh, PACK ? &pk : nullptr);
   }
 }
 
@@ -696,10 +659,10 @@ extern "C" int lsmk_wal_seg_emit(const seg::SegArgs* a, uint64_t at, lsmck_wal_r
 }
 
 extern "C" int lsmk_wal_seg_emit_packed(const seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff,
-                                        uint32_t* plen, uint64_t iend, hipStream_t st) {
+                                        uint32_t* plen, uint32_t* pcrc, uint64_t iend, hipStream_t st) {
   const uint64_t threads = (uint64_t)a->K * a->nsub;
   hipLaunchKernelGGL(wal_seg_emit_packed, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, *a, at, recs, poff,
-                     plen, iend);
+                     plen, pcrc, iend);
   return launch_err();
 }
 
@@ -712,14 +675,6 @@ extern "C" int lsmk_wal_seg_place(const seg::SegArgs* a, uint64_t at, lsmck_wal_
   else
     hipLaunchKernelGGL(wal_seg_place<false>, dim3((a->K + 3u) / 4u), dim3(256), 0, st, *a, at, recs, poff, plen, pcrc,
                        iend);
-  return launch_err();
-}
-
-extern "C" int lsmk_wal_compare_packed(uint32_t* crc, const lsmck_wal_rec* recs, uint64_t i0, uint64_t m,
-                                       unsigned long long* n_bad, unsigned long long* first_bad, hipStream_t st) {
-  if (m <= i0) return 0;
-  const uint64_t blocks = (m - i0 + 255) / 256 < 8192 ? (m - i0 + 255) / 256 : 8192;
-  hipLaunchKernelGGL(wal_compare_packed, dim3((unsigned)blocks), dim3(256), 0, st, crc, recs, i0, m, n_bad, first_bad);
   return launch_err();
 }
 

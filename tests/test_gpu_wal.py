@@ -433,7 +433,7 @@ def test_segment_walk(ctx, seg_opts, seg, shift):
 @pytest.mark.parametrize("seg", [0, 512, 262144])
 def test_segment_walk_packed_spans(ctx, seg_opts, pack, seg, stage):
     """The CRC pass over packed spans ([payload | next header), the headers
-    taken back out by wal_compare_packed) against payload-only spans: empty keys
+    carried into the expected CRCs, seg::pack_crc) against payload-only spans: empty keys
     and values (spans of a header alone), Removes next to Inserts, a corrupted
     payload and header CRC (the computed CRC it reports is the payload's own),
     and a log cut inside the last payload (its span the payload alone).

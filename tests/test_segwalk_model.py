@@ -66,21 +66,21 @@ def sim(tmp_path_factory):
     run.set_nsub = lib.segwalk_sim_set_nsub
     lib.segwalk_sim_set_stage.argtypes = [C.c_uint32]
     run.set_stage = lib.segwalk_sim_set_stage
-    lib.segwalk_sim_pack.argtypes = [u64p, C.POINTER(C.c_uint32), C.c_size_t]
+    lib.segwalk_sim_pack.argtypes = [u64p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_size_t]
     lib.segwalk_sim_unpack.restype = C.c_uint32
     lib.segwalk_sim_unpack.argtypes = [C.c_uint32] * 5
 
     def packed(img, S):
-        """the walk's packed CRC spans (seg::Pack): (offs, lens)"""
+        """the walk's packed CRC spans (seg::Pack): (offs, lens, expected CRCs)"""
         cap = len(img) // 9 + 2
-        po, pl = (C.c_uint64 * cap)(), (C.c_uint32 * cap)()
-        lib.segwalk_sim_pack(po, pl, cap)
+        po, pl, pe = (C.c_uint64 * cap)(), (C.c_uint32 * cap)(), (C.c_uint32 * cap)()
+        lib.segwalk_sim_pack(po, pl, pe, cap)
         try:
             res = run(img, S)
         finally:
-            lib.segwalk_sim_pack(None, None, 0)
+            lib.segwalk_sim_pack(None, None, None, 0)
         m = len(res[0])
-        return list(po[:m]), list(pl[:m])
+        return list(po[:m]), list(pl[:m]), list(pe[:m])
     run.unpack = lib.segwalk_sim_unpack
     run.packed = packed
     return run
@@ -313,8 +313,8 @@ def _mulmod(a, b):
 
 
 def test_unpack_constants():
-    """wal_crc_unpack's constants are x^-72 and x^-104 mod P(x): times x^72
-    (x^104) they give x^0."""
+    """unpack_crc's constants are x^-72 and x^-104 mod P(x): times x^72
+    (x^104) they give x^0; pack_crc's are x^104 and x^72."""
     x8inv = 0x6567cb95  # x^-8: times x^8 (bit 23) is x^0 (bit 31)
     assert _mulmod(x8inv, 1 << 23) == 1 << 31
     r = 1 << 31
@@ -323,6 +323,13 @@ def test_unpack_constants():
         r = _mulmod(r, x8inv)
         pw[k] = r
     assert pw[9] == 0x2fb98a7d and pw[13] == 0x525983aa
+    x8 = 1 << 23
+    r = 1 << 31
+    for k in range(1, 14):
+        r = _mulmod(r, x8)
+        if k == 9:
+            assert r == 0x1eb014d8
+    assert r == 0xe6050901
 
 
 @pytest.mark.parametrize("stage", [0, 3, 100000])
@@ -348,7 +355,7 @@ def test_packed_crc_spans(sim, S, nsub, stage):
             bad[want0[len(want0) // 2]] = 0x55
             for im in (img, bytes(cut), bytes(bad)):
                 offs, _, _ = chain(im)
-                po, pl = sim.packed(im, S)
+                po, pl, pe = sim.packed(im, S)
                 assert len(po) == len(offs)
                 for i, q in enumerate(offs):
                     hl = 13 if im[q] == 1 else 9
@@ -358,6 +365,18 @@ def test_packed_crc_spans(sim, S, nsub, stage):
                     plen = min((klen + vlen) & M, len(im) - q - hl)
                     assert po[i] == q + hl
                     span = zlib.crc32(im[po[i]:po[i] + pl[i]])
+                    stored = struct.unpack_from("<I", im, q + 1)[0]
+                    if i + 1 < len(offs):  # pack_crc: the stored CRC carried over the next header
+                        nq = offs[i + 1]
+                        nh = 13 if im[nq] == 1 else 9
+                        g = ~zlib.crc32(im[nq:nq + nh], M) & M
+                        want = ~(_mulmod(~stored & M, 0xe6050901 if nh == 13 else 0x1eb014d8) ^ g) & M
+                        assert pe[i] == want, i
+                        # ... which is the span's CRC exactly when the stored one is the payload's
+                        pay = zlib.crc32(im[q + hl:q + hl + plen])
+                        assert ~(_mulmod(~pay & M, 0xe6050901 if nh == 13 else 0x1eb014d8) ^ g) & M == span
+                    else:
+                        assert pe[i] == stored
                     if i + 1 < len(offs):
                         nq = offs[i + 1]
                         nh = 13 if im[nq] == 1 else 9

@@ -27,18 +27,19 @@ extern "C" void segwalk_sim_set_nsub(uint32_t v) { g_nsub = v ? v : 1; }
 static uint32_t g_scap = 0;  // walk-time staging: slots per segment (0 = none)
 extern "C" void segwalk_sim_set_stage(uint32_t v) { g_scap = v; }
 // packed CRC spans (seg::Pack): when set, the next walk emits them here --
-// span offsets and lengths
+// span offsets, lengths and expected CRCs
 static uint64_t* g_poff = nullptr;
-static uint32_t* g_plen = nullptr;
+static uint32_t *g_plen = nullptr, *g_pexp = nullptr;
 static size_t g_pcap = 0;
-extern "C" void segwalk_sim_pack(uint64_t* poff, uint32_t* plen, size_t cap) {
+extern "C" void segwalk_sim_pack(uint64_t* poff, uint32_t* plen, uint32_t* pexp, size_t cap) {
   g_poff = poff;
   g_plen = plen;
+  g_pexp = pexp;
   g_pcap = poff ? cap : 0;
 }
 // seg::unpack_crc with wal_compare_packed's tables: the payload CRC from a
 // packed span's CRC c and the next header's fields
-static const uint32_t* crc_tables4() {  // T0..T3, as wal_compare_packed builds them in LDS
+static const uint32_t* crc_tables4() {  // T0..T3, as build_crc_tables (lsmck_wal.hip) makes them in LDS
   static uint32_t T[1024];
   static bool done = false;
   if (!done) {
@@ -128,7 +129,7 @@ extern "C" int segwalk_sim_prefix(const uint8_t* img, uint64_t n, uint64_t start
   std::vector<SimRec> R(m);
   std::vector<uint64_t> poff(m);
   std::vector<uint32_t> plen(m), pcrc(m);
-  const sg::Pack pk{m};
+  const sg::Pack pk{m, crc_tables4()};
   for (uint32_t k = 0; k < K; ++k)
     for (uint32_t j = 0; j < a.nsub; ++j)
       sg::seg_emit_thread(a, k, (uint32_t)info[sg::kInfoJterm], 0, R.data(), poff.data(), plen.data(), pcrc.data(), j,
@@ -138,14 +139,15 @@ extern "C" int segwalk_sim_prefix(const uint8_t* img, uint64_t n, uint64_t start
     if (k <= jt && code[k] != sg::kNone && recs[k] <= scap)
       for (uint32_t r = 0; r < recs[k]; ++r) {
         const uint64_t i = (pre[k] & sg::kRecMask) + r;
-        const uint32_t nt = i + 1 < m ? sg::seg_place_next_type(a, k, r) : 0u;
-        sg::seg_place_rec(a, k, 0, R.data(), poff.data(), plen.data(), pcrc.data(), r, st[(size_t)k * scap + r], nt,
+        const sg::Head nh = i + 1 < m ? sg::seg_place_next_head(a, k, r) : sg::Head{};
+        sg::seg_place_rec(a, k, 0, R.data(), poff.data(), plen.data(), pcrc.data(), r, st[(size_t)k * scap + r], nh,
                           g_pcap ? &pk : nullptr);
       }
   for (uint64_t i = 0; i < m && i < cap; ++i) rec_off[i] = R[i].rec_off;
   for (uint64_t i = 0; i < m && i < g_pcap; ++i) {
     g_poff[i] = poff[i];
     g_plen[i] = plen[i];
+    g_pexp[i] = pcrc[i];
   }
   return 0;
 }
