@@ -236,6 +236,12 @@ int lsmck_device_count(void);
  *                 they need no second walk of the headers: 1 = auto slots
  *                 per segment (default), 0 = off (A/B), N >= 2 = N slots
  *                 (tests).  A segment with more records is walked again.
+ *   "wal_dma_engines"  device replays whose records go to the host: the
+ *                 read-back is dealt over this many SDMA engines through HSA
+ *                 (default 4; 1..16), beside the CRC pass and off the compute
+ *                 units; 0 = hipMemcpyAsync on a staging stream (A/B).
+ *   "wal_dma_chunks"  ... cut in this many pieces (default 32; 1..64); a
+ *                 pageable records array is filled piece by piece as they land.
  * Returns 0, or LSMCK_EINVAL for an unknown key / value. */
 int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
 
@@ -246,6 +252,8 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
  *                    3 = host walk.
  *   "wal_seg_repairs"  its segment walk's repaired check failures.
  *   "wal_segments"   its segment walk's segment count.
+ *   "wal_recs_dma"   its records' read-back to the host: the SDMA engines it
+ *                    was dealt over, 0 = hipMemcpyAsync (or none read back).
  *   "numa_node"      the device's NUMA node (sysfs of its PCI function; -1
  *                    unknown), and "stage_numa_node" the node the context's
  *                    pinned buffers and copy threads are placed on (-1: none).
@@ -332,6 +340,26 @@ typedef struct {
 int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsigned flags, lsmck_wal_rec* recs,
                             size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc,
                             uint32_t* bad_expected);
+
+/* The same replay with compact records: 16 bytes each instead of 32 -- what
+ * MemTable::from_log takes from a record (src/memtable.rs:28-47: the key and
+ * value bytes and the command type).  The header offset is payload_off less
+ * the header (13 bytes for Insert, 9 for Remove), and the stored CRC is not
+ * kept: every accepted record's stored CRC equals its payload's CRC (a bad
+ * one's comes back in *bad_expected).  Half the bytes cross the link when
+ * the records go to the host (LSMCK_RECS_PINNED or a pageable array); with
+ * LSMCK_RECS_DEVICE `recs` is a device array of lsmck_wal_rec16.  Flags,
+ * returns and the other outputs as lsmck_wal_replay_verify.  Replaces the
+ * same reference items. */
+typedef struct {
+  uint64_t payload_type; /* bits 0..62: payload (key) offset; bit 63: set for Remove, clear for Insert */
+  uint32_t klen, vlen;   /* vlen = 0 for Remove */
+} lsmck_wal_rec16;
+#define LSMCK_WAL_REC16_REMOVE 0x8000000000000000ull
+#define LSMCK_WAL_REC16_OFF_MASK 0x7FFFFFFFFFFFFFFFull
+int lsmck_wal_replay_verify16(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsigned flags, lsmck_wal_rec16* recs,
+                              size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc,
+                              uint32_t* bad_expected);
 
 /* Batch framing of Insert records in a device-resident log, in place: payload
  * i (key || value, len[i] bytes) already lies at img + off[i], and its

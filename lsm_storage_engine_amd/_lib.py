@@ -57,6 +57,14 @@ class WalRec(C.Structure):
                 ("vlen", C.c_uint32), ("crc", C.c_uint32), ("type", C.c_uint32)]
 
 
+class WalRec16(C.Structure):
+    """lsmck_wal_rec16: payload offset with the type in bit 63 (set: Remove), klen, vlen."""
+    _fields_ = [("payload_type", C.c_uint64), ("klen", C.c_uint32), ("vlen", C.c_uint32)]
+
+
+WAL_REC16_REMOVE = 1 << 63
+
+
 class TreeReport(C.Structure):
     _fields_ = [("tables", C.c_uint64), ("table_bytes", C.c_uint64), ("bad_tables", C.c_uint64),
                 ("first_index", C.c_uint64), ("first_status", C.c_int), ("reserved", C.c_int),
@@ -102,6 +110,8 @@ SIGNATURES = [
     ("lsmck_sha256_batch_fixed", C.c_int, [vp, vp, sz, C.c_uint32, sz, vp, C.c_uint, vp]),
     ("lsmck_wal_replay_verify", C.c_int,
      [vp, vp, sz, C.c_uint, vp, sz, C.POINTER(sz), u64p, u32p, u32p]),  # recs: lsmck_wal_rec[cap]
+    ("lsmck_wal_replay_verify16", C.c_int,
+     [vp, vp, sz, C.c_uint, vp, sz, C.POINTER(sz), u64p, u32p, u32p]),  # recs: lsmck_wal_rec16[cap]
     ("lsmck_wal_frame_insert_device", C.c_int, [vp, vp, vp, vp, vp, sz, C.c_uint32, vp]),
     ("lsmck_checksums_verify_many", C.c_int,
      [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), sz, C.POINTER(C.c_int)]),

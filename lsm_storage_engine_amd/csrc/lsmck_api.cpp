@@ -38,6 +38,7 @@
 
 #include "lsmck.h"
 #include "lsmck_device.h"
+#include "lsmck_dma.h"
 #include "lsmck_internal.h"
 #include "lsmck_pool.h"
 #include "lsmck_segwalk.h"
@@ -92,14 +93,6 @@ int ensure_dev(T** p, size_t* cap, size_t need) {
 // On a node with several sockets each GPU hangs off one socket's PCIe root;
 // pinned staging on the other socket's memory, or copy threads on its cores,
 // cross the socket link on the way to the device.
-constexpr int kMaxDevs = 64;
-std::atomic<int> g_pin_node[kMaxDevs];  // per device: the node its pinned buffers go to (-1: HIP's choice)
-struct PinNodeInit {
-  PinNodeInit() {
-    for (auto& v : g_pin_node) v.store(-1);
-  }
-} g_pin_node_init;
-
 int read_int_file(const std::string& path, int dflt) {
   FILE* f = fopen(path.c_str(), "r");
   if (!f) return dflt;
@@ -143,13 +136,10 @@ bool node_cpus(int node, cpu_set_t* set) {
   return n > 0;
 }
 constexpr int kMpolDefault = 0, kMpolPreferred = 1;
-// pinned host memory, on the current device's node when one is set: the
+// pinned host memory, on NUMA node `node` when one is given (the context's pin_node): the
 // calling thread's policy prefers that node while HIP allocates and pins
 // the pages (hipHostMallocNumaUser), then goes back to what it was
-hipError_t host_malloc_near(void** p, size_t bytes) {
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  const int node = dev >= 0 && dev < kMaxDevs ? g_pin_node[dev].load() : -1;
+hipError_t host_malloc_near(void** p, size_t bytes, int node) {
   if (node < 0 || node >= 1024) return hipHostMalloc(p, bytes, hipHostMallocDefault);
   int old_mode = kMpolDefault;
   unsigned long old_mask[16] = {0};
@@ -168,14 +158,14 @@ hipError_t host_malloc_near(void** p, size_t bytes) {
 }
 
 template <typename T>
-int ensure_pinned(T** p, size_t* cap, size_t need) {
+int ensure_pinned(int node, T** p, size_t* cap, size_t need) {
   if (*cap >= need && *p) return 0;
   size_t want = std::max(need, *cap * 3 / 2);
   if (want == 0) want = 1;
   if (*p) (void)hipHostFree(*p);
   *p = nullptr;
   *cap = 0;
-  HIPCHK(host_malloc_near((void**)p, want * sizeof(T)));
+  HIPCHK(host_malloc_near((void**)p, want * sizeof(T), node));
   *cap = want;
   return 0;
 }
@@ -319,6 +309,8 @@ struct lsmck_ctx {
     size_t cap_chain = 0;
     lsmck_wal_rec* recs = nullptr;
     size_t cap_recs = 0;
+    lsmck::seg::Compact16* recs16 = nullptr;  // the records in the compact layout (lsmck_wal_replay_verify16)
+    size_t cap_recs16 = 0;
     unsigned long long* info = nullptr;  // [records, terminal, bad position, candidates (u32 at info+3)]
     unsigned long long* h_info = nullptr;  // pinned
     // the segment walk (lsmck_segwalk.h): per segment guess, exit, outcome,
@@ -340,10 +332,11 @@ struct lsmck_ctx {
     size_t cap_sst = 0;
   } wd;
   bool wal_recs_direct = false;  // this replay's records go by DMA into the caller's pinned array (under wal_mu)
+  bool wal_compact = false;      // this replay's records are lsmck_wal_rec16 (under wal_mu)
   // LSMCK_RECS_DEVICE (under wal_mu): the caller's device array and its capacity
   // (the segment walk emits straight into it when every record fits), and
   // whether this replay's emit did
-  lsmck_wal_rec* wal_recs_dev = nullptr;
+  void* wal_recs_dev = nullptr;  // lsmck_wal_rec[] or, wal_compact, lsmck_wal_rec16[]
   size_t wal_recs_dev_cap = 0;
   bool wal_recs_dev_emitted = false;
   int wal_seg = 1;           // device WAL walk: 1 = the segment walk first (default), 0 = candidate doubling only
@@ -355,13 +348,22 @@ struct lsmck_ctx {
   int stage_numa = -2;   // option "stage_numa": -2 the device's node on a multi-node host, -1 off, >= 0 that node
   int pin_node = -1;     // in effect: pinned buffers and copy threads on this node (-1: none)
   // what the last device-walked replay did (lsmck_ctx_get_stat "wal_walk_path" / "wal_seg_repairs" / "wal_segments")
-  int last_walk_path = 0;
-  int last_seg_repairs = 0;
-  uint64_t last_segments = 0;
-  lsmck_wal_rec* h_wrecs = nullptr;  // device WAL replay: the records' pinned landing buffer (grow-only)
+  // (atomic: lsmck_ctx_get_stat reads them under ctx->mu while a replay runs under wal_mu)
+  std::atomic<int> last_walk_path{0};
+  std::atomic<int> last_seg_repairs{0};
+  std::atomic<uint64_t> last_segments{0};
+  uint8_t* h_wrecs = nullptr;  // device WAL replay: the records' pinned landing buffer (bytes; grow-only)
   size_t cap_hwrecs = 0;
-  hipEvent_t wal_emit_ev = nullptr, wal_recs_ev = nullptr;  // records read back beside the CRC pass
-  lsmck_wal_rec* h_wrecs1 = nullptr;  // split host-image replay: the first part's records (pinned, grow-only)
+  // the records' read-back on the SDMA engines (lsmck_dma.h): created on first
+  // use; "wal_dma_engines" engines (0: hipMemcpyAsync on the staging stream,
+  // the round-4 path), the copy cut in "wal_dma_chunks" pieces
+  lsmck_dma::Copier* dma = nullptr;
+  bool dma_tried = false;
+  std::atomic<int> last_recs_dma{0};  // the last read-back: SDMA engines used (0: hipMemcpyAsync)
+  int wal_dma_engines = 4;
+  int wal_dma_chunks = 32;
+  hipEvent_t wal_emit_ev = nullptr;  // the emit's end: the records' read-back beside the CRC pass waits for it
+  uint8_t* h_wrecs1 = nullptr;  // split host-image replay: the first part's records (pinned bytes, grow-only)
   size_t cap_hwrecs1 = 0;
   hipStream_t wal_rs = nullptr;       // ... read back on their own stream while the second part uploads
   hipEvent_t wal_emit1_ev = nullptr;
@@ -602,7 +604,6 @@ lsmck_host::HostPool& host_pool(lsmck_ctx* ctx) {
 // the context's NUMA placement from its option (ctx->mu held or not yet shared)
 void apply_numa(lsmck_ctx* ctx) {
   ctx->pin_node = ctx->stage_numa == -2 ? (numa_node_count() > 1 ? ctx->numa_node : -1) : ctx->stage_numa;
-  if (ctx->dev >= 0 && ctx->dev < kMaxDevs) g_pin_node[ctx->dev].store(ctx->pin_node);
   if (ctx->pool) {
     cpu_set_t set;
     if (ctx->pin_node >= 0 && node_cpus(ctx->pin_node, &set))
@@ -693,13 +694,13 @@ int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
     if ((rc = stage_retire(S, J))) return rc;
     // descriptors (rebased) and payload
     size_t pay_bytes = use_span ? (size_t)(span_hi - span_lo) : (size_t)bytes;
-    if ((rc = ensure_pinned(&S.h_out, &S.cap_h_out, cnt * esz))) return rc;
+    if ((rc = ensure_pinned(ctx->pin_node, &S.h_out, &S.cap_h_out, cnt * esz))) return rc;
     if ((rc = ensure_dev(&S.d_out, &S.cap_d_out, cnt * esz))) return rc;
     if ((rc = ensure_dev(&S.d_pay, &S.cap_d_pay, pay_bytes + 16))) return rc;
     const uint8_t* h_src = nullptr;
     if (J.off) {
-      if ((rc = ensure_pinned(&S.h_off, &S.cap_h_off, cnt))) return rc;
-      if ((rc = ensure_pinned(&S.h_len, &S.cap_h_len, cnt))) return rc;
+      if ((rc = ensure_pinned(ctx->pin_node, &S.h_off, &S.cap_h_off, cnt))) return rc;
+      if ((rc = ensure_pinned(ctx->pin_node, &S.h_len, &S.cap_h_len, cnt))) return rc;
       if ((rc = ensure_dev(&S.d_off, &S.cap_d_off, cnt))) return rc;
       if ((rc = ensure_dev(&S.d_len, &S.cap_d_len, cnt))) return rc;
       uint64_t pos = 0;
@@ -713,7 +714,7 @@ int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
     if (use_span && J.pinned) {
       h_src = J.base + span_lo;
     } else {
-      if ((rc = ensure_pinned(&S.h_pay, &S.cap_h_pay, pay_bytes + 16))) return rc;
+      if ((rc = ensure_pinned(ctx->pin_node, &S.h_pay, &S.cap_h_pay, pay_bytes + 16))) return rc;
       if (use_span) {
         stage_copy(ctx, S.h_pay, J.base + span_lo, pay_bytes, ctx->stage_threads);
       } else if (!J.off) {
@@ -976,6 +977,19 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->wal_seg = (int)value;
     return 0;
   }
+  if (!strcmp(key, "wal_dma_engines")) {  // WAL records to the host: SDMA engines (0 = hipMemcpyAsync; A/B)
+    if (value < 0 || value > 16) return lsmck_host::set_error(LSMCK_EINVAL, "wal_dma_engines: 0..16");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_dma_engines = (int)value;
+    return 0;
+  }
+  if (!strcmp(key, "wal_dma_chunks")) {  // WAL records to the host: pieces of the SDMA copy
+    if (value < 1 || value > lsmck_dma::kMaxChunks)
+      return lsmck_host::set_error(LSMCK_EINVAL, "wal_dma_chunks: 1..64");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_dma_chunks = (int)value;
+    return 0;
+  }
   if (!strcmp(key, "wal_seg_bytes")) {  // segment walk: bytes per segment (0 = auto; tests force small segments)
     if (value < 0 || (value && (value < 64 || value > (1l << 30))))
       return lsmck_host::set_error(LSMCK_EINVAL, "wal_seg_bytes: 0 or 64..2^30");
@@ -1067,11 +1081,13 @@ int lsmck_ctx_get_stat(lsmck_ctx* ctx, const char* key, long* value) {
   if (!key || !value) return lsmck_host::set_error(LSMCK_EINVAL, "null key or value");
   std::lock_guard<std::mutex> lk(ctx->mu);
   if (!strcmp(key, "wal_walk_path")) {
-    *value = ctx->last_walk_path;
+    *value = ctx->last_walk_path.load();
   } else if (!strcmp(key, "wal_seg_repairs")) {
-    *value = ctx->last_seg_repairs;
+    *value = ctx->last_seg_repairs.load();
   } else if (!strcmp(key, "wal_segments")) {
-    *value = (long)ctx->last_segments;
+    *value = (long)ctx->last_segments.load();
+  } else if (!strcmp(key, "wal_recs_dma")) {  // the last records read-back: SDMA engines (0: hipMemcpyAsync)
+    *value = ctx->last_recs_dma.load();
   } else if (!strcmp(key, "numa_node")) {
     *value = ctx->numa_node;
   } else if (!strcmp(key, "stage_numa_node")) {
@@ -1112,8 +1128,9 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
     if (p) (void)hipHostFree(p);
   if (ctx->h_verify) (void)hipHostFree(ctx->h_verify);
   if (ctx->h_wrecs) (void)hipHostFree(ctx->h_wrecs);
+  if (ctx->wd.recs16) (void)hipFree(ctx->wd.recs16);
+  lsmck_dma::destroy(ctx->dma);
   if (ctx->wal_emit_ev) (void)hipEventDestroy(ctx->wal_emit_ev);
-  if (ctx->wal_recs_ev) (void)hipEventDestroy(ctx->wal_recs_ev);
   if (ctx->h_wrecs1) (void)hipHostFree(ctx->h_wrecs1);
   if (ctx->wal_emit1_ev) (void)hipEventDestroy(ctx->wal_emit1_ev);
   if (ctx->wal_rs) (void)hipStreamDestroy(ctx->wal_rs);
@@ -1322,6 +1339,11 @@ static int wal_walk_part(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t 
     rc = lsmk_wal_emit(img, n, W.chain, W.pos, W.info, (uint32_t)out->m, W.recs + at, ctx->d_woff + at,
                        ctx->d_wlen + at, ctx->d_wexp + at, st);
     if (rc) return launch_rc(rc, "wal emit kernel");
+    if (ctx->wal_compact) {  // the caller's layout: lsmck_wal_rec16 (the segment walk emits it directly)
+      if ((rc = ensure_dev_keep(&W.recs16, &W.cap_recs16, tot, at, st))) return rc;
+      if ((rc = lsmk_wal_recs_compact(W.recs + at, W.recs16 + at, out->m, st)))
+        return launch_rc(rc, "wal record compaction kernel");
+    }
   }
   return 0;
 }
@@ -1334,76 +1356,134 @@ static int wal_crc_part(lsmck_ctx* ctx, const uint8_t* img, size_t at, size_t m,
   return crc_desc_device(ctx, ctx->scratch, img, ctx->d_woff + at, ctx->d_wlen + at, m, ctx->d_vcrc + at, st, true);
 }
 
+// This replay's record layout: bytes per record (lsmck_wal_rec, or
+// lsmck_wal_rec16 for lsmck_wal_replay_verify16).
+static size_t wal_rec_size(const lsmck_ctx* ctx) {
+  return ctx->wal_compact ? sizeof(lsmck_wal_rec16) : sizeof(lsmck_wal_rec);
+}
+
+// the context's SDMA copier (lsmck_dma.h), made on first use; nullptr: none
+static lsmck_dma::Copier* dma_copier(lsmck_ctx* ctx) {
+  if (!ctx->dma_tried) {
+    ctx->dma_tried = true;
+    ctx->dma = lsmck_dma::create(ctx->d_verify);  // (any allocation of the device names its agent)
+  }
+  return ctx->dma;
+}
+
+// Record i of this replay as an lsmck_wal_rec, read from the device array src
+// (compact: its 16 bytes, and the stored CRC from its header in the image).
+static int wal_dev_rec(lsmck_ctx* ctx, const uint8_t* img, const uint8_t* src, size_t i, lsmck_wal_rec* r) {
+  if (!ctx->wal_compact) {
+    HIPCHK(hipMemcpy(r, src + i * sizeof(lsmck_wal_rec), sizeof *r, hipMemcpyDeviceToHost));
+    return 0;
+  }
+  lsmck_wal_rec16 c;
+  HIPCHK(hipMemcpy(&c, src + i * sizeof c, sizeof c, hipMemcpyDeviceToHost));
+  r->type = (c.payload_type & LSMCK_WAL_REC16_REMOVE) ? 2u : 1u;
+  r->payload_off = c.payload_type & LSMCK_WAL_REC16_OFF_MASK;
+  r->rec_off = r->payload_off - lsmck::seg::hdr_len(r->type);
+  r->klen = c.klen;
+  r->vlen = c.vlen;
+  uint8_t h[4];
+  HIPCHK(hipMemcpy(h, img + r->rec_off + 1, 4, hipMemcpyDeviceToHost));
+  r->crc = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
+  return 0;
+}
+
+// The records' read-back beside the CRC pass: `bytes` of the device array
+// src into the page-locked `land` once the emit is done (ctx->wal_emit_ev),
+// dealt over "wal_dma_engines" SDMA engines (lsmck_dma.h) -- no copy kernel
+// on the CUs beside the CRC pass -- or, without them, by hipMemcpyAsync on
+// the staging stream.  out (pageable, or null): where the records go from
+// `land`, copied on host threads piece by piece as the pieces land.
+// Returns once all of it is in place.
+static int wal_read_back(lsmck_ctx* ctx, uint8_t* land, const uint8_t* src, size_t bytes, uint8_t* out) {
+  HIPCHK(hipEventSynchronize(ctx->wal_emit_ev));
+  auto copy_out = [&](size_t a, size_t b) {  // land [a, b) -> out, several threads for large pieces
+    const size_t len = b - a;
+    const unsigned T = len >= (4u << 20) ? std::max(1u, std::min(ctx->stage_threads, 8u)) : 1u;
+    host_pool(ctx).run(T, [&](unsigned t) {
+      const size_t x = a + (len * t / T & ~(size_t)4095), y = t + 1 == T ? b : a + (len * (t + 1) / T & ~(size_t)4095);
+      if (y > x) memcpy(out + x, land + x, y - x);
+    });
+  };
+  lsmck_dma::Copier* dc = ctx->wal_dma_engines ? dma_copier(ctx) : nullptr;
+  lsmck_dma::Job job;
+  if (dc && lsmck_dma::d2h(dc, land, src, bytes, ctx->wal_dma_engines, ctx->wal_dma_chunks, &job) == 0) {
+    const int E = std::max(1, std::min(ctx->wal_dma_engines, lsmck_dma::engines(dc)));
+    ctx->last_recs_dma = E;
+    int werr = 0;
+    for (int i = 0; i < job.n;) {  // (a round: the next piece of every engine)
+      const int i1 = std::min(job.n, i + E);
+      for (int k = i; k < i1; ++k)
+        if (lsmck_dma::wait(dc, job, k) && !werr) werr = 1;
+      if (out && !werr) copy_out(job.off[i], job.off[i1]);
+      i = i1;
+    }
+    if (werr) return lsmck_host::set_error(LSMCK_EIO, "SDMA copy of the WAL records failed");
+    return 0;
+  }
+  ctx->last_recs_dma = 0;
+  int rc;
+  if ((rc = stage_init(ctx->stage[0]))) return rc;
+  HIPCHK(hipMemcpyAsync(land, src, bytes, hipMemcpyDeviceToHost, ctx->stage[0].s));
+  HIPCHK(hipStreamSynchronize(ctx->stage[0].s));
+  if (out) copy_out(0, bytes);
+  return 0;
+}
+
 // After the CRC pass of all m records: the compare, the records to the caller
-// (read back on a second stream and copied out on host threads while the
-// compare drains), and the replay's outcome (the first bad record in log
-// order, or a bad type byte after the last record at badq).
+// (read back beside the compare and copied out on host threads), and the
+// replay's outcome (the first bad record in log order, or a bad type byte
+// after the last record at badq).
 // done: records [0, done) are already in the caller's array (the split
-// replay's first part, from ctx->h_wrecs1); the rest land in ctx->h_wrecs.
+// replay's first part); the rest are read back from the device.
+// emit_recorded: ctx->wal_emit_ev marks the end of the emit (the segment
+// walk); otherwise the read-back waits for everything queued on st so far.
 // pack_from: records [pack_from, m) have packed CRC spans (the segment walk's
 // emit, seg::Pack): their expected CRCs are the spans' (seg::pack_crc), and a
 // bad one's computed CRC is taken back to its payload's for the report.
-static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t term, uint64_t badq,
-                      lsmck_wal_rec* recs, size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc,
-                      uint32_t* bad_expected, hipStream_t st, const WalTrace& tr, size_t done = 0,
-                      bool emit_recorded = false, size_t pack_from = ~(size_t)0) {
+static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t term, uint64_t badq, void* recs,
+                      size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected,
+                      hipStream_t st, const WalTrace& tr, size_t done = 0, bool emit_recorded = false,
+                      size_t pack_from = ~(size_t)0) {
   auto& W = ctx->wd;
   int rc;
   uint64_t nbad = 0, first = m;
+  const size_t rsz = wal_rec_size(ctx);
+  ctx->last_recs_dma = 0;
+  // the device array that holds records [0, m): the caller's when the emit wrote them there
+  const uint8_t* dsrc = ctx->wal_recs_dev && ctx->wal_recs_dev_emitted ? (const uint8_t*)recs
+                        : ctx->wal_compact                             ? (const uint8_t*)W.recs16
+                                                                       : (const uint8_t*)W.recs;
   if (m) {
-    std::function<int()> copy_out;
-    const size_t todo = m - done;
     const size_t ntake = std::min(m, cap) > done ? std::min(m, cap) - done : 0;  // records for the caller's array
+    uint8_t* const rb = (uint8_t*)recs;
+    uint8_t* land = nullptr;  // the read-back's page-locked landing: the caller's array or ctx->h_wrecs
     if (ctx->wal_recs_dev) {
       // LSMCK_RECS_DEVICE: the records stay on the device (emitted there, or
       // copied from the walk's own array); nothing crosses the link
       if (recs && ntake && !ctx->wal_recs_dev_emitted)
-        HIPCHK(hipMemcpyAsync(recs + done, W.recs + done, ntake * sizeof(lsmck_wal_rec), hipMemcpyDeviceToDevice, st));
-    } else if (recs && cap && todo && ctx->wal_recs_direct) {
-      // the caller's array is pinned: the records go there by DMA, on the
-      // staging stream, beside the CRC pass and the compare
-      if ((rc = stage_init(ctx->stage[0]))) return rc;
+        HIPCHK(hipMemcpyAsync(rb + done * rsz, dsrc + done * rsz, ntake * rsz, hipMemcpyDeviceToDevice, st));
+    } else if (recs && ntake) {
+      if (ctx->wal_recs_direct) {
+        land = rb + done * rsz;  // page-locked (LSMCK_RECS_PINNED): straight in
+      } else {
+        if ((rc = ensure_pinned(ctx->pin_node, &ctx->h_wrecs, &ctx->cap_hwrecs, ntake * rsz))) return rc;
+        land = ctx->h_wrecs;
+      }
       if (!ctx->wal_emit_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_emit_ev, hipEventDisableTiming));
-      if (!ctx->wal_recs_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_recs_ev, hipEventDisableTiming));
-      hipStream_t s2 = ctx->stage[0].s;
       if (!emit_recorded) HIPCHK(hipEventRecord(ctx->wal_emit_ev, st));
-      HIPCHK(hipStreamWaitEvent(s2, ctx->wal_emit_ev, 0));
-      if (ntake) HIPCHK(hipMemcpyAsync(recs + done, W.recs + done, ntake * sizeof(lsmck_wal_rec), hipMemcpyDeviceToHost, s2));
-      HIPCHK(hipEventRecord(ctx->wal_recs_ev, s2));
-      copy_out = [&]() -> int {
-        HIPCHK(hipEventSynchronize(ctx->wal_recs_ev));
-        return 0;
-      };
-    } else if (recs && cap && todo) {
-      if ((rc = ensure_pinned(&ctx->h_wrecs, &ctx->cap_hwrecs, todo)) || (rc = stage_init(ctx->stage[0]))) return rc;
-      if (!ctx->wal_emit_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_emit_ev, hipEventDisableTiming));
-      if (!ctx->wal_recs_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_recs_ev, hipEventDisableTiming));
-      hipStream_t s2 = ctx->stage[0].s;
-      if (!emit_recorded) HIPCHK(hipEventRecord(ctx->wal_emit_ev, st));
-      HIPCHK(hipStreamWaitEvent(s2, ctx->wal_emit_ev, 0));
-      HIPCHK(hipMemcpyAsync(ctx->h_wrecs, W.recs + done, todo * sizeof(lsmck_wal_rec), hipMemcpyDeviceToHost, s2));
-      HIPCHK(hipEventRecord(ctx->wal_recs_ev, s2));
-      copy_out = [&]() -> int {  // pinned -> the caller's array, on several threads (first touch of its pages)
-        HIPCHK(hipEventSynchronize(ctx->wal_recs_ev));
-        const size_t cnt = std::min(m, cap) > done ? std::min(m, cap) - done : 0, bytes = cnt * sizeof(lsmck_wal_rec);
-        const unsigned T = bytes >= (4u << 20) ? std::max(1u, std::min(ctx->stage_threads, 8u)) : 1u;
-        host_pool(ctx).run(T, [&](unsigned t) {
-          const size_t a = cnt * t / T, b = cnt * (t + 1) / T;
-          memcpy(recs + done + a, ctx->h_wrecs + a, (b - a) * sizeof(lsmck_wal_rec));
-        });
-        return 0;
-      };
     }
     HIPCHK(hipMemsetAsync(ctx->d_verify, 0, 8, st));         // n_bad
     HIPCHK(hipMemsetAsync(ctx->d_verify + 1, 0xFF, 8, st));  // first_bad = ~0
     rc = lsmk_launch_crc32_compare(ctx->d_vcrc, ctx->d_wexp, m, ctx->d_verify, ctx->d_verify + 1, st);
-    if (rc) {
-      if (copy_out) (void)hipEventSynchronize(ctx->wal_recs_ev);
-      return launch_rc(rc, "compare kernel");
-    }
+    if (rc) return launch_rc(rc, "compare kernel");
     HIPCHK(hipMemcpyAsync(ctx->h_verify, ctx->d_verify, 16, hipMemcpyDeviceToHost, st));
-    const int hrc = copy_out ? copy_out() : 0;
-    if (copy_out) (void)hipEventSynchronize(ctx->wal_recs_ev);
+    const int hrc = land ? wal_read_back(ctx, land, dsrc + done * rsz, ntake * rsz,
+                                         ctx->wal_recs_direct ? nullptr : rb + done * rsz)
+                         : 0;
     HIPCHK(hipStreamSynchronize(st));
     if (hrc) return hrc;
     nbad = ctx->h_verify[0];
@@ -1412,25 +1492,15 @@ static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t ter
   tr.mark("crc+compare+records (sync)");
   const size_t accepted = nbad ? (size_t)first : m;
   if (nrec) *nrec = accepted;
-  if (nbad) {
+  if (nbad) {  // the report, from the device's copy of the records
     lsmck_wal_rec r;
     uint32_t got = 0;
-    if (ctx->wal_recs_dev)
-      HIPCHK(hipMemcpy(&r, (ctx->wal_recs_dev_emitted ? recs : W.recs) + first, sizeof r, hipMemcpyDeviceToHost));
-    else if (recs && cap && first < done)
-      r = ctx->h_wrecs1[first];
-    else if (recs && cap && ctx->wal_recs_direct && first < std::min(m, cap))
-      r = recs[first];
-    else if (recs && cap && m > done && !ctx->wal_recs_direct)
-      r = ctx->h_wrecs[first - done];
-    else
-      HIPCHK(hipMemcpy(&r, W.recs + first, sizeof r, hipMemcpyDeviceToHost));
+    if ((rc = wal_dev_rec(ctx, img, dsrc, first, &r))) return rc;
     HIPCHK(hipMemcpy(&got, ctx->d_vcrc + first, 4, hipMemcpyDeviceToHost));
     if (first >= pack_from && first + 1 < m) {  // a packed span's CRC: the next header taken back out
       namespace sg = lsmck::seg;
       lsmck_wal_rec rn;
-      HIPCHK(hipMemcpy(&rn, (ctx->wal_recs_dev && ctx->wal_recs_dev_emitted ? recs : W.recs) + first + 1, sizeof rn,
-                       hipMemcpyDeviceToHost));
+      if ((rc = wal_dev_rec(ctx, img, dsrc, first + 1, &rn))) return rc;
       if (sg::pack_fits(r.klen + r.vlen, sg::hdr_len(rn.type))) {
         sg::Head nh{};
         nh.t = rn.type;
@@ -1552,7 +1622,15 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
       if (K64 >= (1ull << 31)) return kWalSegDecline;  // (tiny forced segments over a huge log)
       const uint32_t K = (uint32_t)K64;
       ctx->last_segments = K;
-      if ((rc = ensure_dev(&W.sbsum, &W.cap_sbsum, (size_t)lsmk_wal_seg_scan_blocks(K) + 1))) return rc;
+      // The walk's own arrays (~40 B per segment).  An allocation that fails
+      // (a log that nearly fills HBM) declines to the candidate-doubling walk,
+      // whose scratch is budgeted against the free memory, instead of failing
+      // the replay: the failed hipMalloc's sticky error is cleared first.
+      auto alloc_fail = [&]() {
+        (void)hipGetLastError();
+        return kWalSegDecline;
+      };
+      if (ensure_dev(&W.sbsum, &W.cap_sbsum, (size_t)lsmk_wal_seg_scan_blocks(K) + 1)) return alloc_fail();
       if (W.cap_seg < (size_t)K + 1) {
         for (void* p : {(void*)W.sg, (void*)W.sx, (void*)W.spre, (void*)W.scode, (void*)W.srecs})
           if (p) (void)hipFree(p);
@@ -1560,15 +1638,25 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
         W.sg = W.sx = W.spre = nullptr;
         W.scode = W.srecs = nullptr;
         W.cap_seg = 0;
-        HIPCHK(hipMalloc((void**)&W.sg, c * 8));
-        HIPCHK(hipMalloc((void**)&W.sx, c * 8));
-        HIPCHK(hipMalloc((void**)&W.spre, c * 8));
-        HIPCHK(hipMalloc((void**)&W.scode, c * 4));
-        HIPCHK(hipMalloc((void**)&W.srecs, c * 4));
+        if (hipMalloc((void**)&W.sg, c * 8) != hipSuccess || hipMalloc((void**)&W.sx, c * 8) != hipSuccess ||
+            hipMalloc((void**)&W.spre, c * 8) != hipSuccess || hipMalloc((void**)&W.scode, c * 4) != hipSuccess ||
+            hipMalloc((void**)&W.srecs, c * 4) != hipSuccess) {
+          for (void** p : {(void**)&W.sg, (void**)&W.sx, (void**)&W.spre, (void**)&W.scode, (void**)&W.srecs}) {
+            if (*p) (void)hipFree(*p);
+            *p = nullptr;
+          }
+          return alloc_fail();
+        }
         W.cap_seg = c;
       }
-      if (!W.sinfo) HIPCHK(hipMalloc((void**)&W.sinfo, sg::kInfoWords * 8));
-      if (!W.h_sinfo) HIPCHK(hipHostMalloc((void**)&W.h_sinfo, sg::kInfoWords * 8, hipHostMallocDefault));
+      if (!W.sinfo && hipMalloc((void**)&W.sinfo, sg::kInfoWords * 8) != hipSuccess) {
+        W.sinfo = nullptr;
+        return alloc_fail();
+      }
+      if (!W.h_sinfo && hipHostMalloc((void**)&W.h_sinfo, sg::kInfoWords * 8, hipHostMallocDefault) != hipSuccess) {
+        W.h_sinfo = nullptr;
+        return alloc_fail();
+      }
       // the emit from checkpoints every 64 KiB (up to 32 per segment): its
       // walks run 32x as many threads, each a 32nd as long
       const uint32_t nsub = S >= (128u << 10) ? (uint32_t)std::min<uint64_t>(32, S >> 16) : 1u;
@@ -1579,23 +1667,38 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
         W.scpc = nullptr;
         W.cap_cp = 0;
         const size_t c = (size_t)K * nsub;
-        HIPCHK(hipMalloc((void**)&W.scpp, c * 8));
-        HIPCHK(hipMalloc((void**)&W.scpc, c * 4));
+        if (hipMalloc((void**)&W.scpp, c * 8) != hipSuccess || hipMalloc((void**)&W.scpc, c * 4) != hipSuccess) {
+          if (W.scpp) (void)hipFree(W.scpp);
+          if (W.scpc) (void)hipFree(W.scpc);
+          W.scpp = nullptr;
+          W.scpc = nullptr;
+          return alloc_fail();
+        }
         W.cap_cp = c;
       }
       // the walk stages each segment's records in scap slots (auto: an
-      // eighth of the walked bytes, 64 MiB .. 8 GiB, over the segments; at
-      // most the records a segment can hold); a segment with more is emitted
-      // by a second walk of its headers
+      // eighth of the walked bytes, 64 MiB .. 8 GiB, over the segments, and
+      // at most a quarter of the free device memory (less the records'
+      // arrays still to come); at most the records a segment can hold); a
+      // segment with more is emitted by a second walk of its headers, and so
+      // is every segment when the slots cannot be had (scap 0)
       uint32_t scap = 0;
       if (ctx->wal_seg_stage) {
         const uint64_t most = S / 9 + 1;
-        const uint64_t budget = std::min<uint64_t>(std::max<uint64_t>((lim - start) / 8, 64ull << 20), 8ull << 30);
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+        const uint64_t have = W.sst ? (uint64_t)W.cap_sst * sizeof(sg::StageRec) : 0;  // (reused, not new)
+        const uint64_t budget = std::min<uint64_t>(
+            std::min<uint64_t>(std::max<uint64_t>((lim - start) / 8, 64ull << 20), 8ull << 30),
+            (uint64_t)free_b / 4 + have);
         const uint64_t c = std::min<uint64_t>(most, ctx->wal_seg_stage >= 2 ? (uint64_t)ctx->wal_seg_stage
                                                                                : budget / (sizeof(sg::StageRec) * K));
         if (c >= 1) {
           scap = (uint32_t)c;
-          if ((rc = ensure_dev(&W.sst, &W.cap_sst, (size_t)K * scap))) return rc;
+          if (ensure_dev(&W.sst, &W.cap_sst, (size_t)K * scap)) {
+            (void)hipGetLastError();  // no slots: every segment is emitted by its second walk
+            scap = 0;
+          }
         }
       }
       a = sg::SegArgs{img, n, start, S, K, W.sg, W.sx, W.scode, W.srecs, W.spre, W.sinfo, lim,
@@ -1637,21 +1740,23 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
     const size_t tot = at + m;
     // LSMCK_RECS_DEVICE with room for every record: emitted into the caller's array
     const bool dev = ctx->wal_recs_dev && at == 0 && tot <= ctx->wal_recs_dev_cap;
-    if ((!dev && (rc = ensure_dev_keep(&W.recs, &W.cap_recs, tot, at, st))) ||
+    const bool c16 = ctx->wal_compact;
+    if ((!dev && !c16 && (rc = ensure_dev_keep(&W.recs, &W.cap_recs, tot, at, st))) ||
+        (!dev && c16 && (rc = ensure_dev_keep(&W.recs16, &W.cap_recs16, tot, at, st))) ||
         (rc = ensure_dev_keep(&ctx->d_woff, &ctx->cap_woff, tot, at, st)) ||
         (rc = ensure_dev_keep(&ctx->d_wlen, &ctx->cap_wlen, tot, at, st)) ||
         (rc = ensure_dev_keep(&ctx->d_wexp, &ctx->cap_wexp, tot, at, st)) ||
         (rc = ensure_dev_keep(&ctx->d_vcrc, &ctx->cap_vcrc, tot, at, st)))
       return rc;
-    lsmck_wal_rec* to = dev ? ctx->wal_recs_dev : W.recs;
+    void* to = dev ? ctx->wal_recs_dev : c16 ? (void*)W.recs16 : (void*)W.recs;
     if (ctx->wal_seg_pack) {
-      rc = lsmk_wal_seg_emit_packed(&a, at, to, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, tot, st);
+      rc = lsmk_wal_seg_emit_packed(&a, at, to, c16, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, tot, st);
     } else {
-      rc = lsmk_wal_seg_emit(&a, at, to, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st);
+      rc = lsmk_wal_seg_emit(&a, at, to, c16, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, st);
     }
     if (rc) return launch_rc(rc, "wal segment emit kernel");
-    if ((rc = lsmk_wal_seg_place(&a, at, to, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, tot, ctx->wal_seg_pack ? 1 : 0,
-                                 st)))
+    if ((rc = lsmk_wal_seg_place(&a, at, to, c16, ctx->d_woff, ctx->d_wlen, ctx->d_wexp, tot,
+                                 ctx->wal_seg_pack ? 1 : 0, st)))
       return launch_rc(rc, "wal segment place kernel");
     out->packed = ctx->wal_seg_pack;
     ctx->wal_recs_dev_emitted = dev;
@@ -1664,7 +1769,7 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
 // A device-resident image (or an uploaded one: `marked`, its candidate bitmap
 // is already in ctx->wd -- wal_upload marks each chunk behind its copy): the
 // walk (in parts when its scratch would not fit), one CRC pass per part.
-static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, lsmck_wal_rec* recs, size_t cap,
+static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, void* recs, size_t cap,
                              size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected,
                              bool marked = false) {
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1757,7 +1862,7 @@ static int wal_upload_prepare(lsmck_ctx* ctx, size_t n, bool direct) {
       HIPCHK(hipStreamSynchronize(S.s));
       S.busy = false;
     }
-    if (!direct && (rc = ensure_pinned(&S.h_pay, &S.cap_h_pay, std::min(n, ctx->wal_stage_bytes)))) return rc;
+    if (!direct && (rc = ensure_pinned(ctx->pin_node, &S.h_pay, &S.cap_h_pay, std::min(n, ctx->wal_stage_bytes)))) return rc;
   }
   return 0;
 }
@@ -1782,17 +1887,19 @@ static int wal_upload(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned)
 
 // The split replay's first m records (emitted on st) into the caller's array
 // on this (helper) thread, through ctx->h_wrecs1 and the records' own stream.
-static int wal_records_early(lsmck_ctx* ctx, size_t m, lsmck_wal_rec* recs, size_t cap, hipStream_t st, size_t* done) {
+static int wal_records_early(lsmck_ctx* ctx, size_t m, void* recs, size_t cap, hipStream_t st, size_t* done) {
   int rc;
-  if ((rc = ensure_pinned(&ctx->h_wrecs1, &ctx->cap_hwrecs1, m))) return rc;
+  const size_t rsz = wal_rec_size(ctx);
+  if ((rc = ensure_pinned(ctx->pin_node, &ctx->h_wrecs1, &ctx->cap_hwrecs1, m * rsz))) return rc;
   if (!ctx->wal_rs) HIPCHK(hipStreamCreateWithFlags(&ctx->wal_rs, hipStreamNonBlocking));
   if (!ctx->wal_emit1_ev) HIPCHK(hipEventCreateWithFlags(&ctx->wal_emit1_ev, hipEventDisableTiming));
   HIPCHK(hipEventRecord(ctx->wal_emit1_ev, st));
   HIPCHK(hipStreamWaitEvent(ctx->wal_rs, ctx->wal_emit1_ev, 0));
-  HIPCHK(hipMemcpyAsync(ctx->h_wrecs1, ctx->wd.recs, m * sizeof(lsmck_wal_rec), hipMemcpyDeviceToHost, ctx->wal_rs));
+  const void* src = ctx->wal_compact ? (const void*)ctx->wd.recs16 : (const void*)ctx->wd.recs;
+  HIPCHK(hipMemcpyAsync(ctx->h_wrecs1, src, m * rsz, hipMemcpyDeviceToHost, ctx->wal_rs));
   HIPCHK(hipStreamSynchronize(ctx->wal_rs));
   const size_t cnt = std::min(m, cap);
-  memcpy(recs, ctx->h_wrecs1, cnt * sizeof(lsmck_wal_rec));  // (one thread: the pool is staging the upload)
+  memcpy(recs, ctx->h_wrecs1, cnt * rsz);  // (one thread: the pool is staging the upload)
   *done = m;
   return 0;
 }
@@ -1808,7 +1915,7 @@ constexpr int kWalNoSplit = 0x7FFF0002;  // internal: the image is too small to 
 // (the next header, or the first record that did not end by a).  The walk's
 // own time then hides behind the upload except for the second part's.
 // Caller holds wal_mu.
-static int wal_replay_split(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned, lsmck_wal_rec* recs,
+static int wal_replay_split(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned, void* recs,
                             size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected) {
   const size_t ch = ctx->wal_stage_bytes;
   const size_t a = (n / 2) / ch * ch;
@@ -1903,57 +2010,72 @@ int lsmck_wal_frame_insert_device(lsmck_ctx* ctx, uint8_t* img, const uint64_t* 
   return rc ? launch_rc(rc, "wal frame kernel") : 0;
 }
 
-int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsigned flags, lsmck_wal_rec* recs,
-                            size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected) {
+}  // extern "C"
+
+// internal flag: the GPU walk of this image already declined (kWalHostWalk): straight to the host walk
+constexpr unsigned kWalNoGpuWalk = 0x40000000u;
+
+// the call's record options on the context, set while wal_mu is held and
+// cleared on every return (wal_finish and the walks read them)
+struct WalCallRecs {
+  lsmck_ctx* c;
+  WalCallRecs(lsmck_ctx* c_, bool compact, bool direct, void* dev, size_t cap) : c(c_) {
+    c->wal_compact = compact;
+    c->wal_recs_direct = direct;
+    c->wal_recs_dev = dev;
+    c->wal_recs_dev_cap = dev ? cap : 0;
+    c->wal_recs_dev_emitted = false;
+  }
+  ~WalCallRecs() {
+    c->wal_compact = false;
+    c->wal_recs_direct = false;
+    c->wal_recs_dev = nullptr;
+    c->wal_recs_dev_cap = 0;
+    c->wal_recs_dev_emitted = false;
+  }
+};
+
+// lsmck_wal_replay_verify (recs: lsmck_wal_rec[cap]) and
+// lsmck_wal_replay_verify16 (compact: lsmck_wal_rec16[cap])
+static int wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsigned flags, void* recs, bool compact,
+                             size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc,
+                             uint32_t* bad_expected) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
+  const size_t rsz = compact ? sizeof(lsmck_wal_rec16) : sizeof(lsmck_wal_rec);
   // LSMCK_RECS_PINNED: the records go by DMA into the caller's pinned array
-  // (the flag is read by wal_finish under wal_mu; the host walk ignores it)
-  struct RecsDirect {  // set while wal_mu is held, cleared on every return
-    bool& f;
-    RecsDirect(bool& f_, bool v) : f(f_) { f = v; }
-    ~RecsDirect() { f = false; }
-  };
+  // (read by wal_finish under wal_mu; the host walk ignores it)
   const bool recs_pinned = (flags & LSMCK_RECS_PINNED) != 0;
+  const bool gpu_walk = (flags & LSMCK_DEVICE) && ctx->wal_gpu_walk && !(flags & kWalNoGpuWalk);
   if (flags & LSMCK_RECS_DEVICE) {
     if (recs_pinned) return lsmck_host::set_error(LSMCK_EINVAL, "LSMCK_RECS_DEVICE with LSMCK_RECS_PINNED");
-    struct RecsDev {  // set while wal_mu is held, cleared on every return
-      lsmck_ctx* c;
-      RecsDev(lsmck_ctx* c_, lsmck_wal_rec* r, size_t cap) : c(c_) {
-        c->wal_recs_dev = r;
-        c->wal_recs_dev_cap = r ? cap : 0;
-        c->wal_recs_dev_emitted = false;
-      }
-      ~RecsDev() {
-        c->wal_recs_dev = nullptr;
-        c->wal_recs_dev_cap = 0;
-        c->wal_recs_dev_emitted = false;
-      }
-    };
-    if ((flags & LSMCK_DEVICE) && ctx->wal_gpu_walk) {
+    unsigned more = 0;
+    if (gpu_walk) {
       std::lock_guard<std::mutex> wl(ctx->wal_mu);
-      RecsDev rd(ctx, recs, cap);
+      WalCallRecs wc(ctx, compact, false, recs, cap);
       rc = wal_replay_device(ctx, wal, n, recs, cap, nrec, bad_index, bad_crc, bad_expected);
       if (rc != kWalHostWalk) return rc;
+      more = kWalNoGpuWalk;  // (the GPU walk declined: no second try below)
     }
     // any other path makes the records on the host: into a host array, then
-    // copied to the caller's device array
-    std::vector<lsmck_wal_rec> tmp(recs ? std::min<size_t>(cap, n / 9 + 1) : 0);
+    // copied to the caller's device array (uninitialised: only what the walk writes is copied)
+    const size_t k0 = recs ? std::min<size_t>(cap, n / 9 + 1) : 0;
+    std::unique_ptr<uint8_t[]> tmp(k0 ? new uint8_t[k0 * rsz] : nullptr);
     size_t got = 0;
-    rc = lsmck_wal_replay_verify(ctx, wal, n, flags & ~LSMCK_RECS_DEVICE, recs ? tmp.data() : nullptr, tmp.size(),
-                                 &got, bad_index, bad_crc, bad_expected);
+    rc = wal_replay_verify(ctx, wal, n, (flags & ~LSMCK_RECS_DEVICE) | more, tmp.get(), compact, k0, &got, bad_index,
+                           bad_crc, bad_expected);
     if (rc < 0) return rc;
     if (nrec) *nrec = got;
-    const size_t k = std::min(got, tmp.size());
+    const size_t k = std::min(got, k0);
     if (k) {
       DevGuard g(ctx->dev);
-      HIPCHK(hipMemcpy(recs, tmp.data(), k * sizeof(lsmck_wal_rec), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(recs, tmp.get(), k * rsz, hipMemcpyHostToDevice));
     }
     return rc;
   }
-  if ((flags & LSMCK_DEVICE) && ctx->wal_gpu_walk) {
+  if (gpu_walk) {
     std::lock_guard<std::mutex> wl(ctx->wal_mu);  // the walk's bitmap (ctx->wd) is shared with the upload path
-    RecsDirect rd(ctx->wal_recs_direct, recs_pinned);
+    WalCallRecs wc(ctx, compact, recs_pinned, nullptr, 0);
     rc = wal_replay_device(ctx, wal, n, recs, cap, nrec, bad_index, bad_crc, bad_expected);
     if (rc != kWalHostWalk) return rc;
     // (the GPU walk declined: the image is copied back and walked on the host below)
@@ -1962,7 +2084,7 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
     // header walk, instead of the serial host walk (~12 GiB/s) -- the records
     // and offsets are the same, they index the caller's image
     std::lock_guard<std::mutex> wl(ctx->wal_mu);
-    RecsDirect rd(ctx->wal_recs_direct, recs_pinned);
+    WalCallRecs wc(ctx, compact, recs_pinned, nullptr, 0);
     const bool pinned = (flags & LSMCK_HOST_PINNED) != 0;
     rc = ctx->wal_split ? wal_replay_split(ctx, wal, n, pinned, recs, cap, nrec, bad_index, bad_crc, bad_expected)
                         : kWalNoSplit;
@@ -1981,7 +2103,7 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
   if (flags & LSMCK_DEVICE) {
     wal_lk.lock();
     DevGuard g(ctx->dev);
-    rc = ensure_pinned(&ctx->wal_host, &ctx->wal_host_cap, n);
+    rc = ensure_pinned(ctx->pin_node, &ctx->wal_host, &ctx->wal_host_cap, n);
     if (rc) return rc;
     if (n) HIPCHK(hipMemcpy(ctx->wal_host, wal, n, hipMemcpyDeviceToHost));
     h = ctx->wal_host;
@@ -2074,8 +2196,8 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
       // only the two counts come back
       std::lock_guard<std::mutex> lk(ctx->mu);
       DevGuard g(ctx->dev);
-      if ((rc = ensure_pinned(&ctx->h_woff, &ctx->cap_hwoff, m)) || (rc = ensure_pinned(&ctx->h_wlen, &ctx->cap_hwlen, m)) ||
-          (rc = ensure_pinned(&ctx->h_wexp, &ctx->cap_hwexp, m)) || (rc = ensure_dev(&ctx->d_woff, &ctx->cap_woff, m)) ||
+      if ((rc = ensure_pinned(ctx->pin_node, &ctx->h_woff, &ctx->cap_hwoff, m)) || (rc = ensure_pinned(ctx->pin_node, &ctx->h_wlen, &ctx->cap_hwlen, m)) ||
+          (rc = ensure_pinned(ctx->pin_node, &ctx->h_wexp, &ctx->cap_hwexp, m)) || (rc = ensure_dev(&ctx->d_woff, &ctx->cap_woff, m)) ||
           (rc = ensure_dev(&ctx->d_wlen, &ctx->cap_wlen, m)) || (rc = ensure_dev(&ctx->d_wexp, &ctx->cap_wexp, m)))
         return rc;
       ScratchOrder so(ctx, ctx->stream0);
@@ -2126,15 +2248,28 @@ int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsign
   }
   if (recs)
     for (size_t i = 0; i < accepted && i < cap; ++i) {
-      recs[i].rec_off = roff[i];
-      recs[i].payload_off = poff[i];
-      recs[i].klen = rk[i];
-      recs[i].vlen = rv[i];
-      recs[i].crc = pcrc[i];
-      recs[i].type = ptype[i];
+      if (compact)
+        lsmck::seg::put_rec((lsmck::seg::Compact16*)recs + i, roff[i], poff[i], rk[i], rv[i], pcrc[i], ptype[i]);
+      else
+        lsmck::seg::put_rec((lsmck_wal_rec*)recs + i, roff[i], poff[i], rk[i], rv[i], pcrc[i], ptype[i]);
     }
   if (nrec) *nrec = accepted;
   return result;
+}
+
+extern "C" {
+
+int lsmck_wal_replay_verify(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsigned flags, lsmck_wal_rec* recs,
+                            size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected) {
+  return wal_replay_verify(ctx, wal, n, flags & ~kWalNoGpuWalk, recs, false, cap, nrec, bad_index, bad_crc,
+                           bad_expected);
+}
+
+int lsmck_wal_replay_verify16(lsmck_ctx* ctx, const uint8_t* wal, size_t n, unsigned flags, lsmck_wal_rec16* recs,
+                              size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc,
+                              uint32_t* bad_expected) {
+  return wal_replay_verify(ctx, wal, n, flags & ~kWalNoGpuWalk, recs, true, cap, nrec, bad_index, bad_crc,
+                           bad_expected);
 }
 
 // ---------------------------------------------------------------------------
@@ -2425,8 +2560,8 @@ static int verify_tables(lsmck_ctx* ctx, const char* const* data_paths, const ch
         }
       }
       const size_t cnt = sv.size();
-      if ((rc = ensure_pinned(&S.h_pay, &S.cap_h_pay, pay + 16))) return rc;
-      if ((rc = ensure_pinned(&S.h_slices, &S.cap_h_slices, cnt))) return rc;
+      if ((rc = ensure_pinned(ctx->pin_node, &S.h_pay, &S.cap_h_pay, pay + 16))) return rc;
+      if ((rc = ensure_pinned(ctx->pin_node, &S.h_slices, &S.cap_h_slices, cnt))) return rc;
       if ((rc = ensure_dev(&S.d_pay, &S.cap_d_pay, pay + 16))) return rc;
       if ((rc = ensure_dev(&S.d_slices, &S.cap_d_slices, cnt))) return rc;
       memcpy(S.h_slices, sv.data(), cnt * sizeof(lsmck::ShaSlice));
@@ -2800,8 +2935,8 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
       std::lock_guard<std::mutex> lk(c->mu);
       DevGuard g(c->dev);
       for (auto& S : c->stage) {
-        if (stage_init(S) || ensure_pinned(&S.h_pay, &S.cap_h_pay, bytes) ||
-            ensure_pinned(&S.h_slices, &S.cap_h_slices, files) || ensure_dev(&S.d_pay, &S.cap_d_pay, bytes) ||
+        if (stage_init(S) || ensure_pinned(c->pin_node, &S.h_pay, &S.cap_h_pay, bytes) ||
+            ensure_pinned(c->pin_node, &S.h_slices, &S.cap_h_slices, files) || ensure_dev(&S.d_pay, &S.cap_d_pay, bytes) ||
             ensure_dev(&S.d_slices, &S.cap_d_slices, files))
           return;  // the verify reports it
         // map the pinned pages now, not on the readers' first touch
@@ -2901,7 +3036,7 @@ void* lsmck_host_alloc_pinned(lsmck_ctx* ctx, size_t bytes) {
   if (!ctx) return nullptr;
   DevGuard g(ctx->dev);
   void* p = nullptr;
-  hipError_t e = host_malloc_near(&p, bytes ? bytes : 1);  // (on the device's node: see stage_numa)
+  hipError_t e = host_malloc_near(&p, bytes ? bytes : 1, ctx->pin_node);  // (on the device's node: see stage_numa)
   if (e != hipSuccess) {
     hip_error(e, "hipHostMalloc");
     return nullptr;

@@ -98,12 +98,15 @@ uint64_t lsmk_wal_seg_scan_blocks(uint32_t K);
 int lsmk_wal_seg_walk(const lsmck::seg::SegArgs* a, hipStream_t st);
 int lsmk_wal_seg_round(const lsmck::seg::SegArgs* a, uint64_t* bsum, hipStream_t st);
 int lsmk_wal_seg_repair(const lsmck::seg::SegArgs* a, uint32_t budget, hipStream_t st);
-int lsmk_wal_seg_emit(const lsmck::seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff, uint32_t* plen,
-                      uint32_t* pcrc, hipStream_t st);
-int lsmk_wal_seg_emit_packed(const lsmck::seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff,
+// recs: lsmck_wal_rec[] or, compact != 0, lsmck_wal_rec16[]
+int lsmk_wal_seg_emit(const lsmck::seg::SegArgs* a, uint64_t at, void* recs, int compact, uint64_t* poff,
+                      uint32_t* plen, uint32_t* pcrc, hipStream_t st);
+int lsmk_wal_seg_emit_packed(const lsmck::seg::SegArgs* a, uint64_t at, void* recs, int compact, uint64_t* poff,
                              uint32_t* plen, uint32_t* pcrc, uint64_t iend, hipStream_t st);
-int lsmk_wal_seg_place(const lsmck::seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff, uint32_t* plen,
-                       uint32_t* pcrc, uint64_t iend, int packed, hipStream_t st);
+int lsmk_wal_seg_place(const lsmck::seg::SegArgs* a, uint64_t at, void* recs, int compact, uint64_t* poff,
+                       uint32_t* plen, uint32_t* pcrc, uint64_t iend, int packed, hipStream_t st);
+// m wide records -> lsmck_wal_rec16 (out)
+int lsmk_wal_recs_compact(const lsmck_wal_rec* in, void* out, uint64_t m, hipStream_t st);
 int lsmk_launch_crc32_compare(const uint32_t* crc, const uint32_t* expected, uint64_t n,
                                unsigned long long* n_bad, unsigned long long* first_bad, hipStream_t st);
 int lsmk_sha_order(const uint32_t* len, size_t n, uint16_t* keys_out, uint32_t* order, void* tmp, size_t* tmp_bytes,

@@ -18,6 +18,11 @@ namespace lsmck_host {
 // the caller and f(1..T-1) on the workers and returns when all are done.
 class HostPool {
  public:
+  HostPool() {
+    CPU_ZERO(&orig_);
+    if (sched_getaffinity(0, sizeof orig_, &orig_) != 0 || CPU_COUNT(&orig_) == 0)
+      for (int c = 0; c < CPU_SETSIZE; ++c) CPU_SET(c, &orig_);
+  }
   ~HostPool() {
     {
       std::lock_guard<std::mutex> lk(m_);
@@ -29,9 +34,12 @@ class HostPool {
   }
   // the workers' CPUs (the device's NUMA node), for the ones running and the
   // ones to come; clear_cpus: any CPU again
+  // (within the CPUs the process started with -- taskset, numactl -- when
+  // the node has any of them)
   void set_cpus(const cpu_set_t& set) {
     std::lock_guard<std::mutex> one(run_mu_);
-    cpus_ = set;
+    CPU_AND(&cpus_, &set, &orig_);
+    if (CPU_COUNT(&cpus_) == 0) cpus_ = set;
     pinned_ = true;
     for (auto& t : th_) (void)pthread_setaffinity_np(t.native_handle(), sizeof cpus_, &cpus_);
   }
@@ -39,8 +47,7 @@ class HostPool {
     std::lock_guard<std::mutex> one(run_mu_);
     if (!pinned_) return;
     pinned_ = false;
-    CPU_ZERO(&cpus_);
-    for (int c = 0; c < CPU_SETSIZE; ++c) CPU_SET(c, &cpus_);
+    cpus_ = orig_;  // the process's own mask again
     for (auto& t : th_) (void)pthread_setaffinity_np(t.native_handle(), sizeof cpus_, &cpus_);
   }
   void run(unsigned T, const std::function<void(unsigned)>& f) {
@@ -101,6 +108,7 @@ class HostPool {
   uint64_t gen_ = 0;
   bool stop_ = false;
   cpu_set_t cpus_{};     // (under run_mu_)
+  cpu_set_t orig_{};     // the affinity the process had when the pool was made
   bool pinned_ = false;
 };
 

@@ -43,9 +43,24 @@
 #define LSMCK_HD static inline
 #endif
 
-// diagnostic builds (LSMCK_SEG_CLOCK, lsmck_wal.hip): per-segment clock marks
-#ifndef LSMCK_SEG_CLOCK_MARK
+// Diagnostic builds (-DLSMCK_DIAG: tools/build_ab.sh A/B builds, the host
+// models of tools/segwalk_repairs.py, clock-mark builds) take the tuning
+// values and the per-segment clock marks from lsmck_diag.h; the product build
+// has these and no marks.
+#ifdef LSMCK_DIAG
+#include "lsmck_diag.h"
+#else
 #define LSMCK_SEG_CLOCK_MARK(k, slot)
+namespace lsmck {
+namespace seg {
+namespace tune {
+constexpr uint64_t kLaterSkipTo = 131072;  // kLaterSkipTo below
+constexpr uint64_t kLaterMin = 65536;      // kLaterMin below
+constexpr int kScanBlocks = 4;             // kScanBlocks below
+constexpr bool kLaterAlways = false;       // (host-model A/B: the later-start rule everywhere)
+}  // namespace tune
+}  // namespace seg
+}  // namespace lsmck
 #endif
 
 namespace lsmck {
@@ -83,10 +98,7 @@ constexpr uint64_t kHop = 65536;
 // log: 0.33 vs 0.42 ms, profiles/r04/o).  Segments shorter than records
 // (under 4 KiB) often hold no true start, and long hops (2 MiB segments)
 // let bogus lengths land on a true record: the rule stays for both.
-#ifndef LSMCK_LATER_SKIP_TO
-#define LSMCK_LATER_SKIP_TO 131072
-#endif
-constexpr uint64_t kLaterSkipFrom = 4096, kLaterSkipTo = LSMCK_LATER_SKIP_TO;
+constexpr uint64_t kLaterSkipFrom = 4096, kLaterSkipTo = tune::kLaterSkipTo;
 // From kLaterSkipTo on, the rule runs only for a guess whose first record is
 // longer than kHop payload bytes.  A bogus start whose random 32-bit length is
 // at most kHop lands on a true record with odds ~(records / bytes) * 2^-16
@@ -95,14 +107,8 @@ constexpr uint64_t kLaterSkipFrom = 4096, kLaterSkipTo = LSMCK_LATER_SKIP_TO;
 // costs no scan of its payload: 7.72 -> ~6.2 ms of walk for the 97.8 GiB log
 // (without the rule at all: 6.21 ms and three repairs of 0.87 ms each,
 // profiles/r04/v).  A wrong guess is caught by the check either way.
-#ifndef LSMCK_LATER_MIN
-#define LSMCK_LATER_MIN 65536
-#endif
-constexpr uint64_t kLaterMin = LSMCK_LATER_MIN;
-#ifndef LSMCK_SCAN_BLOCKS
-#define LSMCK_SCAN_BLOCKS 4
-#endif
-constexpr int kScanBlocks = LSMCK_SCAN_BLOCKS;  // 64-byte blocks the guess scan loads per iteration
+constexpr uint64_t kLaterMin = tune::kLaterMin;
+constexpr int kScanBlocks = tune::kScanBlocks;  // 64-byte blocks the guess scan loads per iteration
 // per-segment record counts and the guessed-segment count share one u64 in
 // the placement scan: guessed segments in the top 24 bits, records below
 constexpr int kSegShift = 40;
@@ -530,20 +536,10 @@ LSMCK_HD void seg_forced(const SegArgs& a, uint32_t k, uint64_t c) {
 // the guess's parameters for the walk's segments
 LSMCK_HD uint64_t seg_hop(const SegArgs& a) { return a.S > kHop ? a.S : kHop; }
 LSMCK_HD bool seg_later(const SegArgs& a) {
-#ifdef LSMCK_SEG_LATER_ALWAYS  // (host model A/B, tools/segwalk_repairs.py)
-  (void)a;
-  return true;
-#else
-  return a.S < kLaterSkipFrom || a.S >= kLaterSkipTo;
-#endif
+  return tune::kLaterAlways || a.S < kLaterSkipFrom || a.S >= kLaterSkipTo;
 }
 LSMCK_HD uint64_t seg_later_min(const SegArgs& a) {
-#ifdef LSMCK_SEG_LATER_ALWAYS
-  (void)a;
-  return 0;
-#else
-  return a.S >= kLaterSkipTo ? kLaterMin : 0;
-#endif
+  return !tune::kLaterAlways && a.S >= kLaterSkipTo ? kLaterMin : 0;
 }
 LSMCK_HD void seg_take_guess(const SegArgs& a, uint32_t k, uint64_t c);
 LSMCK_HD void seg_walk_thread(const SegArgs& a, uint32_t k) {
@@ -655,6 +651,40 @@ LSMCK_HD uint32_t pack_crc(uint32_t crc, const Head& nh, const uint32_t* T) {
   return ~(gf2_mul(~crc, nh.t == 1 ? 0xe6050901u : 0x1eb014d8u) ^ hdr_reg(nh, T));
 }
 
+// The records the emit writes: the 32-byte lsmck_wal_rec layout (any struct
+// with its fields), or the 16-byte compact one (lsmck_wal_rec16, include/
+// lsmck.h): the payload offset with the type in bit 63 (set: Remove), klen,
+// vlen -- what MemTable::from_log takes from a record (src/memtable.rs:28-47);
+// the header offset is the payload's less hdr_len, and the stored CRC is the
+// computed one for every accepted record.
+struct Compact16 {
+  uint64_t payload_type;
+  uint32_t klen, vlen;
+};
+constexpr uint64_t kRemoveBit = 1ull << 63;
+LSMCK_HD void put_rec(Compact16* r, uint64_t rec_off, uint64_t payload_off, uint32_t klen, uint32_t vlen,
+                      uint32_t crc, uint32_t type) {
+  (void)rec_off;
+  (void)crc;
+  Compact16 O;
+  O.payload_type = payload_off | (type == 2u ? kRemoveBit : 0ull);
+  O.klen = klen;
+  O.vlen = vlen;
+  *r = O;
+}
+template <class Rec>
+LSMCK_HD void put_rec(Rec* r, uint64_t rec_off, uint64_t payload_off, uint32_t klen, uint32_t vlen, uint32_t crc,
+                      uint32_t type) {
+  Rec O;
+  O.rec_off = rec_off;
+  O.payload_off = payload_off;
+  O.klen = klen;
+  O.vlen = vlen;
+  O.crc = crc;
+  O.type = type;
+  *r = O;
+}
+
 // step 4 for segment k (after the check passed): its records at `at` + its
 // place, as lsmck_wal_rec entries, CRC descriptors and stored CRCs
 // (sub-segment j of segment k when a.nsub > 1: its records only, from the
@@ -687,14 +717,7 @@ LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint
       plen[pi] = fit ? pgot + hl : pgot;
       pcrc[pi] = fit ? pack_crc(pcv, h, pk->T) : pcv;
     }
-    Rec R;
-    R.rec_off = p;
-    R.payload_off = p + hl;
-    R.klen = h.klen;
-    R.vlen = h.vlen;
-    R.crc = h.crc;
-    R.type = h.t;
-    recs[i] = R;
+    put_rec(recs + i, p, p + hl, h.klen, h.vlen, h.crc, h.t);
     poff[i] = p + hl;
     if (pk) {
       pi = i;
@@ -729,14 +752,7 @@ template <class Rec>
 LSMCK_HD void seg_place_rec(const SegArgs& a, uint32_t k, uint64_t at, Rec* recs, uint64_t* poff, uint32_t* plen,
                             uint32_t* pcrc, uint32_t r, const StageRec& R, const Head& nh, const Pack* pk) {
   const uint64_t i = at + (a.pre[k] & kRecMask) + r;
-  Rec O;
-  O.rec_off = R.rec_off;
-  O.payload_off = R.payload_off;
-  O.klen = R.klen;
-  O.vlen = R.vlen;
-  O.crc = R.crc;
-  O.type = R.type;
-  recs[i] = O;
+  put_rec(recs + i, R.rec_off, R.payload_off, R.klen, R.vlen, R.crc, R.type);
   poff[i] = R.payload_off;
   const uint32_t dlen = R.klen + R.vlen;
   const uint64_t avail = a.n - R.payload_off;

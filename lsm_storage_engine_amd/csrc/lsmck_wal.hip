@@ -24,6 +24,9 @@
 #include <stdint.h>
 
 #ifdef LSMCK_SEG_CLOCK  // diagnostic builds only: the segment walk's clock marks per segment
+#ifndef LSMCK_DIAG
+#define LSMCK_DIAG  // (lsmck_segwalk.h then takes its marks from lsmck_diag.h)
+#endif
 __device__ uint64_t g_seg_clock[3 * 131072];
 #define LSMCK_SEG_CLOCK_MARK(k, slot) \
   do {                                  \
@@ -515,7 +518,8 @@ __global__ void wal_seg_repair(seg::SegArgs a, uint32_t budget) {
   if (j < a.K) seg::seg_repair(a, j, budget);
 }
 
-__global__ __launch_bounds__(256) void wal_seg_emit(seg::SegArgs a, uint64_t at, lsmck_wal_rec* __restrict__ recs,
+template <class Rec>
+__global__ __launch_bounds__(256) void wal_seg_emit(seg::SegArgs a, uint64_t at, Rec* __restrict__ recs,
                                                      uint64_t* __restrict__ poff, uint32_t* __restrict__ plen,
                                                      uint32_t* __restrict__ pcrc) {
   // one thread per sub-segment (a.nsub per segment; 1: per segment)
@@ -543,7 +547,8 @@ __device__ __forceinline__ void build_crc_tables(uint32_t* T) {
 
 // The same with packed CRC spans (seg::Pack): the expected CRC of each span
 // from its record's stored CRC and the next header (seg::pack_crc).
-__global__ __launch_bounds__(256) void wal_seg_emit_packed(seg::SegArgs a, uint64_t at, lsmck_wal_rec* __restrict__ recs,
+template <class Rec>
+__global__ __launch_bounds__(256) void wal_seg_emit_packed(seg::SegArgs a, uint64_t at, Rec* __restrict__ recs,
                                                             uint64_t* __restrict__ poff, uint32_t* __restrict__ plen,
                                                             uint32_t* __restrict__ pcrc, uint64_t iend) {
   __shared__ uint32_t T[1024];
@@ -559,8 +564,8 @@ __global__ __launch_bounds__(256) void wal_seg_emit_packed(seg::SegArgs a, uint6
 // second walk of the headers seg_emit_thread makes for a segment with more
 // records than slots.  A lane takes the next record's header fields from the
 // next lane (lane 63 and the segment's last record read them).
-template <bool PACK>
-__global__ __launch_bounds__(256) void wal_seg_place(seg::SegArgs a, uint64_t at, lsmck_wal_rec* __restrict__ recs,
+template <bool PACK, class Rec>
+__global__ __launch_bounds__(256) void wal_seg_place(seg::SegArgs a, uint64_t at, Rec* __restrict__ recs,
                                                      uint64_t* __restrict__ poff, uint32_t* __restrict__ plen,
                                                      uint32_t* __restrict__ pcrc, uint64_t iend) {
   __shared__ uint32_t T[1024];
@@ -587,6 +592,17 @@ __global__ __launch_bounds__(256) void wal_seg_place(seg::SegArgs a, uint64_t at
       if (r < cnt && (lane == 63u || r + 1u == cnt) && i0 + r + 1u < iend) nh = seg::seg_place_next_head(a, k, r);
     }
     if (r < cnt) seg::seg_place_rec(a, k, at, recs, poff, plen, pcrc, r, R, nh, PACK ? &pk : nullptr);
+  }
+}
+
+// 32-byte records -> the compact form (seg::put_rec), for the walks that
+// emit the wide layout (candidate doubling) when the caller asked for lsmck_wal_rec16
+__global__ __launch_bounds__(256) void wal_recs_compact(const lsmck_wal_rec* __restrict__ in,
+                                                        seg::Compact16* __restrict__ out, uint64_t m) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) {
+    const lsmck_wal_rec r = in[i];
+    seg::put_rec(out + i, r.rec_off, r.payload_off, r.klen, r.vlen, r.crc, r.type);
   }
 }
 
@@ -650,31 +666,58 @@ extern "C" int lsmk_wal_seg_repair(const seg::SegArgs* a, uint32_t budget, hipSt
   return launch_err();
 }
 
-extern "C" int lsmk_wal_seg_emit(const seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff,
+// recs: lsmck_wal_rec[] or, compact, lsmck_wal_rec16[] (seg::Compact16)
+extern "C" int lsmk_wal_seg_emit(const seg::SegArgs* a, uint64_t at, void* recs, int compact, uint64_t* poff,
                                  uint32_t* plen, uint32_t* pcrc, hipStream_t st) {
-  const uint64_t threads = (uint64_t)a->K * a->nsub;
-  hipLaunchKernelGGL(wal_seg_emit, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, *a, at, recs, poff, plen,
-                     pcrc);
+  const dim3 g((unsigned)(((uint64_t)a->K * a->nsub + 255) / 256));
+  if (compact)
+    hipLaunchKernelGGL(wal_seg_emit<seg::Compact16>, g, dim3(256), 0, st, *a, at, (seg::Compact16*)recs, poff, plen,
+                       pcrc);
+  else
+    hipLaunchKernelGGL(wal_seg_emit<lsmck_wal_rec>, g, dim3(256), 0, st, *a, at, (lsmck_wal_rec*)recs, poff, plen,
+                       pcrc);
   return launch_err();
 }
 
-extern "C" int lsmk_wal_seg_emit_packed(const seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff,
+extern "C" int lsmk_wal_seg_emit_packed(const seg::SegArgs* a, uint64_t at, void* recs, int compact, uint64_t* poff,
                                         uint32_t* plen, uint32_t* pcrc, uint64_t iend, hipStream_t st) {
-  const uint64_t threads = (uint64_t)a->K * a->nsub;
-  hipLaunchKernelGGL(wal_seg_emit_packed, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, *a, at, recs, poff,
-                     plen, pcrc, iend);
+  const dim3 g((unsigned)(((uint64_t)a->K * a->nsub + 255) / 256));
+  if (compact)
+    hipLaunchKernelGGL(wal_seg_emit_packed<seg::Compact16>, g, dim3(256), 0, st, *a, at, (seg::Compact16*)recs, poff,
+                       plen, pcrc, iend);
+  else
+    hipLaunchKernelGGL(wal_seg_emit_packed<lsmck_wal_rec>, g, dim3(256), 0, st, *a, at, (lsmck_wal_rec*)recs, poff,
+                       plen, pcrc, iend);
   return launch_err();
 }
 
-extern "C" int lsmk_wal_seg_place(const seg::SegArgs* a, uint64_t at, lsmck_wal_rec* recs, uint64_t* poff,
+template <bool PACK, class Rec>
+static void seg_place_launch(const seg::SegArgs* a, uint64_t at, Rec* recs, uint64_t* poff, uint32_t* plen,
+                             uint32_t* pcrc, uint64_t iend, hipStream_t st) {
+  hipLaunchKernelGGL((wal_seg_place<PACK, Rec>), dim3((a->K + 3u) / 4u), dim3(256), 0, st, *a, at, recs, poff, plen,
+                     pcrc, iend);
+}
+extern "C" int lsmk_wal_seg_place(const seg::SegArgs* a, uint64_t at, void* recs, int compact, uint64_t* poff,
                                   uint32_t* plen, uint32_t* pcrc, uint64_t iend, int packed, hipStream_t st) {
   if (!a->scap || !a->K) return 0;
-  if (packed)
-    hipLaunchKernelGGL(wal_seg_place<true>, dim3((a->K + 3u) / 4u), dim3(256), 0, st, *a, at, recs, poff, plen, pcrc,
-                       iend);
-  else
-    hipLaunchKernelGGL(wal_seg_place<false>, dim3((a->K + 3u) / 4u), dim3(256), 0, st, *a, at, recs, poff, plen, pcrc,
-                       iend);
+  if (compact) {
+    if (packed)
+      seg_place_launch<true>(a, at, (seg::Compact16*)recs, poff, plen, pcrc, iend, st);
+    else
+      seg_place_launch<false>(a, at, (seg::Compact16*)recs, poff, plen, pcrc, iend, st);
+  } else {
+    if (packed)
+      seg_place_launch<true>(a, at, (lsmck_wal_rec*)recs, poff, plen, pcrc, iend, st);
+    else
+      seg_place_launch<false>(a, at, (lsmck_wal_rec*)recs, poff, plen, pcrc, iend, st);
+  }
+  return launch_err();
+}
+
+extern "C" int lsmk_wal_recs_compact(const lsmck_wal_rec* in, void* out, uint64_t m, hipStream_t st) {
+  if (m == 0) return 0;
+  hipLaunchKernelGGL(wal_recs_compact, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, in, (seg::Compact16*)out,
+                     m);
   return launch_err();
 }
 

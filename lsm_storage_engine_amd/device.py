@@ -83,13 +83,13 @@ class PinnedBuffer:
 
 
 class _PinnedRecords:
-    """numpy's view of a PinnedBuffer as lsmck_wal_rec[n]: the arrays made
-    from it keep it (and the page-locked memory) alive."""
+    """numpy's view of a PinnedBuffer as lsmck_wal_rec[n] (or another record
+    dtype): the arrays made from it keep it (and the page-locked memory) alive."""
 
-    def __init__(self, pb, n):
+    def __init__(self, pb, n, dtype):
         self.pb = pb
-        self.__array_interface__ = {"data": (pb.ptr, False), "shape": (n,), "typestr": WAL_REC_DTYPE.str,
-                                    "descr": WAL_REC_DTYPE.descr, "version": 3}
+        self.__array_interface__ = {"data": (pb.ptr, False), "shape": (n,), "typestr": dtype.str,
+                                    "descr": dtype.descr, "version": 3}
 
 
 class Context:
@@ -100,38 +100,42 @@ class Context:
         if not self.handle:
             raise RuntimeError(f"lsmck_ctx_create({device}) failed: {_lib.last_error()}")
         self.device = device
-        self._wal_recs = None  # records array of the last WAL replay, reused once nothing refers to it
-        self._wal_pinned = None  # page-locked records array of pinned_recs replays (reused like _wal_recs)
+        # records arrays of the last WAL replays per record dtype (pageable, page-locked),
+        # reused once nothing refers to them
+        self._wal_recs = {}
+        self._wal_pinned = {}
 
-    def _wal_recs_buffer(self, cap):
-        """An uninitialised WAL_REC_DTYPE array of at least cap entries: the
-        last replay's array again when no result refers to it any more (its
-        pages are already mapped: a fresh worst-case n/9-entry array cost ~1 ms
-        per 0.24 GB replay in allocation, first-touch faults and unmapping),
-        else a new one."""
-        buf = self._wal_recs
-        # references: self._wal_recs, `buf`, getrefcount's argument -- any
-        # more is a returned view still alive
+    def _wal_recs_buffer(self, cap, dtype=None):
+        """An uninitialised record array (WAL_REC_DTYPE, or WAL_REC16_DTYPE) of
+        at least cap entries: the last replay's array again when no result
+        refers to it any more (its pages are already mapped: a fresh worst-case
+        n/9-entry array cost ~1 ms per 0.24 GB replay in allocation,
+        first-touch faults and unmapping), else a new one."""
+        dtype = WAL_REC_DTYPE if dtype is None else dtype
+        buf = self._wal_recs.get(dtype.str)
+        # references: the dict's, `buf`, getrefcount's argument -- any more is
+        # a returned view still alive
         if buf is not None and len(buf) >= cap and sys.getrefcount(buf) <= 3:
             return buf
-        buf = np.empty(cap, dtype=WAL_REC_DTYPE)  # lsmck_wal_rec[cap], uninitialised: no 32-B-per-slot zeroing
-        self._wal_recs = buf
+        buf = np.empty(cap, dtype=dtype)  # uninitialised: no zeroing of every slot
+        self._wal_recs[dtype.str] = buf
         return buf
 
-    def _wal_recs_pinned(self, cap):
-        """A page-locked WAL_REC_DTYPE array of at least cap entries (grow-only,
+    def _wal_recs_pinned(self, cap, dtype=None):
+        """A page-locked record array of at least cap entries (grow-only,
         reused once no result refers to it): the replay DMAs the records into it
         (LSMCK_RECS_PINNED).  The array's base is a holder of its PinnedBuffer,
         so the pinned memory lives as long as any view of it."""
-        arr = self._wal_pinned
+        dtype = WAL_REC_DTYPE if dtype is None else dtype
+        arr = self._wal_pinned.get(dtype.str)
         if arr is not None and len(arr) >= cap and sys.getrefcount(arr) <= 3:
             return arr
-        arr = np.asarray(_PinnedRecords(PinnedBuffer(self, max(1, cap) * WAL_REC_DTYPE.itemsize), max(1, cap)))
-        self._wal_pinned = arr
+        arr = np.asarray(_PinnedRecords(PinnedBuffer(self, max(1, cap) * dtype.itemsize), max(1, cap), dtype))
+        self._wal_pinned[dtype.str] = arr
         return arr
 
     def close(self):
-        self._wal_pinned = None
+        self._wal_pinned = {}
         if self.handle:
             self.lib.lsmck_ctx_destroy(self.handle)
             self.handle = None
@@ -256,13 +260,15 @@ class Context:
         _lib.check(self.lib.lsmck_wal_frame_insert_device(self.handle, img_ptr, off_ptr, len_ptr, crc_ptr, n, kmax,
                                                            stream), "wal_frame_insert_device")
 
-    def wal_replay_verify(self, image, device_ptr=None, cap=None, pinned_recs=False):
+    def wal_replay_verify(self, image, device_ptr=None, cap=None, pinned_recs=False, compact=False):
         """Returns (records, status, (bad_index, bad_crc, bad_expected)).
         cap: records to return at most (default: the n/9 + 1 a log of n
         bytes can hold; a very large log whose record count is known can ask
         for fewer -- the status and the count cover the whole log).
         pinned_recs: the records land in a page-locked array by DMA
-        (LSMCK_RECS_PINNED; cap entries stay pinned for the context's life)."""
+        (LSMCK_RECS_PINNED; cap entries stay pinned for the context's life).
+        compact: 16-byte records (lsmck_wal_replay_verify16, WAL_REC16_DTYPE;
+        decode_rec16 gives the 32-byte form's fields)."""
         if device_ptr is None:
             # any buffer (bytes, bytearray, memoryview, a read-only mmap of the
             # log file) is read in place: no copy of the image
@@ -271,25 +277,27 @@ class Context:
         else:
             ptr, n, flags = device_ptr, image, _lib.DEVICE
         cap = n // 9 + 1 if cap is None else cap  # a record is at least 9 bytes (Remove of an empty key)
+        dtype = WAL_REC16_DTYPE if compact else WAL_REC_DTYPE
         if pinned_recs:
-            recs = self._wal_recs_pinned(cap)
+            recs = self._wal_recs_pinned(cap, dtype)
             flags |= _lib.RECS_PINNED
         else:
-            recs = self._wal_recs_buffer(cap)
+            recs = self._wal_recs_buffer(cap, dtype)
         nrec = C.c_size_t()
         bi, bc, be = C.c_uint64(), C.c_uint32(), C.c_uint32()
-        rc = _lib.check(self.lib.lsmck_wal_replay_verify(self.handle, ptr, n, flags, recs.ctypes.data, cap,
-                                                         C.byref(nrec), C.byref(bi), C.byref(bc), C.byref(be)),
-                        "wal_replay_verify")
+        fn = self.lib.lsmck_wal_replay_verify16 if compact else self.lib.lsmck_wal_replay_verify
+        rc = _lib.check(fn(self.handle, ptr, n, flags, recs.ctypes.data, cap, C.byref(nrec), C.byref(bi),
+                           C.byref(bc), C.byref(be)), "wal_replay_verify")
         # np.recarray: record fields read as attributes (r.payload_off), like the ctypes struct
         # nrec counts the whole log's accepted records; at most cap of them were written
         return recs[:min(nrec.value, cap)].view(np.recarray), rc, (bi.value, bc.value, be.value)
 
-    def wal_replay_verify_to_device(self, image, recs_ptr, cap, device_ptr=None):
+    def wal_replay_verify_to_device(self, image, recs_ptr, cap, device_ptr=None, compact=False):
         """The replay with its records left in device memory (LSMCK_RECS_DEVICE):
         recs_ptr is a device array of cap lsmck_wal_rec entries (32 bytes each,
-        WAL_REC_DTYPE).  Returns (nrec, status, (bad_index, bad_crc, bad_expected));
-        min(nrec, cap) records were written."""
+        WAL_REC_DTYPE; compact: lsmck_wal_rec16, 16 bytes, WAL_REC16_DTYPE).
+        Returns (nrec, status, (bad_index, bad_crc, bad_expected)); min(nrec, cap)
+        records were written."""
         if device_ptr is None:
             img = np.frombuffer(image, dtype=np.uint8) if len(image) else np.zeros(1, dtype=np.uint8)[:0]
             ptr, n, flags = img.ctypes.data, len(img), _lib.HOST
@@ -297,9 +305,9 @@ class Context:
             ptr, n, flags = device_ptr, image, _lib.DEVICE
         nrec = C.c_size_t()
         bi, bc, be = C.c_uint64(), C.c_uint32(), C.c_uint32()
-        rc = _lib.check(self.lib.lsmck_wal_replay_verify(self.handle, ptr, n, flags | _lib.RECS_DEVICE, recs_ptr, cap,
-                                                         C.byref(nrec), C.byref(bi), C.byref(bc), C.byref(be)),
-                        "wal_replay_verify")
+        fn = self.lib.lsmck_wal_replay_verify16 if compact else self.lib.lsmck_wal_replay_verify
+        rc = _lib.check(fn(self.handle, ptr, n, flags | _lib.RECS_DEVICE, recs_ptr, cap, C.byref(nrec), C.byref(bi),
+                           C.byref(bc), C.byref(be)), "wal_replay_verify")
         return nrec.value, rc, (bi.value, bc.value, be.value)
 
     def checksums_verify_many(self, triples):
@@ -440,6 +448,21 @@ class MultiContext:
 WAL_REC_DTYPE = np.dtype([("rec_off", "<u8"), ("payload_off", "<u8"), ("klen", "<u4"), ("vlen", "<u4"),
                           ("crc", "<u4"), ("type", "<u4")])
 assert WAL_REC_DTYPE.itemsize == C.sizeof(_lib.WalRec)
+# include/lsmck.h lsmck_wal_rec16 (16 bytes): lsmck_wal_replay_verify16's compact records
+WAL_REC16_DTYPE = np.dtype([("payload_type", "<u8"), ("klen", "<u4"), ("vlen", "<u4")])
+assert WAL_REC16_DTYPE.itemsize == C.sizeof(_lib.WalRec16)
+
+
+def decode_rec16(recs):
+    """Compact records as the 32-byte form's fields: a dict of arrays rec_off,
+    payload_off, klen, vlen, type (the stored CRC is not kept: it is the
+    computed one for every accepted record)."""
+    pt = np.asarray(recs["payload_type"], dtype=np.uint64)
+    remove = (pt >> np.uint64(63)).astype(bool)
+    payload = pt & np.uint64(_lib.WAL_REC16_REMOVE - 1)
+    typ = np.where(remove, 2, 1).astype(np.uint32)
+    return {"rec_off": payload - np.where(remove, 9, 13).astype(np.uint64), "payload_off": payload,
+            "klen": np.asarray(recs["klen"]), "vlen": np.asarray(recs["vlen"]), "type": typ}
 
 
 def device_count():

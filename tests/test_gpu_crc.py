@@ -317,10 +317,10 @@ def test_config3w_full_size_summary(ctx):
     entry point: the stream kernel takes the gapped batch, and the CRC-32 of
     the whole output array equals the oracle's (make_summaries.py config3w).
     Then the headers are written in front of the payloads (type 1, those CRCs,
-    klen = min(len, 16)) and the 97.8 GiB log is replayed on the GPU: the header
-    walk in parts (its jump tables for the whole log would not fit), every
-    record found at its offset, every stored CRC checked, the records' CRC
-    summary again the oracle's."""
+    klen = min(len, 16)) and the 97.8 GiB log is replayed on the GPU: the
+    segment walk of the headers (lsmck_segwalk.h, one pass over the whole log),
+    every record found at its offset, every stored CRC checked, the records'
+    CRC summary again the oracle's; then once more with compact records.""" 
     import zlib
     from lsm_storage_engine_amd.device import gen_zipf_lengths
     g = _summaries()["config3w"]
@@ -357,6 +357,15 @@ def test_config3w_full_size_summary(ctx):
         assert np.array_equal(recs.rec_off, off - np.uint64(13))
         assert np.array_equal(recs.klen.astype(np.uint64) + recs.vlen, ln.astype(np.uint64))
         assert "%08x" % zlib.crc32(np.ascontiguousarray(recs.crc).astype("<u4").tobytes()) == g["summary_crc32"]
+        del recs
+        # the compact records (lsmck_wal_replay_verify16) into a page-locked
+        # array by the SDMA read-back: every record at its offset, an Insert
+        recs, st, bad = ctx.wal_replay_verify(total, device_ptr=d.ptr, cap=n, pinned_recs=True, compact=True)
+        assert st == 0, bad
+        assert len(recs) == n and recs.dtype.itemsize == 16
+        assert np.array_equal(recs.payload_type, off)  # (bit 63 clear: Insert)
+        assert np.array_equal(recs.klen.astype(np.uint64) + recs.vlen, ln.astype(np.uint64))
+        del recs
     finally:
         for buf in (d, d_o, d_l, out):
             buf.free()

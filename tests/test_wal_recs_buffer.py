@@ -2,31 +2,45 @@
 result still refers to it (host logic; no GPU)."""
 import numpy as np
 
-from lsm_storage_engine_amd.device import Context
+from lsm_storage_engine_amd.device import WAL_REC16_DTYPE, WAL_REC_DTYPE, Context
 
 
 class _Ctx(Context):
     def __init__(self):  # no device: only the buffer logic
-        self._wal_recs = None
+        self._wal_recs = {}
         self.handle = None
 
-    def replay(self, cap=100):
-        recs = self._wal_recs_buffer(cap)
+    def replay(self, cap=100, dtype=WAL_REC_DTYPE):
+        recs = self._wal_recs_buffer(cap, dtype)
         return recs[:10].view(np.recarray), 0
+
+    def cur(self, dtype=WAL_REC_DTYPE):
+        return self._wal_recs[dtype.str]
 
 
 def test_records_array_reused_only_when_released():
     c = _Ctx()
     r1, _ = c.replay()
-    id1 = id(c._wal_recs)
+    id1 = id(c.cur())
     r2, _ = c.replay()
-    assert id(c._wal_recs) != id1  # r1 still alive: a fresh array
-    id2 = id(c._wal_recs)
+    assert id(c.cur()) != id1  # r1 still alive: a fresh array
+    id2 = id(c.cur())
     del r1, r2
     r3, _ = c.replay()
-    assert id(c._wal_recs) == id2  # nothing refers to it: reused
+    assert id(c.cur()) == id2  # nothing refers to it: reused
     r3[0]["crc"] = 5
     r4, _ = c.replay()
-    assert id(c._wal_recs) != id2 and r3[0]["crc"] == 5  # r3 untouched by the next replay
+    assert id(c.cur()) != id2 and r3[0]["crc"] == 5  # r3 untouched by the next replay
     r5, _ = c.replay(cap=10**6)
-    assert len(c._wal_recs) >= 10**6  # grows when a larger log needs it
+    assert len(c.cur()) >= 10**6  # grows when a larger log needs it
+
+
+def test_compact_records_have_their_own_array():
+    c = _Ctx()
+    r1, _ = c.replay()
+    r2, _ = c.replay(dtype=WAL_REC16_DTYPE)
+    assert c.cur(WAL_REC16_DTYPE).dtype.itemsize == 16 and c.cur().dtype.itemsize == 32
+    del r1, r2
+    i16 = id(c.cur(WAL_REC16_DTYPE))
+    c.replay(dtype=WAL_REC16_DTYPE)
+    assert id(c.cur(WAL_REC16_DTYPE)) == i16  # reused within its own dtype

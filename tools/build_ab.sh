@@ -15,5 +15,5 @@ else
   git -C $ROOT archive $REV include lsm_storage_engine_amd/csrc | tar -x -C $D
 fi
 mkdir -p $ROOT/lsm_storage_engine_amd/ab
-make -s -j8 -C $D/lsm_storage_engine_amd/csrc EXTRA="-DLSMCK_AB_ABLATIONS $EXTRA" OUT=$ROOT/lsm_storage_engine_amd/ab/$NAME.so $ROOT/lsm_storage_engine_amd/ab/$NAME.so 2>&1 | grep -v hip-link || true
+make -s -j8 -C $D/lsm_storage_engine_amd/csrc EXTRA="-DLSMCK_AB_ABLATIONS -DLSMCK_DIAG $EXTRA" OUT=$ROOT/lsm_storage_engine_amd/ab/$NAME.so $ROOT/lsm_storage_engine_amd/ab/$NAME.so 2>&1 | grep -v hip-link || true
 ls -la $ROOT/lsm_storage_engine_amd/ab/$NAME.so

@@ -9,7 +9,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 CSRC = os.path.join(ROOT, "lsm_storage_engine_amd", "csrc")
-for so, extra in (("/tmp/segwalk_sim_shipped.so", []), ("/tmp/segwalk_sim_later.so", ["-DLSMCK_SEG_LATER_ALWAYS"])):
+for so, extra in (("/tmp/segwalk_sim_shipped.so", []), ("/tmp/segwalk_sim_later.so", ["-DLSMCK_DIAG", "-DLSMCK_SEG_LATER_ALWAYS"])):
     subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-I", CSRC, *extra, "-o", so,
                     os.path.join(ROOT, "tools", "segwalk_sim.cpp")], check=True)
 from oracle import oracle as O

@@ -11,6 +11,11 @@ copied back to the host (into a page-locked array: LSMCK_RECS_PINNED).
 (LSMCK_RECS_DEVICE), --seg-sweep a segment-size A/B of those.  Every step
 checks the record count and the CRC summary against the oracle's
 (tests/golden/summaries.json config3w), then prints one JSON line.
+--compact 1: the records in the 16-byte form (lsmck_wal_replay_verify16):
+they carry no stored CRC, so every step checks every record against the
+framing instead (payload offset, Insert, klen = min(len, 16), vlen = the
+rest), the replay's status covering the CRCs; --dma-engines sets the SDMA
+engines of the read-back (0: hipMemcpyAsync).
 
   python3 tools/wal_replay_big.py [--steps 3] [--records 67108864] [--device-recs 1]
 (LSMCK_WAL_TRACE=1 prints the replay's phases to stderr.)"""
@@ -48,6 +53,8 @@ def main():
     ap.add_argument("--raw-reps", type=int, default=0,
                     help="A/B: time the plain batch CRC (lsmck_crc32_device) over the framed log's packed spans "
                          "and over its payloads alone, this many times each, before the replays")
+    ap.add_argument("--compact", type=int, default=0, help="1: 16-byte records (lsmck_wal_replay_verify16)")
+    ap.add_argument("--dma-engines", type=int, default=-1, help="wal_dma_engines (-1: the default)")
     a = ap.parse_args()
     n = a.records
     ln = gen_zipf_lengths(0x5EED0003, n)
@@ -64,6 +71,12 @@ def main():
     ctx.set_option("wal_seg_walk", a.seg_walk)
     ctx.set_option("wal_seg_pack", a.seg_pack)
     ctx.set_option("wal_seg_stage", a.seg_stage)
+    if a.dma_engines >= 0:
+        ctx.set_option("wal_dma_engines", a.dma_engines)
+    kl = np.minimum(ln, 16).astype(np.uint32)  # the framing's key / value split (lsmck_wal_frame_insert_device)
+
+    def check_compact(recs):  # every record against the framing
+        assert (recs["payload_type"] == off).all() and (recs["klen"] == kl).all() and (recs["vlen"] == ln - kl).all()
     d = ctx.alloc(total + 64)
     d_o, d_l, out = ctx.alloc(off.nbytes), ctx.alloc(ln.nbytes), ctx.alloc(4 * n)
     ctx.gen_stream(d.ptr, 0x5EED0003, 0, total)
@@ -94,25 +107,31 @@ def main():
     for s in range(a.steps + 1):  # the first replay is a warm-up
         ctx.sync()
         t = time.perf_counter()
-        recs, st, bad = ctx.wal_replay_verify(total, device_ptr=d.ptr, cap=n, pinned_recs=bool(a.pinned_recs))
+        recs, st, bad = ctx.wal_replay_verify(total, device_ptr=d.ptr, cap=n, pinned_recs=bool(a.pinned_recs),
+                                              compact=bool(a.compact))
         dt = time.perf_counter() - t
         assert st == 0 and len(recs) == n, (st, len(recs), bad)
-        summary = "%08x" % zlib.crc32(np.ascontiguousarray(recs.crc).astype("<u4").tobytes())
-        if golden:
-            assert summary == golden["summary_crc32"], summary
+        if a.compact:
+            check_compact(recs)
+            summary = "every record = the framing"
+        else:
+            summary = "%08x" % zlib.crc32(np.ascontiguousarray(recs.crc).astype("<u4").tobytes())
+            if golden:
+                assert summary == golden["summary_crc32"], summary
         if s:
             times.append(dt)
         print(f"replay {s}: {dt * 1e3:.1f} ms", file=sys.stderr, flush=True)
         del recs  # the wrapper reuses its records array once no result refers to it
     dev = None
     if a.device_recs:  # the records stay in HBM: the walk, the CRC pass and the compare, no host link
-        from lsm_storage_engine_amd.device import WAL_REC_DTYPE
-        rb = ctx.alloc(n * WAL_REC_DTYPE.itemsize)
+        from lsm_storage_engine_amd.device import WAL_REC16_DTYPE, WAL_REC_DTYPE
+        RD = WAL_REC16_DTYPE if a.compact else WAL_REC_DTYPE
+        rb = ctx.alloc(n * RD.itemsize)
         dts = []
         for s in range(a.steps + 1):
             ctx.sync()
             t = time.perf_counter()
-            m, st, bad = ctx.wal_replay_verify_to_device(total, rb.ptr, n, device_ptr=d.ptr)
+            m, st, bad = ctx.wal_replay_verify_to_device(total, rb.ptr, n, device_ptr=d.ptr, compact=bool(a.compact))
             dt = time.perf_counter() - t
             assert st == 0 and m == n, (st, m, bad)
             if s:
@@ -125,7 +144,7 @@ def main():
             for s in range(a.steps + 1):
                 ctx.sync()
                 t = time.perf_counter()
-                m, st, bad = ctx.wal_replay_verify_to_device(total, rb.ptr, n, device_ptr=d.ptr)
+                m, st, bad = ctx.wal_replay_verify_to_device(total, rb.ptr, n, device_ptr=d.ptr, compact=bool(a.compact))
                 dt = time.perf_counter() - t
                 assert st == 0 and m == n, (st, m, bad)
                 if s:
@@ -136,13 +155,18 @@ def main():
         ctx.set_option("wal_seg_bytes", 0)
         if a.raw_reps:  # the same batch again after the replays (order effects)
             raw_batch("packed spans, after the replays", lp, "packed_spans_after")
-        crc = rb.download(np.uint8, n * WAL_REC_DTYPE.itemsize).view(WAL_REC_DTYPE)["crc"]
-        dsum = "%08x" % zlib.crc32(np.ascontiguousarray(crc).astype("<u4").tobytes())
+        got = rb.download(np.uint8, n * RD.itemsize).view(RD)
+        if a.compact:
+            check_compact(got)
+            dsum = "every record = the framing"
+        else:
+            dsum = "%08x" % zlib.crc32(np.ascontiguousarray(got["crc"]).astype("<u4").tobytes())
         rb.free()
         dmed = float(np.median(dts))
         dev = {"ms_median": round(dmed * 1e3, 2), "ms_best": round(min(dts) * 1e3, 2),
                "value": round(total / GIB / dmed, 1), "summary_crc32": dsum,
-               "summary_matches_oracle": bool(golden) and dsum == golden["summary_crc32"], "seg_sweep": sweep}
+               "summary_matches_oracle": bool(golden) and (a.compact or dsum == golden["summary_crc32"]),
+               "seg_sweep": sweep}
     for b in (d_o, d_l, out):
         b.free()
     d.free()
@@ -152,7 +176,8 @@ def main():
         "value": round(total / GIB / med, 1), "unit": "GiB/s of log",
         "log_bytes": total, "records": n, "ms_median": round(med * 1e3, 2), "ms_best": round(best * 1e3, 2),
         "steps": a.steps, "summary_crc32": summary, "summary_matches_oracle": bool(golden) and True,
-        "records_out_bytes": 32 * n, "pinned_recs": bool(a.pinned_recs),
+        "records_out_bytes": (16 if a.compact else 32) * n, "pinned_recs": bool(a.pinned_recs),
+        "compact": bool(a.compact), "recs_dma_engines": ctx.get_stat("wal_recs_dma"),
         "walk_path": {1: "segment walk", 2: "candidate doubling", 3: "host walk"}.get(ctx.get_stat("wal_walk_path")),
         "seg_repairs": ctx.get_stat("wal_seg_repairs"), "segments": ctx.get_stat("wal_segments"),
         "records_on_device": dev, "raw_batch_crc_ms": raw,
