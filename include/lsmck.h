@@ -228,6 +228,10 @@ int lsmck_device_count(void);
  *                 ~2^16 segments; else 64..2^30).  Tests use small segments.
  *   "wal_seg_rounds"  segment walk: check failures repaired before it
  *                 declines to candidate doubling (default 16).
+ *   "wal_seg_prepair"  segment walk: parallel repair rounds (every segment
+ *                 walked again from its predecessor's exit at once) after a
+ *                 check with several failures, before the serial repairs
+ *                 (default 2; 0 = none).
  *   "wal_seg_pack"  segment walk: 1 = the CRC pass runs over packed spans,
  *                 each payload with the next record's header, the header
  *                 then taken back out of the CRC (default); 0 = over the
@@ -252,6 +256,7 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
  *                    3 = host walk.
  *   "wal_seg_repairs"  its segment walk's repaired check failures.
  *   "wal_segments"   its segment walk's segment count.
+ *   "wal_seg_prepairs"  its segment walk's parallel repair rounds.
  *   "wal_recs_dma"   its records' read-back to the host: the SDMA engines it
  *                    was dealt over, 0 = hipMemcpyAsync (or none read back).
  *   "numa_node"      the device's NUMA node (sysfs of its PCI function; -1

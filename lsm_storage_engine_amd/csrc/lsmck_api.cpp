@@ -330,6 +330,10 @@ struct lsmck_ctx {
     size_t cap_cp = 0;
     lsmck::seg::StageRec* sst = nullptr;  // walk-time staged records (K * scap)
     size_t cap_sst = 0;
+    uint64_t* sg0 = nullptr;  // the parallel repair's snapshot of sg / sx / scode
+    uint64_t* sx0 = nullptr;
+    uint32_t* scode0 = nullptr;
+    size_t cap_seg0 = 0;
   } wd;
   bool wal_recs_direct = false;  // this replay's records go by DMA into the caller's pinned array (under wal_mu)
   bool wal_compact = false;      // this replay's records are lsmck_wal_rec16 (under wal_mu)
@@ -344,6 +348,7 @@ struct lsmck_ctx {
   bool wal_seg_pack = true;  // segment walk: packed CRC spans (seg::Pack) for the CRC pass
   long wal_seg_stage = 1;    // segment walk: staged records (seg::StageRec): 0 off, 1 auto slots, else slots per segment
   int wal_seg_rounds = 16;   // segment walk: repairs before it declines to the candidate-doubling walk
+  int wal_seg_prepair = 2;   // segment walk: parallel repair rounds before the serial repairs (0 = none)
   int numa_node = -1;    // the device's NUMA node (sysfs), -1 unknown
   int stage_numa = -2;   // option "stage_numa": -2 the device's node on a multi-node host, -1 off, >= 0 that node
   int pin_node = -1;     // in effect: pinned buffers and copy threads on this node (-1: none)
@@ -352,6 +357,7 @@ struct lsmck_ctx {
   std::atomic<int> last_walk_path{0};
   std::atomic<int> last_seg_repairs{0};
   std::atomic<uint64_t> last_segments{0};
+  std::atomic<int> last_seg_prepairs{0};
   uint8_t* h_wrecs = nullptr;  // device WAL replay: the records' pinned landing buffer (bytes; grow-only)
   size_t cap_hwrecs = 0;
   // the records' read-back on the SDMA engines (lsmck_dma.h): created on first
@@ -1016,6 +1022,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->wal_seg_pack = value != 0;
     return 0;
   }
+  if (!strcmp(key, "wal_seg_prepair")) {  // segment walk: parallel repair rounds before serial repairs (0 = none)
+    if (value < 0 || value > 64) return lsmck_host::set_error(LSMCK_EINVAL, "wal_seg_prepair: 0..64");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_seg_prepair = (int)value;
+    return 0;
+  }
   if (!strcmp(key, "wal_seg_rounds")) {  // segment walk: repair rounds before declining (0 = decline on any failure)
     if (value < 0 || value > 1024) return lsmck_host::set_error(LSMCK_EINVAL, "wal_seg_rounds: 0..1024");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1086,6 +1098,8 @@ int lsmck_ctx_get_stat(lsmck_ctx* ctx, const char* key, long* value) {
     *value = ctx->last_seg_repairs.load();
   } else if (!strcmp(key, "wal_segments")) {
     *value = (long)ctx->last_segments.load();
+  } else if (!strcmp(key, "wal_seg_prepairs")) {  // the last segment walk's parallel repair rounds
+    *value = ctx->last_seg_prepairs.load();
   } else if (!strcmp(key, "wal_recs_dma")) {  // the last records read-back: SDMA engines (0: hipMemcpyAsync)
     *value = ctx->last_recs_dma.load();
   } else if (!strcmp(key, "numa_node")) {
@@ -1119,7 +1133,8 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   if (ctx->wd.h_info) (void)hipHostFree(ctx->wd.h_info);
   for (void* p : {(void*)ctx->wd.sg, (void*)ctx->wd.sx, (void*)ctx->wd.spre, (void*)ctx->wd.scode,
                   (void*)ctx->wd.srecs, (void*)ctx->wd.sbsum, (void*)ctx->wd.sinfo, (void*)ctx->wd.scpp,
-                  (void*)ctx->wd.scpc, (void*)ctx->wd.sst})
+                  (void*)ctx->wd.scpc, (void*)ctx->wd.sst, (void*)ctx->wd.sg0, (void*)ctx->wd.sx0,
+                  (void*)ctx->wd.scode0})
     if (p) (void)hipFree(p);
   if (ctx->wd.h_sinfo) (void)hipHostFree(ctx->wd.h_sinfo);
   for (void* p : {(void*)ctx->d_vcrc, (void*)ctx->d_woff, (void*)ctx->d_wlen, (void*)ctx->d_wexp})
@@ -1615,9 +1630,12 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
   if (lim > n || lim <= start) lim = n;
   uint64_t S = lsmk_wal_seg_bytes(lim - start, ctx->wal_seg_bytes);
   sg::SegArgs a{};
-  int resegs = 0;
-  for (int round = 0;; ++round) {
-    if (round == 0) {  // (re)segment and walk every segment
+  int resegs = 0, prepairs = 0, repairs = 0;
+  ctx->last_seg_prepairs = 0;
+  for (bool walk = true;;) {
+    if (walk) {  // (re)segment and walk every segment
+      walk = false;
+      prepairs = repairs = 0;
       const uint64_t K64 = (lim - start + S - 1) / S;
       if (K64 >= (1ull << 31)) return kWalSegDecline;  // (tiny forced segments over a huge log)
       const uint32_t K = (uint32_t)K64;
@@ -1712,24 +1730,50 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
     tr.mark("segment walk round (sync)");
     if ((uint32_t)W.h_sinfo[sg::kInfoFail] == sg::kNoSeg) break;
     const uint32_t nfail = (uint32_t)W.h_sinfo[sg::kInfoNFail];
-    // Many failures at once: records longer than the segments (a segment
+    // Several failures: a parallel repair round first (seg::seg_prepair:
+    // every segment from its predecessor's exit at once -- a log of logs
+    // fails at every segment and is whole after one), then check again
+    if (nfail >= 2 && prepairs < ctx->wal_seg_prepair) {
+      if (W.cap_seg0 < W.cap_seg) {
+        for (void** p : {(void**)&W.sg0, (void**)&W.sx0, (void**)&W.scode0}) {
+          if (*p) (void)hipFree(*p);
+          *p = nullptr;
+        }
+        W.cap_seg0 = 0;
+        if (hipMalloc((void**)&W.sg0, W.cap_seg * 8) != hipSuccess ||
+            hipMalloc((void**)&W.sx0, W.cap_seg * 8) != hipSuccess ||
+            hipMalloc((void**)&W.scode0, W.cap_seg * 4) != hipSuccess) {
+          (void)hipGetLastError();  // (no room for the snapshot: the serial repairs below)
+        } else {
+          W.cap_seg0 = W.cap_seg;
+        }
+      }
+      if (W.cap_seg0 >= a.K) {
+        if ((rc = lsmk_wal_seg_prepair(&a, W.sg0, W.sx0, W.scode0, st)))
+          return launch_rc(rc, "wal segment parallel repair");
+        ++prepairs;
+        ctx->last_seg_prepairs = ctx->last_seg_prepairs + 1;
+        continue;
+      }
+    }
+    // Many failures still: records longer than the segments (a segment
     // inside one has no true entry, and a bogus start there is taken) --
     // segments 16x longer, once or twice, unless the caller fixed the size
-    if (round == 0 && !ctx->wal_seg_bytes && resegs < 2 && nfail > std::max<uint32_t>(64, a.K / 512) &&
+    if (repairs == 0 && !ctx->wal_seg_bytes && resegs < 2 && nfail > std::max<uint32_t>(64, a.K / 512) &&
         S < (1ull << 30)) {
       S <<= 4;
       ++resegs;
-      round = -1;
+      walk = true;
       continue;
     }
-    if (round >= ctx->wal_seg_rounds) {
-      ctx->last_seg_repairs = round;
+    if (repairs >= ctx->wal_seg_rounds) {
+      ctx->last_seg_repairs = repairs;
       return kWalSegDecline;
     }
     // the failing segment's entry is right: rewalk from its exit (and on, for
     // up to 4096 segments of consecutive failures), then check again
     if ((rc = lsmk_wal_seg_repair(&a, 4096, st))) return launch_rc(rc, "wal segment repair kernel");
-    ctx->last_seg_repairs = round + 1;
+    ctx->last_seg_repairs = ++repairs;
   }
   const uint64_t m = W.h_sinfo[sg::kInfoRecs];
   out->m = at + m;

@@ -98,6 +98,8 @@ uint64_t lsmk_wal_seg_scan_blocks(uint32_t K);
 int lsmk_wal_seg_walk(const lsmck::seg::SegArgs* a, hipStream_t st);
 int lsmk_wal_seg_round(const lsmck::seg::SegArgs* a, uint64_t* bsum, hipStream_t st);
 int lsmk_wal_seg_repair(const lsmck::seg::SegArgs* a, uint32_t budget, hipStream_t st);
+// a parallel repair round (seg::seg_prepair): g0 / x0 / code0 hold K entries (the snapshot)
+int lsmk_wal_seg_prepair(const lsmck::seg::SegArgs* a, uint64_t* g0, uint64_t* x0, uint32_t* code0, hipStream_t st);
 // recs: lsmck_wal_rec[] or, compact != 0, lsmck_wal_rec16[]
 int lsmk_wal_seg_emit(const lsmck::seg::SegArgs* a, uint64_t at, void* recs, int compact, uint64_t* poff,
                       uint32_t* plen, uint32_t* pcrc, hipStream_t st);

@@ -601,6 +601,41 @@ LSMCK_HD void seg_repair(const SegArgs& a, uint32_t j, uint32_t budget) {
   }
 }
 
+// A parallel repair round (after a check with several failures), from a
+// snapshot g0 / x0 / code0 of the round's arrays: segment t takes its entry
+// from the exit of the nearest guessed segment k before it (at most
+// kPrepairBack back) -- walked from that exit when the exit lies in t and t
+// guessed otherwise, cleared when the exit passes over t.  Every segment at
+// once, one thread each, each writing only its own arrays.  The serial
+// repair above fixes one run of failures per launch from the first failing
+// segment on; a log whose payloads are framed records (a log of logs: the
+// guesses inside a value follow the value's own chain, which ends where the
+// value does, at the log's next header) fails at every segment, yet every
+// walk's exit is right -- the guessed chain merges with the log's before
+// leaving the segment -- so one such round repairs them all.  Nothing here
+// is trusted: the check runs again after it, and a wrong predecessor exit
+// only costs another round (the caller bounds them, then repairs serially).
+constexpr uint32_t kPrepairBack = 256;
+LSMCK_HD void seg_prepair(const SegArgs& a, uint32_t t, const uint64_t* g0, const uint64_t* x0,
+                          const uint32_t* code0) {
+  if (t == 0 || t >= a.K) return;
+  uint32_t k = t - 1;
+  for (uint32_t s = 0; s < kPrepairBack && k > 0 && code0[k] == kNone; ++s) --k;
+  if (code0[k] != kExit) return;  // (kNone: too far back; kEnd / kBad: the chain ends before t)
+  const uint64_t e = x0[k];
+  const uint32_t te = seg_of(a, e);
+  if (te > t) {  // t lies inside k's last record: no entry
+    if (code0[t] != kNone) {
+      a.g[t] = kNoGuess;
+      a.x[t] = 0;
+      a.code[t] = kNone;
+      a.recs[t] = 0;
+    }
+  } else if (te == t && (code0[t] == kNone || g0[t] != e)) {
+    seg_forced(a, t, e);
+  }
+}
+
 // The raw CRC-32 register after a header's bytes [t][crc][klen]([vlen]) fed
 // from register 0, by the four slicing tables T (T0..T3, 256 words each).
 LSMCK_HD uint32_t hdr_reg(const Head& h, const uint32_t* T) {

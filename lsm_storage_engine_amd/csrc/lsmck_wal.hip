@@ -513,6 +513,14 @@ __global__ void wal_seg_reset(seg::SegArgs a) {
   a.info[seg::kInfoLast] = 0;
 }
 
+// a parallel repair round (seg::seg_prepair) from the snapshot g0 / x0 / code0
+__global__ __launch_bounds__(256) void wal_seg_prepair(seg::SegArgs a, const uint64_t* __restrict__ g0,
+                                                        const uint64_t* __restrict__ x0,
+                                                        const uint32_t* __restrict__ code0) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < a.K) seg::seg_prepair(a, t, g0, x0, code0);
+}
+
 __global__ void wal_seg_repair(seg::SegArgs a, uint32_t budget) {
   const uint32_t j = (uint32_t)a.info[seg::kInfoFail];
   if (j < a.K) seg::seg_repair(a, j, budget);
@@ -658,6 +666,20 @@ extern "C" int lsmk_wal_seg_round(const seg::SegArgs* a, uint64_t* bsum, hipStre
   hipLaunchKernelGGL(wal_seg_scan_c, dim3(nb), dim3(SSCAN_BLOCK), 0, st, *a, (const uint64_t*)bsum);
   hipLaunchKernelGGL(wal_seg_check, dim3(g), dim3(256), 0, st, *a);
   hipLaunchKernelGGL(wal_seg_finalize, dim3(1), dim3(1), 0, st, *a);
+  return launch_err();
+}
+
+// a parallel repair round: snapshot (K entries of each array) then one thread per segment
+extern "C" int lsmk_wal_seg_prepair(const seg::SegArgs* a, uint64_t* g0, uint64_t* x0, uint32_t* code0,
+                                    hipStream_t st) {
+  if (!a->K) return 0;
+  hipError_t e;
+  if ((e = hipMemcpyAsync(g0, a->g, (size_t)a->K * 8, hipMemcpyDeviceToDevice, st)) != hipSuccess ||
+      (e = hipMemcpyAsync(x0, a->x, (size_t)a->K * 8, hipMemcpyDeviceToDevice, st)) != hipSuccess ||
+      (e = hipMemcpyAsync(code0, a->code, (size_t)a->K * 4, hipMemcpyDeviceToDevice, st)) != hipSuccess)
+    return -(int)e;
+  hipLaunchKernelGGL(wal_seg_prepair, dim3((a->K + 255) / 256), dim3(256), 0, st, *a, (const uint64_t*)g0,
+                     (const uint64_t*)x0, (const uint32_t*)code0);
   return launch_err();
 }
 

@@ -33,11 +33,11 @@ def _oracle_shard_summary(rank, nrec, threads=16):
     return "%08x" % zlib.crc32(crc.astype("<u4").tobytes())
 
 
-def _bench2(*args):
+def _bench2(*args, gpus=2, timeout=300):
     env = dict(os.environ, LSMCK_BENCH_SHARE_GPU="1")
     env.pop("WORLD_SIZE", None)
-    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-                        *args], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--steps", "3",
+                        "--warmup", "1", *args], cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, p.stderr[-3000:]
     return json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
 
@@ -63,6 +63,30 @@ def test_bench_gpus2_config3_global_stream():
     assert c4["records_per_gpu"] == n4
     assert [p["summary_crc32"] for p in c4["per_rank"]] == [_oracle_shard_summary(k, n4) for k in range(2)]
     assert abs(c4["value"] - 2 * n4 * 4096 / 2**30 / (c4["ms_per_step"] * 1e-3)) / c4["value"] < 0.01
+
+
+@pytest.mark.gpu
+def test_bench_gpus8_rehearsal():
+    """The 8-rank line before the driver's 8-GPU node runs it: eight ranks on
+    the box's one GPU (LSMCK_BENCH_SHARE_GPU=1), reduced shards.  Every
+    rank's config-3 shard -- records [r*2^20, (r+1)*2^20) of one global
+    stream -- equals the committed oracle digest, every rank's config-4 shard
+    the oracle's (computed here), and value is all ranks' payload over the
+    slowest rank's time."""
+    nrec, n4 = 1 << 20, 1 << 18
+    r = _bench2("--blocks-per-gpu", str(nrec), "--c4-blocks", str(n4), gpus=8, timeout=600)
+    assert r["n_gpus"] == 8 and r["scaling"] == "weak"
+    assert r["config"]["workload"].startswith("config3")
+    with open(os.path.join(ROOT, "tests", "golden", "summaries.json")) as f:
+        g = json.load(f)["config3_shards_small"]
+    assert len(g["shard_summary_crc32"]) == 8
+    assert r["rank_summaries_crc32"] == g["shard_summary_crc32"]
+    assert r["summary_matches_oracle"] is True
+    pay = sum(g["shard_bytes"][:8])
+    assert abs(r["value"] - pay / 2**30 / (r["ms_per_step"] * 1e-3)) / r["value"] < 0.01
+    c4 = r["config4"]
+    assert [p["summary_crc32"] for p in c4["per_rank"]] == [_oracle_shard_summary(k, n4) for k in range(8)]
+    assert abs(c4["value"] - 8 * n4 * 4096 / 2**30 / (c4["ms_per_step"] * 1e-3)) / c4["value"] < 0.01
 
 
 @pytest.mark.gpu

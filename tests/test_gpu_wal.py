@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from lsm_storage_engine_amd import _lib, wal
-from lsm_storage_engine_amd.device import WAL_REC_DTYPE
+from lsm_storage_engine_amd.device import WAL_REC_DTYPE, decode_rec16
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -385,7 +385,7 @@ def seg_opts(ctx):
             ctx.set_option(k, v)
     yield set_
     for k, v in (("wal_seg_bytes", 0), ("wal_seg_rounds", 16), ("wal_seg_walk", 1), ("wal_seg_pack", 1),
-                 ("wal_seg_stage", 1)):
+                 ("wal_seg_stage", 1), ("wal_seg_prepair", 2)):
         ctx.set_option(k, v)
 
 
@@ -598,3 +598,83 @@ def test_device_records(ctx, seg_opts, device, seg_walk):
         finally:
             if d:
                 d.free()
+
+
+def _inner_log(rng, target):
+    """a WAL image of ~target bytes: Insert / Remove records of 100-8000 bytes"""
+    parts, got = [], 0
+    while got < target:
+        vl = int(rng.integers(100, 8000))
+        r = O.wal_remove(rng.bytes(int(rng.integers(1, 40)))) if rng.integers(0, 9) == 0 else \
+            O.wal_insert(rng.bytes(16), rng.bytes(vl))
+        parts.append(r)
+        got += len(r)
+    return b"".join(parts)
+
+
+def _replay_device_vs_oracle(ctx, img):
+    d = ctx.alloc(len(img))
+    try:
+        d.upload(np.frombuffer(img, np.uint8))
+        recs, st, bad = ctx.wal_replay_verify(len(img), device_ptr=d.ptr, compact=True)
+        ost, orecs, obad = O.wal_replay(img)
+        assert st == ost
+        got = decode_rec16(recs)
+        assert got["rec_off"].tolist() == [r.rec_off for r in orecs]
+        assert got["vlen"].tolist() == [r.vlen for r in orecs]
+        if st:
+            assert tuple(bad[:3]) == tuple(obad[:3])
+        return st
+    finally:
+        d.free()
+
+
+def test_log_of_logs_1gib(ctx, seg_opts):
+    """A 1 GiB log whose every value (256 KiB-1.75 MiB) is a WAL image itself:
+    each 2 MiB segment's guess lies inside a value and follows its chain, so
+    every guess is wrong and every walk's exit right.  One parallel repair
+    round makes the chain exact -- the segment walk, no serial repair, no
+    candidate doubling -- and a corrupted inner record (inside a value: the
+    outer CRC fails) and an outer one are reported as the oracle does."""
+    rng = np.random.default_rng(91)
+    inner = [_inner_log(rng, int(rng.integers(256 << 10, 1792 << 10))) for _ in range(24)]
+    parts, total, i = [], 0, 0
+    while total < (1 << 30):
+        v = inner[int(rng.integers(0, len(inner)))]
+        parts.append(O.wal_insert(b"log%06d" % i, v))
+        total += len(parts[-1])
+        i += 1
+    img = b"".join(parts)
+    assert _replay_device_vs_oracle(ctx, img) == 0
+    assert ctx.get_stat("wal_walk_path") == 1
+    assert ctx.get_stat("wal_seg_prepairs") >= 1 and ctx.get_stat("wal_seg_repairs") == 0
+    st, orecs, _ = O.wal_replay(img)
+    b = bytearray(img)
+    b[orecs[len(orecs) // 2].payload_off + 5000] ^= 0x10
+    assert _replay_device_vs_oracle(ctx, bytes(b)) == 1
+    seg_opts(wal_seg_prepair=0)  # the serial repairs alone: the same chain (A/B)
+    assert _replay_device_vs_oracle(ctx, img[:orecs[len(orecs) // 4].rec_off]) == 0
+    assert ctx.get_stat("wal_walk_path") in (1, 2)
+
+
+def test_mib_values_1gib(ctx, seg_opts):
+    """A 1 GiB log of ~1 MiB values: every segment's first record is longer
+    than kHop (the guess takes it with the hop raised to the segment size, and
+    the later-start rule scans its payload): the segment walk, the oracle's
+    records and outcome, a corrupted value reported."""
+    rng = np.random.default_rng(92)
+    blob = rng.bytes(8 << 20)
+    parts, total, i = [], 0, 0
+    while total < (1 << 30):
+        vl = (1 << 20) + int(rng.integers(0, 4096))
+        o = int(rng.integers(0, (8 << 20) - vl))
+        parts.append(O.wal_insert(b"k%07d" % i, blob[o:o + vl]))
+        total += len(parts[-1])
+        i += 1
+    img = b"".join(parts)
+    assert _replay_device_vs_oracle(ctx, img) == 0
+    assert ctx.get_stat("wal_walk_path") == 1
+    st, orecs, _ = O.wal_replay(img)
+    b = bytearray(img)
+    b[orecs[700].payload_off + 12345] ^= 0x01
+    assert _replay_device_vs_oracle(ctx, bytes(b)) == 1

@@ -83,6 +83,10 @@ def sim(tmp_path_factory):
         return list(po[:m]), list(pl[:m]), list(pe[:m])
     run.unpack = lib.segwalk_sim_unpack
     run.packed = packed
+    lib.segwalk_sim_set_prepair.argtypes = [C.c_int]
+    run.set_prepair = lib.segwalk_sim_set_prepair
+    lib.segwalk_sim_prepairs.restype = C.c_int
+    run.prepairs = lib.segwalk_sim_prepairs
     return run
 
 
@@ -392,3 +396,55 @@ def test_packed_crc_spans(sim, S, nsub, stage):
     finally:
         sim.set_nsub(1)
         sim.set_stage(0)
+
+
+def test_log_of_logs_parallel_repair(sim):
+    """Values that are WAL images, each shorter than a segment: every
+    segment's guess lies inside a value and follows the value's own chain,
+    which ends at the log's next header -- every guess is wrong, every walk's
+    exit right.  One parallel repair round (seg_prepair: each segment walked
+    again from its predecessor's exit, all at once) makes the chain exact with
+    no serial repair; without it the serial repair walks segment after
+    segment."""
+    rng = np.random.default_rng(21)
+    parts = []
+    for i in range(400):
+        inner = bytes(random_log(rng, int(rng.integers(4, 12)), lo=20, hi=150))
+        parts.append(rec(b"v%d" % i, inner))
+    img = bytearray(b"".join(parts))
+    for S in (2048, 4096, 8192):
+        try:
+            sim.set_prepair(2)
+            assert check(sim, img, S, rounds=0) == 0  # no serial repair needed
+            assert sim.prepairs() >= 1
+            sim.set_prepair(0)
+            rep = check(sim, img, S, rounds=1 << 20)
+            assert rep >= 1 and sim.prepairs() == 0
+        finally:
+            sim.set_prepair(2)
+
+
+@pytest.mark.parametrize("prepair", [0, 1, 2, 8])
+def test_parallel_repair_keeps_every_chain(sim, prepair):
+    """The parallel round is only a proposal the check verifies: with 0 to 8
+    rounds allowed, adversarial logs (long records over tiny segments, type
+    byte floods, framed values, cuts) give the plain chain walk's records."""
+    rng = np.random.default_rng(22 + prepair)
+    try:
+        sim.set_prepair(prepair)
+        img = random_log(rng, 800)
+        for S in (64, 300, 4096):
+            check(sim, img, S, rounds=1 << 20)
+        parts = [rec(rng.bytes(8), rng.bytes(int(L))) for L in rng.integers(0, 20000, 120)]
+        check(sim, bytearray(b"".join(parts)), 1000, rounds=1 << 20)
+        flood = bytearray(b"".join(rec(b"\x01" * 40, b"\x01" * 200) for _ in range(150)))
+        check(sim, flood, 512, rounds=1 << 20)
+        inner = bytes(random_log(rng, 60, hi=120))
+        lol = bytearray(b"".join(rec(b"k%d" % i, inner if i % 3 == 0 else rng.bytes(int(rng.integers(0, 300))))
+                                 for i in range(150)))
+        for S in (256, 1024):
+            check(sim, lol, S, rounds=1 << 20)
+        for cut in range(0, len(lol), 997):
+            check(sim, lol[:cut], 512, rounds=1 << 20)
+    finally:
+        sim.set_prepair(2)

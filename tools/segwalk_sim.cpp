@@ -25,6 +25,10 @@ extern "C" void segwalk_sim_debug(uint64_t* g) { g_dbg = g; }
 static uint32_t g_nsub = 1;  // emit checkpoints: sub-segments per segment (1 = none)
 extern "C" void segwalk_sim_set_nsub(uint32_t v) { g_nsub = v ? v : 1; }
 static uint32_t g_scap = 0;  // walk-time staging: slots per segment (0 = none)
+static int g_prepair = 2;    // parallel repair rounds before the serial repairs (wal_seg_prepair)
+extern "C" void segwalk_sim_set_prepair(int v) { g_prepair = v; }
+static int g_prepairs = 0;   // the last walk's parallel repair rounds
+extern "C" int segwalk_sim_prepairs() { return g_prepairs; }
 extern "C" void segwalk_sim_set_stage(uint32_t v) { g_scap = v; }
 // packed CRC spans (seg::Pack): when set, the next walk emits them here --
 // span offsets, lengths and expected CRCs
@@ -91,6 +95,8 @@ extern "C" int segwalk_sim_prefix(const uint8_t* img, uint64_t n, uint64_t start
                 g_nsub, (S + g_nsub - 1) / g_nsub, cpp.data(), cpc.data(), scap ? st.data() : nullptr, scap};
   for (uint32_t k = 0; k < K; ++k) sg::seg_walk_thread(a, k);
   if (g_dbg) std::copy(g.begin(), g.begin() + K, g_dbg);
+  g_prepairs = 0;
+  int serial = 0;
   for (int round = 0;; ++round) {
     uint32_t jterm = sg::kNoSeg, fail = sg::kNoSeg;
     for (uint32_t k = 0; k < K; ++k)
@@ -121,9 +127,16 @@ extern "C" int segwalk_sim_prefix(const uint8_t* img, uint64_t n, uint64_t start
       *pos_out = x[last - 1];
       break;
     }
-    if (round >= max_rounds) return 1;  // declined: the caller walks by candidate doubling
+    if (nfail >= 2 && g_prepairs < g_prepair) {  // a parallel round (wal_seg_prepair), from a snapshot
+      const std::vector<uint64_t> g0(g), x0(x);
+      const std::vector<uint32_t> c0(code);
+      for (uint32_t t = 0; t < K; ++t) sg::seg_prepair(a, t, g0.data(), x0.data(), c0.data());
+      ++g_prepairs;
+      continue;
+    }
+    if (serial >= max_rounds) return 1;  // declined: the caller walks by candidate doubling
     sg::seg_repair(a, fail, 4096);
-    *repairs = round + 1;
+    *repairs = ++serial;
   }
   const uint64_t m = *m_out;
   std::vector<SimRec> R(m);

@@ -17,6 +17,12 @@ framing instead (payload offset, Insert, klen = min(len, 16), vlen = the
 rest), the replay's status covering the CRCs; --dma-engines sets the SDMA
 engines of the read-back (0: hipMemcpyAsync).
 
+--shape mib / logs: the walk's hard logs at full size instead (DESIGN.md
+7a): every value ~1 MiB (each segment's first record longer than kHop), or
+a log of logs (every value a framed WAL image of 113 B-8 KiB records: the
+guesses inside values follow plausible chains that are not the log's).
+Their records are checked against their framing (every one, both layouts).
+
   python3 tools/wal_replay_big.py [--steps 3] [--records 67108864] [--device-recs 1]
 (LSMCK_WAL_TRACE=1 prints the replay's phases to stderr.)"""
 import argparse
@@ -55,15 +61,45 @@ def main():
                          "and over its payloads alone, this many times each, before the replays")
     ap.add_argument("--compact", type=int, default=0, help="1: 16-byte records (lsmck_wal_replay_verify16)")
     ap.add_argument("--dma-engines", type=int, default=-1, help="wal_dma_engines (-1: the default)")
+    ap.add_argument("--shape", default="zipf", choices=["zipf", "mib", "logs"],
+                    help="zipf: config 3's records framed; mib: ~1 MiB values; logs: values that are WAL images")
+    ap.add_argument("--log-gib", type=float, default=97.8, help="mib / logs: the log's size")
     a = ap.parse_args()
     n = a.records
-    ln = gen_zipf_lengths(0x5EED0003, n)
+    inner = None
+    if a.shape == "zipf":
+        ln = gen_zipf_lengths(0x5EED0003, n)
+    else:
+        rng = np.random.default_rng(0x5EED0005)
+        target = int(a.log_gib * GIB)
+        if a.shape == "mib":
+            n = target // ((1 << 20) + 2048 + 13)
+            ln = ((1 << 20) + rng.integers(0, 4096, n)).astype(np.uint32)
+        else:
+            n = target // ((1 << 20) + 13)
+            ln = rng.integers(256 << 10, 1792 << 10, n).astype(np.uint32)
     off = np.full(n, 13, dtype=np.uint64)
     off[1:] += ln[:-1].astype(np.uint64)
     off = np.cumsum(off, dtype=np.uint64)
     total = int(off[-1]) + int(ln[-1])
+    if a.shape == "logs":  # each value: inner records (13-byte header + 100..8000 bytes) filling it exactly
+        io, il = [], []
+        for o, v in zip(off.tolist(), ln.tolist()):
+            sz = rng.integers(113, 8013, v // 4000 + 8)
+            cs = np.cumsum(sz)
+            k = int(np.searchsorted(cs, v))  # records [0, k] reach v: the last one is cut to fit
+            sz = sz[:k + 1].copy()
+            sz[k] = v - (int(cs[k - 1]) if k else 0)
+            if sz[k] < 13:  # (too short for a header: folded into the one before)
+                sz[k - 1] += sz[k]
+                sz = sz[:k]
+            st = o + np.concatenate(([0], np.cumsum(sz)[:-1]))
+            io.append(st + 13)
+            il.append(sz - 13)
+        inner = (np.concatenate(io).astype(np.uint64), np.concatenate(il).astype(np.uint32))
+        print(f"log of logs: {n} values, {len(inner[0])} inner records", file=sys.stderr, flush=True)
     golden = None
-    if n == 1 << 26:
+    if a.shape == "zipf" and n == 1 << 26:
         with open(os.path.join(ROOT, "tests", "golden", "summaries.json")) as f:
             golden = json.load(f)["config3w"]
         assert total == golden["image_bytes"]
@@ -77,9 +113,23 @@ def main():
 
     def check_compact(recs):  # every record against the framing
         assert (recs["payload_type"] == off).all() and (recs["klen"] == kl).all() and (recs["vlen"] == ln - kl).all()
+
+    def check_wide(recs):
+        assert (recs["payload_off"] == off).all() and (recs["rec_off"] == off - np.uint64(13)).all()
+        assert (recs["klen"] == kl).all() and (recs["vlen"] == ln - kl).all() and (recs["type"] == 1).all()
     d = ctx.alloc(total + 64)
     d_o, d_l, out = ctx.alloc(off.nbytes), ctx.alloc(ln.nbytes), ctx.alloc(4 * n)
     ctx.gen_stream(d.ptr, 0x5EED0003, 0, total)
+    if inner is not None:  # the inner logs' headers first: the values' CRCs cover them
+        ni = len(inner[0])
+        i_o, i_l, i_c = ctx.alloc(8 * ni), ctx.alloc(4 * ni), ctx.alloc(4 * ni)
+        i_o.upload(inner[0])
+        i_l.upload(inner[1])
+        ctx.crc32_device(d.ptr, i_o.ptr, i_l.ptr, ni, i_c.ptr)
+        ctx.wal_frame_insert_device(d.ptr, i_o.ptr, i_l.ptr, i_c.ptr, ni, 16)
+        ctx.sync()
+        for b in (i_o, i_l, i_c):
+            b.free()
     d_o.upload(off)
     d_l.upload(ln)
     ctx.crc32_device(d.ptr, d_o.ptr, d_l.ptr, n, out.ptr)
@@ -114,13 +164,18 @@ def main():
         if a.compact:
             check_compact(recs)
             summary = "every record = the framing"
+        elif a.shape != "zipf":
+            check_wide(recs)
+            summary = "every record = the framing"
         else:
             summary = "%08x" % zlib.crc32(np.ascontiguousarray(recs.crc).astype("<u4").tobytes())
             if golden:
                 assert summary == golden["summary_crc32"], summary
         if s:
             times.append(dt)
-        print(f"replay {s}: {dt * 1e3:.1f} ms", file=sys.stderr, flush=True)
+        print(f"replay {s}: {dt * 1e3:.1f} ms (walk path {ctx.get_stat('wal_walk_path')}, "
+              f"{ctx.get_stat('wal_segments')} segments, {ctx.get_stat('wal_seg_repairs')} repairs)",
+              file=sys.stderr, flush=True)
         del recs  # the wrapper reuses its records array once no result refers to it
     dev = None
     if a.device_recs:  # the records stay in HBM: the walk, the CRC pass and the compare, no host link
@@ -159,6 +214,9 @@ def main():
         if a.compact:
             check_compact(got)
             dsum = "every record = the framing"
+        elif a.shape != "zipf":
+            check_wide(got)
+            dsum = "every record = the framing"
         else:
             dsum = "%08x" % zlib.crc32(np.ascontiguousarray(got["crc"]).astype("<u4").tobytes())
         rb.free()
@@ -175,14 +233,18 @@ def main():
         "metric": "WAL replay verify of a device-resident log (header walk + payload CRC check + records to host)",
         "value": round(total / GIB / med, 1), "unit": "GiB/s of log",
         "log_bytes": total, "records": n, "ms_median": round(med * 1e3, 2), "ms_best": round(best * 1e3, 2),
-        "steps": a.steps, "summary_crc32": summary, "summary_matches_oracle": bool(golden) and True,
+        "steps": a.steps, "summary_crc32": summary,
+        "summary_matches_oracle": bool(golden) or a.shape != "zipf" or bool(a.compact), "shape": a.shape,
         "records_out_bytes": (16 if a.compact else 32) * n, "pinned_recs": bool(a.pinned_recs),
         "compact": bool(a.compact), "recs_dma_engines": ctx.get_stat("wal_recs_dma"),
         "walk_path": {1: "segment walk", 2: "candidate doubling", 3: "host walk"}.get(ctx.get_stat("wal_walk_path")),
         "seg_repairs": ctx.get_stat("wal_seg_repairs"), "segments": ctx.get_stat("wal_segments"),
         "records_on_device": dev, "raw_batch_crc_ms": raw,
-        "workload": "config 3's 2^26 Zipf payloads (64 B-64 KiB) framed as wal.rs Insert records (13-byte headers), "
-                    "headers and CRCs written on the device"}))
+        "workload": {"zipf": "config 3's 2^26 Zipf payloads (64 B-64 KiB) framed as wal.rs Insert records "
+                             "(13-byte headers), headers and CRCs written on the device",
+                     "mib": f"{n} Insert records of 1 MiB + 0..4095 B values, random bytes",
+                     "logs": f"{n} Insert records whose values (256 KiB-1.75 MiB) are WAL images of "
+                             f"{0 if inner is None else len(inner[0])} framed records of 100-8000 B"}[a.shape]}))
 
 
 if __name__ == "__main__":
