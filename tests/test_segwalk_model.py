@@ -448,3 +448,19 @@ def test_parallel_repair_keeps_every_chain(sim, prepair):
             check(sim, lol[:cut], 512, rounds=1 << 20)
     finally:
         sim.set_prepair(2)
+
+
+def test_first_records_past_the_later_rule(sim):
+    """Segments of 512 KiB - 1 MiB over records of 300-900 KiB: every true
+    first record is longer than kLaterMax, so the later-start rule is skipped
+    for it; a wrong guess it would have refused is caught by the check.  The
+    plain chain either way, with and without the parallel rounds."""
+    rng = np.random.default_rng(23)
+    img = bytearray(b"".join(rec(rng.bytes(16), rng.bytes(int(L))) for L in rng.integers(300 << 10, 900 << 10, 60)))
+    for prepair in (2, 0):
+        try:
+            sim.set_prepair(prepair)
+            for S in (512 << 10, 1 << 20):
+                check(sim, img, S, rounds=1 << 20)
+        finally:
+            sim.set_prepair(2)

@@ -85,7 +85,7 @@ def main():
     if a.shape == "logs":  # each value: inner records (13-byte header + 100..8000 bytes) filling it exactly
         io, il = [], []
         for o, v in zip(off.tolist(), ln.tolist()):
-            sz = rng.integers(113, 8013, v // 4000 + 8)
+            sz = rng.integers(113, 8013, v // 3000 + 16)  # (enough draws to pass v)
             cs = np.cumsum(sz)
             k = int(np.searchsorted(cs, v))  # records [0, k] reach v: the last one is cut to fit
             sz = sz[:k + 1].copy()
