@@ -109,9 +109,12 @@ int main(int argc, char** argv) {
          getenv("HSA_ENABLE_SDMA") ? getenv("HSA_ENABLE_SDMA") : "(unset)");
   hsa_signal_t sig;
   HK(hsa_signal_create(1, 0, nullptr, &sig));
-  hipStream_t s1, s2;
+  hipStream_t s1, s2, sx[4];
   CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+  for (auto& q : sx) CK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+  hipEvent_t xe[4];
+  for (auto& ev : xe) CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   hipEvent_t e0, e1, c0, c1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); CK(hipEventCreate(&c0)); CK(hipEventCreate(&c1));
   int ncu = 0;
@@ -127,18 +130,35 @@ int main(int argc, char** argv) {
     }
   hipEvent_t dep;
   CK(hipEventCreateWithFlags(&dep, hipEventDisableTiming));
-  auto hsa_split = [&](int parts) {
+  auto hsa_split = [&](int parts, bool h2d = false) {
     hsa_signal_store_relaxed(sig, parts);
     const size_t per = (rec_bytes / parts + 4095) & ~(size_t)4095;
     for (int i = 0; i < parts; ++i) {
       const size_t o = per * i, c = o >= rec_bytes ? 0 : std::min(per, rec_bytes - o);
-      HK(hsa_amd_memory_async_copy_on_engine(h_rec + o, g_cpu, d_rec + o, g_gpu, c, 0, nullptr, sig,
-                                             (hsa_amd_sdma_engine_id_t)engs[i % neng], true));
+      if (h2d)
+        HK(hsa_amd_memory_async_copy_on_engine(d_rec + o, g_gpu, h_rec + o, g_cpu, c, 0, nullptr, sig,
+                                               (hsa_amd_sdma_engine_id_t)engs[i % neng], true));
+      else
+        HK(hsa_amd_memory_async_copy_on_engine(h_rec + o, g_cpu, d_rec + o, g_gpu, c, 0, nullptr, sig,
+                                               (hsa_amd_sdma_engine_id_t)engs[i % neng], true));
     }
+  };
+  auto hip_split = [&](int parts, hipMemcpyKind kind) {  // one hipMemcpyAsync per stream, joined on s2
+    const size_t per = (rec_bytes / parts + 4095) & ~(size_t)4095;
+    CK(hipEventRecord(c0, s2));
+    for (int i = 0; i < parts; ++i) {
+      CK(hipStreamWaitEvent(sx[i], c0, 0));
+      const size_t o = per * i, c = std::min(per, rec_bytes - o);
+      if (kind == hipMemcpyDeviceToHost) CK(hipMemcpyAsync(h_rec + o, d_rec + o, c, kind, sx[i]));
+      else CK(hipMemcpyAsync(d_rec + o, h_rec + o, c, kind, sx[i]));
+      CK(hipEventRecord(xe[i], sx[i]));
+      CK(hipStreamWaitEvent(s2, xe[i], 0));
+    }
+    CK(hipEventRecord(c1, s2));
   };
   // variants: 0 hip D2H, 1 hsa auto, 2/3 hsa split over 2/4 engines, 4 kernel stores,
   // 5 hip D2H behind a cross-stream event, 6 hip D2H NumaUser, 7 hsa split 2 NumaUser
-  auto is_hsa = [](int how) { return how == 1 || how == 2 || how == 3 || how == 7; };
+  auto is_hsa = [](int how) { return how == 1 || how == 2 || how == 3 || how == 7 || how == 11; };
   auto copy = [&](int how) {
     h_rec = how >= 6 ? h_numa : h_def;
     if (how == 0 || how == 6) {
@@ -157,6 +177,16 @@ int main(int argc, char** argv) {
       hsa_split(2);
     } else if (how == 3) {
       hsa_split(4);
+    } else if (how == 8) {
+      hip_split(4, hipMemcpyDeviceToHost);
+    } else if (how == 9) {
+      CK(hipEventRecord(c0, s2));
+      CK(hipMemcpyAsync(d_rec, h_rec, rec_bytes, hipMemcpyHostToDevice, s2));
+      CK(hipEventRecord(c1, s2));
+    } else if (how == 10) {
+      hip_split(4, hipMemcpyHostToDevice);
+    } else if (how == 11) {
+      hsa_split(4, true);
     } else {
       CK(hipEventRecord(c0, s2));
       k_store_host<<<8, 256, 0, s2>>>((const u32x4*)d_rec, (u32x4*)h_rec, rec_bytes / 16);
@@ -187,7 +217,8 @@ int main(int argc, char** argv) {
   const char* names[] = {"hipMemcpyAsync D2H", "hsa async copy (cpu dst agent)", "hsa split over 2 sdma engines",
                          "hsa split over 4 sdma engines", "kernel stores to host (8 WG)",
                          "hipMemcpyAsync D2H after an event", "hipMemcpyAsync D2H, NumaUser array",
-                         "hsa split 2 engines, NumaUser array"};
+                         "hsa split 2 engines, NumaUser array", "hipMemcpyAsync D2H over 4 streams",
+                         "hipMemcpyAsync H2D", "hipMemcpyAsync H2D over 4 streams", "hsa H2D split over 4 engines"};
   for (int rep = 0; rep < reps; ++rep) {
     // the stream alone
     CK(hipEventRecord(e0, s1));
@@ -197,7 +228,7 @@ int main(int argc, char** argv) {
     float ms_alone = 0;
     CK(hipEventElapsedTime(&ms_alone, e0, e1));
     printf("rep %d stream alone %.3f ms (%.2f TB/s)\n", rep, ms_alone, big / ms_alone / 1e9);
-    for (int how = 0; how < 8; ++how) {
+    for (int how = 0; how < 12; ++how) {
       memset(h_rec, 0, 4096);
       double t0 = now_ms();
       copy(how);
