@@ -167,7 +167,7 @@ class CommandLog:
         order; raises the error the iterator would raise first."""
         pos = self.file.tell()
         img = self.file.read()
-        records, status, bad = ctx.wal_replay_verify(img)
+        records, status, bad = ctx.wal_replay_verify(img, compact=True)  # 16-byte records: all from_log needs
         if status == _lib.WAL_CORRUPTED:
             raise CorruptedData(bad[1], bad[2])
         if status == _lib.WAL_REMOVE_PANIC:
@@ -176,8 +176,9 @@ class CommandLog:
             raise InvalidCommandType(bad[1])
         out = []
         consumed = 0
-        for k0, kl, vl, t in zip(records.payload_off.tolist(), records.klen.tolist(), records.vlen.tolist(),
-                                 records.type.tolist()):
+        from .device import decode_rec16
+        r = decode_rec16(records)
+        for k0, kl, vl, t in zip(r["payload_off"].tolist(), r["klen"].tolist(), r["vlen"].tolist(), r["type"].tolist()):
             # the payload actually read: u32 data_len (wal.rs:129), short at EOF
             # (read_to_end on take(), :132) -- the same bytes the CRC covered
             data = img[k0:k0 + ((kl + vl) & 0xFFFFFFFF)]
