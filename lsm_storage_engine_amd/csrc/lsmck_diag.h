@@ -18,8 +18,8 @@
 #ifndef LSMCK_LATER_MIN
 #define LSMCK_LATER_MIN 65536
 #endif
-#ifndef LSMCK_LATER_MAX
-#define LSMCK_LATER_MAX 262144
+#ifndef LSMCK_LATER_SCAN
+#define LSMCK_LATER_SCAN 65536
 #endif
 #ifndef LSMCK_SCAN_BLOCKS
 #define LSMCK_SCAN_BLOCKS 4
@@ -30,7 +30,7 @@ namespace seg {
 namespace tune {
 constexpr uint64_t kLaterSkipTo = LSMCK_LATER_SKIP_TO;
 constexpr uint64_t kLaterMin = LSMCK_LATER_MIN;
-constexpr uint64_t kLaterMax = LSMCK_LATER_MAX;
+constexpr uint64_t kLaterScan = LSMCK_LATER_SCAN;
 constexpr int kScanBlocks = LSMCK_SCAN_BLOCKS;
 #ifdef LSMCK_SEG_LATER_ALWAYS  // (host model A/B, tools/segwalk_repairs.py: the later-start rule everywhere)
 constexpr bool kLaterAlways = true;

@@ -56,7 +56,7 @@ namespace seg {
 namespace tune {
 constexpr uint64_t kLaterSkipTo = 131072;  // kLaterSkipTo below
 constexpr uint64_t kLaterMin = 65536;      // kLaterMin below
-constexpr uint64_t kLaterMax = 262144;     // kLaterMax below
+constexpr uint64_t kLaterScan = 65536;     // kLaterScan below
 constexpr int kScanBlocks = 4;             // kScanBlocks below
 constexpr bool kLaterAlways = false;       // (host-model A/B: the later-start rule everywhere)
 }  // namespace tune
@@ -109,12 +109,17 @@ constexpr uint64_t kLaterSkipFrom = 4096, kLaterSkipTo = tune::kLaterSkipTo;
 // (without the rule at all: 6.21 ms and three repairs of 0.87 ms each,
 // profiles/r04/v).  A wrong guess is caught by the check either way.
 constexpr uint64_t kLaterMin = tune::kLaterMin;
-// ... and only for one of at most kLaterMax payload bytes: the rule scans
-// the whole first record, and a true first record of a MiB -- a log of MiB
-// values: every segment's -- cost the 97.8 GiB log 216 ms of walk
-// (profiles/r05/d).  A bogus guess whose first record is longer and lands on
-// a true start is caught by the check and repaired (seg_prepair).
-constexpr uint64_t kLaterMax = tune::kLaterMax;
+// ... and then scans at most kLaterScan bytes past the guess for the later
+// start.  The rule scanned the whole first record, and a true first record of
+// a MiB -- in a log of MiB values, every segment's -- cost the 97.8 GiB log
+// 216 ms of walk (profiles/r05/d).  A bogus merge's true entry is the first
+// true start after it, within one true record: every one of them in a log of
+// records of at most kLaterScan (config 3w) is still found.  Capping the
+// first record's length instead (at 256 KiB) left config 3w's bogus merges
+// to the check: a parallel repair round of ~1 ms in every replay
+// (profiles/r05/kt).  A longer-range merge is caught by the check and
+// repaired (seg_prepair).
+constexpr uint64_t kLaterScan = tune::kLaterScan;
 constexpr int kScanBlocks = tune::kScanBlocks;  // 64-byte blocks the guess scan loads per iteration
 // per-segment record counts and the guessed-segment count share one u64 in
 // the placement scan: guessed segments in the top 24 bits, records below
@@ -398,9 +403,12 @@ LSMCK_HD uint64_t later_rule(Scan& S, const uint8_t* img, uint64_t n, uint64_t c
   for (;;) {
     bool whole;
     const Head hc = head(img, n, c);
-    const uint64_t q1 = next_of(hc, n, c, &whole), lim = q1 < e ? q1 : e;
-    const uint64_t len1 = q1 - c - hdr_len(hc.t);
-    if (later_min && (len1 <= later_min || len1 > kLaterMax)) return c;  // (kLaterMin, kLaterMax)
+    const uint64_t q1 = next_of(hc, n, c, &whole);
+    uint64_t lim = q1 < e ? q1 : e;
+    if (later_min) {
+      if (q1 - c - hdr_len(hc.t) <= later_min) return c;  // (kLaterMin)
+      if (lim > c + 1 + kLaterScan) lim = c + 1 + kLaterScan;  // (kLaterScan)
+    }
     uint64_t c2 = next_cand(S, img, n, c + 1, lim);
     while (c2 != kNoGuess && !reaches(img, n, c2, q1)) c2 = next_cand(S, img, n, c2 + 1, lim);
     if (c2 == kNoGuess) return c;

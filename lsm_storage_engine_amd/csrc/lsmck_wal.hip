@@ -376,6 +376,63 @@ __device__ __forceinline__ uint64_t guess_group(const seg::SegArgs& a, uint32_t 
   }
 }
 
+// seg::later_rule by the same group of G lanes: lane j scans chunks j, j + G,
+// ... of the window after the accepted start c for the first candidate whose
+// chain reaches c's first record's end; the group keeps the lowest found in a
+// round (every chunk before it held none), so each step takes the start the
+// one-lane rule takes.  The rule's scan (up to kLaterScan bytes) runs G-fold
+// shorter on the wave's slowest lane -- in a log of MiB records every true
+// guess scans its whole window.
+template <int G>
+__device__ __forceinline__ uint64_t later_group(const seg::SegArgs& a, uint32_t k, uint32_t j, uint64_t c) {
+  using namespace seg;
+  const uint64_t e = seg_end(a, k), later_min = seg_later_min(a);
+  constexpr uint64_t CH = 64u * kScanBlocks;
+  const uintptr_t base = (uintptr_t)a.img;
+  for (;;) {
+    bool whole;
+    const Head hc = head(a.img, a.n, c);
+    const uint64_t q1 = next_of(hc, a.n, c, &whole);
+    uint64_t lim = q1 < e ? q1 : e;
+    if (later_min) {
+      if (q1 - c - hdr_len(hc.t) <= later_min) return c;  // (kLaterMin)
+      if (lim > c + 1 + kLaterScan) lim = c + 1 + kLaterScan;  // (kLaterScan)
+    }
+    const uint64_t b = c + 1;
+    const uintptr_t A0 = (base + b) & ~(uintptr_t)(CH - 1);
+    uint64_t found = kNoGuess;
+    for (uint32_t r = 0;; ++r) {
+      const int64_t cs = (int64_t)(A0 + ((uint64_t)r * G + j) * CH - base);
+      const bool act = cs < (int64_t)lim;
+      uint64_t f = kNoGuess;
+      if (act) {
+        const uint64_t lo = cs > (int64_t)b ? (uint64_t)cs : b;
+        const uint64_t hi = (uint64_t)(cs + (int64_t)CH) < lim ? (uint64_t)(cs + (int64_t)CH) : lim;
+        Scan S;
+        for (uint64_t c2 = next_cand(S, a.img, a.n, lo, hi); c2 != kNoGuess; c2 = next_cand(S, a.img, a.n, c2 + 1, hi))
+          if (reaches(a.img, a.n, c2, q1)) {
+            f = c2;
+            break;
+          }
+      }
+      uint32_t any = act ? 1u : 0u;
+#pragma unroll
+      for (int s = 1; s < G; s <<= 1) {
+        const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)f, s), hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(f >> 32), s);
+        const uint64_t o = ((uint64_t)hi32 << 32) | lo32;
+        f = o < f ? o : f;
+        any |= (uint32_t)__shfl_xor((int)any, s);
+      }
+      if (f != kNoGuess || !any) {
+        found = f;
+        break;
+      }
+    }
+    if (found == kNoGuess) return c;
+    c = found;
+  }
+}
+
 template <int G>
 __global__ __launch_bounds__(256) void wal_seg_walk_group(seg::SegArgs a) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, k = t / G, j = t % G;
@@ -385,11 +442,8 @@ __global__ __launch_bounds__(256) void wal_seg_walk_group(seg::SegArgs a) {
     return;
   }
   uint64_t c = guess_group<G>(a, k, j);
+  if (c != seg::kNoGuess && seg::seg_later(a)) c = later_group<G>(a, k, j, c);  // (c: the group's, in every lane)
   if (j != 0) return;
-  if (c != seg::kNoGuess && seg::seg_later(a)) {
-    seg::Scan S;
-    c = seg::later_rule(S, a.img, a.n, c, seg::seg_end(a, k), seg::seg_later_min(a));
-  }
   seg::seg_take_guess(a, k, c);
 }
 

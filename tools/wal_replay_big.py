@@ -174,7 +174,8 @@ def main():
         if s:
             times.append(dt)
         print(f"replay {s}: {dt * 1e3:.1f} ms (walk path {ctx.get_stat('wal_walk_path')}, "
-              f"{ctx.get_stat('wal_segments')} segments, {ctx.get_stat('wal_seg_repairs')} repairs)",
+              f"{ctx.get_stat('wal_segments')} segments, {ctx.get_stat('wal_seg_prepairs')} parallel rounds, "
+              f"{ctx.get_stat('wal_seg_repairs')} repairs)",
               file=sys.stderr, flush=True)
         del recs  # the wrapper reuses its records array once no result refers to it
     dev = None
@@ -238,7 +239,7 @@ def main():
         "records_out_bytes": (16 if a.compact else 32) * n, "pinned_recs": bool(a.pinned_recs),
         "compact": bool(a.compact), "recs_dma_engines": ctx.get_stat("wal_recs_dma"),
         "walk_path": {1: "segment walk", 2: "candidate doubling", 3: "host walk"}.get(ctx.get_stat("wal_walk_path")),
-        "seg_repairs": ctx.get_stat("wal_seg_repairs"), "segments": ctx.get_stat("wal_segments"),
+        "seg_repairs": ctx.get_stat("wal_seg_repairs"), "seg_prepairs": ctx.get_stat("wal_seg_prepairs"), "segments": ctx.get_stat("wal_segments"),
         "records_on_device": dev, "raw_batch_crc_ms": raw,
         "workload": {"zipf": "config 3's 2^26 Zipf payloads (64 B-64 KiB) framed as wal.rs Insert records "
                              "(13-byte headers), headers and CRCs written on the device",
