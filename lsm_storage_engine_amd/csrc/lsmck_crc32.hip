@@ -1286,9 +1286,6 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
       qf = end;
     }
   };
-  // the last window's CRCs are pushed at the next tile, after its payload
-  // loads are issued (nothing between a tile's checksum and the next issue)
-  uint32_t dqv = 0, dqcnt = 0;
 
   // a tile without events: the straight chains, the Horner shift of every
   // chunk to the tile end and the carry.  The carry (the open record's raw
@@ -1387,8 +1384,6 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     issue_next();
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(0);
-    if (dqcnt) qpush(dqv, dqcnt);
-    dqcnt = 0;
     if constexpr (ABLATE == 0 || ABLATE >= 4) {
       // (ABLATE 4 / 5, diagnostic: every tile takes this path -- the bulk
       // chains + Horner cost without / with the payload loads)
@@ -1500,8 +1495,9 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     if (cntw) {
       uint32_t fv = finish(cntw, re, rs, lng, sin);
       if (shorts && __any(lane < cntw && !lng)) fv = finish_short(fv, cntw, re, rs, lng);
-      dqv = fv;
-      dqcnt = cntw;
+      // pushed at once (round 5: holding them to the next tile, after its
+      // payload issue, ran 0.1 ms slower on config 3; profiles/r05/f)
+      qpush(fv, cntw);
     }
     // --- carry: the record open at the tile's end started at the tile's last start
     const uint32_t X63 = (uint32_t)__builtin_amdgcn_readlane((int)X, 63);
@@ -1523,7 +1519,6 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
   if (i < ntile) process(U0, t_first + i, none);
   if ((ABLATE == 4 || ABLATE == 5 || ABLATE == 7 || ABLATE == 9 || ABLATE == 10) && carry == 0x9E3779B1u) P.out[0] = carry;  // keeps the ablated chains (and loads) alive
   if (ABLATE == 3) return;
-  if (dqcnt) qpush(dqv, dqcnt);
   qstore(qv, lane >= qs && lane < qf);
 }
 }  // namespace lsmck

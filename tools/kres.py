@@ -8,7 +8,7 @@ import sys
 
 src = sys.argv[1]
 p = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-Iinclude",
-                    "-Ilsm_storage_engine_amd/csrc", "-c", src, "-o", "/tmp/kres.o",
+                    "-Ilsm_storage_engine_amd/csrc", "-c", src, "-o", "/tmp/kres.o"] + sys.argv[2:] + [
                     "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
 cur = None
 rows = {}
