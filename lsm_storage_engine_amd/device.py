@@ -439,9 +439,9 @@ class MultiContext:
                                                     C.byref(rep)), "tree_verify_multi")
         return _tree_report(rep, rc)
 
-    def wal_replay_verify(self, image, device_ptr=None):
-        """The WAL is one log: replayed on the first device."""
-        return self.ctxs[0].wal_replay_verify(image, device_ptr)
+    def wal_replay_verify(self, image, device_ptr=None, cap=None, pinned_recs=False, compact=False):
+        """The WAL is one log: replayed on the first device (Context.wal_replay_verify)."""
+        return self.ctxs[0].wal_replay_verify(image, device_ptr, cap=cap, pinned_recs=pinned_recs, compact=compact)
 
 
 # include/lsmck.h lsmck_wal_rec (32 bytes, no padding)

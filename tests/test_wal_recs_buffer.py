@@ -44,3 +44,17 @@ def test_compact_records_have_their_own_array():
     i16 = id(c.cur(WAL_REC16_DTYPE))
     c.replay(dtype=WAL_REC16_DTYPE)
     assert id(c.cur(WAL_REC16_DTYPE)) == i16  # reused within its own dtype
+
+
+def test_multicontext_replay_takes_the_context_options():
+    """MultiContext.wal_replay_verify (the tree's WAL on the first device)
+    accepts every option Context.wal_replay_verify does: MemTable.from_log
+    calls it with compact=True on either."""
+    import inspect
+
+    from lsm_storage_engine_amd.device import MultiContext
+
+    one = inspect.signature(Context.wal_replay_verify).parameters
+    multi = inspect.signature(MultiContext.wal_replay_verify).parameters
+    assert list(multi) == list(one)
+    assert all(multi[k].default == one[k].default for k in one)
