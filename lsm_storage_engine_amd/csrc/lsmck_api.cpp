@@ -1701,7 +1701,7 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
       // segment with more is emitted by a second walk of its headers, and so
       // is every segment when the slots cannot be had (scap 0)
       uint32_t scap = 0;
-      if (ctx->wal_seg_stage) {
+      if (ctx->wal_seg_stage && S <= sg::kStageMaxSeg) {  // (a staged record keeps its offset in 31 bits)
         const uint64_t most = S / 9 + 1;
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;

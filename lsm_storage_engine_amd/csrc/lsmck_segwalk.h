@@ -35,6 +35,7 @@
 #define LSMCK_SEGWALK_H
 #include <stdint.h>
 #include <string.h>
+#include <assert.h>
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -209,24 +210,31 @@ LSMCK_HD uint64_t next_of(const Head& h, uint64_t n, uint64_t p, bool* whole) {
   return p + hl + (*whole ? (uint64_t)dlen : avail);
 }
 
-// A record as the walk stages it (the lsmck_wal_rec layout): segment k's
-// walk writes its records to its own slots [k * scap, k * scap + scap) as it
-// passes them, so the records need no second walk of the headers when they
-// all fit (seg_place_thread copies them out); a segment with more records
-// than slots is emitted by its second walk as before (seg_emit_thread).
+// A record as the walk stages it: segment k's walk writes its records to its
+// own slots [k * scap, k * scap + scap) as it passes them, so the records need
+// no second walk of the headers when they all fit (seg_place_thread copies
+// them out); a segment with more records than slots is emitted by its second
+// walk as before (seg_emit_thread).  16 bytes: the record's offset from its
+// segment's start (bits 0-30; a segment's records start inside it, and the
+// walk stages only for segments of at most kStageMaxSeg bytes), Remove in bit
+// 31, then the header's CRC and lengths.
 struct StageRec {
-  uint64_t rec_off, payload_off;
-  uint32_t klen, vlen, crc, type;
+  uint32_t rel_t, crc, klen, vlen;
 };
-LSMCK_HD void stage_put(StageRec* st, uint32_t cap, uint32_t cnt, uint64_t p, const Head& h) {
+constexpr uint64_t kStageMaxSeg = 1ull << 31;
+LSMCK_HD uint32_t stage_type(const StageRec& R) { return (R.rel_t >> 31) ? 2u : 1u; }
+LSMCK_HD uint64_t stage_off(const StageRec& R, uint64_t b0) { return b0 + (R.rel_t & 0x7FFFFFFFu); }
+// b0: the segment's start
+LSMCK_HD void stage_put(StageRec* st, uint32_t cap, uint32_t cnt, uint64_t p, const Head& h, uint64_t b0) {
   if (st && cnt < cap) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    assert(p >= b0 && p - b0 < kStageMaxSeg);  // (the host model's runs check the layout's premise)
+#endif
     StageRec R;
-    R.rec_off = p;
-    R.payload_off = p + hdr_len(h.t);
+    R.rel_t = (uint32_t)(p - b0) | (h.t == 2u ? 0x80000000u : 0u);
+    R.crc = h.crc;
     R.klen = h.klen;
     R.vlen = h.vlen;
-    R.crc = h.crc;
-    R.type = h.t;
     st[cnt] = R;
   }
 }
@@ -236,7 +244,7 @@ LSMCK_HD void stage_put(StageRec* st, uint32_t cap, uint32_t cnt, uint64_t p, co
 // first record start at or past e (kExit) or to the chain's end (kEnd / kBad).
 // st: the segment's staging slots (scap of them), or none.
 LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, Head h, uint64_t e, WalkOut* o,
-                   StageRec* st = nullptr, uint32_t scap = 0) {
+                   StageRec* st = nullptr, uint32_t scap = 0, uint64_t b0 = 0) {
   uint64_t p = c;
   uint32_t cnt = 0;
   for (;;) {
@@ -248,7 +256,7 @@ LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, Head h, uint64_t 
     }
     bool whole;
     const uint64_t q = next_of(h, n, p, &whole);
-    stage_put(st, scap, cnt, p, h);
+    stage_put(st, scap, cnt, p, h, b0);
     ++cnt;
     h = head(img, n, q);
     if (h.cl) {  // the chain ends after the record at p
@@ -508,7 +516,7 @@ LSMCK_HD void walk_cp(const SegArgs& a, uint32_t k, uint64_t c, Head h, WalkOut*
     }
     bool whole;
     const uint64_t q = next_of(h, n, p, &whole);
-    stage_put(st, a.scap, cnt, p, h);
+    stage_put(st, a.scap, cnt, p, h, b0);
     ++cnt;
     h = head(img, n, q);
     if (h.cl) {
@@ -540,7 +548,7 @@ LSMCK_HD void seg_forced(const SegArgs& a, uint32_t k, uint64_t c) {
   } else if (a.nsub > 1) {
     walk_cp(a, k, c, h, &o);
   } else {
-    walk(a.img, a.n, c, h, seg_end(a, k), &o, seg_stage(a, k), a.scap);
+    walk(a.img, a.n, c, h, seg_end(a, k), &o, seg_stage(a, k), a.scap, seg_begin(a, k));
   }
   a.g[k] = c;
   a.x[k] = o.pos;
@@ -803,10 +811,12 @@ template <class Rec>
 LSMCK_HD void seg_place_rec(const SegArgs& a, uint32_t k, uint64_t at, Rec* recs, uint64_t* poff, uint32_t* plen,
                             uint32_t* pcrc, uint32_t r, const StageRec& R, const Head& nh, const Pack* pk) {
   const uint64_t i = at + (a.pre[k] & kRecMask) + r;
-  put_rec(recs + i, R.rec_off, R.payload_off, R.klen, R.vlen, R.crc, R.type);
-  poff[i] = R.payload_off;
+  const uint32_t t = stage_type(R);
+  const uint64_t rec_off = stage_off(R, seg_begin(a, k)), payload_off = rec_off + hdr_len(t);
+  put_rec(recs + i, rec_off, payload_off, R.klen, R.vlen, R.crc, t);
+  poff[i] = payload_off;
   const uint32_t dlen = R.klen + R.vlen;
-  const uint64_t avail = a.n - R.payload_off;
+  const uint64_t avail = a.n - payload_off;
   const uint32_t got = dlen <= avail ? dlen : (uint32_t)avail;
   const bool fit = pk && i + 1 < pk->iend && pack_fits(got, hdr_len(nh.t));
   plen[i] = fit ? got + hdr_len(nh.t) : got;
@@ -817,7 +827,7 @@ LSMCK_HD Head seg_place_next_head(const SegArgs& a, uint32_t k, uint32_t r) {
   if (r + 1 < a.recs[k]) {
     const StageRec& N = a.srec[(uint64_t)k * a.scap + r + 1];
     Head h{};
-    h.t = N.type;
+    h.t = stage_type(N);
     h.crc = N.crc;
     h.klen = N.klen;
     h.vlen = N.vlen;

@@ -647,7 +647,7 @@ __global__ __launch_bounds__(256) void wal_seg_place(seg::SegArgs a, uint64_t at
     if (r < cnt) R = st[r];
     seg::Head nh{};
     if (PACK) {
-      nh.t = __shfl_down(R.type, 1);
+      nh.t = seg::stage_type(seg::StageRec{(uint32_t)__shfl_down(R.rel_t, 1), 0u, 0u, 0u});
       nh.crc = __shfl_down(R.crc, 1);
       nh.klen = __shfl_down(R.klen, 1);
       nh.vlen = __shfl_down(R.vlen, 1);
