@@ -215,6 +215,9 @@ int lsmck_device_count(void);
  *   "wal_chunk_bytes"  lsmck_wal_replay_verify of a host image: CRC batches
  *                 of this many payload bytes run on a helper thread while the
  *                 walk goes on (default 32 MiB; 0 = one batch after the walk).
+ *   "tree_stages"  whole-tree verify: pinned slots its rounds cycle through
+ *                 (3, default: a round is read while the two before it upload
+ *                 and hash; 2 = round 4's double buffering).  A/B.
  *   "tree_open_files"  files kept open from their first slice to their last
  *                 (-1 = default: as many as RLIMIT_NOFILE leaves after a
  *                 1024-descriptor reserve; the rest reopen per slice).

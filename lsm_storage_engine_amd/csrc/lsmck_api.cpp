@@ -380,7 +380,10 @@ struct lsmck_ctx {
   size_t cap_hwlen = 0;
   uint32_t* h_wexp = nullptr;
   size_t cap_hwexp = 0;
-  Stage stage[2];
+  // the host-batch pipelines alternate over slots 0 and 1; the whole-tree
+  // verify cycles through the first tree_stages of them
+  Stage stage[3];
+  uint32_t tree_stages = 3;
   int variant = 0;  // A/B and diagnostic bits (crc_ablate, crc_stream, sha_order); 0 = default
   uint32_t tree_active = 0;  // whole-tree verify: files in flight (0 = kTreeActive)
   uint32_t tree_slice = 0;   // whole-tree verify: bytes of a file per round (0 = kTreeSlice)
@@ -907,6 +910,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
       return lsmck_host::set_error(LSMCK_EINVAL, "tree_slice_bytes: a multiple of 64, <= 2^30");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->tree_slice = (uint32_t)value;
+    return 0;
+  }
+  if (!strcmp(key, "tree_stages")) {  // whole-tree verify: pinned slots the rounds cycle through (A/B: 2 or 3)
+    if (value < 2 || value > 3) return lsmck_host::set_error(LSMCK_EINVAL, "tree_stages: 2 or 3");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->tree_stages = (uint32_t)value;
     return 0;
   }
   if (!strcmp(key, "tree_open_files")) {  // whole-tree verify: cap on files kept open (-1 = rlimit budget)
@@ -2550,8 +2559,12 @@ static int verify_tables(lsmck_ctx* ctx, const char* const* data_paths, const ch
     std::vector<uint32_t> free_slots;
     for (uint32_t k = active_max; k-- > 0;) free_slots.push_back(k);
     size_t next_file = 0, active = 0;
-    bool busy[2] = {false, false}, any_kernel = false;
-    int sl = 0;
+    // the rounds cycle through ns slots: a round's reads wait for the round
+    // ns back (its slot), so with three the reads of round r + 2 overlap the
+    // upload and hashing of rounds r and r + 1
+    const uint32_t ns = ctx->tree_stages;
+    bool busy[3] = {false, false, false}, any_kernel = false;
+    uint32_t sl = 0;
     std::vector<uint64_t> rd_off;  // per slice: offset inside its file
     SlotFds fds(active_max);
     if (ctx->tree_open >= 0) fds.cached = (uint32_t)std::min<long>(fds.cached, ctx->tree_open);
@@ -2652,10 +2665,10 @@ static int verify_tables(lsmck_ctx* ctx, const char* const* data_paths, const ch
       HIPCHK(hipEventRecord(S.done, S.s));
       busy[sl] = true;
       any_kernel = true;
-      sl ^= 1;
+      sl = sl + 1 < ns ? sl + 1 : 0;
     }
     clk.lap();
-    for (int k = 0; k < 2; ++k)
+    for (uint32_t k = 0; k < ns; ++k)
       if (busy[k]) HIPCHK(hipEventSynchronize(ctx->stage[k].done));
     if (nf) {  // the GPU's digests land at their files' slots; the CPU threads write theirs in place
       std::vector<uint8_t> gd(32 * nf);

@@ -97,6 +97,14 @@ class Server:
             if line and json.loads(line)["event"] == kind:
                 out.append(json.loads(line))
 
+    def wait_stderr(self, text, timeout=10.0):
+        """The stderr lines once one contains `text` (read by a drain thread,
+        so a line written before an event on stdout can arrive after it)."""
+        t_end = time.monotonic() + timeout
+        while text not in self.stderr_tail() and time.monotonic() < t_end and self.proc.poll() is None:
+            time.sleep(0.02)
+        return self.stderr_tail()
+
     def stderr_tail(self):
         """The last lines the server wrote to stderr (all of them once it has exited)."""
         if self.proc.poll() is not None:

@@ -275,7 +275,7 @@ def test_compaction_tick_reverifies_and_panics_like_the_reference(tmp_path):
             f.write(bytes([b[0] ^ 0x04]))
         ev = srv.wait_event("compact_failed")
         assert ev["panic"] == f"Can't load SSTable from {os.path.basename(m.data_path())}. Checksum is not correct"
-        assert "Compact failed" in srv.stderr_tail()
+        assert "Compact failed" in srv.wait_stderr("Compact failed")
         assert c.call(b"get", b"alpha") == b"one"  # still serving
         c.close()
     finally:

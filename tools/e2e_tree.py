@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=float, default=1.0)
     ap.add_argument("--list-threads", default="", help="comma list of tree_list_threads values to A/B (listing time)")
     ap.add_argument("--ab", default="", help="comma list of active:slice_bytes[:open_files] settings to A/B after the main reps")
+    ap.add_argument("--stages", default="",
+                    help="comma list of tree_stages values to A/B (interleaved, 3 rounds each): the verify's seconds")
     ap.add_argument("--multi", type=int, default=0,
                     help="also time lsmck_tree_verify_multi with this many contexts on device 0 against "
                          "lsmck_tree_verify on one (the multi-GPU split's own cost, measurable on one GPU)")
@@ -86,6 +88,15 @@ def main():
         lt[v] = round(min(tree.load_verify(ctx, a.dir)[1]["list_s"] for _ in range(2)), 3)
         print(f"list threads {v}: {lt[v]} s", file=sys.stderr, flush=True)
     ctx.set_option("tree_list_threads", 0)
+    stages = {}
+    for _ in range(3 if a.stages else 0):
+        for v in filter(None, a.stages.split(",")):
+            ctx.set_option("tree_stages", int(v))
+            r = tree.load_verify(ctx, a.dir)[1]
+            stages.setdefault(v, []).append({"tables_s": round(r["tables_s"], 3), **{
+                k: round(x, 3) for k, x in r["tables_split"].items() if isinstance(x, float)}})
+            print(f"stages {v}: {stages[v][-1]}", file=sys.stderr, flush=True)
+    ctx.set_option("tree_stages", 3)
     multi = None
     if a.multi > 1:
         from lsm_storage_engine_amd.device import MultiContext
@@ -121,6 +132,7 @@ def main():
     tc = time.perf_counter() - t0
 
     res = {
+        "tree_stages_ab": stages or None,
         "metric": "GiB/s end-to-end tree load verify (files in the page cache or tmpfs)",
         "value": round(verified / GIB / best["total_s"], 2),
         "unit": "GiB/s",
