@@ -215,6 +215,11 @@ int lsmck_device_count(void);
  *   "wal_chunk_bytes"  lsmck_wal_replay_verify of a host image: CRC batches
  *                 of this many payload bytes run on a helper thread while the
  *                 walk goes on (default 32 MiB; 0 = one batch after the walk).
+ *   "tree_overlap"  lsmck_tree_verify reads the highest level's directory
+ *                 first and, when it holds at least this many tables (default
+ *                 2048; 0 = never), verifies them while the lower levels are
+ *                 listed, then the lower levels' tables.  The report is the
+ *                 same either way (the first failure in read_dir order).
  *   "tree_stages"  whole-tree verify: pinned slots its rounds cycle through
  *                 (3, default: a round is read while the two before it upload
  *                 and hash; 2 = round 4's double buffering).  A/B.

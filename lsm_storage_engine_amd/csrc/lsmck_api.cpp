@@ -384,6 +384,8 @@ struct lsmck_ctx {
   // verify cycles through the first tree_stages of them
   Stage stage[3];
   uint32_t tree_stages = 3;
+  long tree_overlap = 2048;  // lsmck_tree_verify: the top level's tables verified while the lower levels are
+                             // listed, when it holds at least this many (0 = never)
   int variant = 0;  // A/B and diagnostic bits (crc_ablate, crc_stream, sha_order); 0 = default
   uint32_t tree_active = 0;  // whole-tree verify: files in flight (0 = kTreeActive)
   uint32_t tree_slice = 0;   // whole-tree verify: bytes of a file per round (0 = kTreeSlice)
@@ -910,6 +912,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
       return lsmck_host::set_error(LSMCK_EINVAL, "tree_slice_bytes: a multiple of 64, <= 2^30");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->tree_slice = (uint32_t)value;
+    return 0;
+  }
+  if (!strcmp(key, "tree_overlap")) {  // lsmck_tree_verify: the top level verified while the others are listed
+    if (value < 0 || value > (1l << 30)) return lsmck_host::set_error(LSMCK_EINVAL, "tree_overlap: 0 .. 2^30");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->tree_overlap = (long)value;
     return 0;
   }
   if (!strcmp(key, "tree_stages")) {  // whole-tree verify: pinned slots the rounds cycle through (A/B: 2 or 3)
@@ -2876,8 +2884,9 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
     std::vector<std::unique_ptr<ListBatch>> batches;  // load order
     std::mutex mu;
     std::condition_variable cv;
-    size_t next = 0;
+    size_t next = 0, parsed = 0;
     bool done = false;
+    std::condition_variable cv_parsed;
     std::vector<std::thread> th;
     void finish() {
       {
@@ -2906,6 +2915,11 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
           b->st.assign(b->path.size(), 0);
           for (size_t i = 0; i < b->path.size(); ++i)
             if (lsmck_host::read_metadata_json(b->path[i].c_str(), &b->meta[i])) b->st[i] = LSMCK_META_PANIC;
+          {
+            std::lock_guard<std::mutex> lk(lister.mu);
+            ++lister.parsed;
+          }
+          lister.cv_parsed.notify_all();
         }
       });
   }
@@ -2919,9 +2933,12 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
     lister.cv.notify_one();
     cur.reset(new ListBatch);
   };
-  for (int lv = 0; lv < LSMCK_SSTABLE_MAX_LEVEL; ++lv) {
+  for (int lv = 0; lv < LSMCK_SSTABLE_MAX_LEVEL; ++lv) {  // fs::create_dir_all of every level, in order
     const std::string dir = lsmck_host::path_push(base, "level-" + std::to_string(lv));
     if ((rc = mkdir_p(dir))) return lsmck_host::set_errno_error(-rc, "create_dir_all", dir.c_str());
+  }
+  auto scan = [&](int lv) -> int {  // read_dir of one level: its metadata names, in batches to the parsers
+    const std::string dir = lsmck_host::path_push(base, "level-" + std::to_string(lv));
     DIR* d = opendir(dir.c_str());
     if (!d) return lsmck_host::set_errno_error(errno, "read_dir", dir.c_str());
     for (;;) {
@@ -2942,18 +2959,51 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
       }
     }
     closedir(d);
+    publish();
+    return 0;
+  };
+  // Listing beside the verify (tree_overlap, default): the highest level is
+  // read first -- an LSM tree keeps most of its bytes there (the synthetic
+  // tree 85 %, in its largest tables) -- and its tables are verified while the
+  // lower levels are listed; the lower levels' tables follow in a second
+  // batch.  The verify order is free: statuses land per table and the report
+  // takes the first failure in read_dir order (levels 0, 1, ...).
+  const int top = LSMCK_SSTABLE_MAX_LEVEL - 1;
+  if ((rc = scan(top))) return rc;
+  size_t top_batches = 0;
+  {
+    std::unique_lock<std::mutex> lk(lister.mu);
+    top_batches = lister.batches.size();
+    lister.cv_parsed.wait(lk, [&] { return lister.parsed >= top_batches; });
   }
-  publish();
-  lister.finish();
-  std::vector<std::string> mpath;
-  std::vector<lsmck_host::TableMeta> meta;
-  std::vector<int> st;
-  for (auto& b : lister.batches) {
-    for (auto& x : b->path) mpath.push_back(std::move(x));
-    for (auto& x : b->meta) meta.push_back(std::move(x));
-    st.insert(st.end(), b->st.begin(), b->st.end());
-  }
-  const size_t n = mpath.size();
+  // table paths: construct_path = base_path / level-<level> / file (sstable_metadata.rs:43-48)
+  struct Part {
+    std::vector<std::string> dp, ip, cp;
+    std::vector<size_t> which;  // indices into the part's tables
+    std::vector<int> vst;
+    TreeTiming tm;
+    int rc = 0;
+    std::string err;
+  };
+  auto paths_of = [](const std::vector<lsmck_host::TableMeta>& meta, const std::vector<int>& st, size_t i0, size_t i1,
+                     Part* P) {
+    for (size_t i = i0; i < i1; ++i) {
+      if (st[i]) continue;
+      const std::string lvdir = lsmck_host::path_push(meta[i].base_path, "level-" + std::to_string(meta[i].level));
+      P->dp.push_back(lsmck_host::path_push(lvdir, meta[i].data_filename));
+      P->ip.push_back(lsmck_host::path_push(lvdir, meta[i].index_filename));
+      P->cp.push_back(lsmck_host::path_push(lvdir, meta[i].checksum_filename));
+      P->which.push_back(i);
+    }
+  };
+  auto run_part = [ctxs, nctx](Part* P) {
+    const size_t m = P->which.size();
+    std::vector<const char*> dpp(m), ipp(m), cpp(m);
+    for (size_t j = 0; j < m; ++j) dpp[j] = P->dp[j].c_str(), ipp[j] = P->ip[j].c_str(), cpp[j] = P->cp[j].c_str();
+    P->vst.assign(std::max<size_t>(m, 1), 0);
+    P->rc = verify_tables_multi(ctxs, nctx, dpp.data(), ipp.data(), cpp.data(), m, P->vst.data(), &P->tm);
+    if (P->rc < 0) P->err = lsmck_last_error();  // thread-local: carried back
+  };
   // While the metadata files are parsed, each context's staging slots, device
   // buffers and digest table are allocated and the pinned pages mapped: a
   // fresh process otherwise pays for them inside the stream (the first
@@ -2965,7 +3015,7 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
         if (x.joinable()) x.join();
     }
   } prewarm;
-  if (n) {
+  auto start_prewarm = [&](size_t tables) {
     // Grow the process's descriptor table now, in one step: the verify keeps
     // up to 8192 files open, and a table grown descriptor by descriptor under
     // 16 reader threads is resized ~8 times, each resize waiting for an RCU
@@ -2982,39 +3032,77 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
       if (hi >= 0) close(hi);
       close(fd);
     });
+    for (size_t k = 0; k < nctx; ++k)
+      prewarm.t.emplace_back([c = ctxs[k], n = tables]() {
+        const uint32_t active = c->tree_active ? c->tree_active : kTreeActive;
+        const uint32_t slice = c->tree_slice ? c->tree_slice : kTreeSlice;
+        const size_t files = std::min<size_t>(active, 2 * n);
+        const size_t bytes = files * ((size_t)slice + 16) + 16;  // slices are 16-B aligned in the slot
+        std::lock_guard<std::mutex> lk(c->mu);
+        DevGuard g(c->dev);
+        for (auto& S : c->stage) {
+          if (stage_init(S) || ensure_pinned(c->pin_node, &S.h_pay, &S.cap_h_pay, bytes) ||
+              ensure_pinned(c->pin_node, &S.h_slices, &S.cap_h_slices, files) ||
+              ensure_dev(&S.d_pay, &S.cap_d_pay, bytes) || ensure_dev(&S.d_slices, &S.cap_d_slices, files))
+            return;  // the verify reports it
+          // map the pinned pages now, not on the readers' first touch
+          if (madvise(S.h_pay, S.cap_h_pay, 23 /* MADV_POPULATE_WRITE */) != 0)
+            for (size_t o = 0; o < S.cap_h_pay; o += 4096) ((volatile uint8_t*)S.h_pay)[o] = 0;
+        }
+        (void)ensure_dev(&c->tree.state, &c->tree.cap_state, 8ull * active);
+        (void)ensure_dev(&c->tree.digests, &c->tree.cap_digests, 32 * 2 * n);
+      });
+  };
+  // the top level's tables, parsed: verified now (at least tree_overlap of them: enough to pay for a second batch)
+  std::vector<lsmck_host::TableMeta> top_meta;
+  std::vector<std::string> top_mpath;
+  std::vector<int> top_st;
+  for (size_t k = 0; k < top_batches; ++k) {
+    ListBatch& B = *lister.batches[k];
+    top_mpath.insert(top_mpath.end(), B.path.begin(), B.path.end());
+    top_meta.insert(top_meta.end(), B.meta.begin(), B.meta.end());
+    top_st.insert(top_st.end(), B.st.begin(), B.st.end());
   }
-  for (size_t k = 0; k < nctx && n; ++k)
-    prewarm.t.emplace_back([c = ctxs[k], n]() {
-      const uint32_t active = c->tree_active ? c->tree_active : kTreeActive;
-      const uint32_t slice = c->tree_slice ? c->tree_slice : kTreeSlice;
-      const size_t files = std::min<size_t>(active, 2 * n);
-      const size_t bytes = files * ((size_t)slice + 16) + 16;  // slices are 16-B aligned in the slot
-      std::lock_guard<std::mutex> lk(c->mu);
-      DevGuard g(c->dev);
-      for (auto& S : c->stage) {
-        if (stage_init(S) || ensure_pinned(c->pin_node, &S.h_pay, &S.cap_h_pay, bytes) ||
-            ensure_pinned(c->pin_node, &S.h_slices, &S.cap_h_slices, files) || ensure_dev(&S.d_pay, &S.cap_d_pay, bytes) ||
-            ensure_dev(&S.d_slices, &S.cap_d_slices, files))
-          return;  // the verify reports it
-        // map the pinned pages now, not on the readers' first touch
-        if (madvise(S.h_pay, S.cap_h_pay, 23 /* MADV_POPULATE_WRITE */) != 0)
-          for (size_t o = 0; o < S.cap_h_pay; o += 4096) ((volatile uint8_t*)S.h_pay)[o] = 0;
-      }
-      (void)ensure_dev(&c->tree.state, &c->tree.cap_state, 8ull * active);
-      (void)ensure_dev(&c->tree.digests, &c->tree.cap_digests, 32 * 2 * n);
+  const size_t n_top = top_mpath.size();
+  const bool early = ctx->tree_overlap > 0 && n_top >= (size_t)ctx->tree_overlap;
+  Part ptop, prest;
+  std::thread early_th;
+  struct ThreadJoin {
+    std::thread* t;
+    ~ThreadJoin() {
+      if (t->joinable()) t->join();
+    }
+  } early_join{&early_th};
+  if (early) {
+    paths_of(top_meta, top_st, 0, n_top, &ptop);
+    start_prewarm(n_top);
+    early_th = std::thread([&]() {
+      for (auto& x : prewarm.t) x.join();
+      run_part(&ptop);
     });
-  // table paths: construct_path = base_path / level-<level> / file (sstable_metadata.rs:43-48)
-  std::vector<std::string> dp, ip, cp;
-  std::vector<size_t> which;
-  for (size_t i = 0; i < n; ++i) {
-    if (st[i]) continue;
-    const std::string lvdir =
-        lsmck_host::path_push(meta[i].base_path, "level-" + std::to_string(meta[i].level));
-    dp.push_back(lsmck_host::path_push(lvdir, meta[i].data_filename));
-    ip.push_back(lsmck_host::path_push(lvdir, meta[i].index_filename));
-    cp.push_back(lsmck_host::path_push(lvdir, meta[i].checksum_filename));
-    which.push_back(i);
   }
+  for (int lv = 0; lv < top; ++lv)
+    if ((rc = scan(lv))) return rc;
+  lister.finish();
+  // the listing in read_dir order: levels 0 .. top - 1, then the top level (scanned first)
+  std::vector<std::string> mpath;
+  std::vector<lsmck_host::TableMeta> meta;
+  std::vector<int> st;
+  for (size_t k = top_batches; k < lister.batches.size(); ++k) {
+    ListBatch& B = *lister.batches[k];
+    for (auto& x : B.path) mpath.push_back(std::move(x));
+    for (auto& x : B.meta) meta.push_back(std::move(x));
+    st.insert(st.end(), B.st.begin(), B.st.end());
+  }
+  const size_t n_low = mpath.size();
+  for (size_t i = 0; i < n_top; ++i) {
+    mpath.push_back(std::move(top_mpath[i]));
+    meta.push_back(std::move(top_meta[i]));
+    st.push_back(top_st[i]);
+  }
+  const size_t n = mpath.size();
+  if (!early && n) start_prewarm(n);
+  paths_of(meta, st, 0, early ? n_low : n, &prest);
   rep->tables = n;
   rep->list_seconds = seconds_since(t0);
   if (fn) {  // the caller's half of Db::load starts from this listing
@@ -3042,14 +3130,20 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
     listed.cps.swap(cps);
     fn(user, listed.ents.data(), n);
   }
-  for (auto& x : prewarm.t) x.join();
-  const size_t m = which.size();
-  std::vector<const char*> dpp(m), ipp(m), cpp(m);
-  for (size_t j = 0; j < m; ++j) dpp[j] = dp[j].c_str(), ipp[j] = ip[j].c_str(), cpp[j] = cp[j].c_str();
-  std::vector<int> vst(std::max<size_t>(m, 1), 0);
-  TreeTiming tm;
-  rc = verify_tables_multi(ctxs, nctx, dpp.data(), ipp.data(), cpp.data(), m, vst.data(), &tm);
-  if (rc < 0) return rc;
+  if (!early)
+    for (auto& x : prewarm.t) x.join();
+  run_part(&prest);  // (beside the top level's verify: its host half; its GPU half waits for the context)
+  if (early_th.joinable()) early_th.join();
+  for (Part* P : {&prest, &ptop})
+    if (P->rc < 0) return lsmck_host::set_error(P->rc, P->err.c_str());
+  TreeTiming tm = prest.tm;
+  tm.bytes += ptop.tm.bytes;
+  tm.rounds += ptop.tm.rounds;
+  tm.stat += ptop.tm.stat;
+  tm.read += ptop.tm.read;
+  tm.wait += ptop.tm.wait;
+  tm.compare += ptop.tm.compare;
+  tm.fds_cached = std::max(tm.fds_cached, ptop.tm.fds_cached);
   rep->table_bytes = tm.bytes;
   rep->rounds = tm.rounds;
   rep->stat_seconds = tm.stat;
@@ -3057,7 +3151,8 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
   rep->gpu_wait_seconds = tm.wait;
   rep->compare_seconds = tm.compare;
   rep->fds_cached = tm.fds_cached;
-  for (size_t j = 0; j < m; ++j) st[which[j]] = vst[j];
+  for (size_t j = 0; j < prest.which.size(); ++j) st[prest.which[j]] = prest.vst[j];
+  for (size_t j = 0; j < ptop.which.size(); ++j) st[n_low + ptop.which[j]] = ptop.vst[j];
   rep->verify_seconds = seconds_since(t0) - rep->list_seconds;
   for (size_t i = 0; i < n; ++i) {
     if (!st[i]) continue;

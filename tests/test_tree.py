@@ -269,3 +269,52 @@ def test_multicontext_tree_verify(ctx, tmp_path):
     finally:
         for c in mc.ctxs:
             c.close()
+
+
+@pytest.mark.gpu
+def test_tree_verify_top_level_beside_the_listing(ctx, small_tree, tmp_path):
+    """"tree_overlap": the highest level's tables verified while the lower
+    levels are listed (forced on this small tree) reports exactly what one
+    batch does: the same listing, statuses and first failure in read_dir order
+    (db.rs:37-59), with corruptions in either part."""
+    import shutil
+    base = str(tmp_path / "o")
+    shutil.copytree(small_tree[0], base)
+    for p in tree.scan_order(base):
+        d = json.load(open(p))
+        d["base_path"] = base
+        with open(p, "w") as f:
+            f.write(json.dumps(d, separators=(",", ":")))
+    paths = tree.scan_order(base)
+    order = [SsTableMetadata.load(p) for p in paths]
+    top = max(m.level for m in order)
+    it = next(i for i, m in enumerate(order) if m.level == top)
+    il = next(i for i, m in enumerate(order) if m.level == 1)
+    keys = ("tables", "table_bytes", "bad_tables", "first_index", "first_status", "first_metadata_path")
+
+    def both():
+        out = []
+        for v in (0, 1):
+            ctx.set_option("tree_overlap", v)
+            listed = []
+            r = ctx.tree_verify(base, listed=listed)
+            out.append(({k: r[k] for k in keys}, [(e["metadata_path"], e["status"]) for e in listed]))
+        assert out[0] == out[1]
+        return out[0][0]
+
+    try:
+        r = both()
+        assert r["bad_tables"] == 0 and r["tables"] == len(order)
+        with open(order[it].data_path(), "r+b") as f:  # a top-level table: verified in the early batch
+            f.seek(5)
+            f.write(b"\x7f")
+        r = both()
+        assert (r["bad_tables"], r["first_index"], r["first_status"]) == (1, it, 1)
+        with open(order[il].index_path(), "r+b") as f:  # a level-1 table: earlier in read_dir order
+            f.seek(9)
+            f.write(b"\xff")
+        r = both()
+        assert (r["bad_tables"], r["first_index"], r["first_status"]) == (2, il, 2)
+        assert r["first_metadata_path"] == paths[il]
+    finally:
+        ctx.set_option("tree_overlap", 2048)

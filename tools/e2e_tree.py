@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--ab", default="", help="comma list of active:slice_bytes[:open_files] settings to A/B after the main reps")
     ap.add_argument("--stages", default="",
                     help="comma list of tree_stages values to A/B (interleaved, 3 rounds each): the verify's seconds")
+    ap.add_argument("--overlap", default="",
+                    help="comma list of tree_overlap values to A/B (interleaved, 3 rounds each): list + verify seconds")
     ap.add_argument("--multi", type=int, default=0,
                     help="also time lsmck_tree_verify_multi with this many contexts on device 0 against "
                          "lsmck_tree_verify on one (the multi-GPU split's own cost, measurable on one GPU)")
@@ -97,6 +99,15 @@ def main():
                 k: round(x, 3) for k, x in r["tables_split"].items() if isinstance(x, float)}})
             print(f"stages {v}: {stages[v][-1]}", file=sys.stderr, flush=True)
     ctx.set_option("tree_stages", 3)
+    overlap = {}
+    for _ in range(3 if a.overlap else 0):
+        for v in filter(None, a.overlap.split(",")):
+            ctx.set_option("tree_overlap", int(v))
+            r = tree.load_verify(ctx, a.dir)[1]
+            overlap.setdefault(v, []).append({"list_s": round(r["list_s"], 3), "tables_s": round(r["tables_s"], 3),
+                                              "list_plus_tables_s": round(r["list_s"] + r["tables_s"], 3)})
+            print(f"overlap {v}: {overlap[v][-1]}", file=sys.stderr, flush=True)
+    ctx.set_option("tree_overlap", 2048)
     multi = None
     if a.multi > 1:
         from lsm_storage_engine_amd.device import MultiContext
@@ -133,6 +144,7 @@ def main():
 
     res = {
         "tree_stages_ab": stages or None,
+        "tree_overlap_ab": overlap or None,
         "metric": "GiB/s end-to-end tree load verify (files in the page cache or tmpfs)",
         "value": round(verified / GIB / best["total_s"], 2),
         "unit": "GiB/s",
