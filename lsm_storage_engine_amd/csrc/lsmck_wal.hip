@@ -437,6 +437,7 @@ template <int G>
 __global__ __launch_bounds__(256) void wal_seg_walk_group(seg::SegArgs a) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, k = t / G, j = t % G;
   if (k >= a.K) return;  // (the whole group)
+  if (j == 0) LSMCK_SEG_CLOCK_MARK(k, 0);
   if (k == 0) {
     if (j == 0) seg::seg_forced(a, 0, a.start);
     return;
@@ -444,7 +445,9 @@ __global__ __launch_bounds__(256) void wal_seg_walk_group(seg::SegArgs a) {
   uint64_t c = guess_group<G>(a, k, j);
   if (c != seg::kNoGuess && seg::seg_later(a)) c = later_group<G>(a, k, j, c);  // (c: the group's, in every lane)
   if (j != 0) return;
+  LSMCK_SEG_CLOCK_MARK(k, 1);
   seg::seg_take_guess(a, k, c);
+  LSMCK_SEG_CLOCK_MARK(k, 2);
 }
 
 __global__ __launch_bounds__(256) void wal_seg_jterm(seg::SegArgs a) {

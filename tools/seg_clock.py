@@ -20,6 +20,8 @@ from lsm_storage_engine_amd.device import Context, gen_zipf_lengths, WAL_REC_DTY
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 26
+    lanes = int(os.environ.get("SEG_CLOCK_LANES", "1"))  # lanes per segment of the build (LSMCK_SEG_GUESS_LANES)
+    seg_bytes = int(os.environ.get("SEG_CLOCK_SEG_BYTES", "0"))  # wal_seg_bytes (0: automatic)
     ln = gen_zipf_lengths(0x5EED0003, n)
     off = np.full(n, 13, dtype=np.uint64)
     off[1:] += ln[:-1].astype(np.uint64)
@@ -35,6 +37,7 @@ def main():
     ctx.wal_frame_insert_device(d.ptr, d_o.ptr, d_l.ptr, out.ptr, n, 16)
     ctx.sync()
     rb = ctx.alloc(n * WAL_REC_DTYPE.itemsize)
+    ctx.set_option("wal_seg_bytes", seg_bytes)
     for _ in range(3):
         m, st, bad = ctx.wal_replay_verify_to_device(total, rb.ptr, n, device_ptr=d.ptr)
         assert st == 0 and m == n
@@ -49,10 +52,11 @@ def main():
     guess = (t[:, 1] - t[:, 0]) / 100.0  # us
     walk = (t[:, 2] - t[:, 1]) / 100.0
     end = (t[:, 2] - t0) / 100.0
-    W = K // 64
-    wg = guess[:W * 64].reshape(W, 64)
-    ww = walk[:W * 64].reshape(W, 64)
-    res = {"segments": int(K), "kernel_span_us": float(end.max()),
+    per = 64 // lanes  # segments per wave
+    W = K // per
+    wg = guess[:W * per].reshape(W, per)
+    ww = walk[:W * per].reshape(W, per)
+    res = {"segments": int(K), "lanes_per_segment": lanes, "seg_bytes": seg_bytes, "kernel_span_us": float(end.max()),
            "lane_guess_us": {"mean": float(guess.mean()), "p50": float(np.median(guess)), "p99": float(np.percentile(guess, 99)), "max": float(guess.max())},
            "lane_walk_us": {"mean": float(walk.mean()), "p50": float(np.median(walk)), "p99": float(np.percentile(walk, 99)), "max": float(walk.max())},
            "wave_max_guess_us": {"mean": float(wg.max(1).mean()), "p50": float(np.median(wg.max(1)))},
