@@ -22,7 +22,7 @@
 #define LSMCK_LATER_SCAN 65536
 #endif
 #ifndef LSMCK_SCAN_BLOCKS
-#define LSMCK_SCAN_BLOCKS 4
+#define LSMCK_SCAN_BLOCKS 1
 #endif
 
 namespace lsmck {

@@ -58,7 +58,7 @@ namespace tune {
 constexpr uint64_t kLaterSkipTo = 131072;  // kLaterSkipTo below
 constexpr uint64_t kLaterMin = 65536;      // kLaterMin below
 constexpr uint64_t kLaterScan = 65536;     // kLaterScan below
-constexpr int kScanBlocks = 4;             // kScanBlocks below
+constexpr int kScanBlocks = 1;             // kScanBlocks below
 constexpr bool kLaterAlways = false;       // (host-model A/B: the later-start rule everywhere)
 }  // namespace tune
 }  // namespace seg
@@ -121,7 +121,12 @@ constexpr uint64_t kLaterMin = tune::kLaterMin;
 // (profiles/r05/kt).  A longer-range merge is caught by the check and
 // repaired (seg_prepair).
 constexpr uint64_t kLaterScan = tune::kLaterScan;
-constexpr int kScanBlocks = tune::kScanBlocks;  // 64-byte blocks the guess scan loads per iteration
+// 64-byte blocks the guess scan loads per iteration.  One (round 5): the
+// walk kernel then needs 63 VGPRs instead of 123 -- eight waves a SIMD, so
+// twice the segments' groups in flight -- and each guess takes eight lanes
+// (97.8 GiB config-3w log 25.0-25.15 -> 24.8-24.9 ms in HBM, ~1 MiB values
+// 40.8 -> 35.3 ms; profiles/r05/sb/)
+constexpr int kScanBlocks = tune::kScanBlocks;
 // per-segment record counts and the guessed-segment count share one u64 in
 // the placement scan: guessed segments in the top 24 bits, records below
 constexpr int kSegShift = 40;

@@ -698,7 +698,7 @@ extern "C" uint64_t lsmk_wal_seg_scan_blocks(uint32_t K) {
 #define LSMCK_SEG_GUESS_LANES 1  // (the clock marks are in the one-lane walk)
 #endif
 #ifndef LSMCK_SEG_GUESS_LANES
-#define LSMCK_SEG_GUESS_LANES 4
+#define LSMCK_SEG_GUESS_LANES 8  // (round 5: four lanes with four-block scan steps before)
 #endif
 extern "C" int lsmk_wal_seg_walk(const seg::SegArgs* a, hipStream_t st) {
   constexpr int G = LSMCK_SEG_GUESS_LANES;
