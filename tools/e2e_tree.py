@@ -47,6 +47,9 @@ def main():
                     help="comma list of tree_stages values to A/B (interleaved, 3 rounds each): the verify's seconds")
     ap.add_argument("--overlap", default="",
                     help="comma list of tree_overlap values to A/B (interleaved, 3 rounds each): list + verify seconds")
+    ap.add_argument("--tick", default="",
+                    help="comma list of tree_json_threads[:tree_active_files] values: the compaction tick's batch (levels 0..3 through "
+                         "lsmck_checksums_verify_many), interleaved, 3 rounds each")
     ap.add_argument("--multi", type=int, default=0,
                     help="also time lsmck_tree_verify_multi with this many contexts on device 0 against "
                          "lsmck_tree_verify on one (the multi-GPU split's own cost, measurable on one GPU)")
@@ -108,6 +111,25 @@ def main():
                                               "list_plus_tables_s": round(r["list_s"] + r["tables_s"], 3)})
             print(f"overlap {v}: {overlap[v][-1]}", file=sys.stderr, flush=True)
     ctx.set_option("tree_overlap", 2048)
+    tick = {}
+    if a.tick:
+        low = [m for m in tree.list_tables(a.dir) if m.level <= 3]
+        triples = [(m.data_path(), m.index_path(), m.checksum_path()) for m in low]
+        nbytes = sum(os.path.getsize(x) + os.path.getsize(y) for x, y, _ in triples)
+        for _ in range(3):
+            for v in filter(None, a.tick.split(",")):
+                jt, act = ([int(x) for x in v.split(":")] + [0])[:2]  # json threads[:active files]
+                ctx.set_option("tree_json_threads", jt)
+                ctx.set_option("tree_active_files", act)
+                t = time.perf_counter()
+                st = ctx.checksums_verify_many(triples)
+                dt = time.perf_counter() - t
+                assert not any(st)
+                tick.setdefault(v, []).append(round(dt, 3))
+                print(f"tick json threads[:active] {v}: {len(triples)} tables, {nbytes / GIB:.2f} GiB, {dt:.3f} s",
+                      file=sys.stderr, flush=True)
+        ctx.set_option("tree_json_threads", 0)
+        ctx.set_option("tree_active_files", 0)
     multi = None
     if a.multi > 1:
         from lsm_storage_engine_amd.device import MultiContext
@@ -145,6 +167,7 @@ def main():
     res = {
         "tree_stages_ab": stages or None,
         "tree_overlap_ab": overlap or None,
+        "tick_json_threads_ab": tick or None,
         "metric": "GiB/s end-to-end tree load verify (files in the page cache or tmpfs)",
         "value": round(verified / GIB / best["total_s"], 2),
         "unit": "GiB/s",
