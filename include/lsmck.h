@@ -220,6 +220,9 @@ int lsmck_device_count(void);
  *                 2048; 0 = never), verifies them while the lower levels are
  *                 listed, then the lower levels' tables.  The report is the
  *                 same either way (the first failure in read_dir order).
+ *   "tree_json_threads"  whole-tree verify: threads reading the tables'
+ *                 checksum files beside the stream (0 = default: 2, or 4 for
+ *                 a batch of 16k tables or more).
  *   "tree_stages"  whole-tree verify: pinned slots its rounds cycle through
  *                 (3, default: a round is read while the two before it upload
  *                 and hash; 2 = round 4's double buffering).  A/B.
