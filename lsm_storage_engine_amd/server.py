@@ -29,7 +29,7 @@ class ServerExited(RuntimeError):
 
 class Server:
     def __init__(self, base, port=0, memtable_limit=4096, device=0, timeout=600, exit_after_load=False,
-                 compact_interval_ms=None):
+                 compact_interval_ms=None, index_threads=None):
         if not os.path.exists(BIN):
             raise FileNotFoundError(f"{BIN} is not built (make -C lsm_storage_engine_amd/csrc)")
         cmd = [BIN, "--base", str(base), "--port", str(port), "--memtable-limit", str(memtable_limit),
@@ -38,6 +38,8 @@ class Server:
             cmd.append("--exit-after-load")
         if compact_interval_ms is not None:  # the server's default is the reference's 10 s tick
             cmd += ["--compact-interval", str(int(compact_interval_ms))]
+        if index_threads is not None:  # Db::load's index-loading threads (A/B)
+            cmd += ["--index-threads", str(int(index_threads))]
         self.proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
         # stderr is drained on its own thread into a bounded tail: an undrained
         # pipe fills at 64 KiB (LSMCK_TREE_TRACE prints a line per round) and

@@ -107,6 +107,8 @@ def main():
     ap.add_argument("--compact-interval", type=int, default=10000,
                     help="ms between the server's compaction ticks (server.rs:94; each re-verifies levels 0..3)")
     ap.add_argument("--keep", action="store_true")
+    ap.add_argument("--load-ab", default="",
+                    help="comma list of --index-threads values: more restarts (Db::load only), interleaved, 3 each")
     a = ap.parse_args()
 
     marker = os.path.join(a.dir, "e2e_tree.json")
@@ -168,6 +170,14 @@ def main():
             mismatches += 1
     c.close()
     srv.kill()
+    load_ab = {}
+    for _ in range(3 if a.load_ab else 0):
+        for v in filter(None, a.load_ab.split(",")):
+            s2 = Server(a.dir, memtable_limit=a.memtable_limit, exit_after_load=True, index_threads=int(v))
+            ld = s2.loaded
+            s2.kill()
+            load_ab.setdefault(v, []).append({k: ld[k] for k in ("load_s", "tree_verify_s", "tree_list_s", "index_load_s")})
+            print(f"load index threads {v}: {load_ab[v][-1]}", file=sys.stderr, flush=True)
 
     # CPU baseline: the oracle's SHA-256, one thread, the first tables' files
     from oracle import oracle as O
@@ -196,6 +206,7 @@ def main():
                     "commands_per_s": round(a.conns * a.ops / wall, 1),
                     "mix": "per connection: 80% insert, 10% get, 10% delete, pipelined 512 per round trip"},
         "restart": {**load2, "process_start_s": round(start2, 3)},
+        "load_index_threads_ab": load_ab or None,
         "compaction_ticks": {"interval_ms": a.compact_interval, "ticks_during_traffic": len(ticks),
                              "what": "Db::compact's re-verify of levels 0..3 (SsTable::clone = SsTable::load -> "
                                      "Checksums::verify) in one GPU batch per tick, beside the traffic",
