@@ -644,17 +644,31 @@ __global__ __launch_bounds__(256) void wal_seg_place(seg::SegArgs a, uint64_t at
   const seg::StageRec* st = a.srec + (uint64_t)k * a.scap;
   const uint64_t i0 = at + (a.pre[k] & seg::kRecMask);
   const seg::Pack pk{iend, T};
+  // The slots two windows of 64 ahead are loaded while a window is placed (a
+  // wave walks its segment's slots in ~20 windows); the record after a
+  // window's lane 63 is the next window's lane 0, already loaded.
+  seg::StageRec W0{}, W1{};
+  if (lane < cnt) W0 = st[lane];
+  if (64u + lane < cnt) W1 = st[64u + lane];
   for (uint32_t r0 = 0; r0 < cnt; r0 += 64u) {  // (wave-uniform)
     const uint32_t r = r0 + lane;
-    seg::StageRec R{};
-    if (r < cnt) R = st[r];
+    const seg::StageRec R = W0;
+    W0 = W1;
+    W1 = seg::StageRec{};
+    if (r + 128u < cnt) W1 = st[r + 128u];
     seg::Head nh{};
     if (PACK) {
-      nh.t = seg::stage_type(seg::StageRec{(uint32_t)__shfl_down(R.rel_t, 1), 0u, 0u, 0u});
-      nh.crc = __shfl_down(R.crc, 1);
-      nh.klen = __shfl_down(R.klen, 1);
-      nh.vlen = __shfl_down(R.vlen, 1);
-      if (r < cnt && (lane == 63u || r + 1u == cnt) && i0 + r + 1u < iend) nh = seg::seg_place_next_head(a, k, r);
+      const bool l63 = lane == 63u;  // (the next window's lane 0)
+      const uint32_t nrel = (uint32_t)__shfl_down(R.rel_t, 1), frel = (uint32_t)__shfl(W0.rel_t, 0);
+      const uint32_t ncrc = (uint32_t)__shfl_down(R.crc, 1), fcrc = (uint32_t)__shfl(W0.crc, 0);
+      const uint32_t nkl = (uint32_t)__shfl_down(R.klen, 1), fkl = (uint32_t)__shfl(W0.klen, 0);
+      const uint32_t nvl = (uint32_t)__shfl_down(R.vlen, 1), fvl = (uint32_t)__shfl(W0.vlen, 0);
+      nh.t = seg::stage_type(seg::StageRec{l63 ? frel : nrel, 0u, 0u, 0u});
+      nh.crc = l63 ? fcrc : ncrc;
+      nh.klen = l63 ? fkl : nkl;
+      nh.vlen = l63 ? fvl : nvl;
+      // the segment's last record: the header at its exit (another segment's first)
+      if (r < cnt && r + 1u == cnt && i0 + r + 1u < iend) nh = seg::seg_place_next_head(a, k, r);
     }
     if (r < cnt) seg::seg_place_rec(a, k, at, recs, poff, plen, pcrc, r, R, nh, PACK ? &pk : nullptr);
   }
