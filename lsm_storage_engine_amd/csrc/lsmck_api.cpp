@@ -136,10 +136,80 @@ bool node_cpus(int node, cpu_set_t* set) {
   return n > 0;
 }
 constexpr int kMpolDefault = 0, kMpolPreferred = 1;
+
+// Large pinned buffers are anonymous huge pages, populated and then
+// registered (hipHostRegister): 1 GiB costs a fresh process ~0.04 s that way
+// against ~0.2 s through hipHostMalloc, and ~0.04 s against ~0.13 s to free,
+// at the same upload rate (tools/microbench_pin.hip, profiles/r05/pin; the
+// tree verify's three ~1 GiB slots are allocated while the tree is listed).
+// The registry tells host_free which way a pointer came.
+constexpr size_t kHugePinMin = 2u << 20;
+struct HugePins {
+  std::mutex mu;
+  std::vector<std::pair<void*, size_t>> v;
+};
+HugePins& huge_pins() {
+  static HugePins h;
+  return h;
+}
+hipError_t host_malloc_huge(void** p, size_t bytes, int node) {
+  const size_t len = (bytes + kHugePinMin - 1) & ~(kHugePinMin - 1);
+  void* q = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (q == MAP_FAILED) return hipErrorOutOfMemory;
+  (void)madvise(q, len, MADV_HUGEPAGE);
+  if (node >= 0 && node < 1024) {  // pages on the device's node, as hipHostMallocNumaUser places them
+    unsigned long mask[16] = {0};
+    mask[node / 64] |= 1ul << (node % 64);
+    (void)syscall(SYS_mbind, q, len, kMpolPreferred, mask, 16 * 64, 0);
+  }
+  (void)madvise(q, len, 23 /* MADV_POPULATE_WRITE; hipHostRegister faults in what it leaves */);
+  const hipError_t e = hipHostRegister(q, len, hipHostRegisterPortable | hipHostRegisterMapped);
+  if (e != hipSuccess) {
+    munmap(q, len);
+    return e;
+  }
+  {
+    std::lock_guard<std::mutex> lk(huge_pins().mu);
+    huge_pins().v.emplace_back(q, len);
+  }
+  *p = q;
+  return hipSuccess;
+}
+// frees what host_malloc_near (or hipHostMalloc) gave
+void host_free(void* p) {
+  if (!p) return;
+  size_t len = 0;
+  {
+    std::lock_guard<std::mutex> lk(huge_pins().mu);
+    auto& v = huge_pins().v;
+    for (size_t i = 0; i < v.size(); ++i)
+      if (v[i].first == p) {
+        len = v[i].second;
+        v[i] = v.back();
+        v.pop_back();
+        break;
+      }
+  }
+  if (len) {
+    (void)hipHostUnregister(p);
+    munmap(p, len);
+  } else {
+    (void)hipHostFree(p);
+  }
+}
+
 // pinned host memory, on NUMA node `node` when one is given (the context's pin_node): the
 // calling thread's policy prefers that node while HIP allocates and pins
 // the pages (hipHostMallocNumaUser), then goes back to what it was
-hipError_t host_malloc_near(void** p, size_t bytes, int node) {
+// huge: large buffers as registered huge pages (the tree verify's slots;
+// not the buffers the SDMA read-back of lsmck_dma lands in, which take
+// HIP's own pinned allocations)
+hipError_t host_malloc_near(void** p, size_t bytes, int node, bool huge = false) {
+  if (huge && bytes >= kHugePinMin) {
+    const hipError_t e = host_malloc_huge(p, bytes, node);
+    if (e == hipSuccess) return e;
+    (void)hipGetLastError();  // (then as before)
+  }
   if (node < 0 || node >= 1024) return hipHostMalloc(p, bytes, hipHostMallocDefault);
   int old_mode = kMpolDefault;
   unsigned long old_mask[16] = {0};
@@ -158,14 +228,14 @@ hipError_t host_malloc_near(void** p, size_t bytes, int node) {
 }
 
 template <typename T>
-int ensure_pinned(int node, T** p, size_t* cap, size_t need) {
+int ensure_pinned(int node, T** p, size_t* cap, size_t need, bool huge = false) {
   if (*cap >= need && *p) return 0;
   size_t want = std::max(need, *cap * 3 / 2);
   if (want == 0) want = 1;
-  if (*p) (void)hipHostFree(*p);
+  if (*p) host_free(*p);
   *p = nullptr;
   *cap = 0;
-  HIPCHK(host_malloc_near((void**)p, want * sizeof(T), node));
+  HIPCHK(host_malloc_near((void**)p, want * sizeof(T), node, huge));
   *cap = want;
   return 0;
 }
@@ -249,15 +319,15 @@ struct Stage {
   // bookkeeping of the chunk in flight
   size_t rec0 = 0, nrec = 0;
   void release() {
-    if (h_pay) (void)hipHostFree(h_pay);
-    if (h_off) (void)hipHostFree(h_off);
-    if (h_len) (void)hipHostFree(h_len);
-    if (h_out) (void)hipHostFree(h_out);
+    if (h_pay) host_free(h_pay);
+    if (h_off) host_free(h_off);
+    if (h_len) host_free(h_len);
+    if (h_out) host_free(h_out);
     if (d_pay) (void)hipFree(d_pay);
     if (d_off) (void)hipFree(d_off);
     if (d_len) (void)hipFree(d_len);
     if (d_out) (void)hipFree(d_out);
-    if (h_slices) (void)hipHostFree(h_slices);
+    if (h_slices) host_free(h_slices);
     if (d_slices) (void)hipFree(d_slices);
     scratch.release();
     if (done) (void)hipEventDestroy(done);
@@ -1154,26 +1224,26 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   for (void* p : {(void*)ctx->wd.bits, (void*)ctx->wd.pre, (void*)ctx->wd.bsum, (void*)ctx->wd.pos, (void*)ctx->wd.J,
                   (void*)ctx->wd.badpos, (void*)ctx->wd.chain, (void*)ctx->wd.recs, (void*)ctx->wd.info})
     if (p) (void)hipFree(p);
-  if (ctx->wd.h_info) (void)hipHostFree(ctx->wd.h_info);
+  if (ctx->wd.h_info) host_free(ctx->wd.h_info);
   for (void* p : {(void*)ctx->wd.sg, (void*)ctx->wd.sx, (void*)ctx->wd.spre, (void*)ctx->wd.scode,
                   (void*)ctx->wd.srecs, (void*)ctx->wd.sbsum, (void*)ctx->wd.sinfo, (void*)ctx->wd.scpp,
                   (void*)ctx->wd.scpc, (void*)ctx->wd.sst, (void*)ctx->wd.sg0, (void*)ctx->wd.sx0,
                   (void*)ctx->wd.scode0})
     if (p) (void)hipFree(p);
-  if (ctx->wd.h_sinfo) (void)hipHostFree(ctx->wd.h_sinfo);
+  if (ctx->wd.h_sinfo) host_free(ctx->wd.h_sinfo);
   for (void* p : {(void*)ctx->d_vcrc, (void*)ctx->d_woff, (void*)ctx->d_wlen, (void*)ctx->d_wexp})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)ctx->h_woff, (void*)ctx->h_wlen, (void*)ctx->h_wexp})
-    if (p) (void)hipHostFree(p);
-  if (ctx->h_verify) (void)hipHostFree(ctx->h_verify);
-  if (ctx->h_wrecs) (void)hipHostFree(ctx->h_wrecs);
+    if (p) host_free(p);
+  if (ctx->h_verify) host_free(ctx->h_verify);
+  if (ctx->h_wrecs) host_free(ctx->h_wrecs);
   if (ctx->wd.recs16) (void)hipFree(ctx->wd.recs16);
   lsmck_dma::destroy(ctx->dma);
   if (ctx->wal_emit_ev) (void)hipEventDestroy(ctx->wal_emit_ev);
-  if (ctx->h_wrecs1) (void)hipHostFree(ctx->h_wrecs1);
+  if (ctx->h_wrecs1) host_free(ctx->h_wrecs1);
   if (ctx->wal_emit1_ev) (void)hipEventDestroy(ctx->wal_emit1_ev);
   if (ctx->wal_rs) (void)hipStreamDestroy(ctx->wal_rs);
-  if (ctx->wal_host) (void)hipHostFree(ctx->wal_host);
+  if (ctx->wal_host) host_free(ctx->wal_host);
   if (ctx->d_wimg) (void)hipFree(ctx->d_wimg);
   if (ctx->scratch_ev) (void)hipEventDestroy(ctx->scratch_ev);
   if (ctx->stream0) (void)hipStreamDestroy(ctx->stream0);
@@ -2634,8 +2704,8 @@ static int verify_tables(lsmck_ctx* ctx, const char* const* data_paths, const ch
         }
       }
       const size_t cnt = sv.size();
-      if ((rc = ensure_pinned(ctx->pin_node, &S.h_pay, &S.cap_h_pay, pay + 16))) return rc;
-      if ((rc = ensure_pinned(ctx->pin_node, &S.h_slices, &S.cap_h_slices, cnt))) return rc;
+      if ((rc = ensure_pinned(ctx->pin_node, &S.h_pay, &S.cap_h_pay, pay + 16, true))) return rc;
+      if ((rc = ensure_pinned(ctx->pin_node, &S.h_slices, &S.cap_h_slices, cnt, true))) return rc;
       if ((rc = ensure_dev(&S.d_pay, &S.cap_d_pay, pay + 16))) return rc;
       if ((rc = ensure_dev(&S.d_slices, &S.cap_d_slices, cnt))) return rc;
       memcpy(S.h_slices, sv.data(), cnt * sizeof(lsmck::ShaSlice));
@@ -3050,8 +3120,8 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
         std::lock_guard<std::mutex> lk(c->mu);
         DevGuard g(c->dev);
         for (auto& S : c->stage) {
-          if (stage_init(S) || ensure_pinned(c->pin_node, &S.h_pay, &S.cap_h_pay, bytes) ||
-              ensure_pinned(c->pin_node, &S.h_slices, &S.cap_h_slices, files) ||
+          if (stage_init(S) || ensure_pinned(c->pin_node, &S.h_pay, &S.cap_h_pay, bytes, true) ||
+              ensure_pinned(c->pin_node, &S.h_slices, &S.cap_h_slices, files, true) ||
               ensure_dev(&S.d_pay, &S.cap_d_pay, bytes) || ensure_dev(&S.d_slices, &S.cap_d_slices, files))
             return;  // the verify reports it
           // map the pinned pages now, not on the readers' first touch
@@ -3207,7 +3277,7 @@ void* lsmck_host_alloc_pinned(lsmck_ctx* ctx, size_t bytes) {
 void lsmck_host_free_pinned(lsmck_ctx* ctx, void* p) {
   if (!ctx || !p) return;
   DevGuard g(ctx->dev);
-  (void)hipHostFree(p);
+  host_free(p);
 }
 int lsmck_memcpy_h2d(lsmck_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream) {
   if (!ctx) return LSMCK_EINVAL;
