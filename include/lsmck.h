@@ -218,8 +218,12 @@ int lsmck_device_count(void);
  *   "tree_overlap"  lsmck_tree_verify reads the highest level's directory
  *                 first and, when it holds at least this many tables (default
  *                 2048; 0 = never), verifies them while the lower levels are
- *                 listed, then the lower levels' tables.  The report is the
- *                 same either way (the first failure in read_dir order).
+ *                 listed -- its first 8x this many as soon as they are
+ *                 parsed, the rest once the level is read -- then the lower
+ *                 levels' tables.  The report is the same either way (the
+ *                 first failure in read_dir order).
+ *   "tree_list_batch"  lsmck_tree_verify: metadata names per listing batch
+ *                 (0 = 1024).  Tests use small values.
  *   "tree_json_threads"  whole-tree verify: threads reading the tables'
  *                 checksum files beside the stream (0 = default: 2, or 4 for
  *                 a batch of 16k tables or more).

@@ -455,6 +455,7 @@ struct lsmck_ctx {
   Stage stage[3];
   uint32_t tree_stages = 3;
   unsigned tree_json_threads = 0;  // whole-tree verify: checksum-file reader threads (0 = 2, 4 from 16k tables)
+  size_t tree_list_batch = 0;  // lsmck_tree_verify: metadata names per listing batch (0 = 1024)
   long tree_overlap = 2048;  // lsmck_tree_verify: the top level's tables verified while the lower levels are
                              // listed, when it holds at least this many (0 = never)
   int variant = 0;  // A/B and diagnostic bits (crc_ablate, crc_stream, sha_order); 0 = default
@@ -983,6 +984,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
       return lsmck_host::set_error(LSMCK_EINVAL, "tree_slice_bytes: a multiple of 64, <= 2^30");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->tree_slice = (uint32_t)value;
+    return 0;
+  }
+  if (!strcmp(key, "tree_list_batch")) {  // lsmck_tree_verify: metadata names per listing batch (0 = 1024; tests)
+    if (value < 0 || value > (1l << 20)) return lsmck_host::set_error(LSMCK_EINVAL, "tree_list_batch: 0 .. 2^20");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->tree_list_batch = (size_t)value;
     return 0;
   }
   if (!strcmp(key, "tree_overlap")) {  // lsmck_tree_verify: the top level verified while the others are listed
@@ -2958,6 +2965,7 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
     std::vector<std::string> path;
     std::vector<lsmck_host::TableMeta> meta;
     std::vector<int> st;
+    bool done = false;  // parsed (under the lister's mutex)
   };
   struct Lister {
     std::vector<std::unique_ptr<ListBatch>> batches;  // load order
@@ -2997,6 +3005,7 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
           {
             std::lock_guard<std::mutex> lk(lister.mu);
             ++lister.parsed;
+            b->done = true;
           }
           lister.cv_parsed.notify_all();
         }
@@ -3016,7 +3025,10 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
     const std::string dir = lsmck_host::path_push(base, "level-" + std::to_string(lv));
     if ((rc = mkdir_p(dir))) return lsmck_host::set_errno_error(-rc, "create_dir_all", dir.c_str());
   }
-  auto scan = [&](int lv) -> int {  // read_dir of one level: its metadata names, in batches to the parsers
+  // read_dir of one level: its metadata names, in batches to the parsers;
+  // hook(batches published so far) after each full batch
+  const size_t list_batch = ctx->tree_list_batch ? ctx->tree_list_batch : 1024u;
+  auto scan = [&](int lv, const std::function<void(size_t)>& hook) -> int {
     const std::string dir = lsmck_host::path_push(base, "level-" + std::to_string(lv));
     DIR* d = opendir(dir.c_str());
     if (!d) return lsmck_host::set_errno_error(errno, "read_dir", dir.c_str());
@@ -3034,7 +3046,17 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
       if (!strcmp(e->d_name, ".") || !strcmp(e->d_name, "..")) continue;
       if (strstr(e->d_name, "metadata") && valid_utf8(e->d_name)) {
         cur->path.push_back(dir + "/" + e->d_name);
-        if (cur->path.size() == 1024) publish();
+        if (cur->path.size() >= list_batch) {
+          publish();
+          if (hook) {
+            size_t nb;
+            {
+              std::lock_guard<std::mutex> lk(lister.mu);
+              nb = lister.batches.size();
+            }
+            hook(nb);
+          }
+        }
       }
     }
     closedir(d);
@@ -3047,14 +3069,6 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
   // lower levels are listed; the lower levels' tables follow in a second
   // batch.  The verify order is free: statuses land per table and the report
   // takes the first failure in read_dir order (levels 0, 1, ...).
-  const int top = LSMCK_SSTABLE_MAX_LEVEL - 1;
-  if ((rc = scan(top))) return rc;
-  size_t top_batches = 0;
-  {
-    std::unique_lock<std::mutex> lk(lister.mu);
-    top_batches = lister.batches.size();
-    lister.cv_parsed.wait(lk, [&] { return lister.parsed >= top_batches; });
-  }
   // table paths: construct_path = base_path / level-<level> / file (sstable_metadata.rs:43-48)
   struct Part {
     std::vector<std::string> dp, ip, cp;
@@ -3132,7 +3146,84 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
         (void)ensure_dev(&c->tree.digests, &c->tree.cap_digests, 32 * 2 * n);
       });
   };
-  // the top level's tables, parsed: verified now (at least tree_overlap of them: enough to pay for a second batch)
+  // The top level in two parts: its first 8 x tree_overlap tables (16k by
+  // default) go to the verify as soon as they are parsed, while the rest of
+  // its directory is read; the rest of it follows as a second part (a top
+  // level with fewer tables is one part, started once read).  Each part runs
+  // verify_tables_multi on its own thread; their GPU halves take the
+  // context in turn.
+  const size_t early_tables = 8u * (size_t)std::max<long>(ctx->tree_overlap, 1);
+  const int top = LSMCK_SSTABLE_MAX_LEVEL - 1;
+  struct TopPart {
+    std::vector<ListBatch*> batches;
+    Part part;
+    size_t first = 0, tables = 0;  // its first table's index in the top level, its tables
+    std::thread th;
+  };
+  TopPart ta, tb;
+  struct PartJoin {
+    TopPart* a;
+    TopPart* b;
+    ~PartJoin() {
+      if (a->th.joinable()) a->th.join();
+      if (b->th.joinable()) b->th.join();
+    }
+  } part_join{&ta, &tb};
+  auto start_top = [&](TopPart* P, size_t b0, size_t b1, bool prewarm_first) {
+    {
+      std::lock_guard<std::mutex> lk(lister.mu);
+      for (size_t k = b0; k < b1; ++k) P->batches.push_back(lister.batches[k].get());
+      for (size_t k = 0; k < b0; ++k) P->first += lister.batches[k]->path.size();  // (published: sizes final)
+      for (ListBatch* B : P->batches) P->tables += B->path.size();
+    }
+    if (prewarm_first) start_prewarm(P->tables);
+    P->th = std::thread([&, P, prewarm_first]() {
+      {
+        std::unique_lock<std::mutex> lk(lister.mu);
+        lister.cv_parsed.wait(lk, [&] {
+          for (ListBatch* B : P->batches)
+            if (!B->done) return false;
+          return true;
+        });
+      }
+      std::vector<lsmck_host::TableMeta> m;
+      std::vector<int> sv;
+      for (ListBatch* B : P->batches) {
+        m.insert(m.end(), B->meta.begin(), B->meta.end());
+        sv.insert(sv.end(), B->st.begin(), B->st.end());
+      }
+      paths_of(m, sv, 0, m.size(), &P->part);
+      if (prewarm_first)
+        for (auto& x : prewarm.t) x.join();
+      run_part(&P->part);
+    });
+  };
+  const bool overlap = ctx->tree_overlap > 0;
+  bool early = false;
+  size_t ka = 0;  // top-level batches in the first part
+  if ((rc = scan(top, [&](size_t nb) {
+         if (overlap && !early && nb * list_batch >= early_tables) {
+           early = true;
+           ka = nb;
+           start_top(&ta, 0, nb, true);
+         }
+       })))
+    return rc;
+  size_t top_batches = 0;
+  {
+    std::unique_lock<std::mutex> lk(lister.mu);
+    top_batches = lister.batches.size();
+    lister.cv_parsed.wait(lk, [&] { return lister.parsed >= top_batches; });
+  }
+  size_t n_top = 0;
+  for (size_t k = 0; k < top_batches; ++k) n_top += lister.batches[k]->path.size();
+  if (early) {
+    if (top_batches > ka) start_top(&tb, ka, top_batches, false);
+  } else if (overlap && n_top >= (size_t)ctx->tree_overlap) {
+    early = true;
+    ka = top_batches;
+    start_top(&ta, 0, top_batches, true);
+  }
   std::vector<lsmck_host::TableMeta> top_meta;
   std::vector<std::string> top_mpath;
   std::vector<int> top_st;
@@ -3142,26 +3233,9 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
     top_meta.insert(top_meta.end(), B.meta.begin(), B.meta.end());
     top_st.insert(top_st.end(), B.st.begin(), B.st.end());
   }
-  const size_t n_top = top_mpath.size();
-  const bool early = ctx->tree_overlap > 0 && n_top >= (size_t)ctx->tree_overlap;
-  Part ptop, prest;
-  std::thread early_th;
-  struct ThreadJoin {
-    std::thread* t;
-    ~ThreadJoin() {
-      if (t->joinable()) t->join();
-    }
-  } early_join{&early_th};
-  if (early) {
-    paths_of(top_meta, top_st, 0, n_top, &ptop);
-    start_prewarm(n_top);
-    early_th = std::thread([&]() {
-      for (auto& x : prewarm.t) x.join();
-      run_part(&ptop);
-    });
-  }
+  Part prest;
   for (int lv = 0; lv < top; ++lv)
-    if ((rc = scan(lv))) return rc;
+    if ((rc = scan(lv, {}))) return rc;
   lister.finish();
   // the listing in read_dir order: levels 0 .. top - 1, then the top level (scanned first)
   std::vector<std::string> mpath;
@@ -3212,17 +3286,20 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
   if (!early)
     for (auto& x : prewarm.t) x.join();
   run_part(&prest);  // (beside the top level's verify: its host half; its GPU half waits for the context)
-  if (early_th.joinable()) early_th.join();
-  for (Part* P : {&prest, &ptop})
+  for (TopPart* P : {&ta, &tb})
+    if (P->th.joinable()) P->th.join();
+  for (Part* P : {&prest, &ta.part, &tb.part})
     if (P->rc < 0) return lsmck_host::set_error(P->rc, P->err.c_str());
   TreeTiming tm = prest.tm;
-  tm.bytes += ptop.tm.bytes;
-  tm.rounds += ptop.tm.rounds;
-  tm.stat += ptop.tm.stat;
-  tm.read += ptop.tm.read;
-  tm.wait += ptop.tm.wait;
-  tm.compare += ptop.tm.compare;
-  tm.fds_cached = std::max(tm.fds_cached, ptop.tm.fds_cached);
+  for (Part* P : {&ta.part, &tb.part}) {
+    tm.bytes += P->tm.bytes;
+    tm.rounds += P->tm.rounds;
+    tm.stat += P->tm.stat;
+    tm.read += P->tm.read;
+    tm.wait += P->tm.wait;
+    tm.compare += P->tm.compare;
+    tm.fds_cached = std::max(tm.fds_cached, P->tm.fds_cached);
+  }
   rep->table_bytes = tm.bytes;
   rep->rounds = tm.rounds;
   rep->stat_seconds = tm.stat;
@@ -3231,7 +3308,8 @@ static int tree_verify_impl(lsmck_ctx* const* ctxs, size_t nctx, const char* bas
   rep->compare_seconds = tm.compare;
   rep->fds_cached = tm.fds_cached;
   for (size_t j = 0; j < prest.which.size(); ++j) st[prest.which[j]] = prest.vst[j];
-  for (size_t j = 0; j < ptop.which.size(); ++j) st[n_low + ptop.which[j]] = ptop.vst[j];
+  for (TopPart* P : {&ta, &tb})
+    for (size_t j = 0; j < P->part.which.size(); ++j) st[n_low + P->first + P->part.which[j]] = P->part.vst[j];
   rep->verify_seconds = seconds_since(t0) - rep->list_seconds;
   for (size_t i = 0; i < n; ++i) {
     if (!st[i]) continue;

@@ -271,15 +271,22 @@ def test_multicontext_tree_verify(ctx, tmp_path):
             c.close()
 
 
+@pytest.fixture(scope="module")
+def tree_24mib(tmp_path_factory):
+    base = str(tmp_path_factory.mktemp("tree24"))
+    tree.synthesize_tree(base, 24 << 20, wal_records=1000, threads=4)
+    return base
+
+
 @pytest.mark.gpu
-def test_tree_verify_top_level_beside_the_listing(ctx, small_tree, tmp_path):
+def test_tree_verify_top_level_beside_the_listing(ctx, tree_24mib, tmp_path):
     """"tree_overlap": the highest level's tables verified while the lower
     levels are listed (forced on this small tree) reports exactly what one
     batch does: the same listing, statuses and first failure in read_dir order
     (db.rs:37-59), with corruptions in either part."""
     import shutil
     base = str(tmp_path / "o")
-    shutil.copytree(small_tree[0], base)
+    shutil.copytree(tree_24mib, base)
     for p in tree.scan_order(base):
         d = json.load(open(p))
         d["base_path"] = base
@@ -288,18 +295,22 @@ def test_tree_verify_top_level_beside_the_listing(ctx, small_tree, tmp_path):
     paths = tree.scan_order(base)
     order = [SsTableMetadata.load(p) for p in paths]
     top = max(m.level for m in order)
-    it = next(i for i, m in enumerate(order) if m.level == top)
+    assert sum(m.level == top for m in order) > 8  # (the two-part form has a second part)
+    it = [i for i, m in enumerate(order) if m.level == top][-1]  # (in the second part when there is one)
     il = next(i for i, m in enumerate(order) if m.level == 1)
     keys = ("tables", "table_bytes", "bad_tables", "first_index", "first_status", "first_metadata_path")
 
     def both():
         out = []
-        for v in (0, 1):
+        # one batch; the top level beside the listing in one part; in two (the
+        # first 8 tables early, listing batches of 2 names)
+        for v, lb in ((0, 0), (3, 0), (1, 2)):
             ctx.set_option("tree_overlap", v)
+            ctx.set_option("tree_list_batch", lb)
             listed = []
             r = ctx.tree_verify(base, listed=listed)
             out.append(({k: r[k] for k in keys}, [(e["metadata_path"], e["status"]) for e in listed]))
-        assert out[0] == out[1]
+        assert out[0] == out[1] == out[2]
         return out[0][0]
 
     try:
@@ -318,3 +329,4 @@ def test_tree_verify_top_level_beside_the_listing(ctx, small_tree, tmp_path):
         assert r["first_metadata_path"] == paths[il]
     finally:
         ctx.set_option("tree_overlap", 2048)
+        ctx.set_option("tree_list_batch", 0)
