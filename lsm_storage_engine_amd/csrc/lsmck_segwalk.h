@@ -154,41 +154,60 @@ struct Head {
   uint32_t cl;
   uint32_t t, crc, klen, vlen;  // vlen 0 for Remove
 };
-LSMCK_HD Head head(const uint8_t* img, uint64_t n, uint64_t q) {
-  Head h{};
+// head() in two halves, so that a walk can issue the next header's load,
+// then the stores of the record it has passed, and only then wait for the
+// load (head_dec's first use): on gfx950 one counter covers loads and stores
+// and completes in issue order, so a store issued before the load would be
+// waited for with it.
+struct RawHead {
+  uint32_t d0, d1, d2, d3;  // the four dwords holding bytes q .. q+15 (from byte s of d0)
+  uint32_t s;
+  uint32_t end;  // q at or past EOF
+};
+LSMCK_HD RawHead head_raw(const uint8_t* img, uint64_t n, uint64_t q) {
+  RawHead r{};
   if (q >= n) {
-    h.cl = kEnd;
-    return h;
+    r.end = 1;
+    return r;
   }
   const uintptr_t A = ((uintptr_t)img + q) & ~(uintptr_t)3;
   const int64_t a0 = (int64_t)(A - (uintptr_t)img);
-  uint32_t e0, e1, e2, e3;  // bytes q .. q+15
   if (a0 >= 0 && (uint64_t)a0 + 16 <= n) {
-    uint32_t d[4];
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
     const u32x4a4 v = *(const __attribute__((address_space(1))) u32x4a4*)A;  // global_load_dwordx4
-    d[0] = v.x;
-    d[1] = v.y;
-    d[2] = v.z;
-    d[3] = v.w;
+    r.d0 = v.x;
+    r.d1 = v.y;
+    r.d2 = v.z;
+    r.d3 = v.w;
 #else
+    uint32_t d[4];
     memcpy(d, (const void*)A, 16);
+    r.d0 = d[0];
+    r.d1 = d[1];
+    r.d2 = d[2];
+    r.d3 = d[3];
 #endif
-    const uint32_t s = (uint32_t)(((uintptr_t)img + q) & 3u);
-    e0 = fsh(d[1], d[0], s);
-    e1 = fsh(d[2], d[1], s);
-    e2 = fsh(d[3], d[2], s);
-    e3 = fsh(0u, d[3], s);
+    r.s = (uint32_t)(((uintptr_t)img + q) & 3u);
   } else {
     uint32_t w[4] = {0u, 0u, 0u, 0u};
     for (uint32_t i = 0; i < 16u; ++i)
       if (q + i < n) w[i >> 2] |= (uint32_t)img[q + i] << (8u * (i & 3u));
-    e0 = w[0];
-    e1 = w[1];
-    e2 = w[2];
-    e3 = w[3];
+    r.d0 = w[0];
+    r.d1 = w[1];
+    r.d2 = w[2];
+    r.d3 = w[3];
   }
+  return r;
+}
+LSMCK_HD Head head_dec(const RawHead& r, uint64_t n, uint64_t q) {
+  Head h{};
+  if (r.end) {
+    h.cl = kEnd;
+    return h;
+  }
+  const uint32_t e0 = fsh(r.d1, r.d0, r.s), e1 = fsh(r.d2, r.d1, r.s), e2 = fsh(r.d3, r.d2, r.s),
+                 e3 = fsh(0u, r.d3, r.s);
   h.t = e0 & 0xFFu;
   if (h.t != 1u && h.t != 2u) {
     h.cl = kBad;
@@ -203,6 +222,7 @@ LSMCK_HD Head head(const uint8_t* img, uint64_t n, uint64_t q) {
   h.vlen = h.t == 1u ? ((e2 >> 8) | (e3 << 24)) : 0u;
   return h;
 }
+LSMCK_HD Head head(const uint8_t* img, uint64_t n, uint64_t q) { return head_dec(head_raw(img, n, q), n, q); }
 
 // the record at p with header h: where the next one starts -- its payload cut
 // at EOF (wal.rs:130-133) -- and whether the payload is whole.  The length is
@@ -229,18 +249,23 @@ struct StageRec {
 constexpr uint64_t kStageMaxSeg = 1ull << 31;
 LSMCK_HD uint32_t stage_type(const StageRec& R) { return (R.rel_t >> 31) ? 2u : 1u; }
 LSMCK_HD uint64_t stage_off(const StageRec& R, uint64_t b0) { return b0 + (R.rel_t & 0x7FFFFFFFu); }
-// b0: the segment's start
+// b0: the segment's start.  Staged (S) walks store every record: past the
+// segment's cap slots the last slot is overwritten, harmlessly -- a segment
+// with more records than slots is emitted by its second walk and its slots are
+// not read -- so the store is not branched around, and the wait for the next
+// header's load (issued before it) need not cover it (head_raw).
+template <bool S>
 LSMCK_HD void stage_put(StageRec* st, uint32_t cap, uint32_t cnt, uint64_t p, const Head& h, uint64_t b0) {
-  if (st && cnt < cap) {
+  if (S) {
 #if !defined(__HIP_DEVICE_COMPILE__)
-    assert(p >= b0 && p - b0 < kStageMaxSeg);  // (the host model's runs check the layout's premise)
+    assert(st && cap && p >= b0 && p - b0 < kStageMaxSeg);  // (the host model's runs check the layout's premise)
 #endif
     StageRec R;
     R.rel_t = (uint32_t)(p - b0) | (h.t == 2u ? 0x80000000u : 0u);
     R.crc = h.crc;
     R.klen = h.klen;
     R.vlen = h.vlen;
-    st[cnt] = R;
+    st[cnt < cap ? cnt : cap - 1] = R;
   }
 }
 
@@ -248,8 +273,9 @@ LSMCK_HD void stage_put(StageRec* st, uint32_t cap, uint32_t cnt, uint64_t p, co
 // the guess; h its header): the walk through the segment ending at e, to the
 // first record start at or past e (kExit) or to the chain's end (kEnd / kBad).
 // st: the segment's staging slots (scap of them), or none.
-LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, Head h, uint64_t e, WalkOut* o,
-                   StageRec* st = nullptr, uint32_t scap = 0, uint64_t b0 = 0) {
+template <bool S>
+LSMCK_HD void walk_t(const uint8_t* img, uint64_t n, uint64_t c, Head h, uint64_t e, WalkOut* o, StageRec* st,
+                     uint32_t scap, uint64_t b0) {
   uint64_t p = c;
   uint32_t cnt = 0;
   for (;;) {
@@ -261,9 +287,10 @@ LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, Head h, uint64_t 
     }
     bool whole;
     const uint64_t q = next_of(h, n, p, &whole);
-    stage_put(st, scap, cnt, p, h, b0);
+    const RawHead r = head_raw(img, n, q);  // (issued before the record's store: head_raw)
+    stage_put<S>(st, scap, cnt, p, h, b0);
     ++cnt;
-    h = head(img, n, q);
+    h = head_dec(r, n, q);
     if (h.cl) {  // the chain ends after the record at p
       o->code = h.cl;
       o->pos = q;
@@ -272,6 +299,11 @@ LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, Head h, uint64_t 
     }
     p = q;
   }
+}
+LSMCK_HD void walk(const uint8_t* img, uint64_t n, uint64_t c, Head h, uint64_t e, WalkOut* o,
+                   StageRec* st = nullptr, uint32_t scap = 0, uint64_t b0 = 0) {
+  if (st) walk_t<true>(img, n, c, h, e, o, st, scap, b0);
+  else walk_t<false>(img, n, c, h, e, o, st, scap, b0);
 }
 
 // Whether a candidate start c (a type byte whose header fits) is plausible:
@@ -499,7 +531,8 @@ LSMCK_HD uint32_t seg_of(const SegArgs& a, uint64_t pos) {
 // the forced walk of segment k from its entry c (a position on the chain)
 // walk() of segment k from its entry c (header h), noting the emit
 // checkpoints as it passes each sub-segment's start
-LSMCK_HD void walk_cp(const SegArgs& a, uint32_t k, uint64_t c, Head h, WalkOut* o) {
+template <bool S>
+LSMCK_HD void walk_cp_t(const SegArgs& a, uint32_t k, uint64_t c, Head h, WalkOut* o) {
   const uint8_t* img = a.img;
   const uint64_t n = a.n, e = seg_end(a, k), b0 = seg_begin(a, k);
   uint64_t* cpp = a.cpp + (uint64_t)k * a.nsub;
@@ -521,9 +554,10 @@ LSMCK_HD void walk_cp(const SegArgs& a, uint32_t k, uint64_t c, Head h, WalkOut*
     }
     bool whole;
     const uint64_t q = next_of(h, n, p, &whole);
-    stage_put(st, a.scap, cnt, p, h, b0);
+    const RawHead r = head_raw(img, n, q);  // (issued before the record's store: head_raw)
+    stage_put<S>(st, a.scap, cnt, p, h, b0);
     ++cnt;
-    h = head(img, n, q);
+    h = head_dec(r, n, q);
     if (h.cl) {
       o->code = h.cl;
       o->pos = q;
@@ -537,6 +571,10 @@ LSMCK_HD void walk_cp(const SegArgs& a, uint32_t k, uint64_t c, Head h, WalkOut*
     cpp[j] = p;
     cpc[j] = cnt;
   }
+}
+LSMCK_HD void walk_cp(const SegArgs& a, uint32_t k, uint64_t c, Head h, WalkOut* o) {
+  if (a.scap) walk_cp_t<true>(a, k, c, h, o);
+  else walk_cp_t<false>(a, k, c, h, o);
 }
 
 LSMCK_HD void seg_forced(const SegArgs& a, uint32_t k, uint64_t c) {
