@@ -844,16 +844,18 @@ LSMCK_HD void seg_emit_thread(const SegArgs& a, uint32_t k, uint32_t jterm, uint
 }
 
 // Record r of staged segment k (every record it walked fit its slots), R
-// its staged form: the record to `at` + its place, its CRC span -- packed
+// its staged form: the record to its place, its CRC span -- packed
 // (pk; its expected CRC then pack_crc's) or the payload alone -- and its
 // expected CRC.  nh: the header of the record after it (the next slot's, or
 // the one at the segment's exit for its last record), used only when the
 // walk has a record after it.  The payload is cut at EOF only for the walk's
 // last record.
 template <class Rec>
-LSMCK_HD void seg_place_rec(const SegArgs& a, uint32_t k, uint64_t at, Rec* recs, uint64_t* poff, uint32_t* plen,
+// i0: the segment's first record's index in recs (at + its placement prefix,
+// read once by the caller rather than per window)
+LSMCK_HD void seg_place_rec(const SegArgs& a, uint32_t k, uint64_t i0, Rec* recs, uint64_t* poff, uint32_t* plen,
                             uint32_t* pcrc, uint32_t r, const StageRec& R, const Head& nh, const Pack* pk) {
-  const uint64_t i = at + (a.pre[k] & kRecMask) + r;
+  const uint64_t i = i0 + r;
   const uint32_t t = stage_type(R);
   const uint64_t rec_off = stage_off(R, seg_begin(a, k)), payload_off = rec_off + hdr_len(t);
   put_rec(recs + i, rec_off, payload_off, R.klen, R.vlen, R.crc, t);

@@ -646,23 +646,28 @@ __global__ __launch_bounds__(256) void wal_seg_place(seg::SegArgs a, uint64_t at
   const seg::Pack pk{iend, T};
   // The slots two windows of 64 ahead are loaded while a window is placed (a
   // wave walks its segment's slots in ~20 windows); the record after a
-  // window's lane 63 is the next window's lane 0, already loaded.
-  seg::StageRec W0{}, W1{};
-  if (lane < cnt) W0 = st[lane];
-  if (64u + lane < cnt) W1 = st[64u + lane];
-  for (uint32_t r0 = 0; r0 < cnt; r0 += 64u) {  // (wave-uniform)
+  // window's lane 63 is the next window's lane 0, already loaded.  Three
+  // buffers in turn (the loop unrolled by three), so no register copy of a
+  // window still in flight makes the wave wait for it a window early.
+  // The loads are not branched around (a lane past the segment's records
+  // re-reads its last slot, and never uses what it reads): a load into a
+  // register that keeps its old value on the other path is a copy the wave
+  // waits for at once.
+  if (cnt == 0) return;
+  const uint32_t last = cnt - 1u;
+  seg::StageRec W0 = st[lane < last ? lane : last], W1 = st[64u + lane < last ? 64u + lane : last], W2;
+  // window r0: its records R, the next window N (lane 0: the record after
+  // lane 63's), and L, free since the window before, refilled with window r0 + 128
+  auto window = [&](uint32_t r0, const seg::StageRec& R, const seg::StageRec& N, seg::StageRec& L) {
     const uint32_t r = r0 + lane;
-    const seg::StageRec R = W0;
-    W0 = W1;
-    W1 = seg::StageRec{};
-    if (r + 128u < cnt) W1 = st[r + 128u];
+    L = st[r + 128u < last ? r + 128u : last];
     seg::Head nh{};
     if (PACK) {
       const bool l63 = lane == 63u;  // (the next window's lane 0)
-      const uint32_t nrel = (uint32_t)__shfl_down(R.rel_t, 1), frel = (uint32_t)__shfl(W0.rel_t, 0);
-      const uint32_t ncrc = (uint32_t)__shfl_down(R.crc, 1), fcrc = (uint32_t)__shfl(W0.crc, 0);
-      const uint32_t nkl = (uint32_t)__shfl_down(R.klen, 1), fkl = (uint32_t)__shfl(W0.klen, 0);
-      const uint32_t nvl = (uint32_t)__shfl_down(R.vlen, 1), fvl = (uint32_t)__shfl(W0.vlen, 0);
+      const uint32_t nrel = (uint32_t)__shfl_down(R.rel_t, 1), frel = (uint32_t)__shfl(N.rel_t, 0);
+      const uint32_t ncrc = (uint32_t)__shfl_down(R.crc, 1), fcrc = (uint32_t)__shfl(N.crc, 0);
+      const uint32_t nkl = (uint32_t)__shfl_down(R.klen, 1), fkl = (uint32_t)__shfl(N.klen, 0);
+      const uint32_t nvl = (uint32_t)__shfl_down(R.vlen, 1), fvl = (uint32_t)__shfl(N.vlen, 0);
       nh.t = seg::stage_type(seg::StageRec{l63 ? frel : nrel, 0u, 0u, 0u});
       nh.crc = l63 ? fcrc : ncrc;
       nh.klen = l63 ? fkl : nkl;
@@ -670,7 +675,14 @@ __global__ __launch_bounds__(256) void wal_seg_place(seg::SegArgs a, uint64_t at
       // the segment's last record: the header at its exit (another segment's first)
       if (r < cnt && r + 1u == cnt && i0 + r + 1u < iend) nh = seg::seg_place_next_head(a, k, r);
     }
-    if (r < cnt) seg::seg_place_rec(a, k, at, recs, poff, plen, pcrc, r, R, nh, PACK ? &pk : nullptr);
+    if (r < cnt) seg::seg_place_rec(a, k, i0, recs, poff, plen, pcrc, r, R, nh, PACK ? &pk : nullptr);
+  };
+  for (uint32_t r0 = 0; r0 < cnt; r0 += 192u) {  // (wave-uniform)
+    window(r0, W0, W1, W2);
+    if (r0 + 64u >= cnt) break;
+    window(r0 + 64u, W1, W2, W0);
+    if (r0 + 128u >= cnt) break;
+    window(r0 + 128u, W2, W0, W1);
   }
 }
 
