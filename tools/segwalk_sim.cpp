@@ -153,7 +153,8 @@ extern "C" int segwalk_sim_prefix(const uint8_t* img, uint64_t n, uint64_t start
       for (uint32_t r = 0; r < recs[k]; ++r) {
         const uint64_t i = (pre[k] & sg::kRecMask) + r;
         const sg::Head nh = i + 1 < m ? sg::seg_place_next_head(a, k, r) : sg::Head{};
-        sg::seg_place_rec(a, k, 0, R.data(), poff.data(), plen.data(), pcrc.data(), r, st[(size_t)k * scap + r], nh,
+        sg::seg_place_rec(a, k, pre[k] & sg::kRecMask, R.data(), poff.data(), plen.data(), pcrc.data(), r,
+                          st[(size_t)k * scap + r], nh,
                           g_pcap ? &pk : nullptr);
       }
   for (uint64_t i = 0; i < m && i < cap; ++i) rec_off[i] = R[i].rec_off;
