@@ -2773,6 +2773,8 @@ static int verify_tables(lsmck_ctx* ctx, const char* const* data_paths, const ch
   }
   for (auto& x : want_th.t) x.join();
   want_th.t.clear();
+  const double json_join = clk.lap();  // (the checksum-file readers still running after the last round)
+  tm->compare += json_join;
   for (auto& x : cpu_th.t) x.join();
   cpu_th.t.clear();
   host_parallel(n, [&](size_t i) {
@@ -2790,6 +2792,12 @@ static int verify_tables(lsmck_ctx* ctx, const char* const* data_paths, const ch
   for (size_t i = 0; i < n; ++i) bad += status[i] != 0;
   tm->bytes = std::accumulate(fsize.begin(), fsize.end(), (uint64_t)0);
   tm->compare += clk.lap();
+  if (getenv("LSMCK_TREE_TRACE"))  // diagnostic: where the batch's time went
+    fprintf(stderr,
+            "tree verify: %zu tables, %.2f GB: stat %.3f s, read %.3f s, slot wait + last rounds %.3f s, "
+            "checksum-file readers after the last round %.3f s, compare %.3f s, %llu rounds\n",
+            n, tm->bytes / 1e9, tm->stat, tm->read, tm->wait, json_join, tm->compare - json_join,
+            (unsigned long long)tm->rounds);
   return bad;
 }
 
