@@ -259,7 +259,10 @@ struct SsTable {
       if (pos + kl + 8 > n) return false;
       std::string k((const char*)p + pos, (size_t)kl);
       pos += kl;
-      index[k] = get_u64(p + pos);
+      // bincode writes a BTreeMap in key order, so the end is the hint (a
+      // repeated key keeps its last value, as the map's deserializer does)
+      const uint64_t v = get_u64(p + pos);
+      index.emplace_hint(index.end(), std::move(k), v)->second = v;
       pos += 8;
     }
     return true;
