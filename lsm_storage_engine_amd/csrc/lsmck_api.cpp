@@ -919,6 +919,10 @@ lsmck_ctx* lsmck_ctx_create(int device) {
   lsmck_ctx* ctx = new lsmck_ctx();
   ctx->dev = device;
   ctx->ncu = pr.multiProcessorCount;
+  if (const char* e = getenv("LSMCK_CUS")) {  // diagnostic: the persistent kernels on fewer workgroups than CUs
+    const int c = atoi(e);
+    if (c > 0 && c < ctx->ncu) ctx->ncu = c;
+  }
   ctx->numa_node = device_numa_node(device);
   apply_numa(ctx);
   // combination tables
