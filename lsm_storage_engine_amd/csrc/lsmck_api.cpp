@@ -335,6 +335,7 @@ struct Stage {
     *this = Stage();
   }
 };
+constexpr int kHostSlots = 2;  // slots the host batches and the WAL upload alternate
 
 }  // namespace
 
@@ -452,7 +453,7 @@ struct lsmck_ctx {
   size_t cap_hwexp = 0;
   // the host-batch pipelines alternate over slots 0 and 1; the whole-tree
   // verify cycles through the first tree_stages of them
-  Stage stage[3];
+  Stage stage[3];  // host batches and the WAL upload alternate 0 and 1 (kHostSlots); the tree verify uses all 3
   uint32_t tree_stages = 3;
   unsigned tree_json_threads = 0;  // whole-tree verify: checksum-file reader threads (0 = 2, 4 from 16k tables)
   size_t tree_list_batch = 0;  // lsmck_tree_verify: metadata names per listing batch (0 = 1024)
@@ -738,7 +739,8 @@ int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
   size_t esz = J.kind == CRC ? 4 : 32;
   int rc;
   StageGuard guard{ctx};
-  for (auto& S : ctx->stage) {
+  for (int k = 0; k < kHostSlots; ++k) {  // (the batches alternate slots 0 and 1; slot 2 is the tree verify's)
+    Stage& S = ctx->stage[k];
     if ((rc = stage_init(S))) return rc;
     if (S.busy) {  // left by a call that failed before its guard existed: never retire it here
       HIPCHK(hipStreamSynchronize(S.s));
@@ -919,10 +921,12 @@ lsmck_ctx* lsmck_ctx_create(int device) {
   lsmck_ctx* ctx = new lsmck_ctx();
   ctx->dev = device;
   ctx->ncu = pr.multiProcessorCount;
-  if (const char* e = getenv("LSMCK_CUS")) {  // diagnostic: the persistent kernels on fewer workgroups than CUs
+#ifdef LSMCK_DIAG
+  if (const char* e = getenv("LSMCK_CUS")) {  // diagnostic builds only: the persistent kernels on fewer CUs
     const int c = atoi(e);
     if (c > 0 && c < ctx->ncu) ctx->ncu = c;
   }
+#endif
   ctx->numa_node = device_numa_node(device);
   apply_numa(ctx);
   // combination tables
@@ -2005,7 +2009,8 @@ struct HostRegistration {
 static int wal_upload_prepare(lsmck_ctx* ctx, size_t n, bool direct) {
   int rc;
   if ((rc = ensure_dev(&ctx->d_wimg, &ctx->cap_wimg, n + 16)) || (rc = wal_walk_setup(ctx, n))) return rc;
-  for (auto& S : ctx->stage) {
+  for (int k = 0; k < kHostSlots; ++k) {  // (the upload alternates slots 0 and 1)
+    Stage& S = ctx->stage[k];
     if ((rc = stage_init(S))) return rc;
     if (S.busy) {  // a failed host batch's slot: nothing to retire here
       HIPCHK(hipStreamSynchronize(S.s));

@@ -2,6 +2,7 @@
 #pragma once
 #include <pthread.h>
 #include <sched.h>
+#include <unistd.h>
 
 #include <condition_variable>
 #include <cstdint>
@@ -19,8 +20,10 @@ namespace lsmck_host {
 class HostPool {
  public:
   HostPool() {
+    // the process's mask (its main thread's, pid = tid), not the mask of
+    // whichever thread builds the pool first: that one may be narrowed already
     CPU_ZERO(&orig_);
-    if (sched_getaffinity(0, sizeof orig_, &orig_) != 0 || CPU_COUNT(&orig_) == 0)
+    if (sched_getaffinity(getpid(), sizeof orig_, &orig_) != 0 || CPU_COUNT(&orig_) == 0)
       for (int c = 0; c < CPU_SETSIZE; ++c) CPU_SET(c, &orig_);
   }
   ~HostPool() {
@@ -108,7 +111,7 @@ class HostPool {
   uint64_t gen_ = 0;
   bool stop_ = false;
   cpu_set_t cpus_{};     // (under run_mu_)
-  cpu_set_t orig_{};     // the affinity the process had when the pool was made
+  cpu_set_t orig_{};     // the process's affinity when the pool was made
   bool pinned_ = false;
 };
 

@@ -246,6 +246,7 @@ LSMCK_HD uint64_t next_of(const Head& h, uint64_t n, uint64_t p, bool* whole) {
 struct StageRec {
   uint32_t rel_t, crc, klen, vlen;
 };
+static_assert(sizeof(StageRec) == 16, "the staging budget and the place kernel assume 16-byte slots");
 constexpr uint64_t kStageMaxSeg = 1ull << 31;
 LSMCK_HD uint32_t stage_type(const StageRec& R) { return (R.rel_t >> 31) ? 2u : 1u; }
 LSMCK_HD uint64_t stage_off(const StageRec& R, uint64_t b0) { return b0 + (R.rel_t & 0x7FFFFFFFu); }
@@ -764,6 +765,15 @@ struct Compact16 {
   uint32_t klen, vlen;
 };
 constexpr uint64_t kRemoveBit = 1ull << 63;
+static_assert(sizeof(Compact16) == 16, "Compact16 is lsmck_wal_rec16 (include/lsmck.h)");
+#ifdef LSMCK_H  // (the host side: the public layout is in scope -- tie the two together)
+static_assert(sizeof(Compact16) == sizeof(lsmck_wal_rec16) &&
+                  offsetof(Compact16, payload_type) == offsetof(lsmck_wal_rec16, payload_type) &&
+                  offsetof(Compact16, klen) == offsetof(lsmck_wal_rec16, klen) &&
+                  offsetof(Compact16, vlen) == offsetof(lsmck_wal_rec16, vlen) &&
+                  kRemoveBit == LSMCK_WAL_REC16_REMOVE,
+              "seg::Compact16 and lsmck_wal_rec16 must share one layout");
+#endif
 LSMCK_HD void put_rec(Compact16* r, uint64_t rec_off, uint64_t payload_off, uint32_t klen, uint32_t vlen,
                       uint32_t crc, uint32_t type) {
   (void)rec_off;

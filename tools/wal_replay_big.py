@@ -178,6 +178,10 @@ def main():
               f"{ctx.get_stat('wal_seg_repairs')} repairs)",
               file=sys.stderr, flush=True)
         del recs  # the wrapper reuses its records array once no result refers to it
+    # the engines of the host-record replays' read-back, read before the
+    # records-on-device replays below (which read nothing back: the stat is 0)
+    host_dma = ctx.get_stat("wal_recs_dma")
+    host_stats = {k: ctx.get_stat(k) for k in ("wal_walk_path", "wal_seg_repairs", "wal_seg_prepairs", "wal_segments")}
     dev = None
     if a.device_recs:  # the records stay in HBM: the walk, the CRC pass and the compare, no host link
         from lsm_storage_engine_amd.device import WAL_REC16_DTYPE, WAL_REC_DTYPE
@@ -238,9 +242,10 @@ def main():
         "steps": a.steps, "summary_crc32": summary,
         "summary_matches_oracle": bool(golden) or a.shape != "zipf" or bool(a.compact), "shape": a.shape,
         "records_out_bytes": (16 if a.compact else 32) * n, "pinned_recs": bool(a.pinned_recs),
-        "compact": bool(a.compact), "recs_dma_engines": ctx.get_stat("wal_recs_dma"),
-        "walk_path": {1: "segment walk", 2: "candidate doubling", 3: "host walk"}.get(ctx.get_stat("wal_walk_path")),
-        "seg_repairs": ctx.get_stat("wal_seg_repairs"), "seg_prepairs": ctx.get_stat("wal_seg_prepairs"), "segments": ctx.get_stat("wal_segments"),
+        "compact": bool(a.compact), "recs_dma_engines": host_dma,
+        "walk_path": {1: "segment walk", 2: "candidate doubling", 3: "host walk"}.get(host_stats["wal_walk_path"]),
+        "seg_repairs": host_stats["wal_seg_repairs"], "seg_prepairs": host_stats["wal_seg_prepairs"],
+        "segments": host_stats["wal_segments"],
         "records_on_device": dev, "raw_batch_crc_ms": raw,
         "workload": {"zipf": "config 3's 2^26 Zipf payloads (64 B-64 KiB) framed as wal.rs Insert records "
                              "(13-byte headers), headers and CRCs written on the device",
