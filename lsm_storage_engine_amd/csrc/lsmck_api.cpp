@@ -420,6 +420,24 @@ struct lsmck_ctx {
   long wal_seg_stage = 1;    // segment walk: staged records (seg::StageRec): 0 off, 1 auto slots, else slots per segment
   int wal_seg_rounds = 16;   // segment walk: repairs before it declines to the candidate-doubling walk
   int wal_seg_prepair = 2;   // segment walk: parallel repair rounds before the serial repairs (0 = none)
+  // The pipelined device replay (wal_replay_pipelined): the log walked in
+  // wal_pipe parts, each part's CRC pass on a CU-masked stream beside the next
+  // part's walk on the CUs left over (0 = off: the walk, then one CRC pass)
+  int wal_pipe = 0;
+  int wal_pipe_first = 4;   // the first part, in 64ths of the log (walked on every CU, nothing beside it)
+  int wal_pipe_cus = 32;    // CUs the walk keeps; the CRC passes take the rest
+  int wal_pipe_layout = 0;  // which CUs the walk keeps: 0 the last wal_pipe_cus, 1 spread (every ncu/cus-th)
+  size_t wal_pipe_min = (size_t)1 << 30;  // logs from this size take the pipeline (when wal_pipe is on)
+  uint64_t wal_pipe_seg = 0;  // the walk parts' segment bytes (0: sized to the walk CUs' resident lanes)
+  uint64_t wal_seg_auto = 0;  // (set by the pipeline) the segment bytes of an auto-sized walk, 0: lsmk_wal_seg_bytes
+  hipStream_t wal_pw = nullptr;  // the walk's CU-masked stream
+  hipStream_t wal_pc = nullptr;  // the CRC passes' CU-masked stream
+  int wal_pipe_key = -1;         // (cus, layout) the two streams were made for
+  std::vector<hipEvent_t> wal_pipe_ev;  // per part: its records emitted (the CRC pass waits for it)
+  // set while a pipelined replay runs: called before the walk grows the record
+  // arrays, so nothing beside it still reads the old ones
+  std::function<int()> wal_grow_hook;
+  std::atomic<int> last_pipe_parts{0};  // the last device replay's parts (0: not pipelined)
   int numa_node = -1;    // the device's NUMA node (sysfs), -1 unknown
   int stage_numa = -2;   // option "stage_numa": -2 the device's node on a multi-node host, -1 off, >= 0 that node
   int pin_node = -1;     // in effect: pinned buffers and copy threads on this node (-1: none)
@@ -578,8 +596,10 @@ int crc_fixed_device(lsmck_ctx* ctx, const uint8_t* base, size_t stride, uint32_
 // trusted: the library's own batch (host-staged chunks, WAL payloads): sorted,
 // not overlapping, the bytes between records inside the same buffer -- the
 // stream kernel takes it without the device check or the walking kernel.
+// ncu: the stream kernel's grid in workgroups (0: every CU; the pipelined WAL
+// replay runs it on a CU-masked stream of fewer)
 int crc_desc_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const uint64_t* off, const uint32_t* len,
-                    size_t n, uint32_t* out, hipStream_t st, bool trusted = false) {
+                    size_t n, uint32_t* out, hipStream_t st, bool trusted = false, int ncu = 0) {
   if (n == 0) return 0;
   if (n >= (1ull << 32)) return lsmck_host::set_error(LSMCK_EINVAL, "more than 2^32-1 records in one batch");
   // walking kernel: scratch sized by the record count, nothing read back,
@@ -599,10 +619,11 @@ int crc_desc_device(lsmck_ctx* ctx, DescScratch& sc, const uint8_t* base, const 
     // caller's batch is checked on the device; when it is not eligible the
     // walking kernel below takes it, else that kernel exits at once)
     if (!sc.sflag) HIPCHK(hipMalloc((void**)&sc.sflag, 16));
+    const int g = ncu > 0 && ncu < ctx->ncu ? ncu : ctx->ncu;
     if ((rc = ensure_dev(&sc.scuts, &sc.cap_cuts, (size_t)lsmk_stream_waves(ctx->ncu) + 1))) return rc;
     P.sflag = sc.sflag;
     P.scuts = sc.scuts;
-    rc = lsmk_launch_crc32_stream(&P, ctx->ncu, ctx->variant, trusted ? 1 : 0, st);
+    rc = lsmk_launch_crc32_stream(&P, g, ctx->variant, trusted ? 1 : 0, st);
     if (rc) return launch_rc(rc, "crc32_stream kernel");
     if (trusted || (ctx->variant & kVariantStreamOnly)) return 0;
   }
@@ -850,8 +871,8 @@ int run_host_job(lsmck_ctx* ctx, const HostJob& J) {
     r = r1;
     slot ^= 1;
   }
-  for (auto& S : ctx->stage)
-    if ((rc = stage_retire(S, J))) return rc;
+  for (int k = 0; k < kHostSlots; ++k)
+    if ((rc = stage_retire(ctx->stage[k], J))) return rc;
   guard.ok = true;
   return 0;
 }
@@ -1143,6 +1164,43 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     ctx->wal_seg_rounds = (int)value;
     return 0;
   }
+  if (!strcmp(key, "wal_pipe")) {  // device WAL replay: parts walked beside the CRC passes (0 = off)
+    if (value < 0 || value > 64) return lsmck_host::set_error(LSMCK_EINVAL, "wal_pipe: 0..64");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_pipe = (int)value;
+    return 0;
+  }
+  if (!strcmp(key, "wal_pipe_first")) {  // the pipeline's first part, in 64ths of the log
+    if (value < 1 || value > 63) return lsmck_host::set_error(LSMCK_EINVAL, "wal_pipe_first: 1..63");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_pipe_first = (int)value;
+    return 0;
+  }
+  if (!strcmp(key, "wal_pipe_cus")) {  // the pipeline's walk CUs (the CRC passes take the rest)
+    if (value < 1 || value >= ctx->ncu) return lsmck_host::set_error(LSMCK_EINVAL, "wal_pipe_cus: 1..ncu-1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_pipe_cus = (int)value;
+    return 0;
+  }
+  if (!strcmp(key, "wal_pipe_min")) {  // the pipeline's smallest log (tests: small logs through every part)
+    if (value < 0) return lsmck_host::set_error(LSMCK_EINVAL, "wal_pipe_min: >= 0");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_pipe_min = (size_t)value;
+    return 0;
+  }
+  if (!strcmp(key, "wal_pipe_seg")) {  // the pipeline walk parts' segment bytes (0 = sized to the walk's CUs)
+    if (value < 0 || (value && (value < 4096 || value > (1l << 30))))
+      return lsmck_host::set_error(LSMCK_EINVAL, "wal_pipe_seg: 0 or 4096..2^30");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_pipe_seg = (uint64_t)value;
+    return 0;
+  }
+  if (!strcmp(key, "wal_pipe_layout")) {  // which CUs the walk keeps: 0 the last ones, 1 spread
+    if (value != 0 && value != 1) return lsmck_host::set_error(LSMCK_EINVAL, "wal_pipe_layout: 0 or 1");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->wal_pipe_layout = (int)value;
+    return 0;
+  }
   if (!strcmp(key, "wal_prefetch")) {  // A/B: bytes the WAL header walk prefetches ahead (0 = off)
     if (value < 0 || value > (1l << 24)) return lsmck_host::set_error(LSMCK_EINVAL, "wal_prefetch: 0..16 MiB");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1209,6 +1267,8 @@ int lsmck_ctx_get_stat(lsmck_ctx* ctx, const char* key, long* value) {
     *value = (long)ctx->last_segments.load();
   } else if (!strcmp(key, "wal_seg_prepairs")) {  // the last segment walk's parallel repair rounds
     *value = ctx->last_seg_prepairs.load();
+  } else if (!strcmp(key, "wal_pipe_parts")) {  // the last device replay's pipelined parts (0: one walk, one pass)
+    *value = ctx->last_pipe_parts.load();
   } else if (!strcmp(key, "wal_recs_dma")) {  // the last records read-back: SDMA engines (0: hipMemcpyAsync)
     *value = ctx->last_recs_dma.load();
   } else if (!strcmp(key, "numa_node")) {
@@ -1258,6 +1318,9 @@ void lsmck_ctx_destroy(lsmck_ctx* ctx) {
   if (ctx->h_wrecs1) host_free(ctx->h_wrecs1);
   if (ctx->wal_emit1_ev) (void)hipEventDestroy(ctx->wal_emit1_ev);
   if (ctx->wal_rs) (void)hipStreamDestroy(ctx->wal_rs);
+  if (ctx->wal_pw) (void)hipStreamDestroy(ctx->wal_pw);
+  if (ctx->wal_pc) (void)hipStreamDestroy(ctx->wal_pc);
+  for (hipEvent_t e : ctx->wal_pipe_ev) (void)hipEventDestroy(e);
   if (ctx->wal_host) host_free(ctx->wal_host);
   if (ctx->d_wimg) (void)hipFree(ctx->d_wimg);
   if (ctx->scratch_ev) (void)hipEventDestroy(ctx->scratch_ev);
@@ -1475,9 +1538,10 @@ static int wal_walk_part(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t 
 // The CRC pass over records [at, at + m): their spans in log order (the
 // stream kernel, no eligibility check), CRCs into d_vcrc + at.  (Packed spans,
 // seg::Pack, are taken apart by the compare, wal_finish.)  Asynchronous.
-static int wal_crc_part(lsmck_ctx* ctx, const uint8_t* img, size_t at, size_t m, hipStream_t st) {
+static int wal_crc_part(lsmck_ctx* ctx, const uint8_t* img, size_t at, size_t m, hipStream_t st, int ncu = 0) {
   if (!m) return 0;
-  return crc_desc_device(ctx, ctx->scratch, img, ctx->d_woff + at, ctx->d_wlen + at, m, ctx->d_vcrc + at, st, true);
+  return crc_desc_device(ctx, ctx->scratch, img, ctx->d_woff + at, ctx->d_wlen + at, m, ctx->d_vcrc + at, st, true,
+                         ncu);
 }
 
 // This replay's record layout: bytes per record (lsmck_wal_rec, or
@@ -1571,7 +1635,7 @@ static int wal_read_back(lsmck_ctx* ctx, uint8_t* land, const uint8_t* src, size
 static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t term, uint64_t badq, void* recs,
                       size_t cap, size_t* nrec, uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected,
                       hipStream_t st, const WalTrace& tr, size_t done = 0, bool emit_recorded = false,
-                      size_t pack_from = ~(size_t)0) {
+                      size_t pack_from = ~(size_t)0, const std::vector<size_t>* unpacked = nullptr) {
   auto& W = ctx->wd;
   int rc;
   uint64_t nbad = 0, first = m;
@@ -1621,7 +1685,9 @@ static int wal_finish(lsmck_ctx* ctx, const uint8_t* img, size_t m, uint32_t ter
     uint32_t got = 0;
     if ((rc = wal_dev_rec(ctx, img, dsrc, first, &r))) return rc;
     HIPCHK(hipMemcpy(&got, ctx->d_vcrc + first, 4, hipMemcpyDeviceToHost));
-    if (first >= pack_from && first + 1 < m) {  // a packed span's CRC: the next header taken back out
+    // (unpacked: the pipelined parts' last records, whose spans are their payloads alone)
+    const bool alone = unpacked && std::binary_search(unpacked->begin(), unpacked->end(), (size_t)first);
+    if (first >= pack_from && first + 1 < m && !alone) {  // a packed span's CRC: the next header taken back out
       namespace sg = lsmck::seg;
       lsmck_wal_rec rn;
       if ((rc = wal_dev_rec(ctx, img, dsrc, first + 1, &rn))) return rc;
@@ -1722,6 +1788,9 @@ static int wal_walk_from(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t 
 // payloads that look like framed records along the chain; the caller walks
 // by candidate doubling instead.
 constexpr int kWalSegDecline = 0x7FFF0004;
+// internal: a pipelined part's records no longer fit the caller's device array
+// the earlier parts were emitted into (the replay starts over, not pipelined)
+constexpr int kWalPipeRestart = 0x7FFF0005;
 static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t start, uint64_t lim, size_t at,
                         hipStream_t st, const WalTrace& tr, WalPart* out) {
   namespace sg = lsmck::seg;
@@ -1737,7 +1806,7 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
     return 0;
   }
   if (lim > n || lim <= start) lim = n;
-  uint64_t S = lsmk_wal_seg_bytes(lim - start, ctx->wal_seg_bytes);
+  uint64_t S = lsmk_wal_seg_bytes(lim - start, ctx->wal_seg_bytes ? ctx->wal_seg_bytes : ctx->wal_seg_auto);
   sg::SegArgs a{};
   int resegs = 0, prepairs = 0, repairs = 0;
   ctx->last_seg_prepairs = 0;
@@ -1891,9 +1960,17 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
   out->tpos = W.h_sinfo[sg::kInfoPos];
   if (m) {
     const size_t tot = at + m;
-    // LSMCK_RECS_DEVICE with room for every record: emitted into the caller's array
-    const bool dev = ctx->wal_recs_dev && at == 0 && tot <= ctx->wal_recs_dev_cap;
+    // LSMCK_RECS_DEVICE with room for every record: emitted into the caller's
+    // array (a pipelined part after the first: when the parts before it were)
+    const bool dev = ctx->wal_recs_dev && (at == 0 || ctx->wal_recs_dev_emitted) && tot <= ctx->wal_recs_dev_cap;
+    if (ctx->wal_recs_dev_emitted && at > 0 && !dev) return kWalPipeRestart;
     const bool c16 = ctx->wal_compact;
+    if (ctx->wal_grow_hook) {  // (a pipelined replay: the CRC passes and read-backs beside it let go first)
+      const size_t rcap = dev ? tot : c16 ? W.cap_recs16 : W.cap_recs;
+      if ((rcap < tot || ctx->cap_woff < tot || ctx->cap_wlen < tot || ctx->cap_wexp < tot || ctx->cap_vcrc < tot) &&
+          (rc = ctx->wal_grow_hook()))
+        return rc;
+    }
     if ((!dev && !c16 && (rc = ensure_dev_keep(&W.recs, &W.cap_recs, tot, at, st))) ||
         (!dev && c16 && (rc = ensure_dev_keep(&W.recs16, &W.cap_recs16, tot, at, st))) ||
         (rc = ensure_dev_keep(&ctx->d_woff, &ctx->cap_woff, tot, at, st)) ||
@@ -1919,6 +1996,231 @@ static int wal_seg_walk(lsmck_ctx* ctx, const uint8_t* img, size_t n, uint64_t s
   return 0;
 }
 
+// The pipelined replay's two CU-masked streams: the walk keeps wal_pipe_cus
+// CUs (the last ones, or spread over the chip), the CRC passes get the rest.
+// A persistent stream kernel sized to the rest's CU count keeps each of its
+// CUs to itself, so neither side's workgroups wait for the other's.
+static int wal_pipe_streams(lsmck_ctx* ctx) {
+  const int N = ctx->ncu, cus = std::min(ctx->wal_pipe_cus, N - 1);
+  const int key = cus * 2 + ctx->wal_pipe_layout;
+  if (ctx->wal_pw && ctx->wal_pc && ctx->wal_pipe_key == key) return 0;
+  for (hipStream_t* s : {&ctx->wal_pw, &ctx->wal_pc})
+    if (*s) {
+      (void)hipStreamSynchronize(*s);
+      (void)hipStreamDestroy(*s);
+      *s = nullptr;
+    }
+  std::vector<uint32_t> mw((size_t)(N + 31) / 32, 0u), mc((size_t)(N + 31) / 32, 0u);
+  std::vector<char> walk((size_t)N, 0);
+  if (ctx->wal_pipe_layout == 0) {
+    for (int i = N - cus; i < N; ++i) walk[(size_t)i] = 1;
+  } else {
+    for (int j = 0; j < cus; ++j) walk[(size_t)(((int64_t)j * N) / cus + N / cus - 1)] = 1;
+  }
+  for (int i = 0; i < N; ++i) (walk[(size_t)i] ? mw : mc)[(size_t)i / 32] |= 1u << (i % 32);
+  HIPCHK(hipExtStreamCreateWithCUMask(&ctx->wal_pw, (uint32_t)mw.size(), mw.data()));
+  HIPCHK(hipExtStreamCreateWithCUMask(&ctx->wal_pc, (uint32_t)mc.size(), mc.data()));
+  ctx->wal_pipe_key = key;
+  return 0;
+}
+
+// The device replay in parts ("wal_pipe" parts, logs of "wal_pipe_min" bytes
+// and more): the segment walk of part k+1 runs on wal_pipe_cus CUs while the
+// CRC pass of part k runs on the others.  The walk is latency-bound (HBM
+// nearly idle, ~1.2 TB/s), the pass is bound by its compute at the clock the
+// chip holds, so the walk's time hides inside the pass except for the first
+// part's, which is walked on every CU before anything runs beside it.  Each
+// part is a prefix walk (records that start in [start, lim); the next part
+// starts at the first record at or past lim, exactly as the split host replay
+// resumes), its records emitted after the parts before it.  A part's last
+// record keeps its payload alone as its CRC span (the next header is the next
+// part's), so the compare's report unpacks no header from it (`ends`).
+// Records to the host are read back part by part on the SDMA engines as each
+// part is emitted.  Returns kWalSegDecline / kWalPipeRestart, everything
+// beside it drained, when a part's segment walk declines or its records
+// outgrow the caller's device array: the caller then replays unpipelined.
+static int wal_replay_pipelined(lsmck_ctx* ctx, const uint8_t* img, size_t n, void* recs, size_t cap, size_t* nrec,
+                                uint64_t* bad_index, uint32_t* bad_crc, uint32_t* bad_expected, hipStream_t st,
+                                const WalTrace& tr) {
+  auto& Wd = ctx->wd;
+  int rc;
+  if ((rc = wal_pipe_streams(ctx))) return rc;
+  const int P = ctx->wal_pipe;
+  const int crc_cus = ctx->ncu - std::min(ctx->wal_pipe_cus, ctx->ncu - 1);
+  hipStream_t W = ctx->wal_pw, C = ctx->wal_pc;
+  while ((int)ctx->wal_pipe_ev.size() < P) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ctx->wal_pipe_ev.push_back(e);
+  }
+  const size_t rsz = wal_rec_size(ctx);
+  const bool c16 = ctx->wal_compact;
+  // records to the host, part by part on the SDMA engines (no engines: the
+  // whole read-back in wal_finish, after the last part)
+  const bool host_recs = !ctx->wal_recs_dev && recs && cap;
+  lsmck_dma::Copier* dc = host_recs && ctx->wal_dma_engines ? dma_copier(ctx) : nullptr;
+  const int E = dc ? std::max(1, std::min(ctx->wal_dma_engines, lsmck_dma::engines(dc))) : 0;
+  const bool direct = ctx->wal_recs_direct;
+  struct RB {
+    lsmck_dma::Job job;
+    size_t lo;    // its first record
+    int cur = 0;  // pieces landed (and copied out)
+  };
+  std::vector<RB> jobs;
+  int sig_next = 0, derr = 0;
+  auto copy_out = [&](size_t a, size_t b) {  // the landing's bytes [a, b) -> the caller's pageable array
+    const size_t len = b - a;
+    const unsigned T = len >= (4u << 20) ? std::max(1u, std::min(ctx->stage_threads, 8u)) : 1u;
+    host_pool(ctx).run(T, [&](unsigned t) {
+      const size_t x = a + (len * t / T & ~(size_t)4095), y = t + 1 == T ? b : a + (len * (t + 1) / T & ~(size_t)4095);
+      if (y > x) memcpy((uint8_t*)recs + x, ctx->h_wrecs + x, y - x);
+    });
+  };
+  auto drain = [&](bool block) {  // landed pieces copied out, in order; block: all of them
+    for (auto& J : jobs)
+      for (; J.cur < J.job.n; ++J.cur) {
+        if (!block && !lsmck_dma::landed(dc, J.job, J.cur)) return;
+        if (lsmck_dma::wait(dc, J.job, J.cur) && !derr) derr = 1;
+        if (!direct && !derr) copy_out(J.lo * rsz + J.job.off[J.cur], J.lo * rsz + J.job.off[J.cur + 1]);
+      }
+    jobs.clear();
+    sig_next = 0;
+  };
+  auto quiesce = [&]() -> int {  // nothing beside the walk reads the record arrays any more
+    HIPCHK(hipStreamSynchronize(C));
+    HIPCHK(hipStreamSynchronize(W));
+    if (dc) drain(true);
+    return derr ? lsmck_host::set_error(LSMCK_EIO, "SDMA copy of the WAL records failed") : 0;
+  };
+  struct Hook {  // (cleared on every return)
+    lsmck_ctx* c;
+    ~Hook() {
+      c->wal_grow_hook = nullptr;
+      c->wal_seg_auto = 0;
+    }
+  } hook{ctx};
+  ctx->wal_grow_hook = quiesce;
+  auto readback = [&](size_t lo, size_t hi) -> int {  // records [lo, hi) to the host (hi <= cap)
+    if (!dc || hi <= lo) return 0;
+    uint8_t* land;
+    if (direct) {
+      land = (uint8_t*)recs + lo * rsz;
+    } else {
+      if (hi * rsz > ctx->cap_hwrecs) {  // (the landing grows only with nothing in flight)
+        drain(true);
+        if ((rc = ensure_pinned(ctx->pin_node, &ctx->h_wrecs, &ctx->cap_hwrecs, hi * rsz + hi * rsz / 4))) return rc;
+      }
+      land = ctx->h_wrecs + lo * rsz;
+    }
+    const int chunks = std::max(E, ctx->wal_dma_chunks / 4);
+    if (sig_next + chunks > lsmck_dma::kMaxSignals) drain(true);
+    const uint8_t* src = c16 ? (const uint8_t*)Wd.recs16 : (const uint8_t*)Wd.recs;
+    RB J;
+    J.lo = lo;
+    if (lsmck_dma::d2h(dc, land, src + lo * rsz, (hi - lo) * rsz, E, chunks, &J.job, sig_next) != 0) {
+      drain(true);  // (the engines refused: one plain copy of this part)
+      HIPCHK(hipMemcpy(land, src + lo * rsz, (hi - lo) * rsz, hipMemcpyDeviceToHost));
+      if (!direct) copy_out(lo * rsz, hi * rsz);
+      return 0;
+    }
+    sig_next += J.job.n;
+    jobs.push_back(J);
+    return 0;
+  };
+  // part bounds: the first part on every CU (st), the rest in P - 1 parts on W
+  const uint64_t a0 = std::max<uint64_t>(n * (uint64_t)ctx->wal_pipe_first / 64, 1);
+  std::vector<size_t> ends;  // the parts' last records (their spans are their payloads alone)
+  uint64_t start = 0;
+  size_t at = 0;
+  int parts = 0, repairs = 0, prepairs = 0;
+  uint64_t segs = 0;
+  WalPart Pk;
+  for (int k = 0;; ++k) {
+    const uint64_t lim = k + 1 >= P ? n : k == 0 ? a0 : a0 + (n - a0) * (uint64_t)k / (uint64_t)(P - 1);
+    hipStream_t ws = k == 0 ? st : W;
+    // the parts on W in segments for the lanes the walk CUs hold at once
+    // (8 waves a SIMD, a segment per 8 lanes): one round of waves, each
+    // chain as long as that allows; part 0 on every CU keeps the auto size
+    if (k == 1) {
+      const uint64_t lanes = (uint64_t)std::min(ctx->wal_pipe_cus, ctx->ncu - 1) * 4 * 8 * 64 / 8;
+      uint64_t S = ctx->wal_pipe_seg;
+      if (!S) {
+        S = 4096;
+        while (S < (16ull << 20) && ((n - a0) / (uint64_t)(P - 1) + S - 1) / S > lanes) S <<= 1;
+      }
+      ctx->wal_seg_auto = S;
+    }
+    rc = wal_seg_walk(ctx, img, n, start, lim, at, ws, tr, &Pk);
+    repairs += ctx->last_seg_repairs;
+    prepairs += ctx->last_seg_prepairs;
+    segs += ctx->last_segments;
+    if (rc) {
+      const int q = quiesce();
+      return q ? q : rc;
+    }
+    const size_t m = Pk.m - at;
+    const bool more = Pk.term == kWalStop && Pk.tpos < n && lim < n;
+    if (more && !m) {  // (no record started in the part: not expected, the plain replay instead)
+      const int q = quiesce();
+      return q ? q : kWalPipeRestart;
+    }
+    if (k == 0 && more && m) {
+      // the record arrays sized once for the whole log from the first part's
+      // density (+15 %), before anything runs beside the walk; a later part
+      // that outgrows them drains first (wal_grow_hook)
+      const size_t est = (size_t)((double)m * ((double)n / (double)std::max<uint64_t>(Pk.tpos, 1)) * 1.15) + 65536;
+      const bool dev = ctx->wal_recs_dev_emitted;
+      if ((!dev && !c16 && (rc = ensure_dev_keep(&Wd.recs, &Wd.cap_recs, est, m, st))) ||
+          (!dev && c16 && (rc = ensure_dev_keep(&Wd.recs16, &Wd.cap_recs16, est, m, st))) ||
+          (rc = ensure_dev_keep(&ctx->d_woff, &ctx->cap_woff, est, m, st)) ||
+          (rc = ensure_dev_keep(&ctx->d_wlen, &ctx->cap_wlen, est, m, st)) ||
+          (rc = ensure_dev_keep(&ctx->d_wexp, &ctx->cap_wexp, est, m, st)) ||
+          (rc = ensure_dev_keep(&ctx->d_vcrc, &ctx->cap_vcrc, est, m, st)))
+        return rc;
+      if (dc && !direct && (rc = ensure_pinned(ctx->pin_node, &ctx->h_wrecs, &ctx->cap_hwrecs, std::min(est, cap) * rsz)))
+        return rc;
+    }
+    hipEvent_t ev = ctx->wal_pipe_ev[(size_t)k % ctx->wal_pipe_ev.size()];
+    HIPCHK(hipEventRecord(ev, ws));
+    if (k == 0) HIPCHK(hipStreamWaitEvent(W, ev, 0));  // (the walk's arrays: part 0's place is done)
+    HIPCHK(hipStreamWaitEvent(C, ev, 0));
+    if ((rc = wal_crc_part(ctx, img, at, m, C, crc_cus))) {
+      const int q = quiesce();
+      return q ? q : rc;
+    }
+    ++parts;
+    tr.mark(k == 0 ? "pipe: part 0 walked, its CRC pass queued" : "pipe: part walked, its CRC pass queued");
+    if (dc && at < cap) {  // this part's records to the host once its emit is done
+      HIPCHK(hipEventSynchronize(ev));
+      if ((rc = readback(at, std::min(at + m, cap)))) return rc;
+    }
+    if (more && m) ends.push_back(at + m - 1);
+    at += m;
+    if (!more) break;
+    start = Pk.tpos;
+    if (dc) drain(false);
+  }
+  ctx->last_pipe_parts = parts;
+  ctx->last_walk_path = 1;
+  ctx->last_seg_repairs = repairs;
+  ctx->last_seg_prepairs = prepairs;
+  ctx->last_segments = segs;
+  // the compare on st once the last pass is done
+  hipEvent_t evc = ctx->wal_pipe_ev[(size_t)parts % ctx->wal_pipe_ev.size()];
+  HIPCHK(hipEventRecord(evc, C));
+  HIPCHK(hipStreamWaitEvent(st, evc, 0));
+  const size_t done = dc ? std::min(at, cap) : 0;  // (read back already, or landing as wal_finish returns)
+  rc = wal_finish(ctx, img, at, Pk.term, Pk.tpos, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr, done, true,
+                  Pk.packed ? 0 : ~(size_t)0, &ends);
+  if (dc) {
+    drain(true);
+    if (dc) ctx->last_recs_dma = E;
+    tr.mark("pipe: records read back");
+    if (derr && rc >= 0) return lsmck_host::set_error(LSMCK_EIO, "SDMA copy of the WAL records failed");
+  }
+  return rc;
+}
+
 // A device-resident image (or an uploaded one: `marked`, its candidate bitmap
 // is already in ctx->wd -- wal_upload marks each chunk behind its copy): the
 // walk (in parts when its scratch would not fit), one CRC pass per part.
@@ -1932,6 +2234,13 @@ static int wal_replay_device(lsmck_ctx* ctx, const uint8_t* img, size_t n, void*
   ScratchOrder so(ctx, ctx->stream0);
   if (so.e != hipSuccess) return hip_error(so.e, "hipStreamWaitEvent(scratch)");
   hipStream_t st = so.st;
+  ctx->last_pipe_parts = 0;
+  if (ctx->wal_pipe >= 2 && ctx->wal_seg && !ctx->wal_part_bytes && n >= ctx->wal_pipe_min && n >= 64) {
+    rc = wal_replay_pipelined(ctx, img, n, recs, cap, nrec, bad_index, bad_crc, bad_expected, st, tr);
+    if (rc != kWalSegDecline && rc != kWalPipeRestart) return rc;
+    ctx->last_pipe_parts = 0;  // (a part declined, or outgrew the caller's array: the whole log, unpipelined)
+    ctx->wal_recs_dev_emitted = false;
+  }
   WalPart P;
   rc = ctx->wal_seg && !ctx->wal_part_bytes ? wal_seg_walk(ctx, img, n, 0, n, 0, st, tr, &P) : kWalSegDecline;
   if (rc == 0) {  // the CRC pass over every record, then the compare and the records
@@ -1983,7 +2292,8 @@ static int wal_upload_range(lsmck_ctx* ctx, WalUpload& U, size_t lo, size_t hi) 
 
 // the slots' work so far, ordered before stream st
 static int wal_upload_fence(lsmck_ctx* ctx, hipStream_t st) {
-  for (auto& S : ctx->stage) {
+  for (int k = 0; k < kHostSlots; ++k) {  // (the upload's slots)
+    Stage& S = ctx->stage[k];
     HIPCHK(hipEventRecord(S.done, S.s));
     HIPCHK(hipStreamWaitEvent(st, S.done, 0));
   }
@@ -2033,7 +2343,7 @@ static int wal_upload(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool pinned)
   if ((rc = wal_upload_prepare(ctx, n, U.direct))) return rc;
   StageGuard guard{ctx};
   if ((rc = wal_upload_range(ctx, U, 0, n))) return rc;
-  for (auto& S : ctx->stage) HIPCHK(hipStreamSynchronize(S.s));
+  for (int k = 0; k < kHostSlots; ++k) HIPCHK(hipStreamSynchronize(ctx->stage[k].s));
   tr.mark("upload");
   guard.ok = true;
   return 0;
@@ -2122,7 +2432,7 @@ static int wal_replay_split(lsmck_ctx* ctx, const uint8_t* img, size_t n, bool p
     }
     if (pr.first) {
       if (pr.first != kWalHostWalk) lsmck_host::set_error(pr.first, pr.second.c_str());
-      for (auto& S : ctx->stage) HIPCHK(hipStreamSynchronize(S.s));
+      for (int k = 0; k < kHostSlots; ++k) HIPCHK(hipStreamSynchronize(ctx->stage[k].s));
       guard.ok = true;
       return pr.first;  // (kWalHostWalk: the image is whole on the device; the caller walks it on the host)
     }

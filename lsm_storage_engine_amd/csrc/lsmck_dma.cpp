@@ -17,7 +17,7 @@ struct Copier {
   hsa_agent_t cpu{};  // the first CPU agent (a host array's own agent is used when HSA names one)
   uint32_t eng[16] = {};
   int neng = 0;
-  hsa_signal_t sig[kMaxChunks] = {};
+  hsa_signal_t sig[kMaxSignals] = {};
   int nsig = 0;
 };
 
@@ -83,9 +83,10 @@ void destroy(Copier* c) {
 
 int engines(const Copier* c) { return c ? c->neng : 0; }
 
-int d2h(Copier* c, void* dst, const void* src, size_t bytes, int engines, int chunks, Job* j) {
+int d2h(Copier* c, void* dst, const void* src, size_t bytes, int engines, int chunks, Job* j, int sig_base) {
   j->n = 0;
-  if (!c || !dst || !src) return -1;
+  j->base = sig_base;
+  if (!c || !dst || !src || sig_base < 0) return -1;
   if (!bytes) return 0;
   hsa_amd_pointer_info_t pd, ps;
   if (!pointer(dst, &pd) || (pd.type != HSA_EXT_POINTER_TYPE_HSA && pd.type != HSA_EXT_POINTER_TYPE_LOCKED))
@@ -101,7 +102,8 @@ int d2h(Copier* c, void* dst, const void* src, size_t bytes, int engines, int ch
   size_t per = (bytes + (size_t)chunks - 1) / (size_t)chunks;
   per = (per + 4095) & ~(size_t)4095;
   const int n = (int)((bytes + per - 1) / per);
-  while (c->nsig < n) {
+  if (sig_base + n > kMaxSignals) return -7;
+  while (c->nsig < sig_base + n) {
     if (hsa_signal_create(1, 0, nullptr, &c->sig[c->nsig]) != HSA_STATUS_SUCCESS) return -4;
     ++c->nsig;
   }
@@ -109,9 +111,9 @@ int d2h(Copier* c, void* dst, const void* src, size_t bytes, int engines, int ch
     const size_t o = per * (size_t)i, len = std::min(per, bytes - o);
     j->off[i] = o;
     j->off[i + 1] = o + len;
-    hsa_signal_store_relaxed(c->sig[i], 1);
+    hsa_signal_store_relaxed(c->sig[sig_base + i], 1);
     const hsa_status_t s = hsa_amd_memory_async_copy_on_engine(
-        d + o, dst_agent, (const uint8_t*)src + o, c->gpu, len, 0, nullptr, c->sig[i],
+        d + o, dst_agent, (const uint8_t*)src + o, c->gpu, len, 0, nullptr, c->sig[sig_base + i],
         (hsa_amd_sdma_engine_id_t)c->eng[i % engines], true);
     if (s != HSA_STATUS_SUCCESS) {
       // the chunks already issued must land before the caller reuses dst
@@ -128,10 +130,15 @@ int d2h(Copier* c, void* dst, const void* src, size_t bytes, int engines, int ch
 int wait(Copier* c, const Job& j, int i) {
   if (i < 0 || i >= j.n) return 0;
   hsa_signal_value_t v;
-  while ((v = hsa_signal_wait_scacquire(c->sig[i], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+  while ((v = hsa_signal_wait_scacquire(c->sig[j.base + i], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
                                         HSA_WAIT_STATE_BLOCKED)) > 0) {
   }
   return v < 0 ? -6 : 0;
+}
+
+bool landed(Copier* c, const Job& j, int i) {
+  if (i < 0 || i >= j.n) return true;
+  return hsa_signal_load_scacquire(c->sig[j.base + i]) < 1;
 }
 
 int wait_all(Copier* c, const Job& j) {

@@ -15,6 +15,7 @@
 namespace lsmck_dma {
 
 constexpr int kMaxChunks = 64;
+constexpr int kMaxSignals = 256;  // completion signals per copier: several jobs in flight use disjoint ranges
 
 struct Copier;  // one per context: the GPU's agent, its SDMA engines, a pool of completion signals
 
@@ -30,12 +31,18 @@ int engines(const Copier* c);  // SDMA engines usable for device -> host
 // order), so the copied prefix grows about evenly.  dst must be page-locked
 // (hipHostMalloc / hipHostRegister).  Issue returns at once; one job per
 // copier at a time.  0 or a negative code (the copy did not start: use
-// hipMemcpyAsync).
+// hipMemcpyAsync).  sig_base: the job's first completion signal; jobs in
+// flight together take disjoint ranges [sig_base, sig_base + chunks) of the
+// copier's kMaxSignals (the pipelined WAL replay reads each part back as its
+// records are emitted).
 struct Job {
   int n = 0;                      // chunks issued
+  int base = 0;                   // its signals: [base, base + n)
   size_t off[kMaxChunks + 1] = {};  // chunk i: bytes [off[i], off[i+1])
 };
-int d2h(Copier* c, void* dst, const void* src, size_t bytes, int engines, int chunks, Job* j);
+int d2h(Copier* c, void* dst, const void* src, size_t bytes, int engines, int chunks, Job* j, int sig_base = 0);
+// whether chunk i has landed (no wait); a failed chunk counts as landed (wait() reports it)
+bool landed(Copier* c, const Job& j, int i);
 // wait for chunk i (every chunk: wait_all).  0, or a negative code if the
 // engine reported an error.
 int wait(Copier* c, const Job& j, int i);

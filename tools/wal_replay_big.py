@@ -64,6 +64,11 @@ def main():
     ap.add_argument("--shape", default="zipf", choices=["zipf", "mib", "logs"],
                     help="zipf: config 3's records framed; mib: ~1 MiB values; logs: values that are WAL images")
     ap.add_argument("--log-gib", type=float, default=97.8, help="mib / logs: the log's size")
+    ap.add_argument("--opt", action="append", default=[], help="key=value: a context option for every replay")
+    ap.add_argument("--variants", default="",
+                    help="A/B after the replays: 'name:key=val,key=val;name2:...' -- each variant's options set in "
+                         "turn, --ab-rounds interleaved rounds, records to the pinned host array and in HBM")
+    ap.add_argument("--ab-rounds", type=int, default=3)
     a = ap.parse_args()
     n = a.records
     inner = None
@@ -109,6 +114,9 @@ def main():
     ctx.set_option("wal_seg_stage", a.seg_stage)
     if a.dma_engines >= 0:
         ctx.set_option("wal_dma_engines", a.dma_engines)
+    for kv in a.opt:
+        k, v = kv.split("=")
+        ctx.set_option(k, int(v))
     kl = np.minimum(ln, 16).astype(np.uint32)  # the framing's key / value split (lsmck_wal_frame_insert_device)
 
     def check_compact(recs):  # every record against the framing
@@ -181,7 +189,8 @@ def main():
     # the engines of the host-record replays' read-back, read before the
     # records-on-device replays below (which read nothing back: the stat is 0)
     host_dma = ctx.get_stat("wal_recs_dma")
-    host_stats = {k: ctx.get_stat(k) for k in ("wal_walk_path", "wal_seg_repairs", "wal_seg_prepairs", "wal_segments")}
+    host_stats = {k: ctx.get_stat(k) for k in ("wal_walk_path", "wal_seg_repairs", "wal_seg_prepairs", "wal_segments",
+                                               "wal_pipe_parts")}
     dev = None
     if a.device_recs:  # the records stay in HBM: the walk, the CRC pass and the compare, no host link
         from lsm_storage_engine_amd.device import WAL_REC16_DTYPE, WAL_REC_DTYPE
@@ -231,6 +240,54 @@ def main():
                # (as the host line's: compact and non-Zipf records are each checked against the framing)
                "summary_matches_oracle": bool(a.compact) or a.shape != "zipf" or (bool(golden) and dsum == golden["summary_crc32"]),
                "seg_sweep": sweep}
+    ab = {}
+    if a.variants:  # interleaved A/B of option sets: records to the pinned host array, then in HBM
+        from lsm_storage_engine_amd.device import WAL_REC16_DTYPE, WAL_REC_DTYPE
+        RD = WAL_REC16_DTYPE if a.compact else WAL_REC_DTYPE
+        rb = ctx.alloc(n * RD.itemsize)
+        vs = []
+        for item in a.variants.split(";"):
+            name, _, kvs = item.partition(":")
+            vs.append((name, [(k, int(v)) for k, v in (kv.split("=") for kv in kvs.split(",") if kv)]))
+        # (every variant names the options it sets; a key one variant sets and another does not keeps the last value)
+        res = {name: {"host": [], "dev": [], "parts": None} for name, _ in vs}
+        for r in range(a.ab_rounds + 1):  # (round 0: warm-up)
+            for name, o in vs:
+                for k, v in o:
+                    ctx.set_option(k, v)
+                ctx.sync()
+                t = time.perf_counter()
+                recs, st, bad = ctx.wal_replay_verify(total, device_ptr=d.ptr, cap=n, pinned_recs=bool(a.pinned_recs),
+                                                      compact=bool(a.compact))
+                th = time.perf_counter() - t
+                assert st == 0 and len(recs) == n, (name, st, len(recs), bad)
+                if a.compact:
+                    check_compact(recs)
+                elif a.shape != "zipf":
+                    check_wide(recs)
+                del recs
+                ctx.sync()
+                t = time.perf_counter()
+                m, st, bad = ctx.wal_replay_verify_to_device(total, rb.ptr, n, device_ptr=d.ptr, compact=bool(a.compact))
+                td = time.perf_counter() - t
+                assert st == 0 and m == n, (name, st, m, bad)
+                if r:
+                    res[name]["host"].append(th)
+                    res[name]["dev"].append(td)
+                res[name]["parts"] = ctx.get_stat("wal_pipe_parts")
+                print(f"ab round {r} {name}: host {th * 1e3:.2f} ms, HBM {td * 1e3:.2f} ms, "
+                      f"{res[name]['parts']} parts", file=sys.stderr, flush=True)
+            got = rb.download(np.uint8, n * RD.itemsize).view(RD)
+            if a.compact:
+                check_compact(got)
+            elif a.shape != "zipf":
+                check_wide(got)
+        rb.free()
+        for name, v in res.items():
+            ab[name] = {"host_ms_median": round(float(np.median(v["host"])) * 1e3, 2),
+                        "dev_ms_median": round(float(np.median(v["dev"])) * 1e3, 2),
+                        "host_ms": [round(x * 1e3, 2) for x in v["host"]],
+                        "dev_ms": [round(x * 1e3, 2) for x in v["dev"]], "pipe_parts": v["parts"]}
     for b in (d_o, d_l, out):
         b.free()
     d.free()
@@ -245,7 +302,8 @@ def main():
         "compact": bool(a.compact), "recs_dma_engines": host_dma,
         "walk_path": {1: "segment walk", 2: "candidate doubling", 3: "host walk"}.get(host_stats["wal_walk_path"]),
         "seg_repairs": host_stats["wal_seg_repairs"], "seg_prepairs": host_stats["wal_seg_prepairs"],
-        "segments": host_stats["wal_segments"],
+        "segments": host_stats["wal_segments"], "pipe_parts": host_stats["wal_pipe_parts"], "options": a.opt,
+        "variants_ab": ab,
         "records_on_device": dev, "raw_batch_crc_ms": raw,
         "workload": {"zipf": "config 3's 2^26 Zipf payloads (64 B-64 KiB) framed as wal.rs Insert records "
                              "(13-byte headers), headers and CRCs written on the device",
