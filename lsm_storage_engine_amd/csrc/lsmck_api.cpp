@@ -487,6 +487,7 @@ struct lsmck_ctx {
   int sha_pair = 1;  // SHA-256 batches: two blocks per load window (A/B: DESIGN.md 3.2)
   int sha_short_blocks = 12;  // SHA-256 ordered batches: messages of at most this many blocks on the lean kernel (0 = off)
   unsigned tree_list_threads = 0;  // lsmck_tree_verify: metadata parsing threads (0 = kListThreads)
+  unsigned tree_readers = 16;      // whole-tree verify: threads reading a round's slices into its pinned slot
   size_t wal_prefetch = 4096;  // lsmck_wal_replay_verify: host walk's prefetch distance in bytes (0 = off)
   uint8_t* wal_host = nullptr;  // lsmck_wal_replay_verify of a device image: pinned host copy (grow-only)
   size_t wal_host_cap = 0;
@@ -1055,6 +1056,12 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
     if (value < 0 || value > 256) return lsmck_host::set_error(LSMCK_EINVAL, "tree_list_threads: 0..256");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->tree_list_threads = (unsigned)value;
+    return 0;
+  }
+  if (!strcmp(key, "tree_readers")) {  // A/B: whole-tree verify's slice reader threads
+    if (value < 1 || value > 64) return lsmck_host::set_error(LSMCK_EINVAL, "tree_readers: 1..64");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->tree_readers = (unsigned)value;
     return 0;
   }
   if (!strcmp(key, "stage_threads")) {  // A/B: threads of the pageable -> pinned staging copy (1 = one memcpy)
@@ -3049,7 +3056,7 @@ static int verify_tables(lsmck_ctx* ctx, const char* const* data_paths, const ch
           if (e) ferr[d.msg] = e == SlotFds::kOpenFailed ? open_panic(d.msg) : e;
         }
       };
-      const unsigned nt = (unsigned)std::min<size_t>(kTreeReaders, cnt);
+      const unsigned nt = (unsigned)std::min<size_t>(ctx->tree_readers, cnt);
       std::vector<std::thread> th;
       for (unsigned t = 1; t < nt; ++t) th.emplace_back(work);
       work();

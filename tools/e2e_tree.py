@@ -50,6 +50,9 @@ def main():
     ap.add_argument("--tick", default="",
                     help="comma list of tree_json_threads[:tree_active_files] values: the compaction tick's batch (levels 0..3 through "
                          "lsmck_checksums_verify_many), interleaved, 3 rounds each")
+    ap.add_argument("--readers", default="",
+                    help="comma list of tree_readers values: the tree verify and the compaction tick's batch per "
+                         "value, interleaved, 3 rounds")
     ap.add_argument("--multi", type=int, default=0,
                     help="also time lsmck_tree_verify_multi with this many contexts on device 0 against "
                          "lsmck_tree_verify on one (the multi-GPU split's own cost, measurable on one GPU)")
@@ -130,6 +133,25 @@ def main():
                       file=sys.stderr, flush=True)
         ctx.set_option("tree_json_threads", 0)
         ctx.set_option("tree_active_files", 0)
+    readers = {}
+    if a.readers:
+        low = [m for m in tree.list_tables(a.dir) if m.level <= 3]
+        triples = [(m.data_path(), m.index_path(), m.checksum_path()) for m in low]
+        for _ in range(3):
+            for v in filter(None, a.readers.split(",")):
+                ctx.set_option("tree_readers", int(v))
+                r = tree.load_verify(ctx, a.dir)[1]
+                t = time.perf_counter()
+                st = ctx.checksums_verify_many(triples)
+                dt = time.perf_counter() - t
+                assert not any(st)
+                e = readers.setdefault(v, {"tables_s": [], "tick_s": [], "read_s": []})
+                e["tables_s"].append(round(r["tables_s"], 3))
+                e["read_s"].append(round(r["tables_split"]["read_seconds"], 3))
+                e["tick_s"].append(round(dt, 3))
+                print(f"readers {v}: tree verify {r['tables_s']:.3f} s, tick batch {dt:.3f} s", file=sys.stderr,
+                      flush=True)
+        ctx.set_option("tree_readers", 16)
     multi = None
     if a.multi > 1:
         from lsm_storage_engine_amd.device import MultiContext
@@ -191,6 +213,8 @@ def main():
         res["list_s_by_threads"] = lt
     if multi:
         res["tree_verify_multi_same_gpu"] = multi
+    if readers:
+        res["tree_readers_ab"] = readers
     print(json.dumps(res), flush=True)
     ctx.close()
     if not a.keep:
