@@ -1012,12 +1012,10 @@ __global__ __launch_bounds__(1024) void crc32_walk_kernel(CrcParams P) {
 // the walking kernel, launched after this one, takes it when it is not.
 #define STREAM_LONG 64u      // records of at least this many bytes go through the chains
 #define STREAM_MAX_GAP 64u   // caller batches: at most this many bytes between two records
-// LDS columns K (x) x^i, i = 0..31 (128 B per factor K) of the finish factors,
-// in areas this kernel does not otherwise use: x^(8m) for m = 0..31 over the
-// shift-by-32-bytes table, m = 32..63 over the shift-by-96-bytes table (only
-// shift-by-64 is used here), x^(-8(4-t)) for t = 0..3 in the klo area
+// LDS columns K (x) x^i, i = 0..31 (128 B per factor K) of the finish
+// factors x^(8m): m = 0..31 over the shift-by-32-bytes table,
+// m = 32..63 over the shift-by-96-bytes table (only shift-by-64 is used here)
 #define LDS_XMC_OFF(m) ((m) < 32u ? LDS_SHIFT_OFF + (m) * 128u : LDS_SHIFT_OFF + 8192u + ((m) - 32u) * 128u)
-#define LDS_XIC_OFF(t) (LDS_KLO_OFF + (t) * 128u)
 
 // v (x) K from K's 32 LDS columns at `base` (8 ds_read_b128 + 32 v_bitop3).
 // (The generic gf2_mulmod here had its factor folded into 32 hoisted shifted
@@ -1035,6 +1033,69 @@ __device__ __forceinline__ uint32_t stream_mulcol(uint32_t v, uint32_t base) {
   return p;
 }
 
+// The Horner shift v (x) x^(8*128*d), d = 0..63 (round 6): nibble tables
+// instead of walk_mulcol's 32 bit columns (32 v_bfe_i32 + 32 v_bitop3 +
+// 8 ds_read_b128).  d = 4a + b: v (x) K^b, then (x) K^(4a); each stage is 8
+// lookups of (nibble q at position j) (x) K^e, by linearity.  A lookup's
+// address is one v_and_or_b32 of v shifted so that the nibble sits in the
+// table's index bits: stage 1 (4 factors) at bits 4-7, 16-byte rows of the
+// 4 factors; stage 2 (16 factors) at bits 8-11, 256-byte rows of 4 nibble
+// positions x 16 factors.  10 KiB over the walk columns' area (COLS + KHI,
+// which this kernel does not otherwise use).  Banks: stage 1 (4q + b) mod
+// 32, stage 2 (16 j' + a) mod 32 -- some lanes share one, and the LDS pipe
+// has the room.
+#define LDS_NIB2_OFF LDS_COLS_OFF            // [2 groups of 4 j][16 q][4 j'][16 a] u32, 8 KiB
+#define LDS_NIB1_OFF (LDS_COLS_OFF + 8192u)  // [8 j][16 q][4 b] u32, 2 KiB
+static_assert((LDS_NIB2_OFF & 4095u) == 0u && (LDS_NIB1_OFF & 255u) == 0u, "the or-addressing needs these alignments");
+static_assert(LDS_NIB1_OFF + 2048u <= LDS_KLO_OFF, "the nibble tables end where the finish's x^-8(4-t) columns start");
+
+// Tables of both stages: entry (j, q, e) = (q << 4j) (x) factor(e), with the
+// stage-1 factors e = 0..3 and the stage-2 factors e = 4a (a = 0..15).
+template <uint32_t N1, uint32_t N2, uint32_t GS, class F>
+__device__ __forceinline__ void build_nib(F factor) {
+  for (uint32_t i = threadIdx.x; i < 2560u; i += blockDim.x) {
+    uint32_t addr, q, j, e;
+    if (i < 512u) {  // stage 1: i = (j * 16 + q) * 4 + b
+      const uint32_t b = i & 3u;
+      q = (i >> 2) & 15u;
+      j = i >> 6;
+      e = b;
+      addr = N1 + 256u * j + 16u * q + 4u * b;
+    } else {  // stage 2: k = ((G * 16 + q) * 4 + j') * 16 + a, nibble j = 4G + j'
+      const uint32_t k = i - 512u, a = k & 15u, jp = (k >> 4) & 3u, G = k >> 10;
+      q = (k >> 6) & 15u;
+      j = 4u * G + jp;
+      e = 4u * a;
+      addr = N2 + GS * G + 256u * q + 64u * jp + 4u * a;
+    }
+    *(__attribute__((address_space(3))) uint32_t*)(size_t)addr = gf2_mulmod(q << (4u * j), factor(e));
+  }
+}
+
+// v (x) factor(d), d = 0..63, from the tables build_nib<N1, N2, GS> made
+template <uint32_t N1, uint32_t N2, uint32_t GS>
+__device__ __forceinline__ uint32_t nib_mul(uint32_t v, uint32_t d) {
+  const uint32_t b1 = N1 + ((d & 3u) << 2), b2 = N2 + (d & ~3u);
+  // stage 1: nibble j of v at bits 4-7 of v shifted right by 4j - 4
+  uint32_t u = __builtin_amdgcn_bitop3_b32(lds_ld(nullptr, (((v << 4) & 0xF0u) | b1)),
+                                           lds_ld(nullptr, ((v & 0xF0u) | b1) + 256u),
+                                           lds_ld(nullptr, (((v >> 4) & 0xF0u) | b1) + 512u), 0x96);
+  u = __builtin_amdgcn_bitop3_b32(u, lds_ld(nullptr, (((v >> 8) & 0xF0u) | b1) + 768u),
+                                  lds_ld(nullptr, (((v >> 12) & 0xF0u) | b1) + 1024u), 0x96);
+  u = __builtin_amdgcn_bitop3_b32(u, lds_ld(nullptr, (((v >> 16) & 0xF0u) | b1) + 1280u),
+                                  lds_ld(nullptr, (((v >> 20) & 0xF0u) | b1) + 1536u), 0x96);
+  u ^= lds_ld(nullptr, (((v >> 24) & 0xF0u) | b1) + 1792u);
+  // stage 2: nibble j of u at bits 8-11 of u shifted by 4j - 8
+  uint32_t y = __builtin_amdgcn_bitop3_b32(lds_ld(nullptr, ((u << 8) & 0xF00u) | b2),
+                                           lds_ld(nullptr, (((u << 4) & 0xF00u) | b2) + 64u),
+                                           lds_ld(nullptr, ((u & 0xF00u) | b2) + 128u), 0x96);
+  y = __builtin_amdgcn_bitop3_b32(y, lds_ld(nullptr, (((u >> 4) & 0xF00u) | b2) + 192u),
+                                  lds_ld(nullptr, (((u >> 8) & 0xF00u) | b2) + GS), 0x96);
+  y = __builtin_amdgcn_bitop3_b32(y, lds_ld(nullptr, (((u >> 12) & 0xF00u) | b2) + GS + 64u),
+                                  lds_ld(nullptr, (((u >> 16) & 0xF00u) | b2) + GS + 128u), 0x96);
+  return y ^ lds_ld(nullptr, (((u >> 20) & 0xF00u) | b2) + GS + 192u);
+}
+
 // The exact capture at an end at byte t of word u: the register s before the
 // word advanced over the word's t bytes before the end (the ending record's
 // last bytes), slicing-by-t from cx = s ^ u:
@@ -1050,9 +1111,6 @@ __device__ __forceinline__ uint32_t stream_capture(const unsigned char* smem, ui
   return ((cx ^ u) >> (t << 3)) ^ (t >= 1u ? l0 : 0u) ^ (t >= 2u ? l1 : 0u) ^ (t >= 3u ? l2 : 0u);
 }
 
-__device__ __forceinline__ uint32_t stream_xinv(uint32_t t) {  // x^(-8(4-t))
-  return t == 0u ? 0x5b358fd3u : (t == 1u ? 0x1f81b6e1u : (t == 2u ? 0xd7125358u : 0x6567cb95u));
-}
 
 // A caller's device batch takes the stream kernel when its records are sorted
 // and do not overlap, at most STREAM_MAX_GAP bytes apart, record 0 is not
@@ -1199,24 +1257,39 @@ __device__ __forceinline__ uint32_t stream_short(const CrcParams& P, const unsig
   return ~(c ^ lds_ld(smem, LDS_TINIT_OFF + (L << 2)));
 }
 
+// the Horner shift of a chunk's value to its target chunk, d chunks on
+__device__ __forceinline__ uint32_t horner(uint32_t v, uint32_t d) {
+#ifdef LSMCK_HORNER_COLS
+  return walk_mulcol(v, d);
+#else
+  return nib_mul<LDS_NIB1_OFF, LDS_NIB2_OFF, 4096u>(v, d);
+#endif
+}
+
+// the finish's factor: v (x) x^(8m), m = 0..63, from the bit columns.  (The
+// nibble tables here too, over the shift-by-32/96 and klo areas, ran slower:
+// config 3 19.87-19.93 against 19.11-19.20 ms, config 3w 21.10-21.22 against
+// 20.36-20.40 ms, same box, 4 / 3 interleaved rounds, profiles/r06/horner --
+// the finish runs in the few lanes that hold a record, whose LDS reads cost
+// per active lane, and its tables put the kernel at 8 spilled SGPRs.)
+__device__ __forceinline__ uint32_t finish_mul(uint32_t v, uint32_t m) { return stream_mulcol(v, LDS_XMC_OFF(m)); }
+
 template <int ABLATE = 0>
 __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
   if (!*P.sflag) return;  // a caller's batch that is not sorted / packed enough: the walking kernel takes it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   build_lds_tables(smem, P);
-  __syncthreads();  // the walk columns reuse the khi area, x^(8m) the klo area
-  build_walk_cols(P);
-  if (threadIdx.x >= 128u && threadIdx.x < 196u) {  // the finish factors' columns
+  __syncthreads();  // the Horner tables reuse the cols + khi areas, x^(8m) the shift tables', x^-8(4-t) the klo area
+#ifdef LSMCK_HORNER_COLS
+  build_walk_cols(P);  // (A/B: round 5's bit-column Horner)
+#else
+  build_nib<LDS_NIB1_OFF, LDS_NIB2_OFF, 4096u>([&](uint32_t e) { return P.kseg[e]; });  // x^(8*128*e)
+#endif
+  if (threadIdx.x >= 128u && threadIdx.x < 192u) {  // the finish factors' bit columns, x^(8m)
     const uint32_t f = threadIdx.x - 128u;
-    uint32_t K, base;
-    if (f < 64u) {  // x^(8m): m zero-byte steps of the register from x^0
-      K = 0x80000000u;
-      for (uint32_t i = 0; i < f; ++i) K = (K >> 8) ^ lds_ld(smem, 256u * (K & 0xFFu));  // T0 (replica 0)
-      base = LDS_XMC_OFF(f);
-    } else {
-      K = stream_xinv(f - 64u);
-      base = LDS_XIC_OFF(f - 64u);
-    }
+    uint32_t K = 0x80000000u;  // m zero-byte steps of the register from x^0
+    for (uint32_t i = 0; i < f; ++i) K = (K >> 8) ^ lds_ld(smem, 256u * (K & 0xFFu));  // T0 (replica 0)
+    const uint32_t base = LDS_XMC_OFF(f);
     for (uint32_t i = 0; i < 32u; ++i) {
       *(__attribute__((address_space(3))) uint32_t*)(size_t)(base + 4u * i) = K;
       K = (K >> 1) ^ (0xEDB88320u & (0u - (K & 1u)));
@@ -1301,7 +1374,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     }
     uint32_t dz = 63u - lane;
     asm volatile("" : "+v"(dz));  // not hoisted: eight loop-invariant column addresses spilled
-    const uint32_t XZ = wave_prefix_xor(walk_mulcol(shift_bytes32<2>(smem, z0) ^ z1, dz));
+    const uint32_t XZ = wave_prefix_xor(horner(shift_bytes32<2>(smem, z0) ^ z1, dz));
     carry = (uint32_t)__builtin_amdgcn_readlane((int)XZ, 63);
   };
 
@@ -1448,7 +1521,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     asm volatile("" : "+v"(l1));  // not hoisted: the loop-invariant lane mask spilled (a vmcnt(0) reload)
     const uint64_t above = lane == 63u ? 0ull : (M1 >> l1) << l1;
     const uint32_t cn = above ? (uint32_t)__builtin_ctzll(above) : 64u;
-    const uint32_t X = wave_prefix_xor(walk_mulcol(T, cn - 1u - lane));
+    const uint32_t X = wave_prefix_xor(horner(T, cn - 1u - lane));
     // --- records: the window lane of a record finishes it
     auto finish = [&](uint32_t cnt, int32_t re_, int32_t rs_, bool lng_, bool sin_) -> uint32_t {
       const uint32_t c = (uint32_t)re_ >> 7, j = (uint32_t)re_ & 127u;
@@ -1467,7 +1540,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
       if (in && lng_ && ABLATE != 7) {  // (ABLATE 7, diagnostic: no finish multiply -- results invalid)
         const bool h = j >= 64u;
         const uint32_t Pv = h ? (shift_bytes32<2>(smem, H) ^ R0c) : H;
-        fv = ~(stream_mulcol(Pv, LDS_XMC_OFF(j & 63u)) ^ (h ? A1c : A0c));
+        fv = ~(finish_mul(Pv, j & 63u) ^ (h ? A1c : A0c));
       }
       return fv;
     };
