@@ -1035,65 +1035,72 @@ __device__ __forceinline__ uint32_t stream_mulcol(uint32_t v, uint32_t base) {
 
 // The Horner shift v (x) x^(8*128*d), d = 0..63 (round 6): nibble tables
 // instead of walk_mulcol's 32 bit columns (32 v_bfe_i32 + 32 v_bitop3 +
-// 8 ds_read_b128).  d = 4a + b: v (x) K^b, then (x) K^(4a); each stage is 8
-// lookups of (nibble q at position j) (x) K^e, by linearity.  A lookup's
+// 8 ds_read_b128).  d = 16h + f: v (x) K^f, then (x) K^(16h); each stage is
+// 8 lookups of (nibble q at position j) (x) K^e, by linearity.  A lookup's
 // address is one v_and_or_b32 of v shifted so that the nibble sits in the
-// table's index bits: stage 1 (4 factors) at bits 4-7, 16-byte rows of the
-// 4 factors; stage 2 (16 factors) at bits 8-11, 256-byte rows of 4 nibble
-// positions x 16 factors.  10 KiB over the walk columns' area (COLS + KHI,
-// which this kernel does not otherwise use).  Banks: stage 1 (4q + b) mod
-// 32, stage 2 (16 j' + a) mod 32 -- some lanes share one, and the LDS pipe
-// has the room.
-#define LDS_NIB2_OFF LDS_COLS_OFF            // [2 groups of 4 j][16 q][4 j'][16 a] u32, 8 KiB
-#define LDS_NIB1_OFF (LDS_COLS_OFF + 8192u)  // [8 j][16 q][4 b] u32, 2 KiB
-static_assert((LDS_NIB2_OFF & 4095u) == 0u && (LDS_NIB1_OFF & 255u) == 0u, "the or-addressing needs these alignments");
-static_assert(LDS_NIB1_OFF + 2048u <= LDS_KLO_OFF, "the nibble tables end where the finish's x^-8(4-t) columns start");
+// table's index bits.  The layout is chosen for the LDS banks (bank = address
+// bits 2-6 within each 32-lane half of a ds_read_b32, MI355X_MICROARCH.md
+// "LDS"): stage A (16 factors f) has f in bits 2-5 and q in bits 6-9, so
+// two lanes of a half meet on a bank only when they share f and q's low
+// bit; stage B (4 factors h) has q in bits 2-5 and h in bits 6-7, so lanes
+// that share h -- a Horner's lanes mostly do -- never conflict (equal q is
+// one address, a broadcast).  Modelled (tools/lds_conflicts.py) and counted
+// (SQ_LDS_BANK_CONFLICT): 64 -> 16 extra LDS cycles per Horner of a tile
+// without events, 128 -> 30 in an event tile, against round 6's first
+// layout ([j][q][b] / [G][q][j'][a], whose stage-2 bank ignored q).
+// 10 KiB over the walk columns' area (COLS + KHI, which this kernel does not
+// otherwise use).
+#define LDS_NIBA_OFF LDS_COLS_OFF            // [8 j][16 q][16 f] u32, 8 KiB
+#define LDS_NIBB_OFF (LDS_COLS_OFF + 8192u)  // [8 j][4 h][16 q] u32, 2 KiB
+static_assert((LDS_NIBA_OFF & 0x3FCu) == 0u && (LDS_NIBB_OFF & 0xFCu) == 0u, "the or-addressing needs these bits clear");
+static_assert(LDS_NIBB_OFF + 2048u <= LDS_KLO_OFF, "the nibble tables end where the finish's x^-8(4-t) columns start");
 
 // Tables of both stages: entry (j, q, e) = (q << 4j) (x) factor(e), with the
-// stage-1 factors e = 0..3 and the stage-2 factors e = 4a (a = 0..15).
-template <uint32_t N1, uint32_t N2, uint32_t GS, class F>
+// stage-A factors e = f = 0..15 and the stage-B factors e = 16h (h = 0..3).
+template <uint32_t NA, uint32_t NB, class F>
 __device__ __forceinline__ void build_nib(F factor) {
   for (uint32_t i = threadIdx.x; i < 2560u; i += blockDim.x) {
     uint32_t addr, q, j, e;
-    if (i < 512u) {  // stage 1: i = (j * 16 + q) * 4 + b
-      const uint32_t b = i & 3u;
-      q = (i >> 2) & 15u;
-      j = i >> 6;
-      e = b;
-      addr = N1 + 256u * j + 16u * q + 4u * b;
-    } else {  // stage 2: k = ((G * 16 + q) * 4 + j') * 16 + a, nibble j = 4G + j'
-      const uint32_t k = i - 512u, a = k & 15u, jp = (k >> 4) & 3u, G = k >> 10;
-      q = (k >> 6) & 15u;
-      j = 4u * G + jp;
-      e = 4u * a;
-      addr = N2 + GS * G + 256u * q + 64u * jp + 4u * a;
+    if (i < 2048u) {  // stage A: i = (j * 16 + q) * 16 + f
+      const uint32_t f = i & 15u;
+      q = (i >> 4) & 15u;
+      j = i >> 8;
+      e = f;
+      addr = NA + 1024u * j + 64u * q + 4u * f;
+    } else {  // stage B: k = (j * 4 + h) * 16 + q
+      const uint32_t k = i - 2048u;
+      q = k & 15u;
+      const uint32_t h = (k >> 4) & 3u;
+      j = k >> 6;
+      e = 16u * h;
+      addr = NB + 256u * j + 64u * h + 4u * q;
     }
     *(__attribute__((address_space(3))) uint32_t*)(size_t)addr = gf2_mulmod(q << (4u * j), factor(e));
   }
 }
 
-// v (x) factor(d), d = 0..63, from the tables build_nib<N1, N2, GS> made
-template <uint32_t N1, uint32_t N2, uint32_t GS>
+// v (x) factor(d), d = 0..63, from the tables build_nib<NA, NB> made
+template <uint32_t NA, uint32_t NB>
 __device__ __forceinline__ uint32_t nib_mul(uint32_t v, uint32_t d) {
-  const uint32_t b1 = N1 + ((d & 3u) << 2), b2 = N2 + (d & ~3u);
-  // stage 1: nibble j of v at bits 4-7 of v shifted right by 4j - 4
-  uint32_t u = __builtin_amdgcn_bitop3_b32(lds_ld(nullptr, (((v << 4) & 0xF0u) | b1)),
-                                           lds_ld(nullptr, ((v & 0xF0u) | b1) + 256u),
-                                           lds_ld(nullptr, (((v >> 4) & 0xF0u) | b1) + 512u), 0x96);
-  u = __builtin_amdgcn_bitop3_b32(u, lds_ld(nullptr, (((v >> 8) & 0xF0u) | b1) + 768u),
-                                  lds_ld(nullptr, (((v >> 12) & 0xF0u) | b1) + 1024u), 0x96);
-  u = __builtin_amdgcn_bitop3_b32(u, lds_ld(nullptr, (((v >> 16) & 0xF0u) | b1) + 1280u),
-                                  lds_ld(nullptr, (((v >> 20) & 0xF0u) | b1) + 1536u), 0x96);
-  u ^= lds_ld(nullptr, (((v >> 24) & 0xF0u) | b1) + 1792u);
-  // stage 2: nibble j of u at bits 8-11 of u shifted by 4j - 8
-  uint32_t y = __builtin_amdgcn_bitop3_b32(lds_ld(nullptr, ((u << 8) & 0xF00u) | b2),
-                                           lds_ld(nullptr, (((u << 4) & 0xF00u) | b2) + 64u),
-                                           lds_ld(nullptr, ((u & 0xF00u) | b2) + 128u), 0x96);
-  y = __builtin_amdgcn_bitop3_b32(y, lds_ld(nullptr, (((u >> 4) & 0xF00u) | b2) + 192u),
-                                  lds_ld(nullptr, (((u >> 8) & 0xF00u) | b2) + GS), 0x96);
-  y = __builtin_amdgcn_bitop3_b32(y, lds_ld(nullptr, (((u >> 12) & 0xF00u) | b2) + GS + 64u),
-                                  lds_ld(nullptr, (((u >> 16) & 0xF00u) | b2) + GS + 128u), 0x96);
-  return y ^ lds_ld(nullptr, (((u >> 20) & 0xF00u) | b2) + GS + 192u);
+  const uint32_t bA = NA + ((d & 15u) << 2), bB = NB + ((d >> 4) << 6);
+  // stage A: nibble j of v at bits 6-9 of v shifted right by 4j - 6
+  uint32_t u = __builtin_amdgcn_bitop3_b32(lds_ld(nullptr, ((v << 6) & 0x3C0u) | bA),
+                                           lds_ld(nullptr, (((v << 2) & 0x3C0u) | bA) + 1024u),
+                                           lds_ld(nullptr, (((v >> 2) & 0x3C0u) | bA) + 2048u), 0x96);
+  u = __builtin_amdgcn_bitop3_b32(u, lds_ld(nullptr, (((v >> 6) & 0x3C0u) | bA) + 3072u),
+                                  lds_ld(nullptr, (((v >> 10) & 0x3C0u) | bA) + 4096u), 0x96);
+  u = __builtin_amdgcn_bitop3_b32(u, lds_ld(nullptr, (((v >> 14) & 0x3C0u) | bA) + 5120u),
+                                  lds_ld(nullptr, (((v >> 18) & 0x3C0u) | bA) + 6144u), 0x96);
+  u ^= lds_ld(nullptr, (((v >> 22) & 0x3C0u) | bA) + 7168u);
+  // stage B: nibble j of u at bits 2-5 of u shifted right by 4j - 2
+  uint32_t y = __builtin_amdgcn_bitop3_b32(lds_ld(nullptr, ((u << 2) & 0x3Cu) | bB),
+                                           lds_ld(nullptr, (((u >> 2) & 0x3Cu) | bB) + 256u),
+                                           lds_ld(nullptr, (((u >> 6) & 0x3Cu) | bB) + 512u), 0x96);
+  y = __builtin_amdgcn_bitop3_b32(y, lds_ld(nullptr, (((u >> 10) & 0x3Cu) | bB) + 768u),
+                                  lds_ld(nullptr, (((u >> 14) & 0x3Cu) | bB) + 1024u), 0x96);
+  y = __builtin_amdgcn_bitop3_b32(y, lds_ld(nullptr, (((u >> 18) & 0x3Cu) | bB) + 1280u),
+                                  lds_ld(nullptr, (((u >> 22) & 0x3Cu) | bB) + 1536u), 0x96);
+  return y ^ lds_ld(nullptr, (((u >> 26) & 0x3Cu) | bB) + 1792u);
 }
 
 // The exact capture at an end at byte t of word u: the register s before the
@@ -1262,7 +1269,7 @@ __device__ __forceinline__ uint32_t horner(uint32_t v, uint32_t d) {
 #ifdef LSMCK_HORNER_COLS
   return walk_mulcol(v, d);
 #else
-  return nib_mul<LDS_NIB1_OFF, LDS_NIB2_OFF, 4096u>(v, d);
+  return nib_mul<LDS_NIBA_OFF, LDS_NIBB_OFF>(v, d);
 #endif
 }
 
@@ -1283,7 +1290,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
 #ifdef LSMCK_HORNER_COLS
   build_walk_cols(P);  // (A/B: round 5's bit-column Horner)
 #else
-  build_nib<LDS_NIB1_OFF, LDS_NIB2_OFF, 4096u>([&](uint32_t e) { return P.kseg[e]; });  // x^(8*128*e)
+  build_nib<LDS_NIBA_OFF, LDS_NIBB_OFF>([&](uint32_t e) { return P.kseg[e]; });  // x^(8*128*e)
 #endif
   if (threadIdx.x >= 128u && threadIdx.x < 192u) {  // the finish factors' bit columns, x^(8m)
     const uint32_t f = threadIdx.x - 128u;

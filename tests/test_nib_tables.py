@@ -1,5 +1,6 @@
 """Host model of the stream kernel's Horner shift by nibble tables
-(lsmck_crc32.hip: build_nib / nib_mul, round 6): the tables are laid out in a
+(lsmck_crc32.hip: build_nib / nib_mul, round 6, the bank-aware layout
+d = 16h + f): the tables are laid out in a
 model of the LDS at the kernel's byte addresses, each lookup's address is
 formed exactly as the kernel forms it (one OR of the shifted value's nibble
 with a per-lane base, plus the instruction's immediate offset), and the result
@@ -10,8 +11,8 @@ import random
 
 POLY = 0xEDB88320
 LDS_COLS_OFF = 131072 + 12288  # LDS_SHIFT_OFF + LDS_SHIFT_BYTES
-NIB2 = LDS_COLS_OFF
-NIB1 = LDS_COLS_OFF + 8192
+NA = LDS_COLS_OFF          # LDS_NIBA_OFF: [8 j][16 q][16 f]
+NB = LDS_COLS_OFF + 8192   # LDS_NIBB_OFF: [8 j][4 h][16 q]
 KLO = LDS_COLS_OFF + 8192 + 2048  # LDS_KLO_OFF (COLS 8 KiB + KHI 2 KiB)
 
 
@@ -40,40 +41,33 @@ for _ in range(63):
 
 def build(lds):
     for i in range(2560):
-        if i < 512:
-            b = i & 3
-            q = (i >> 2) & 15
-            j = i >> 6
-            e = b
-            addr = NIB1 + 256 * j + 16 * q + 4 * b
+        if i < 2048:
+            f, q, j = i & 15, (i >> 4) & 15, i >> 8
+            e = f
+            addr = NA + 1024 * j + 64 * q + 4 * f
         else:
-            k = i - 512
-            a, jp, g = k & 15, (k >> 4) & 3, k >> 10
-            q = (k >> 6) & 15
-            j = 4 * g + jp
-            e = 4 * a
-            addr = NIB2 + 4096 * g + 256 * q + 64 * jp + 4 * a
+            k = i - 2048
+            q, h, j = k & 15, (k >> 4) & 3, k >> 6
+            e = 16 * h
+            addr = NB + 256 * j + 64 * h + 4 * q
         assert addr not in lds
         lds[addr] = gf2_mulmod((q << (4 * j)) & 0xFFFFFFFF, KSEG[e])
 
 
+def sh(v, s):
+    """v shifted right by s (left by -s), 32 bits"""
+    return (v >> s) if s >= 0 else (v << -s) & 0xFFFFFFFF
+
+
 def nib_mul(lds, v, d):
-    m = 0xFFFFFFFF
-    b1 = NIB1 + ((d & 3) << 2)
-    b2 = NIB2 + (d & ~3)
-    ld = lambda a: lds[a]  # noqa: E731
-    st1 = [((v << 4) & 0xF0) | b1, ((v & 0xF0) | b1) + 256, (((v >> 4) & 0xF0) | b1) + 512,
-           (((v >> 8) & 0xF0) | b1) + 768, (((v >> 12) & 0xF0) | b1) + 1024, (((v >> 16) & 0xF0) | b1) + 1280,
-           (((v >> 20) & 0xF0) | b1) + 1536, (((v >> 24) & 0xF0) | b1) + 1792]
+    bA = NA + ((d & 15) << 2)
+    bB = NB + ((d >> 4) << 6)
     u = 0
-    for a in st1:
-        u ^= ld(a)
-    st2 = [(((u << 8) & m) & 0xF00) | b2, ((((u << 4) & m) & 0xF00) | b2) + 64, ((u & 0xF00) | b2) + 128,
-           (((u >> 4) & 0xF00) | b2) + 192, (((u >> 8) & 0xF00) | b2) + 4096, (((u >> 12) & 0xF00) | b2) + 4160,
-           (((u >> 16) & 0xF00) | b2) + 4224, (((u >> 20) & 0xF00) | b2) + 4288]
+    for j in range(8):  # stage A: nibble j at bits 6-9 of v >> (4j - 6), row j by the immediate
+        u ^= lds[((sh(v, 4 * j - 6) & 0x3C0) | bA) + 1024 * j]
     y = 0
-    for a in st2:
-        y ^= ld(a)
+    for j in range(8):  # stage B: nibble j at bits 2-5 of u >> (4j - 2)
+        y ^= lds[((sh(u, 4 * j - 2) & 0x3C) | bB) + 256 * j]
     return y
 
 
@@ -81,7 +75,7 @@ def test_layout_fits_between_the_shift_tables_and_klo():
     lds = {}
     build(lds)
     assert min(lds) == LDS_COLS_OFF and max(lds) + 4 == KLO  # COLS + KHI exactly, nothing over klo
-    assert NIB2 % 4096 == 0 and NIB1 % 256 == 0
+    assert NA & 0x3FC == 0 and NB & 0xFC == 0  # the or-addressing's index bits are clear in the bases
 
 
 def test_nib_mul_equals_the_gf2_product():

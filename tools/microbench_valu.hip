@@ -30,6 +30,22 @@ __device__ __forceinline__ uint32_t step(uint32_t x, uint32_t k, uint32_t m) {
   if (OP == 9) asm("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(k), "v"(m));
   if (OP == 10) asm("v_cndmask_b32 %0, %1, %2, vcc" : "=v"(r) : "v"(x), "v"(k));
   if (OP == 11) asm("v_lshrrev_b32 %0, 3, %1" : "=v"(r) : "v"(x));
+  // (round 6) the stream kernel's LDS address byte: SDWA byte move into byte 1, rest kept
+  if (OP == 12) {
+    r = x;  // in place: the chain's own register (no copy)
+    asm("v_mov_b32_sdwa %0, %0 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(r));
+  }
+  if (OP == 13) asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(k), "v"(m));
+  if (OP == 14) asm("v_or_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD" : "=v"(r) : "v"(x), "v"(k));
+  if (OP == 15) asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=v"(r) : "v"(x), "s"(k), "v"(m));
+  if (OP == 16) asm("v_lshlrev_b32_e64 %0, 3, %1" : "=v"(r) : "v"(x));
+  if (OP == 17) asm("v_xor_b32_e64 %0, %1, %2" : "=v"(r) : "v"(x), "s"(k));
+  if (OP == 18) asm("v_bitop3_b32 %0, %1, 0x3f, %2 bitop3:0xea" : "=v"(r) : "v"(x), "v"(m));
+  // selects: the event path's v_cndmask forms against a bitop3 select on a VGPR lane mask
+  if (OP == 19) asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(k), "s"((unsigned long long)m * 0x100000001ull));
+  if (OP == 20) asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(m), "v"(k), "v"(x));
+  if (OP == 21) asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD" : "=v"(r) : "v"(x), "v"(k));
+  if (OP == 22) asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(x), "v"(k), "v"(x));
   return r;
 }
 
@@ -60,12 +76,16 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const char* names[] = {"v_add_u32", "v_xor_b32", "v_alignbit_b32", "v_bitop3_b32", "v_add3_u32", "v_perm_b32",
                          "v_alignbyte_b32", "v_bfe_i32", "v_lshl_or_b32", "v_xad_u32", "v_cndmask_b32",
-                         "v_lshrrev_b32"};
+                         "v_lshrrev_b32", "v_mov_b32_sdwa", "v_and_or_b32", "v_or_b32_sdwa PAD", "v_bitop3 (s op)", "v_lshlrev_b32_e64", "v_xor_b32_e64 (s)", "v_bitop3 (const)", "v_cndmask_e64 (s mask)", "v_bitop3 select", "v_add_u32_sdwa", "v_bitop3 (x,k,x)"};
   const void* fns[] = {(const void*)k_valu<0>, (const void*)k_valu<1>, (const void*)k_valu<2>,
                        (const void*)k_valu<3>, (const void*)k_valu<4>, (const void*)k_valu<5>,
                        (const void*)k_valu<6>, (const void*)k_valu<7>, (const void*)k_valu<8>,
-                       (const void*)k_valu<9>, (const void*)k_valu<10>, (const void*)k_valu<11>};
-  for (int i = 0; i < 12; ++i) {
+                       (const void*)k_valu<9>, (const void*)k_valu<10>, (const void*)k_valu<11>,
+                       (const void*)k_valu<12>, (const void*)k_valu<13>, (const void*)k_valu<14>,
+                       (const void*)k_valu<15>, (const void*)k_valu<16>, (const void*)k_valu<17>,
+                       (const void*)k_valu<18>, (const void*)k_valu<19>, (const void*)k_valu<20>,
+                       (const void*)k_valu<21>, (const void*)k_valu<22>};
+  for (int i = 0; i < 23; ++i) {
     uint32_t k = 12345, m = 777;
     void* args[] = {&out, &iters, &k, &m};
     CK(hipLaunchKernel(fns[i], dim3(blocks), dim3(512), args, 0, 0));
