@@ -995,9 +995,9 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value) {
   if (!key) return lsmck_host::set_error(LSMCK_EINVAL, "null key");
   if (!strcmp(key, "crc_ablate")) {  // diagnostic only (results are garbage): 3 = payload loads only (the
                                      // bench's loads-only ceiling), 2 = stream kernel without payload loads
-    if (value != 0 && value != 3 && (!lsmk_ab_ablations() || value < 2 || value > 10))
-      return lsmck_host::set_error(LSMCK_EINVAL, lsmk_ab_ablations() ? "crc_ablate must be 0 or 2..10"
-                                                                     : "crc_ablate must be 0 or 3 (2, 4..10: an A/B "
+    if (value != 0 && value != 3 && (!lsmk_ab_ablations() || value < 2 || value > 12))
+      return lsmck_host::set_error(LSMCK_EINVAL, lsmk_ab_ablations() ? "crc_ablate must be 0 or 2..12"
+                                                                     : "crc_ablate must be 0 or 3 (2, 4..12: an A/B "
                                                                        "library built with -DLSMCK_AB_ABLATIONS)");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->variant = (ctx->variant & ~0xF00) | ((int)value << 8);

@@ -1211,7 +1211,7 @@ __device__ __forceinline__ void stream_issue(const CrcParams& P, int64_t tb, uin
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<unsigned char*>(P.base + tb), (short)0, (int)(span < 0x7FFFFFFFull ? span : 0x7FFFFFFFull), 0x00020000);
   const uint32_t vo = lane * 128u;
-  if (ABLATE == 2 || ABLATE == 4 || ABLATE == 10) {  // diagnostic: compute only (no payload loads; results invalid)
+  if (ABLATE == 2 || ABLATE == 4 || ABLATE == 10 || ABLATE == 11) {  // diagnostic: compute only (no payload loads; results invalid)
 #pragma unroll
     for (int j = 0; j < 32; ++j) u[j] = (uint32_t)tb * 0x9E3779B1u + lane + j;
     return;
@@ -1373,6 +1373,21 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
   // register: the Horner shift of lane 0 then carries it to the tile end with
   // the chunk.
   auto bulk = [&](const uint32_t (&U)[32]) {
+    if constexpr (ABLATE == 11 || ABLATE == 12) {  // diagnostic: four chains of 8 words, XOR for the combine (results invalid)
+      uint32_t y0 = U[0] ^ (lane == 0u ? carry : 0u), y1 = U[8], y2 = U[16], y3 = U[24];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        y0 = crc_step_x(smem, y0, k + 1 < 8 ? U[k + 1] : 0u, lo, hi);
+        y1 = crc_step_x(smem, y1, k + 1 < 8 ? U[9 + k] : 0u, lo, hi);
+        y2 = crc_step_x(smem, y2, k + 1 < 8 ? U[17 + k] : 0u, lo, hi);
+        y3 = crc_step_x(smem, y3, k + 1 < 8 ? U[25 + k] : 0u, lo, hi);
+      }
+      uint32_t dy = 63u - lane;
+      asm volatile("" : "+v"(dy));
+      const uint32_t XY = wave_prefix_xor(horner(shift_bytes32<2>(smem, y0 ^ y1) ^ y2 ^ y3, dy));
+      carry = (uint32_t)__builtin_amdgcn_readlane((int)XY, 63);
+      return;
+    }
     uint32_t z0 = U[0] ^ (lane == 0u ? carry : 0u), z1 = U[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -1387,7 +1402,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
 
   auto process = [&](const uint32_t (&U)[32], uint64_t t, auto&& issue_next) {
     const int64_t tb = tbase(t);
-    if constexpr (ABLATE == 9 || ABLATE == 10) {  // diagnostic: the bulk chains + Horner alone, no window / map
+    if constexpr (ABLATE == 9 || ABLATE == 10 || ABLATE == 11) {  // diagnostic: the bulk chains + Horner alone, no window / map
       issue_next();                               // (10: without the payload loads); results invalid
       __builtin_amdgcn_sched_barrier(0);
       bulk(U);
@@ -1467,7 +1482,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     if constexpr (ABLATE == 0 || ABLATE >= 4) {
       // (ABLATE 4 / 5, diagnostic: every tile takes this path -- the bulk
       // chains + Horner cost without / with the payload loads)
-      if (z || ABLATE == 4 || ABLATE == 5) {  // (uniform) no event in the tile
+      if (z || ABLATE == 4 || ABLATE == 5 || ABLATE == 12) {  // (uniform) no event in the tile
         bulk(U);
         return;
       }
@@ -1597,7 +1612,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     process(U1, t_first + i + 1, [&] { stream_issue<ABLATE>(P, tcl(i + 2), end4, lane, U0); });
   }
   if (i < ntile) process(U0, t_first + i, none);
-  if ((ABLATE == 4 || ABLATE == 5 || ABLATE == 7 || ABLATE == 9 || ABLATE == 10) && carry == 0x9E3779B1u) P.out[0] = carry;  // keeps the ablated chains (and loads) alive
+  if ((ABLATE == 4 || ABLATE == 5 || ABLATE == 7 || ABLATE >= 9) && carry == 0x9E3779B1u) P.out[0] = carry;  // keeps the ablated chains (and loads) alive
   if (ABLATE == 3) return;
   qstore(qv, lane >= qs && lane < qf);
 }
@@ -1680,7 +1695,9 @@ extern "C" int lsmk_launch_crc32_stream(const CrcParams* P, int ncu, int variant
 #ifdef LSMCK_AB_ABLATIONS
   // the stream kernel's diagnostic ablations: only in the
   // A/B libraries tools/build_ab.sh builds with EXTRA=-DLSMCK_AB_ABLATIONS
-  const void* fn = ablate == 9 ? (const void*)crc32_stream_kernel<9>
+  const void* fn = ablate == 11 ? (const void*)crc32_stream_kernel<11>
+                 : ablate == 12 ? (const void*)crc32_stream_kernel<12>
+                 : ablate == 9 ? (const void*)crc32_stream_kernel<9>
                  : ablate == 10 ? (const void*)crc32_stream_kernel<10>
                  : ablate == 4 ? (const void*)crc32_stream_kernel<4>
                  : ablate == 5 ? (const void*)crc32_stream_kernel<5>
