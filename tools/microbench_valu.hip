@@ -46,6 +46,20 @@ __device__ __forceinline__ uint32_t step(uint32_t x, uint32_t k, uint32_t m) {
   if (OP == 20) asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(m), "v"(k), "v"(x));
   if (OP == 21) asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD" : "=v"(r) : "v"(x), "v"(k));
   if (OP == 22) asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(x), "v"(k), "v"(x));
+  // SHA-256's forms: the round constant from an SGPR, and a rotate by a 64-bit shift of a register pair
+  if (OP == 23) asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(k), "v"(m));
+  if (OP == 24) asm("v_add_u32_e32 %0, %1, %2" : "=v"(r) : "s"(k), "v"(x));
+  if (OP == 25) {
+    uint64_t p = ((uint64_t)x << 32) | m, q;
+    asm("v_lshrrev_b64 %0, 13, %1" : "=v"(q) : "v"(p));
+    r = (uint32_t)q;
+  }
+  // the event path's select on VCC: a compare writing VCC, then the select reading it
+  if (OP == 26) asm("v_cmp_gt_u32 vcc, %1, %2\n\tv_cndmask_b32 %0, %1, %2, vcc" : "=v"(r) : "v"(x), "v"(k) : "vcc");
+  // the same select with the mask in an SGPR pair written by a VOP3 compare
+  if (OP == 27) asm("v_cmp_gt_u32_e64 s[100:101], %1, %2\n\tv_cndmask_b32_e64 %0, %1, %2, s[100:101]" : "=v"(r) : "v"(x), "v"(k) : "s100", "s101");
+  // a VOP2 op with a literal (non-inline) constant
+  if (OP == 28) asm("v_and_b32_e32 %0, 0xff00ff, %1" : "=v"(r) : "v"(x));
   return r;
 }
 
@@ -76,7 +90,7 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const char* names[] = {"v_add_u32", "v_xor_b32", "v_alignbit_b32", "v_bitop3_b32", "v_add3_u32", "v_perm_b32",
                          "v_alignbyte_b32", "v_bfe_i32", "v_lshl_or_b32", "v_xad_u32", "v_cndmask_b32",
-                         "v_lshrrev_b32", "v_mov_b32_sdwa", "v_and_or_b32", "v_or_b32_sdwa PAD", "v_bitop3 (s op)", "v_lshlrev_b32_e64", "v_xor_b32_e64 (s)", "v_bitop3 (const)", "v_cndmask_e64 (s mask)", "v_bitop3 select", "v_add_u32_sdwa", "v_bitop3 (x,k,x)"};
+                         "v_lshrrev_b32", "v_mov_b32_sdwa", "v_and_or_b32", "v_or_b32_sdwa PAD", "v_bitop3 (s op)", "v_lshlrev_b32_e64", "v_xor_b32_e64 (s)", "v_bitop3 (const)", "v_cndmask_e64 (s mask)", "v_bitop3 select", "v_add_u32_sdwa", "v_bitop3 (x,k,x)", "v_add3_u32 (s op)", "v_add_u32_e32 (s src0)", "v_lshrrev_b64", "v_cmp vcc + v_cndmask_e32", "v_cmp_e64 + v_cndmask_e64", "v_and_b32 literal"};
   const void* fns[] = {(const void*)k_valu<0>, (const void*)k_valu<1>, (const void*)k_valu<2>,
                        (const void*)k_valu<3>, (const void*)k_valu<4>, (const void*)k_valu<5>,
                        (const void*)k_valu<6>, (const void*)k_valu<7>, (const void*)k_valu<8>,
@@ -84,8 +98,10 @@ int main(int argc, char** argv) {
                        (const void*)k_valu<12>, (const void*)k_valu<13>, (const void*)k_valu<14>,
                        (const void*)k_valu<15>, (const void*)k_valu<16>, (const void*)k_valu<17>,
                        (const void*)k_valu<18>, (const void*)k_valu<19>, (const void*)k_valu<20>,
-                       (const void*)k_valu<21>, (const void*)k_valu<22>};
-  for (int i = 0; i < 23; ++i) {
+                       (const void*)k_valu<21>, (const void*)k_valu<22>, (const void*)k_valu<23>,
+                       (const void*)k_valu<24>, (const void*)k_valu<25>, (const void*)k_valu<26>,
+                       (const void*)k_valu<27>, (const void*)k_valu<28>};
+  for (int i = 0; i < 29; ++i) {
     uint32_t k = 12345, m = 777;
     void* args[] = {&out, &iters, &k, &m};
     CK(hipLaunchKernel(fns[i], dim3(blocks), dim3(512), args, 0, 0));
