@@ -86,3 +86,26 @@ def test_nib_mul_equals_the_gf2_product():
     for d in range(64):
         for v in vals:
             assert nib_mul(lds, v, d) == gf2_mulmod(v, KSEG[d]), (hex(v), d)
+
+
+def test_layout_bank_conflicts_model():
+    """The bank-aware layout against round 6's first one, in the LDS model of
+    tools/lds_conflicts.py (ds_read_b32: two 32-lane groups, bank = address/4
+    mod 32): a Horner without events conflicts only in stage A (lanes l and
+    l + 16 share f), and an event tile's Horner a quarter as much as before."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "lds_conflicts", os.path.join(os.path.dirname(__file__), "..", "tools", "lds_conflicts.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    # the model's addresses are the kernel's (the same bases as build() above)
+    assert m.horner_bank(0x12345678, 0, 37, 3)[0] == NA + 1024 * 3 + 64 * 5 + 4 * (37 & 15)
+    assert m.horner_bank(0, 0x9ABCDEF0, 37, 5)[1] == NB + 256 * 5 + 64 * (37 >> 4) + 4 * 0xB
+    a1, b1 = m.horner_cycles(m.horner_bank, "bulk", tiles=60)
+    assert b1 == 0.0 and a1 <= 16.0
+    fa, fb = m.horner_cycles(m.horner_first, "bulk", tiles=60)
+    assert fa + fb >= 3 * (a1 + b1)
+    ea, eb = m.horner_cycles(m.horner_bank, "event", tiles=60)
+    ga, gb = m.horner_cycles(m.horner_first, "event", tiles=60)
+    assert ga + gb >= 3 * (ea + eb)
