@@ -1509,25 +1509,33 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     // capture, R0 or the Horner value of chunk 0; a reset drops it.
     uint32_t c0 = U[0] ^ (lane == 0u ? carry : 0u), c1 = U[16], x0 = 0u, x1 = 0u, ub0 = 0u, ub1 = 0u;
     // (ABLATE 8, diagnostic: no per-word event bodies -- results invalid)
-    const uint32_t Km = ABLATE == 8 ? 0u : (Kw & 0xFFFFu) | (Kw >> 16);
+    const uint32_t Km = ABLATE == 8 ? 0u : Kw;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const uint32_t w0 = k + 1 < 16 ? U[k + 1] : 0u, w1 = k + 1 < 16 ? U[17 + k] : 0u;
       uint32_t i0 = c0, i1 = c1, n0 = w0, n1 = w1;
+      // each chain's body only where some lane has an event in that chain's
+      // word k (uniform), not wherever either chain has one
       if (Km & (1u << k)) {
         uint32_t e = ev;
         asm volatile("" : "+v"(e));  // recomputed here, not hoisted: fewer VGPRs through the loop
-        const uint32_t be0 = e & 0xFFu, bs0 = (e >> 8) & 0xFFu, be1 = (e >> 16) & 0xFFu, bs1 = e >> 24;
+        const uint32_t be0 = e & 0xFFu, bs0 = (e >> 8) & 0xFFu;
         // chain byte j + 1 at word k: (j >> 2) == k  <=>  ((b - 1) >> 2) == k, b != 0
         const bool me0 = be0 && ((be0 - 1u) >> 2) == (uint32_t)k, ms0 = bs0 && ((bs0 - 1u) >> 2) == (uint32_t)k;
-        const bool me1 = be1 && ((be1 - 1u) >> 2) == (uint32_t)k, ms1 = bs1 && ((bs1 - 1u) >> 2) == (uint32_t)k;
-        const uint32_t mlo0 = (1u << (((bs0 - 1u) & 3u) << 3)) - 1u, mlo1 = (1u << (((bs1 - 1u) & 3u) << 3)) - 1u;
+        const uint32_t mlo0 = (1u << (((bs0 - 1u) & 3u) << 3)) - 1u;
         x0 = me0 ? c0 : x0;
         ub0 = me0 ? U[k] : ub0;
-        x1 = me1 ? c1 : x1;
-        ub1 = me1 ? U[16 + k] : ub1;
         i0 = ms0 ? ~(U[k] | mlo0) : c0;
         n0 = ms0 ? (w0 ^ mlo0) : w0;
+      }
+      if (Km & (1u << (16 + k))) {
+        uint32_t e = ev;
+        asm volatile("" : "+v"(e));
+        const uint32_t be1 = (e >> 16) & 0xFFu, bs1 = e >> 24;
+        const bool me1 = be1 && ((be1 - 1u) >> 2) == (uint32_t)k, ms1 = bs1 && ((bs1 - 1u) >> 2) == (uint32_t)k;
+        const uint32_t mlo1 = (1u << (((bs1 - 1u) & 3u) << 3)) - 1u;
+        x1 = me1 ? c1 : x1;
+        ub1 = me1 ? U[16 + k] : ub1;
         i1 = ms1 ? ~(U[16 + k] | mlo1) : c1;
         n1 = ms1 ? (w1 ^ mlo1) : w1;
       }
