@@ -1053,11 +1053,11 @@ __device__ __forceinline__ uint32_t stream_mulcol(uint32_t v, uint32_t base) {
 #define LDS_NIBA_OFF LDS_COLS_OFF            // [8 j][16 q][16 f] u32, 8 KiB
 #define LDS_NIBB_OFF (LDS_COLS_OFF + 8192u)  // [8 j][4 h][16 q] u32, 2 KiB
 static_assert((LDS_NIBA_OFF & 0x3FCu) == 0u && (LDS_NIBB_OFF & 0xFCu) == 0u, "the or-addressing needs these bits clear");
-static_assert(LDS_NIBB_OFF + 2048u <= LDS_KLO_OFF, "the nibble tables end where the finish's x^-8(4-t) columns start");
+static_assert(LDS_NIBB_OFF + 2048u <= LDS_KLO_OFF, "the nibble tables end where the klo table starts");
 
 // Tables of both stages: entry (j, q, e) = (q << 4j) (x) factor(e), with the
 // stage-A factors e = f = 0..15 and the stage-B factors e = 16h (h = 0..3).
-template <uint32_t NA, uint32_t NB, uint32_t GAP = 0u, class F>
+template <uint32_t NA, uint32_t NB, class F>
 __device__ __forceinline__ void build_nib(F factor) {
   for (uint32_t i = threadIdx.x; i < 2560u; i += blockDim.x) {
     uint32_t addr, q, j, e;
@@ -1066,7 +1066,7 @@ __device__ __forceinline__ void build_nib(F factor) {
       q = (i >> 4) & 15u;
       j = i >> 8;
       e = f;
-      addr = NA + 1024u * j + (j >= 4u ? GAP : 0u) + 64u * q + 4u * f;
+      addr = NA + 1024u * j + 64u * q + 4u * f;
     } else {  // stage B: k = (j * 4 + h) * 16 + q
       const uint32_t k = i - 2048u;
       q = k & 15u;
@@ -1079,9 +1079,8 @@ __device__ __forceinline__ void build_nib(F factor) {
   }
 }
 
-// v (x) factor(d), d = 0..63, from the tables build_nib<NA, NB, GAP> made
-// (GAP: stage A's rows j = 4..7 start GAP bytes further on)
-template <uint32_t NA, uint32_t NB, uint32_t GAP = 0u>
+// v (x) factor(d), d = 0..63, from the tables build_nib<NA, NB> made
+template <uint32_t NA, uint32_t NB>
 __device__ __forceinline__ uint32_t nib_mul(uint32_t v, uint32_t d) {
   const uint32_t bA = NA + ((d & 15u) << 2), bB = NB + ((d >> 4) << 6);
   // stage A: nibble j of v at bits 6-9 of v shifted right by 4j - 6
@@ -1089,10 +1088,10 @@ __device__ __forceinline__ uint32_t nib_mul(uint32_t v, uint32_t d) {
                                            lds_ld(nullptr, (((v << 2) & 0x3C0u) | bA) + 1024u),
                                            lds_ld(nullptr, (((v >> 2) & 0x3C0u) | bA) + 2048u), 0x96);
   u = __builtin_amdgcn_bitop3_b32(u, lds_ld(nullptr, (((v >> 6) & 0x3C0u) | bA) + 3072u),
-                                  lds_ld(nullptr, (((v >> 10) & 0x3C0u) | bA) + 4096u + GAP), 0x96);
-  u = __builtin_amdgcn_bitop3_b32(u, lds_ld(nullptr, (((v >> 14) & 0x3C0u) | bA) + 5120u + GAP),
-                                  lds_ld(nullptr, (((v >> 18) & 0x3C0u) | bA) + 6144u + GAP), 0x96);
-  u ^= lds_ld(nullptr, (((v >> 22) & 0x3C0u) | bA) + 7168u + GAP);
+                                  lds_ld(nullptr, (((v >> 10) & 0x3C0u) | bA) + 4096u), 0x96);
+  u = __builtin_amdgcn_bitop3_b32(u, lds_ld(nullptr, (((v >> 14) & 0x3C0u) | bA) + 5120u),
+                                  lds_ld(nullptr, (((v >> 18) & 0x3C0u) | bA) + 6144u), 0x96);
+  u ^= lds_ld(nullptr, (((v >> 22) & 0x3C0u) | bA) + 7168u);
   // stage B: nibble j of u at bits 2-5 of u shifted right by 4j - 2
   uint32_t y = __builtin_amdgcn_bitop3_b32(lds_ld(nullptr, ((u << 2) & 0x3Cu) | bB),
                                            lds_ld(nullptr, (((u >> 2) & 0x3Cu) | bB) + 256u),
@@ -1275,47 +1274,27 @@ __device__ __forceinline__ uint32_t horner(uint32_t v, uint32_t d) {
 }
 
 // the finish's factor: v (x) x^(8m), m = 0..63, from the bit columns.  (The
-// nibble tables here too, over the shift-by-32/96 and klo areas, ran slower:
+// nibble tables here too -- in the bank-aware layout as well: 18.94 against
+// 18.58 ms, config 3w 19.8 against 19.3, profiles/r06/finish -- over the
+// shift-by-32/96 and klo areas, ran slower:
 // config 3 19.87-19.93 against 19.11-19.20 ms, config 3w 21.10-21.22 against
 // 20.36-20.40 ms, same box, 4 / 3 interleaved rounds, profiles/r06/horner --
 // the finish runs in the few lanes that hold a record, whose LDS reads cost
 // per active lane, and its tables put the kernel at 8 spilled SGPRs.)
-#ifdef LSMCK_FINISH_NIB
-// (A/B) the finish's factor x^(8m) by the bank-aware nibble tables: stage A
-// over the shift-by-32 and shift-by-96 tables' areas (rows j = 0..3 and
-// 4..7, 8 KiB apart), stage B over the klo area (which this kernel does not
-// otherwise read)
-#define LDS_FNA_OFF LDS_SHIFT_OFF
-#define LDS_FNB_OFF LDS_KLO_OFF
-static_assert((LDS_FNA_OFF & 0x3FCu) == 0u && (LDS_FNB_OFF & 0xFCu) == 0u, "the or-addressing needs these bits clear");
-__device__ __forceinline__ uint32_t finish_mul(uint32_t v, uint32_t m) {
-  return nib_mul<LDS_FNA_OFF, LDS_FNB_OFF, 4096u>(v, m);
-}
-#else
 __device__ __forceinline__ uint32_t finish_mul(uint32_t v, uint32_t m) { return stream_mulcol(v, LDS_XMC_OFF(m)); }
-#endif
 
 template <int ABLATE = 0>
 __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
   if (!*P.sflag) return;  // a caller's batch that is not sorted / packed enough: the walking kernel takes it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   build_lds_tables(smem, P);
-  __syncthreads();  // the Horner tables reuse the cols + khi areas, x^(8m) the shift tables', x^-8(4-t) the klo area
+  __syncthreads();  // the Horner tables reuse the cols + khi areas, the finish's x^(8m) the shift-by-32/96 tables' areas
 #ifdef LSMCK_HORNER_COLS
   build_walk_cols(P);  // (A/B: round 5's bit-column Horner)
 #else
   build_nib<LDS_NIBA_OFF, LDS_NIBB_OFF>([&](uint32_t e) { return P.kseg[e]; });  // x^(8*128*e)
 #endif
-#ifdef LSMCK_FINISH_NIB
-  build_nib<LDS_FNA_OFF, LDS_FNB_OFF, 4096u>([&](uint32_t e) {  // x^(8e): e zero-byte steps of the register from x^0
-    uint32_t K = 0x80000000u;
-    for (uint32_t i = 0; i < e; ++i) K = (K >> 8) ^ lds_ld(smem, 256u * (K & 0xFFu));  // T0 (replica 0)
-    return K;
-  });
-  if (false) {
-#else
   if (threadIdx.x >= 128u && threadIdx.x < 192u) {  // the finish factors' bit columns, x^(8m)
-#endif
     const uint32_t f = threadIdx.x - 128u;
     uint32_t K = 0x80000000u;  // m zero-byte steps of the register from x^0
     for (uint32_t i = 0; i < f; ++i) K = (K >> 8) ^ lds_ld(smem, 256u * (K & 0xFFu));  // T0 (replica 0)
