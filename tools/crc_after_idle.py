@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Does the stream kernel start slow after the GPU idles or runs
+latency-bound work?  (Inside the WAL replay the CRC pass follows ~4 ms of
+the header walk and runs ~0.8 ms longer than the same pass back to back,
+profiles/r06/final2.)  Config 3's batch (bench.py's records and bytes), the
+CRC pass timed with HIP events on its stream after each kind of prelude:
+
+  back-to-back   the previous pass
+  host-idle      a 4 ms host sleep after a synchronize
+  gpu-spin       a 4 ms spin kernel on the stream (torch.cuda._sleep)
+  hbm-copy       a 4 GiB device copy on the stream (HBM busy right before)
+
+  python3 tools/crc_after_idle.py [--rounds 4]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--idle-ms", type=float, default=4.0)
+    a = ap.parse_args()
+    import torch
+    import bench
+    from lsm_storage_engine_amd.device import Context, gen_zipf_lengths
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream()
+    sptr = stream.cuda_stream
+    ctx = Context(0)
+    nrec = 1 << 26
+    offs, lens, nbytes, byte_off = bench.config3_shard(gen_zipf_lengths, bench.SEED[3], nrec, 0)
+    data = ctx.alloc(nbytes + 64)
+    ctx.gen_stream(data.ptr, bench.SEED[3], byte_off, nbytes, sptr)
+    out = ctx.alloc(4 * nrec)
+    d_off, d_len = ctx.alloc(8 * nrec), ctx.alloc(4 * nrec)
+    d_off.upload(offs)
+    d_len.upload(lens)
+    ctx.sync(sptr)
+    src = torch.empty(1 << 30, dtype=torch.int32, device="cuda")  # 4 GiB
+    dst = torch.empty_like(src)
+    # the spin kernel's rate: cycles per ms
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(1_000_000)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        e0.record(stream)
+        torch.cuda._sleep(10_000_000)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    cyc_per_ms = 10_000_000 / e0.elapsed_time(e1)
+
+    def crc():
+        ctx.crc32_device(data.ptr, d_off.ptr, d_len.ptr, nrec, out.ptr, sptr)
+
+    def timed_crc():
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(stream)
+        crc()
+        e.record(stream)
+        return s, e
+
+    res = {k: [] for k in ("back-to-back", "host-idle", "gpu-spin", "hbm-copy")}
+    crc()
+    ctx.sync(sptr)
+    for _ in range(a.rounds):
+        # back-to-back: the second of two passes
+        crc()
+        s, e = timed_crc()
+        torch.cuda.synchronize()
+        res["back-to-back"].append(s.elapsed_time(e))
+        ctx.sync(sptr)
+        time.sleep(a.idle_ms / 1e3)
+        s, e = timed_crc()
+        torch.cuda.synchronize()
+        res["host-idle"].append(s.elapsed_time(e))
+        with torch.cuda.stream(stream):
+            torch.cuda._sleep(int(cyc_per_ms * a.idle_ms))
+        s, e = timed_crc()
+        torch.cuda.synchronize()
+        res["gpu-spin"].append(s.elapsed_time(e))
+        with torch.cuda.stream(stream):
+            dst.copy_(src)
+        s, e = timed_crc()
+        torch.cuda.synchronize()
+        res["hbm-copy"].append(s.elapsed_time(e))
+    print(json.dumps({"what": "config-3 stream-kernel pass (ms, HIP events) after each prelude",
+                      "idle_ms": a.idle_ms, "spin_cycles_per_ms": round(cyc_per_ms),
+                      "ms": {k: [round(x, 3) for x in v] for k, v in res.items()},
+                      "median_ms": {k: round(sorted(v)[len(v) // 2], 3) for k, v in res.items()}}))
+
+
+if __name__ == "__main__":
+    main()
