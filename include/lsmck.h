@@ -261,6 +261,20 @@ int lsmck_device_count(void);
  *                 units; 0 = hipMemcpyAsync on a staging stream (A/B).
  *   "wal_dma_chunks"  ... cut in this many pieces (default 32; 1..64); a
  *                 pageable records array is filled piece by piece as they land.
+ *   "wal_pipe"    device replays of at least "wal_pipe_min" bytes (default
+ *                 1 GiB): the log is walked in this many parts (2..64) on a
+ *                 CU-masked stream while the previous part's CRC pass runs
+ *                 on the other CUs; 0 or 1 = off (default 0: measured slower,
+ *                 DESIGN.md 8).  "wal_pipe_first" the first part in 64ths
+ *                 of the log (1..63, default 4), "wal_pipe_cus" the walk's
+ *                 CUs (default 32), "wal_pipe_layout" which ones (0 the last,
+ *                 1 spread), "wal_pipe_seg" the parts' segment bytes (0 =
+ *                 sized to the walk's CUs).  A/B; results are the same.
+ *   "tree_readers"  whole-tree verify: reader threads per context (default
+ *                 16; 1..64).  A/B.
+ *   "crc_ablate"  diagnostic: 3 = the stream kernel with payload loads only
+ *                 (the bench's loads-only ceiling; results are garbage); 2,
+ *                 4..12 only in A/B libraries built with -DLSMCK_AB_ABLATIONS.
  * Returns 0, or LSMCK_EINVAL for an unknown key / value. */
 int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
 
@@ -274,6 +288,7 @@ int lsmck_ctx_set_option(lsmck_ctx* ctx, const char* key, long value);
  *   "wal_seg_prepairs"  its segment walk's parallel repair rounds.
  *   "wal_recs_dma"   its records' read-back to the host: the SDMA engines it
  *                    was dealt over, 0 = hipMemcpyAsync (or none read back).
+ *   "wal_pipe_parts"  its pipelined parts ("wal_pipe"; 0 = one walk, one pass).
  *   "numa_node"      the device's NUMA node (sysfs of its PCI function; -1
  *                    unknown), and "stage_numa_node" the node the context's
  *                    pinned buffers and copy threads are placed on (-1: none).
