@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--idle-ms", type=float, default=4.0)
+    ap.add_argument("--sweep", default="", help="comma list of host-idle ms: the pass after each (instead of the preludes)")
     a = ap.parse_args()
     import torch
     import bench
@@ -68,6 +69,22 @@ def main():
     res = {k: [] for k in ("back-to-back", "host-idle", "gpu-spin", "hbm-copy")}
     crc()
     ctx.sync(sptr)
+    if a.sweep:  # the pass after host idles of several lengths, interleaved
+        idles = [float(x) for x in a.sweep.split(",")]
+        sw = {x: [] for x in idles}
+        for _ in range(a.rounds):
+            for x in idles:
+                crc()
+                crc()
+                ctx.sync(sptr)
+                time.sleep(x / 1e3)
+                s, e = timed_crc()
+                torch.cuda.synchronize()
+                sw[x].append(s.elapsed_time(e))
+        print(json.dumps({"what": "config-3 stream-kernel pass (ms, HIP events) after a host idle of each length",
+                          "ms": {str(k): [round(v, 3) for v in vs] for k, vs in sw.items()},
+                          "median_ms": {str(k): round(sorted(vs)[len(vs) // 2], 3) for k, vs in sw.items()}}))
+        return
     for _ in range(a.rounds):
         # back-to-back: the second of two passes
         crc()
