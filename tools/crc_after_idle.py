@@ -9,6 +9,7 @@ CRC pass timed with HIP events on its stream after each kind of prelude:
   host-idle      a 4 ms host sleep after a synchronize
   gpu-spin       a 4 ms spin kernel on the stream (torch.cuda._sleep)
   hbm-copy       a 4 GiB device copy on the stream (HBM busy right before)
+  mfma-4ms       ~4 ms of bf16 matmuls on the stream (power-hungry right before)
 
   python3 tools/crc_after_idle.py [--rounds 4]"""
 import argparse
@@ -66,7 +67,18 @@ def main():
         e.record(stream)
         return s, e
 
-    res = {k: [] for k in ("back-to-back", "host-idle", "gpu-spin", "hbm-copy")}
+    res = {k: [] for k in ("back-to-back", "host-idle", "gpu-spin", "hbm-copy", "mfma-4ms")}
+    ma = torch.randn(8192, 8192, dtype=torch.bfloat16, device="cuda")
+    mb = torch.randn(8192, 8192, dtype=torch.bfloat16, device="cuda")
+    mc = torch.empty(8192, 8192, dtype=torch.bfloat16, device="cuda")
+    with torch.cuda.stream(stream):  # the matmul's time: iterations for ~idle_ms
+        torch.matmul(ma, mb, out=mc)
+        e0.record(stream)
+        for _ in range(4):
+            torch.matmul(ma, mb, out=mc)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    mm_iters = max(1, int(round(a.idle_ms / (e0.elapsed_time(e1) / 4))))
     crc()
     ctx.sync(sptr)
     if a.sweep:  # the pass after host idles of several lengths, interleaved
@@ -106,6 +118,12 @@ def main():
         s, e = timed_crc()
         torch.cuda.synchronize()
         res["hbm-copy"].append(s.elapsed_time(e))
+        with torch.cuda.stream(stream):  # a power-hungry prelude: bf16 matmuls on the MFMA units
+            for _ in range(mm_iters):
+                torch.matmul(ma, mb, out=mc)
+        s, e = timed_crc()
+        torch.cuda.synchronize()
+        res["mfma-4ms"].append(s.elapsed_time(e))
     print(json.dumps({"what": "config-3 stream-kernel pass (ms, HIP events) after each prelude",
                       "idle_ms": a.idle_ms, "spin_cycles_per_ms": round(cyc_per_ms),
                       "ms": {k: [round(x, 3) for x in v] for k, v in res.items()},
