@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--idle-ms", type=float, default=4.0)
     ap.add_argument("--sweep", default="", help="comma list of host-idle ms: the pass after each (instead of the preludes)")
+    ap.add_argument("--mfma-sweep", default="",
+                    help="comma list of ms of bf16 matmuls run after an --idle-ms host idle, right before the pass")
     a = ap.parse_args()
     import torch
     import bench
@@ -81,6 +83,26 @@ def main():
     mm_iters = max(1, int(round(a.idle_ms / (e0.elapsed_time(e1) / 4))))
     crc()
     ctx.sync(sptr)
+    if a.mfma_sweep:  # idle, then X ms of matmuls, then the pass (X = 0: idle alone)
+        per = (e0.elapsed_time(e1) / 4)
+        xs = [float(x) for x in a.mfma_sweep.split(",")]
+        sw = {x: [] for x in xs}
+        for _ in range(a.rounds):
+            for x in xs:
+                crc()
+                ctx.sync(sptr)
+                time.sleep(a.idle_ms / 1e3)
+                with torch.cuda.stream(stream):
+                    for _ in range(int(round(x / per))):
+                        torch.matmul(ma, mb, out=mc)
+                s, e = timed_crc()
+                torch.cuda.synchronize()
+                sw[x].append(s.elapsed_time(e))
+        print(json.dumps({"what": f"config-3 pass (ms) after a {a.idle_ms} ms idle and X ms of bf16 matmuls",
+                          "matmul_ms": round(per, 3),
+                          "ms": {str(k): [round(v, 3) for v in vs] for k, vs in sw.items()},
+                          "median_ms": {str(k): round(sorted(vs)[len(vs) // 2], 3) for k, vs in sw.items()}}))
+        return
     if a.sweep:  # the pass after host idles of several lengths, interleaved
         idles = [float(x) for x in a.sweep.split(",")]
         sw = {x: [] for x in idles}
