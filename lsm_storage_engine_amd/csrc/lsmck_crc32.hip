@@ -1489,6 +1489,13 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
         return;
       }
     }
+    // An event tile runs at wave priority 1 (above the bulk tiles' 0, below
+    // the payload issue's 3): the VALU-heavy event bodies win the issue
+    // arbitration over waves whose bulk chains wait on the LDS.  Same box,
+    // 3 interleaved rounds: config 3 19.09-19.14 -> 18.87-18.88 ms, config 3w
+    // 19.61-19.68 -> 19.21-19.32 (profiles/r06/prio; priority 2 over the word
+    // loop alone 18.90 / 19.23).
+    __builtin_amdgcn_s_setprio(1);
     // --- chunk-lane view: this chunk's events (byte + 1 in its chain, 0 = none)
     typedef __attribute__((address_space(3))) uint32_t lds_u32w_t;
     uint32_t ev = *(lds_u32w_t*)(size_t)(smap + 4u * lane);
@@ -1501,6 +1508,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
 #pragma unroll
       for (int k = 0; k < 32; ++k) x ^= U[k];
       if (x == 0x9E3779B1u) P.out[0] = x ^ ev;
+      __builtin_amdgcn_s_setprio(0);
       return;
     }
     // --- the chunk's two chains: resets at the starts, captures at the ends.
@@ -1608,6 +1616,7 @@ __global__ __launch_bounds__(1024) void crc32_stream_kernel(CrcParams P) {
     const uint32_t X63 = (uint32_t)__builtin_amdgcn_readlane((int)X, 63);
     const uint32_t cl = Ms ? 63u - (uint32_t)__builtin_clzll(Ms) : 0u;
     carry = X63 ^ (cl ? (uint32_t)__builtin_amdgcn_readlane((int)X, (int)(cl - 1u)) : 0u);
+    __builtin_amdgcn_s_setprio(0);
   };
 
   // payload slots: one tile in flight while one is checksummed; tiles past
